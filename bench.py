@@ -1,0 +1,194 @@
+"""bench.py — BASELINE.json's headline metric on config C2:
+1024 random trees (size U{1..30}, ops + - * / cos exp) x 1M rows x 5 features, Float32, fused L2
+loss, one MI355X per rank.  A step = one srhip_eval_loss over the whole population (dataset
+and compiled population resident in HBM; per-step host work: launch, per-tree did_succeed
+decisions, 1024 losses back to the host).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-seconds S]
+
+N > 1 (launched by torch.distributed.run): each rank evaluates its own population on its own
+GPU (islands are independent, src/SymbolicRegression.jl:746-793): weak scaling, no collective on
+the data path; barrier + max-over-ranks timing via torch.distributed.
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "symbolicregression.jl_amd"))
+
+PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector (= FP32 MFMA) peak, MI355X_MICROARCH.md
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--ntrees", type=int, default=1024)
+    ap.add_argument("--rows", type=int, default=1_000_000)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        # torch first: libsrhip then binds to the already-loaded HIP runtime (same soname)
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import numpy as np
+
+    import srhip
+
+    opts = srhip.Options(binary_operators=("+", "-", "*", "/"), unary_operators=("cos", "exp"))
+    nfeat, n = 5, args.rows
+    rng = np.random.default_rng(0 + 1000 * rank)
+    X = rng.standard_normal((nfeat, n)).astype(np.float32)
+    rng_y = np.random.default_rng(1 + 1000 * rank)
+    y = (2 * np.cos(X[3].astype(np.float64)) + X[0].astype(np.float64) ** 2 - 2
+         + 0.1 * rng_y.standard_normal(n)).astype(np.float32)
+    trees = srhip.random_population(args.ntrees, opts, nfeat, np.float32, seed=2 + 1000 * rank, max_size=30)
+    nodes, offs = srhip.flatten(trees, opts, np.float32)
+
+    ctx = srhip.get_context(local_rank)
+    ds = srhip.DeviceDataset(ctx, X, y)
+    loss = srhip.L2DistLoss()
+    t0 = time.perf_counter()
+    prog = srhip.Program(ctx, nodes, offs, opts, np.float32)
+    compile_ms = (time.perf_counter() - t0) * 1e3
+    st = prog.stats()
+    nodes_total, ops_total = st["total_nodes"], st["total_opnodes"]
+    work = nodes_total * n                    # tree-node x row evaluations per step
+    flops = (ops_total + 3 * args.ntrees) * n  # 1 flop / operator node / row + 3 (fused L2)
+
+    def barrier():
+        ctx.synchronize()
+        if dist is not None:
+            import torch
+
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        prog.eval_loss(ds, loss)
+    barrier()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(args.steps):
+        l, ok = prog.eval_loss(ds, loss)
+        kms.append(ctx.last_kernel_ms())
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ms_per_step = dt * 1e3 / args.steps
+    value = work * world * args.steps / dt
+    kern_ms = float(np.mean(kms))
+    achieved = flops / (kern_ms * 1e-3) / 1e12
+
+    # end-to-end per population (host compile of 1024 fresh trees + upload + eval)
+    t0 = time.perf_counter()
+    p2 = srhip.Program(ctx, nodes, offs, opts, np.float32)
+    p2.eval_loss(ds, loss)
+    e2e_ms = (time.perf_counter() - t0) * 1e3
+    p2.close()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(nodes, offs, opts, X, y, args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": "tree-node x row evals/sec (whole node), 1k trees x 1M rows f32; % VALU peak",
+            "value": value,
+            "unit": "node-row evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (X ~ N(0,1) 5x1M, y = 2cos(x4) + x1^2 - 2 + 0.1 N(0,1); trees from the "
+                    "reference's gen_random_tree_fixed_size distribution, sizes U{1..30})",
+            "config": {
+                "workload": "C2 eval-only: 1024 random trees (size<=30) x 1M rows x 5 features Float32, fused L2 loss",
+                "ntrees_per_gpu": args.ntrees, "rows": n, "features": nfeat,
+                "nodes_per_step": int(nodes_total), "opnodes_per_step": int(ops_total),
+                "parallelism": f"islands{world}" if world > 1 else "single",
+                "trees_ok": int(ok.sum()),
+            },
+            "roofline": {
+                "bound": "valu",
+                "achieved": achieved,
+                "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / PEAK_FP32_TFLOPS,
+                "traffic": None,
+                "kernel": "srhip::eval_kernel<float,8,K,0,true>",
+                "kernel_ms": kern_ms,
+                "flops_per_launch": int(flops),
+            },
+            "cpu_baseline": cpu,
+            "extra": {"compile_ms_1024_trees": compile_ms, "end_to_end_ms_per_population": e2e_ms},
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(nodes, offs, opts, X, y, target_s):
+    """The oracle (C restatement of the reference's array-at-a-time evaluator, OpenMP across
+    trees like the reference's per-population tasks) on a bounded row sample of the same
+    population, scaled to ~target_s seconds."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    threads = min(threads, os.cpu_count() or 1)
+    nodes_total = int(offs[-1])
+    m = 4096
+    t0 = time.perf_counter()
+    oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, X[:, :m].copy(), y[:m].copy(),
+                           nthreads=threads)
+    t1 = time.perf_counter() - t0
+    m2 = int(min(X.shape[1], max(m, m * target_s / max(t1, 1e-6))))
+    Xs, ys = X[:, :m2].copy(), y[:m2].copy()
+    t0 = time.perf_counter()
+    _, _, _, used = oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, Xs, ys, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": nodes_total * m2 / dt,
+        "unit": "node-row evals/s",
+        "cores": int(used),
+        "kind": "port",
+        "sample": f"all {len(offs) - 1} trees x first {m2} of the 1M rows ({dt:.1f} s), oracle/sr_oracle.c "
+                  f"array-at-a-time restatement, OpenMP over trees",
+    }
+
+
+if __name__ == "__main__":
+    main()

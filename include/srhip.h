@@ -1,0 +1,179 @@
+/*
+ * srhip.h — C ABI of libsrhip.so, the MI355X (gfx950) batched expression-evaluation
+ * engine for SymbolicRegression.jl's hot path (eval_tree_array -> _eval_loss -> score_func).
+ *
+ * Every entry point is plain C: opaque handles, plain pointers and sizes, integer status.
+ * No C++ exception crosses this boundary.  `did_succeed == false` is DATA (out_ok[t] == 0),
+ * not an error.  On a nonzero status, srhip_last_error() returns a thread-local message.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference repo):
+ *   srhip_eval_loss        <- _eval_loss / eval_loss            src/LossFunctions.jl:45-75, 97-112
+ *                             (batched over a population:       src/Population.jl:36-62,162-176,
+ *                              src/SingleIteration.jl:64-82)
+ *   srhip_eval_predict     <- eval_tree_array(tree, X, options) src/InterfaceDynamicExpressions.jl:56-63
+ *                             (-> DynamicExpressions.eval_tree_array, external v0.16)
+ *   srhip_dataset_create   <- Dataset{T,L}(X, y; weights)      src/Dataset.jl:98-225
+ *   srhip_program_create   <- the Node{T} trees + options.operators (OperatorEnum)
+ *                                                               src/Options.jl:92-150,673-681
+ *   srhip_program_set_constants <- set_constants!/Optim's constant vector (constant optimizer)
+ *                                                               src/ConstantOptimization.jl:43-81
+ *   srhip_eval_loss_batch  <- score_func over many members (convenience: create+eval+destroy)
+ *                                                               src/LossFunctions.jl:161-174
+ */
+#ifndef SRHIP_H
+#define SRHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------------------------- */
+enum {
+  SRHIP_OK = 0,
+  SRHIP_ERR_INVALID = 1,     /* malformed argument (bad tree, out-of-range feature, ...) */
+  SRHIP_ERR_UNSUPPORTED = 2, /* operator / dtype / loss the device does not implement   */
+  SRHIP_ERR_DEVICE = 3,      /* HIP runtime error                                       */
+  SRHIP_ERR_NOMEM = 4
+};
+
+/* ---- element types (Dataset{T}) --------------------------------------------------------- */
+enum { SRHIP_F32 = 0, SRHIP_F64 = 1, SRHIP_I32 = 2 };
+
+/* ---- operator codes: the device's op table (reference src/Operators.jl + Julia Base).
+ * options.operators.binops[i] / unaops[i] (1-based op index stored in Node.op) are mapped to
+ * these codes by the host binding (Julia glue / Python mirror), after the reference's own
+ * aliasing binopmap/unaopmap (src/Options.jl:92-150): ^ -> safe_pow, log -> safe_log, ...    */
+enum {
+  /* binary */
+  SRHIP_OP_ADD = 1, SRHIP_OP_SUB = 2, SRHIP_OP_MUL = 3, SRHIP_OP_DIV = 4,
+  SRHIP_OP_POW = 5,         /* safe_pow   src/Operators.jl:28-36 */
+  SRHIP_OP_GREATER = 6,     /* greater    src/Operators.jl:82-84 */
+  SRHIP_OP_COND = 7,        /* cond       src/Operators.jl:85-87 */
+  SRHIP_OP_LOGICAL_OR = 8,  /* src/Operators.jl:91-93 */
+  SRHIP_OP_LOGICAL_AND = 9, /* src/Operators.jl:94-96 */
+  SRHIP_OP_MAX = 10, SRHIP_OP_MIN = 11, /* Julia Base max/min (NaN-propagating) */
+  SRHIP_OP_MOD = 12,        /* Julia Base mod (floored, sign of divisor) */
+  SRHIP_OP_ATAN2 = 13,      /* Julia Base atan(y, x) */
+  /* unary */
+  SRHIP_OP_NEG = 32, SRHIP_OP_SQUARE = 33, SRHIP_OP_CUBE = 34, SRHIP_OP_ABS = 35,
+  SRHIP_OP_RELU = 36,       /* src/Operators.jl:88-90 (Bool strong zero) */
+  SRHIP_OP_COS = 37, SRHIP_OP_SIN = 38, SRHIP_OP_TAN = 39, SRHIP_OP_EXP = 40,
+  SRHIP_OP_LOG = 41,        /* safe_log   src/Operators.jl:37-40 */
+  SRHIP_OP_LOG2 = 42, SRHIP_OP_LOG10 = 43, SRHIP_OP_LOG1P = 44,
+  SRHIP_OP_SQRT = 45,       /* safe_sqrt  src/Operators.jl:57-60 */
+  SRHIP_OP_ACOSH = 46,      /* safe_acosh src/Operators.jl:53-56 */
+  SRHIP_OP_ATANH_CLIP = 47, /* atanh_clip src/Operators.jl:17   */
+  SRHIP_OP_SINH = 48, SRHIP_OP_COSH = 49, SRHIP_OP_TANH = 50,
+  SRHIP_OP_ASIN = 51, SRHIP_OP_ACOS = 52, SRHIP_OP_ATAN = 53, SRHIP_OP_ASINH = 54,
+  SRHIP_OP_ERF = 55, SRHIP_OP_ERFC = 56,
+  SRHIP_OP_GAMMA = 57,      /* gamma (Inf -> NaN) src/Operators.jl:11-15 */
+  SRHIP_OP_ROUND = 58, SRHIP_OP_FLOOR = 59, SRHIP_OP_CEIL = 60, SRHIP_OP_SIGN = 61,
+  SRHIP_OP_EXP2 = 62, SRHIP_OP_EXPM1 = 63, SRHIP_OP_CBRT = 64
+};
+
+/* ---- loss kinds (LossFunctions.jl 0.10/0.11 distance losses; src/LossFunctions.jl:13-33) - */
+enum {
+  SRHIP_LOSS_L2 = 0,          /* L2DistLoss (default, src/Options.jl:534-535) */
+  SRHIP_LOSS_L1 = 1,          /* L1DistLoss */
+  SRHIP_LOSS_LP = 2,          /* LPDistLoss{P}: p0 = P */
+  SRHIP_LOSS_HUBER = 3,       /* HuberLoss(d): p0 = d */
+  SRHIP_LOSS_L1_EPS_INS = 4,  /* L1EpsilonInsLoss(eps): p0 = eps */
+  SRHIP_LOSS_L2_EPS_INS = 5,  /* L2EpsilonInsLoss(eps): p0 = eps */
+  SRHIP_LOSS_LOGIT_DIST = 6,  /* LogitDistLoss */
+  SRHIP_LOSS_PERIODIC = 7,    /* PeriodicLoss(c): p0 = c */
+  SRHIP_LOSS_QUANTILE = 8     /* QuantileLoss(tau): p0 = tau */
+};
+
+/* One Node{T} (DynamicExpressions v0.16 fields: degree, constant, val, feature, op, l, r;
+ * used in the reference at src/Complexity.jl:36-42, src/MutationFunctions.jl:39,52-57).
+ * A tree is a contiguous run of nodes; node 0 of the run is the root; l/r index into the run. */
+typedef struct srhip_node {
+  uint8_t degree;   /* 0 = leaf, 1 = unary, 2 = binary */
+  uint8_t constant; /* leaf only: 1 = constant (val), 0 = feature */
+  uint16_t op;      /* 1-based index into the binary (degree 2) or unary (degree 1) op list */
+  uint16_t feature; /* 1-based feature index (feature leaf) */
+  uint16_t pad;
+  int32_t l, r;     /* child indices within the tree's node run (-1 = none) */
+  double val;       /* constant value; converted to T (exact for F32/I32 values of that type) */
+} srhip_node;
+
+typedef struct srhip_operators {
+  int32_t nbin, nuna;
+  const int32_t* binops; /* [nbin] SRHIP_OP_* code of options.operators.binops[i] */
+  const int32_t* unaops; /* [nuna] */
+} srhip_operators;
+
+typedef struct srhip_loss {
+  int32_t kind; /* SRHIP_LOSS_* */
+  int32_t pad;
+  double p0, p1;
+} srhip_loss;
+
+typedef struct srhip_ctx srhip_ctx;
+typedef struct srhip_dataset srhip_dataset;
+typedef struct srhip_program srhip_program;
+
+/* thread-local description of the last nonzero status on this thread */
+const char* srhip_last_error(void);
+/* version string, e.g. "srhip 0.1.0 gfx950" */
+const char* srhip_version(void);
+/* number of visible HIP devices (0 if none / no driver); never fails */
+int srhip_device_count(void);
+
+/* A context owns one device, one stream and device scratch. Not thread-safe: use one
+ * context per host thread (e.g. one per Julia task / per island), any number per device. */
+int srhip_ctx_create(int device_ordinal, srhip_ctx** out);
+void srhip_ctx_destroy(srhip_ctx* ctx);
+int srhip_ctx_synchronize(srhip_ctx* ctx);
+
+/* Dataset{T} upload.  Element (feature f, row j) is read from X[f*stride_feature + j*stride_row]
+ * (Julia's features x rows column-major matrix: stride_feature = 1, stride_row = nfeatures;
+ *  a C/NumPy (nfeatures, n) array: stride_feature = n, stride_row = 1).
+ * y may be NULL (prediction-only dataset); weights may be NULL (unweighted).
+ * The library copies everything before returning: no host pointer is retained. */
+int srhip_dataset_create(srhip_ctx* ctx, int dtype, const void* X, int64_t nfeatures, int64_t n,
+                         int64_t stride_feature, int64_t stride_row, const void* y,
+                         const void* weights, srhip_dataset** out);
+void srhip_dataset_destroy(srhip_dataset* ds);
+
+/* Compile + upload a batch of trees (the population) for one operator table. */
+int srhip_program_create(srhip_ctx* ctx, int dtype, const srhip_node* nodes,
+                         const int64_t* tree_offsets /* [ntrees+1] into nodes */, int32_t ntrees,
+                         const srhip_operators* ops, srhip_program** out);
+void srhip_program_destroy(srhip_program* prog);
+/* Number of constant leaves of each tree (DynamicExpressions count_constants order). */
+int srhip_program_num_constants(const srhip_program* prog, int32_t* out_nconst /*[ntrees]*/);
+/* Replace constant leaves (depth-first, left-to-right = get_constants order), all trees:
+ * consts holds sum(nconst) values, tree-major. Re-folds and re-uploads. */
+int srhip_program_set_constants(srhip_program* prog, const double* consts);
+
+/* Fused evaluate + loss for every tree of prog on ds (rows = all, or idx[0..nidx) 0-based).
+ * out_loss[t] = loss in double (L(Inf) = +Inf when !ok), out_ok[t] = did_succeed. */
+int srhip_eval_loss(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* prog,
+                    const srhip_loss* loss, const int64_t* idx, int64_t nidx,
+                    double* out_loss, uint8_t* out_ok);
+
+/* eval_tree_array for every tree: out_pred is T[ntrees][m] (m = n or nidx), row-contiguous. */
+int srhip_eval_predict(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* prog,
+                       const int64_t* idx, int64_t nidx, void* out_pred, uint8_t* out_ok);
+
+/* Convenience: program_create + eval_loss + program_destroy. */
+int srhip_eval_loss_batch(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_node* nodes,
+                          const int64_t* tree_offsets, int32_t ntrees, const srhip_operators* ops,
+                          const srhip_loss* loss, const int64_t* idx, int64_t nidx,
+                          double* out_loss, uint8_t* out_ok);
+
+/* ---- measurement hooks (bench / profiling) --------------------------------------------- */
+/* Device time (ms) of the last srhip_eval_loss/predict's main evaluation kernel, measured with
+ * HIP events recorded on the context's stream; < 0 if unavailable. */
+double srhip_last_kernel_ms(const srhip_ctx* ctx);
+/* Per-program work counters: sum over trees of count_nodes / operator nodes. */
+int srhip_program_stats(const srhip_program* prog, int64_t* total_nodes, int64_t* total_opnodes,
+                        int32_t* max_stack);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SRHIP_H */

@@ -1,0 +1,120 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes wrapper over oracle/build/liboracle.so, the C restatement of the reference's hot path
+(DynamicExpressions v0.16 eval_tree_array + src/LossFunctions.jl _loss/_weighted_loss/_eval_loss;
+see sr_oracle.c for the file:line map).  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this module; the product (srhip / libsrhip.so) never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+_lib = None
+
+_SFX = {np.dtype(np.float32): "f32", np.dtype(np.float64): "f64", np.dtype(np.int32): "i32"}
+
+
+def build() -> None:
+    subprocess.run(["make", "-C", HERE], check=True, capture_output=True)
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(LIB_PATH)
+    return _lib
+
+
+def _p(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def _setup(fn, restype, argtypes):
+    fn.restype = restype
+    fn.argtypes = argtypes
+    return fn
+
+
+def eval_tree(nodes, binops, unaops, X):
+    """eval_tree_array(tree, X, operators) -> (out, ok); X is (nfeatures, n)."""
+    lib = load()
+    X = np.ascontiguousarray(X)
+    sfx = _SFX[X.dtype]
+    n = X.shape[1]
+    out = np.empty(n, dtype=X.dtype)
+    nodes = np.ascontiguousarray(nodes)
+    b = np.ascontiguousarray(binops, dtype=np.int32)
+    u = np.ascontiguousarray(unaops, dtype=np.int32)
+    fn = _setup(getattr(lib, f"oracle_eval_tree_{sfx}"), ctypes.c_int,
+                [ctypes.c_void_p] * 4 + [ctypes.c_int64, ctypes.c_void_p])
+    ok = fn(_p(nodes), _p(b), _p(u), _p(X), n, _p(out))
+    return out, bool(ok)
+
+
+def eval_loss(nodes, binops, unaops, X, y, w=None, kind=0, p0=0.0):
+    """_eval_loss(regularization=false) -> (loss_exact, loss_reference_order, ok)."""
+    lib = load()
+    X = np.ascontiguousarray(X)
+    sfx = _SFX[X.dtype]
+    n = X.shape[1]
+    y = np.ascontiguousarray(y, dtype=X.dtype)
+    w = None if w is None else np.ascontiguousarray(w, dtype=X.dtype)
+    nodes = np.ascontiguousarray(nodes)
+    b = np.ascontiguousarray(binops, dtype=np.int32)
+    u = np.ascontiguousarray(unaops, dtype=np.int32)
+    le, lr = ctypes.c_double(), ctypes.c_double()
+    fn = _setup(getattr(lib, f"oracle_eval_loss_{sfx}"), ctypes.c_int,
+                [ctypes.c_void_p] * 6 + [ctypes.c_int64, ctypes.c_int, ctypes.c_double,
+                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)])
+    ok = fn(_p(nodes), _p(b), _p(u), _p(X), _p(y), _p(w), n, int(kind), float(p0), ctypes.byref(le),
+            ctypes.byref(lr))
+    return le.value, lr.value, bool(ok)
+
+
+def eval_loss_batch(nodes, offsets, binops, unaops, X, y, w=None, kind=0, p0=0.0, nthreads=0):
+    """Every tree, OpenMP over trees. Returns (loss_exact, loss_ref, ok, threads_used)."""
+    lib = load()
+    X = np.ascontiguousarray(X)
+    sfx = _SFX[X.dtype]
+    n = X.shape[1]
+    y = np.ascontiguousarray(y, dtype=X.dtype)
+    w = None if w is None else np.ascontiguousarray(w, dtype=X.dtype)
+    nodes = np.ascontiguousarray(nodes)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    nt = len(offsets) - 1
+    b = np.ascontiguousarray(binops, dtype=np.int32)
+    u = np.ascontiguousarray(unaops, dtype=np.int32)
+    le = np.empty(nt, dtype=np.float64)
+    lr = np.empty(nt, dtype=np.float64)
+    ok = np.empty(nt, dtype=np.uint8)
+    fn = _setup(getattr(lib, f"oracle_eval_loss_batch_{sfx}"), ctypes.c_int,
+                [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double,
+                 ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p])
+    used = fn(_p(nodes), _p(offsets), nt, _p(b), _p(u), _p(X), _p(y), _p(w), n, int(kind), float(p0),
+              int(nthreads), _p(le), _p(lr), _p(ok))
+    return le, lr, ok.astype(bool), used
+
+
+def scalar_bin(op, a, b, dtype):
+    lib = load()
+    sfx = _SFX[np.dtype(dtype)]
+    ct = {"f32": ctypes.c_float, "f64": ctypes.c_double, "i32": ctypes.c_int32}[sfx]
+    fn = _setup(getattr(lib, f"oracle_bin_{sfx}"), ct, [ctypes.c_int, ct, ct])
+    return np.dtype(dtype).type(fn(int(op), ct(a), ct(b)))
+
+
+def scalar_un(op, x, dtype):
+    lib = load()
+    sfx = _SFX[np.dtype(dtype)]
+    ct = {"f32": ctypes.c_float, "f64": ctypes.c_double, "i32": ctypes.c_int32}[sfx]
+    fn = _setup(getattr(lib, f"oracle_un_{sfx}"), ct, [ctypes.c_int, ct])
+    return np.dtype(dtype).type(fn(int(op), ct(x)))

@@ -1,0 +1,282 @@
+/* sr_oracle.c — CPU oracle for the srhip parity tests.
+ *
+ * ORACLE — TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load liboracle.so, as the checker or the timed CPU baseline; the product
+ * (libsrhip.so, the srhip package) never links or calls it.
+ *
+ * Restates, independently of the product sources:
+ *   - operator semantics: reference src/Operators.jl:11-96 (safe_pow :28-36, safe_log* :37-48,
+ *     safe_log1p :49-52, safe_acosh :53-56, safe_sqrt :57-60, square/cube/neg :65-80,
+ *     greater/cond/relu/logical_or/logical_and :82-96 with Julia's Bool strong zero),
+ *     atanh_clip :17, gamma :11-15, and the Julia Base functions they alias
+ *     (src/Options.jl:92-150);
+ *   - DynamicExpressions v0.16 eval_tree_array (sr_oracle_impl.h);
+ *   - LossFunctions.jl 0.10/0.11 distance losses used by src/LossFunctions.jl:13-33.
+ * Pinned by the reference's known-answer tests restated in tests/golden (see
+ * tests/golden/make_golden.py) — Julia is not available in this container.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/srhip.h"
+
+#define CAT_(a, b) a##b
+#define CAT(a, b) CAT_(a, b)
+
+/* ---------------- Float32 ---------------- */
+static float julia_modf32(float x, float y) {
+  const float r = fmodf(x, y);
+  if (r == 0.0f) return copysignf(r, y);
+  if ((r > 0.0f) != (y > 0.0f)) return r + y;
+  return r;
+}
+static float bin_f32(int op, float a, float b) {
+  switch (op) {
+    case SRHIP_OP_ADD: return a + b;
+    case SRHIP_OP_SUB: return a - b;
+    case SRHIP_OP_MUL: return a * b;
+    case SRHIP_OP_DIV: return a / b;
+    case SRHIP_OP_POW: {
+      const int yint = (b - truncf(b)) == 0.0f;
+      if (yint) {
+        if (b < 0.0f && a == 0.0f) return NAN;
+      } else {
+        if (b > 0.0f && a < 0.0f) return NAN;
+        if (b < 0.0f && a <= 0.0f) return NAN;
+      }
+      return (float)pow((double)a, (double)b);
+    }
+    case SRHIP_OP_GREATER: return (a > b) ? 1.0f : 0.0f;
+    case SRHIP_OP_COND: return (a > 0.0f) ? b : copysignf(0.0f, b);
+    case SRHIP_OP_LOGICAL_OR: return ((a > 0.0f) || (b > 0.0f)) ? 1.0f : 0.0f;
+    case SRHIP_OP_LOGICAL_AND: return ((a > 0.0f) && (b > 0.0f)) ? 1.0f : 0.0f;
+    case SRHIP_OP_MAX:
+      if (isnan(a) || isnan(b)) return NAN;
+      if (a == b) return signbit(a) ? b : a;
+      return a > b ? a : b;
+    case SRHIP_OP_MIN:
+      if (isnan(a) || isnan(b)) return NAN;
+      if (a == b) return signbit(a) ? a : b;
+      return a < b ? a : b;
+    case SRHIP_OP_MOD: return julia_modf32(a, b);
+    case SRHIP_OP_ATAN2: return atan2f(a, b);
+    default: return NAN;
+  }
+}
+static float un_f32(int op, float x) {
+  switch (op) {
+    case SRHIP_OP_NEG: return -x;
+    case SRHIP_OP_SQUARE: return x * x;
+    case SRHIP_OP_CUBE: return x * x * x;
+    case SRHIP_OP_ABS: return fabsf(x);
+    case SRHIP_OP_RELU: return x > 0.0f ? x : copysignf(0.0f, x);
+    case SRHIP_OP_COS: return cosf(x);
+    case SRHIP_OP_SIN: return sinf(x);
+    case SRHIP_OP_TAN: return tanf(x);
+    case SRHIP_OP_EXP: return expf(x);
+    case SRHIP_OP_LOG: return x <= 0.0f ? NAN : logf(x);
+    case SRHIP_OP_LOG2: return x <= 0.0f ? NAN : log2f(x);
+    case SRHIP_OP_LOG10: return x <= 0.0f ? NAN : log10f(x);
+    case SRHIP_OP_LOG1P: return x <= -1.0f ? NAN : log1pf(x);
+    case SRHIP_OP_SQRT: return x < 0.0f ? NAN : sqrtf(x);
+    case SRHIP_OP_ACOSH: return x < 1.0f ? NAN : acoshf(x);
+    case SRHIP_OP_ATANH_CLIP: return atanhf(julia_modf32(x + 1.0f, 2.0f) - 1.0f);
+    case SRHIP_OP_SINH: return sinhf(x);
+    case SRHIP_OP_COSH: return coshf(x);
+    case SRHIP_OP_TANH: return tanhf(x);
+    case SRHIP_OP_ASIN: return asinf(x);
+    case SRHIP_OP_ACOS: return acosf(x);
+    case SRHIP_OP_ATAN: return atanf(x);
+    case SRHIP_OP_ASINH: return asinhf(x);
+    case SRHIP_OP_ERF: return erff(x);
+    case SRHIP_OP_ERFC: return erfcf(x);
+    case SRHIP_OP_GAMMA: { const float g = tgammaf(x); return isinf(g) ? NAN : g; }
+    case SRHIP_OP_ROUND: return rintf(x);
+    case SRHIP_OP_FLOOR: return floorf(x);
+    case SRHIP_OP_CEIL: return ceilf(x);
+    case SRHIP_OP_SIGN: return x < 0.0f ? -1.0f : (x > 0.0f ? 1.0f : x);
+    case SRHIP_OP_EXP2: return exp2f(x);
+    case SRHIP_OP_EXPM1: return expm1f(x);
+    case SRHIP_OP_CBRT: return cbrtf(x);
+    default: return NAN;
+  }
+}
+static float loss_f32(int kind, float d, float p0) {
+  switch (kind) {
+    case SRHIP_LOSS_L2: return d * d;
+    case SRHIP_LOSS_L1: return fabsf(d);
+    case SRHIP_LOSS_LP: return (float)pow((double)fabsf(d), (double)p0);
+    case SRHIP_LOSS_HUBER: { const float a = fabsf(d); return a <= p0 ? 0.5f * (d * d) : p0 * (a - 0.5f * p0); }
+    case SRHIP_LOSS_L1_EPS_INS: { const float e = fabsf(d) - p0; return e > 0.0f ? e : 0.0f; }
+    case SRHIP_LOSS_L2_EPS_INS: { const float e = fabsf(d) - p0; const float m = e > 0.0f ? e : 0.0f; return m * m; }
+    case SRHIP_LOSS_LOGIT_DIST: { const float er = expf(d); const float den = 1.0f + er; return -logf(4.0f * er / (den * den)); }
+    case SRHIP_LOSS_PERIODIC: return 1.0f - cosf(d * (2.0f * 3.14159265358979323846f) / p0);
+    case SRHIP_LOSS_QUANTILE: return d * (p0 - (d < 0.0f ? 1.0f : 0.0f));
+    default: return NAN;
+  }
+}
+
+/* ---------------- Float64 ---------------- */
+static double julia_modf64(double x, double y) {
+  const double r = fmod(x, y);
+  if (r == 0.0) return copysign(r, y);
+  if ((r > 0.0) != (y > 0.0)) return r + y;
+  return r;
+}
+static double bin_f64(int op, double a, double b) {
+  switch (op) {
+    case SRHIP_OP_ADD: return a + b;
+    case SRHIP_OP_SUB: return a - b;
+    case SRHIP_OP_MUL: return a * b;
+    case SRHIP_OP_DIV: return a / b;
+    case SRHIP_OP_POW: {
+      const int yint = (b - trunc(b)) == 0.0;
+      if (yint) {
+        if (b < 0.0 && a == 0.0) return NAN;
+      } else {
+        if (b > 0.0 && a < 0.0) return NAN;
+        if (b < 0.0 && a <= 0.0) return NAN;
+      }
+      return pow(a, b);
+    }
+    case SRHIP_OP_GREATER: return (a > b) ? 1.0 : 0.0;
+    case SRHIP_OP_COND: return (a > 0.0) ? b : copysign(0.0, b);
+    case SRHIP_OP_LOGICAL_OR: return ((a > 0.0) || (b > 0.0)) ? 1.0 : 0.0;
+    case SRHIP_OP_LOGICAL_AND: return ((a > 0.0) && (b > 0.0)) ? 1.0 : 0.0;
+    case SRHIP_OP_MAX:
+      if (isnan(a) || isnan(b)) return NAN;
+      if (a == b) return signbit(a) ? b : a;
+      return a > b ? a : b;
+    case SRHIP_OP_MIN:
+      if (isnan(a) || isnan(b)) return NAN;
+      if (a == b) return signbit(a) ? a : b;
+      return a < b ? a : b;
+    case SRHIP_OP_MOD: return julia_modf64(a, b);
+    case SRHIP_OP_ATAN2: return atan2(a, b);
+    default: return NAN;
+  }
+}
+static double un_f64(int op, double x) {
+  switch (op) {
+    case SRHIP_OP_NEG: return -x;
+    case SRHIP_OP_SQUARE: return x * x;
+    case SRHIP_OP_CUBE: return x * x * x;
+    case SRHIP_OP_ABS: return fabs(x);
+    case SRHIP_OP_RELU: return x > 0.0 ? x : copysign(0.0, x);
+    case SRHIP_OP_COS: return cos(x);
+    case SRHIP_OP_SIN: return sin(x);
+    case SRHIP_OP_TAN: return tan(x);
+    case SRHIP_OP_EXP: return exp(x);
+    case SRHIP_OP_LOG: return x <= 0.0 ? NAN : log(x);
+    case SRHIP_OP_LOG2: return x <= 0.0 ? NAN : log2(x);
+    case SRHIP_OP_LOG10: return x <= 0.0 ? NAN : log10(x);
+    case SRHIP_OP_LOG1P: return x <= -1.0 ? NAN : log1p(x);
+    case SRHIP_OP_SQRT: return x < 0.0 ? NAN : sqrt(x);
+    case SRHIP_OP_ACOSH: return x < 1.0 ? NAN : acosh(x);
+    case SRHIP_OP_ATANH_CLIP: return atanh(julia_modf64(x + 1.0, 2.0) - 1.0);
+    case SRHIP_OP_SINH: return sinh(x);
+    case SRHIP_OP_COSH: return cosh(x);
+    case SRHIP_OP_TANH: return tanh(x);
+    case SRHIP_OP_ASIN: return asin(x);
+    case SRHIP_OP_ACOS: return acos(x);
+    case SRHIP_OP_ATAN: return atan(x);
+    case SRHIP_OP_ASINH: return asinh(x);
+    case SRHIP_OP_ERF: return erf(x);
+    case SRHIP_OP_ERFC: return erfc(x);
+    case SRHIP_OP_GAMMA: { const double g = tgamma(x); return isinf(g) ? NAN : g; }
+    case SRHIP_OP_ROUND: return rint(x);
+    case SRHIP_OP_FLOOR: return floor(x);
+    case SRHIP_OP_CEIL: return ceil(x);
+    case SRHIP_OP_SIGN: return x < 0.0 ? -1.0 : (x > 0.0 ? 1.0 : x);
+    case SRHIP_OP_EXP2: return exp2(x);
+    case SRHIP_OP_EXPM1: return expm1(x);
+    case SRHIP_OP_CBRT: return cbrt(x);
+    default: return NAN;
+  }
+}
+static double loss_f64(int kind, double d, double p0) {
+  switch (kind) {
+    case SRHIP_LOSS_L2: return d * d;
+    case SRHIP_LOSS_L1: return fabs(d);
+    case SRHIP_LOSS_LP: return pow(fabs(d), p0);
+    case SRHIP_LOSS_HUBER: { const double a = fabs(d); return a <= p0 ? 0.5 * (d * d) : p0 * (a - 0.5 * p0); }
+    case SRHIP_LOSS_L1_EPS_INS: { const double e = fabs(d) - p0; return e > 0.0 ? e : 0.0; }
+    case SRHIP_LOSS_L2_EPS_INS: { const double e = fabs(d) - p0; const double m = e > 0.0 ? e : 0.0; return m * m; }
+    case SRHIP_LOSS_LOGIT_DIST: { const double er = exp(d); const double den = 1.0 + er; return -log(4.0 * er / (den * den)); }
+    case SRHIP_LOSS_PERIODIC: return 1.0 - cos(d * (2.0 * 3.14159265358979323846) / p0);
+    case SRHIP_LOSS_QUANTILE: return d * (p0 - (d < 0.0 ? 1.0 : 0.0));
+    default: return NAN;
+  }
+}
+
+/* ---------------- Int32 (Julia wrap-around) ---------------- */
+static int32_t wrap(uint32_t v) { return (int32_t)v; }
+static int32_t bin_i32(int op, int32_t a, int32_t b) {
+  switch (op) {
+    case SRHIP_OP_ADD: return wrap((uint32_t)a + (uint32_t)b);
+    case SRHIP_OP_SUB: return wrap((uint32_t)a - (uint32_t)b);
+    case SRHIP_OP_MUL: return wrap((uint32_t)a * (uint32_t)b);
+    case SRHIP_OP_GREATER: return a > b;
+    case SRHIP_OP_COND: return a > 0 ? b : 0;
+    case SRHIP_OP_LOGICAL_OR: return (a > 0) || (b > 0);
+    case SRHIP_OP_LOGICAL_AND: return (a > 0) && (b > 0);
+    case SRHIP_OP_MAX: return a > b ? a : b;
+    case SRHIP_OP_MIN: return a < b ? a : b;
+    default: return 0;
+  }
+}
+static int32_t un_i32(int op, int32_t x) {
+  switch (op) {
+    case SRHIP_OP_NEG: return wrap(0u - (uint32_t)x);
+    case SRHIP_OP_SQUARE: return wrap((uint32_t)x * (uint32_t)x);
+    case SRHIP_OP_CUBE: return wrap((uint32_t)x * (uint32_t)x * (uint32_t)x);
+    case SRHIP_OP_ABS: return x < 0 ? wrap(0u - (uint32_t)x) : x;
+    case SRHIP_OP_RELU: return x > 0 ? x : 0;
+    case SRHIP_OP_SIGN: return x > 0 ? 1 : (x < 0 ? -1 : 0);
+    default: return 0;
+  }
+}
+
+/* scalar entry points (used by tests to check operator semantics one value at a time) */
+float oracle_bin_f32(int op, float a, float b) { return bin_f32(op, a, b); }
+float oracle_un_f32(int op, float x) { return un_f32(op, x); }
+double oracle_bin_f64(int op, double a, double b) { return bin_f64(op, a, b); }
+double oracle_un_f64(int op, double x) { return un_f64(op, x); }
+int32_t oracle_bin_i32(int op, int32_t a, int32_t b) { return bin_i32(op, a, b); }
+int32_t oracle_un_i32(int op, int32_t x) { return un_i32(op, x); }
+
+#define T float
+#define SFX f32
+#define IS_INT 0
+#define OVF_T (ldexpl(1.0L, 128) - ldexpl(1.0L, 103))
+#include "sr_oracle_impl.h"
+#undef T
+#undef SFX
+#undef IS_INT
+#undef OVF_T
+
+#define T double
+#define SFX f64
+#define IS_INT 0
+#define OVF_T (ldexpl(1.0L, 1024) - ldexpl(1.0L, 970))
+#include "sr_oracle_impl.h"
+#undef T
+#undef SFX
+#undef IS_INT
+#undef OVF_T
+
+#define T int32_t
+#define SFX i32
+#define IS_INT 1
+#define OVF_T 0
+static int32_t loss_i32(int kind, int32_t d, int32_t p0) { (void)p0; return kind == SRHIP_LOSS_L1 ? (d < 0 ? wrap(0u - (uint32_t)d) : d) : wrap((uint32_t)d * (uint32_t)d); }
+#include "sr_oracle_impl.h"
+#undef T
+#undef SFX
+#undef IS_INT
+#undef OVF_T

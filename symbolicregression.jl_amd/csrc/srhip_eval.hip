@@ -1,0 +1,571 @@
+// srhip_eval.hip — gfx950 kernels of the batched expression evaluator.
+//
+// Hot kernel: eval_kernel<T, R, K, MODE, XLDS>.  One workgroup owns a block of RB dataset rows
+// (staged once into LDS: X[f][RB], y, w) and its waves interpret many trees over those rows.
+// A wave holds R rows per lane (64*R rows = one tile) in VGPRs; the bytecode is wave-uniform
+// and read with scalar loads, so the interpreter's dispatch runs on the SALU/branch unit while
+// the VALU does the arithmetic.  MUST be compiled with
+//     -mllvm -structurizecfg-skip-uniform-regions=true
+// so the uniform opcode switch lowers to a scalar branch tree with in-place VGPR updates
+// (without it, the CFG structurizer inserts R phi copies per case per dispatch).
+//
+// Replaces (reference): DynamicExpressions.eval_tree_array's array-at-a-time recursion (one
+// Vector{T}(n) per node + an isfinite(sum) pass per child array) and LossFunctions' mean/sum
+// (src/LossFunctions.jl:13-33, 45-75).  See DESIGN.md for the did_succeed mapping.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "srhip_isa.h"
+#include "srhip_kernels.h"
+#include "srhip_ops.h"
+
+#define UNR _Pragma("unroll")
+#ifndef SRHIP_ROW_FENCE
+#define SRHIP_ROW_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
+
+namespace srhip {
+
+template <typename T> constexpr bool kIsInt = std::is_same<T, int32_t>::value;
+
+template <typename T>
+using OpsT = typename std::conditional<kIsInt<T>, IOps, FOps<typename std::conditional<kIsInt<T>, float, T>::type>>::type;
+
+// Which handlers exist for T (Int32 trees: ring ops and comparisons only).
+template <typename T> __device__ constexpr bool sb_ok(int sb) {
+  return !kIsInt<T> || sb != SB_DIV;
+}
+template <typename T> __device__ constexpr bool hb_ok(int) { return !kIsInt<T>; }
+template <typename T> __device__ constexpr bool un_ok(int u) {
+  return !kIsInt<T> || u == UN_NEG || u == UN_SQUARE || u == UN_CUBE || u == UN_ABS ||
+         u == UN_RELU || u == UN_SIGN;
+}
+
+// 16-byte vector of T
+template <typename T> struct Vec16;
+template <> struct Vec16<float> { typedef float __attribute__((ext_vector_type(4))) type; };
+template <> struct Vec16<int32_t> { typedef int32_t __attribute__((ext_vector_type(4))) type; };
+template <> struct Vec16<double> { typedef double __attribute__((ext_vector_type(2))) type; };
+
+// Rows of one tile owned by a lane: register r holds tile row
+//   (r / VEC) * 64 * VEC + lane * VEC + (r % VEC)        (VEC = 16 / sizeof(T))
+// so every access to a column is one 16-byte load per lane, contiguous across the wave.
+template <typename T, int R>
+__device__ __attribute__((always_inline)) inline void load_rows(const T* base, int lane, T (&v)[R]) {
+  constexpr int VEC = 16 / sizeof(T);
+  using V = typename Vec16<T>::type;
+  UNR for (int j = 0; j < R / VEC; ++j) {
+    const V q = reinterpret_cast<const V*>(base)[j * 64 + lane];
+    UNR for (int e = 0; e < VEC; ++e) v[j * VEC + e] = q[e];
+  }
+}
+
+template <typename T> __device__ __attribute__((always_inline)) inline T imm_as(uint64_t bits) {
+  if constexpr (sizeof(T) == 8) {
+    return __builtin_bit_cast(T, bits);
+  } else {
+    return __builtin_bit_cast(T, (uint32_t)bits);
+  }
+}
+
+// Check accumulator: max |v| over every operator output (NaN-propagating, v_maximum3_f32) for
+// Float32; sum of |v| * 2^-512 for Float64 (Inf/NaN propagate, cannot overflow otherwise).
+template <typename T> struct Chk {
+  using type = T;
+};
+template <int R> __device__ __attribute__((always_inline)) inline void chk_update(float& M, const float (&A)[R]) {
+  UNR for (int r = 0; r < R; r += 2)
+    M = __builtin_elementwise_maximum(M, __builtin_elementwise_maximum(__builtin_fabsf(A[r]), __builtin_fabsf(A[r + 1])));
+}
+template <int R> __device__ __attribute__((always_inline)) inline void chk_update(double& M, const double (&A)[R]) {
+  UNR for (int r = 0; r < R; ++r) M = __builtin_fma(__builtin_fabs(A[r]), 0x1p-512, M);
+}
+template <int R> __device__ __attribute__((always_inline)) inline void chk_update(int32_t&, const int32_t (&)[R]) {}
+
+template <typename T> using LAccT = typename std::conditional<kIsInt<T>, long long, double>::type;
+
+
+__device__ __attribute__((always_inline)) inline double wave_sum(double v) {
+  UNR for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __attribute__((always_inline)) inline double wave_sum_d(double v) { return wave_sum(v); }
+__device__ __attribute__((always_inline)) inline long long wave_sum(long long v) {
+  UNR for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __attribute__((always_inline)) inline float wave_chk(float v) {
+  UNR for (int o = 32; o > 0; o >>= 1) v = __builtin_elementwise_maximum(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __attribute__((always_inline)) inline double wave_chk(double v) { return wave_sum(v); }
+__device__ __attribute__((always_inline)) inline int32_t wave_chk(int32_t v) { return v; }
+
+// MODE_PRECISE: exact per-(tree, operator node, row block) sums, used only for the rare trees
+// whose fast max|v| bound cannot decide DynamicExpressions' isfinite(sum(array)) checks.
+// One wave owns a (tree, row block), so plain read-modify-write of its slab entry is race-free.
+template <typename T, int R>
+__device__ __attribute__((always_inline)) inline void precise_hook(const EvalArgs& p, uint32_t a, const T (&A)[R],
+                                                                   int ti, int rb, int lane, int64_t row0) {
+  if constexpr (!kIsInt<T>) {
+    const uint32_t opidx = a >> 16;
+    if (opidx == 0) return;
+    constexpr int VEC = 16 / sizeof(T);
+    double s = 0.0;
+    UNR for (int r = 0; r < R; ++r) {
+      const int64_t row = row0 + (r / VEC) * 64 * VEC + lane * VEC + (r % VEC);
+      const double v = sizeof(T) == 8 ? (double)A[r] * 0x1p-64 : (double)A[r];
+      s += row < p.nvalid ? v : 0.0;
+    }
+    s = wave_sum_d(s);
+    if (lane == 0) {
+      double* slot = reinterpret_cast<double*>(p.slab_prec) + ((int64_t)ti * p.prec_stride + (opidx - 1)) * p.nrb + rb;
+      *slot += s;
+    }
+  }
+}
+
+// Per-tile loss epilogue for a given loss kind (KIND < 0: runtime kind).
+template <typename T, int R>
+__device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& p, const T (&A)[R], const T* ybase,
+                                                                const T* wbase, int lane, int64_t row0,
+                                                                LAccT<T>& lacc) {
+  T yv[R];
+  load_rows<T, R>(ybase, lane, yv);
+  constexpr int VEC = 16 / sizeof(T);
+  const bool full = row0 + 64 * R <= p.nvalid;  // wave-uniform
+  if constexpr (kIsInt<T>) {
+    UNR for (int r = 0; r < R; ++r) {
+      int32_t l = loss_elem_int(p.loss_kind, IOps::sub(A[r], yv[r]));
+      long long c = (long long)l;
+      if (!full) {
+        const int64_t row = row0 + (r / VEC) * 64 * VEC + lane * VEC + (r % VEC);
+        c = row < p.nvalid ? c : 0;
+      }
+      lacc += c;
+    }
+  } else {
+    T wv[R];
+    if (p.weighted) load_rows<T, R>(wbase, lane, wv);
+    const T p0 = (T)p.loss_p0;
+    T lv[R];
+    if (p.loss_kind == SRHIP_LOSS_L2) {
+      UNR for (int r = 0; r < R; ++r) { const T d = A[r] - yv[r]; lv[r] = d * d; }
+    } else if (p.loss_kind == SRHIP_LOSS_L1) {
+      UNR for (int r = 0; r < R; ++r) lv[r] = m_abs(A[r] - yv[r]);
+    } else {
+      UNR for (int r = 0; r < R; ++r) lv[r] = loss_elem<T>(p.loss_kind, A[r] - yv[r], p0);
+    }
+    if (p.weighted) {
+      // padded rows carry w = 0 and a replicated (finite when ok) prediction
+      UNR for (int r = 0; r < R; ++r) lacc += (double)(wv[r] * lv[r]);
+    } else if (full) {
+      UNR for (int r = 0; r < R; ++r) lacc += (double)lv[r];
+    } else {
+      UNR for (int r = 0; r < R; ++r) {
+        const int64_t row = row0 + (r / VEC) * 64 * VEC + lane * VEC + (r % VEC);
+        lacc += row < p.nvalid ? (double)lv[r] : 0.0;
+      }
+    }
+  }
+}
+
+template <typename T, int R>
+__device__ __attribute__((always_inline)) inline void store_pred(const EvalArgs& p, const T (&A)[R], int tree, int lane,
+                                                                 int64_t row0) {
+  constexpr int VEC = 16 / sizeof(T);
+  using V = typename Vec16<T>::type;
+  T* out = reinterpret_cast<T*>(p.out_pred) + (int64_t)tree * p.nvalid;
+  UNR for (int j = 0; j < R / VEC; ++j) {
+    const int64_t row = row0 + j * 64 * VEC + lane * VEC;
+    if (row + VEC <= p.nvalid && ((p.nvalid % VEC) == 0)) {
+      V q;
+      UNR for (int e = 0; e < VEC; ++e) q[e] = A[j * VEC + e];
+      *reinterpret_cast<V*>(out + row) = q;
+    } else {
+      UNR for (int e = 0; e < VEC; ++e)
+        if (row + e < p.nvalid) out[row + e] = A[j * VEC + e];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// The interpreter kernel.
+//   grid.x = row blocks (RB rows each), grid.y = tree groups; block = WAVES wavefronts.
+//   MODE_LOSS: fused loss partial + check partial per (tree, row block) -> slabs
+//   MODE_PRED: prediction rows -> out_pred[tree][row], check partial -> slab
+// ------------------------------------------------------------------------------------------------
+template <typename T, int R, int K, int MODE, bool XLDS>
+__global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
+  using O = OpsT<T>;
+  using CT = typename Chk<T>::type;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int TILE = 64 * R;
+  const int lane = threadIdx.x & 63;
+  const int rb = blockIdx.x;
+  const int64_t row_base = (int64_t)rb * p.rb_rows;
+  const int ntiles = p.rb_rows / TILE;
+
+  // ---- stage this block's rows of X (and y, w) into LDS ----
+  const T* xsrc;
+  const T* ysrc;
+  const T* wsrc;
+  int64_t xstride;
+  int* counter;
+  if constexpr (XLDS) {
+    T* lx = reinterpret_cast<T*>(smem);
+    const int rbb = p.rb_rows;
+    const int ncols = p.nfeat + (p.has_y ? 1 : 0) + (p.weighted ? 1 : 0);
+    using V = typename Vec16<T>::type;
+    constexpr int VEC = 16 / sizeof(T);
+    const int vec_per_col = rbb / VEC;
+    const T* gX = reinterpret_cast<const T*>(p.X);
+    const T* gy = reinterpret_cast<const T*>(p.y);
+    const T* gw = reinterpret_cast<const T*>(p.w);
+    for (int i = threadIdx.x; i < ncols * vec_per_col; i += blockDim.x) {
+      const int c = i / vec_per_col;
+      const int v = i - c * vec_per_col;
+      const T* src = c < p.nfeat ? gX + (int64_t)c * p.ld : (c == p.nfeat ? gy : gw);
+      reinterpret_cast<V*>(lx + (int64_t)c * rbb)[v] = reinterpret_cast<const V*>(src + row_base)[v];
+    }
+    counter = reinterpret_cast<int*>(smem + (size_t)ncols * rbb * sizeof(T));
+    xsrc = lx;
+    ysrc = lx + (int64_t)p.nfeat * rbb;
+    wsrc = lx + (int64_t)(p.nfeat + 1) * rbb;
+    xstride = rbb;
+  } else {
+    counter = reinterpret_cast<int*>(smem);
+    xsrc = reinterpret_cast<const T*>(p.X) + row_base;
+    ysrc = reinterpret_cast<const T*>(p.y) + row_base;
+    wsrc = reinterpret_cast<const T*>(p.w) + row_base;
+    xstride = p.ld;
+  }
+  if (threadIdx.x == 0) *counter = 0;
+  __syncthreads();
+
+  const int group_base = blockIdx.y * p.trees_per_group;
+  const int group_n = min(p.trees_per_group, p.ntrees - group_base);
+
+  for (;;) {
+    int ti = 0;
+    if (lane == 0) ti = atomicAdd(counter, 1);
+    ti = __builtin_amdgcn_readfirstlane(__shfl(ti, 0));
+    if (ti >= group_n) break;
+    const int tree = __builtin_amdgcn_readfirstlane(p.order[group_base + ti]);
+    const int pc0 = __builtin_amdgcn_readfirstlane(p.prog_off[tree]);
+
+    LAccT<T> lacc = 0;
+    CT M = 0;
+    for (int tile = 0; tile < ntiles; ++tile) {
+      const int64_t row0 = row_base + (int64_t)tile * TILE;
+      if (row0 >= p.nvalid) break;  // whole tile is padding
+      const T* xt = xsrc + (int64_t)tile * TILE;
+      T A[R], B[R], S[K][R];
+      UNR for (int r = 0; r < R; ++r) { A[r] = T(0); B[r] = T(0); }
+      UNR for (int k = 0; k < K; ++k) UNR for (int r = 0; r < R; ++r) S[k][r] = T(0);
+      int pc = pc0;
+      for (;;) {
+        const Ins ins = p.code[pc];
+        ++pc;
+        switch (ins.h) {
+          case H_END: goto done;
+          case H_LOADF: load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A); break;
+          case H_LOADC: { const T c = imm_as<T>(ins.imm); UNR for (int r = 0; r < R; ++r) A[r] = c; break; }
+          case H_FETCHF: load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, B); break;
+          case H_FETCHC: { const T c = imm_as<T>(ins.imm); UNR for (int r = 0; r < R; ++r) B[r] = c; break; }
+#define SRHIP_K_CASES(BASE, ...)                                                            \
+  case BASE + 0: if constexpr (0 < K) { constexpr int k = 0; __VA_ARGS__ } break;                 \
+  case BASE + 1: if constexpr (1 < K) { constexpr int k = 1; __VA_ARGS__ } break;                 \
+  case BASE + 2: if constexpr (2 < K) { constexpr int k = 2; __VA_ARGS__ } break;                 \
+  case BASE + 3: if constexpr (3 < K) { constexpr int k = 3; __VA_ARGS__ } break;                 \
+  case BASE + 4: if constexpr (4 < K) { constexpr int k = 4; __VA_ARGS__ } break;                 \
+  case BASE + 5: if constexpr (5 < K) { constexpr int k = 5; __VA_ARGS__ } break;                 \
+  case BASE + 6: if constexpr (6 < K) { constexpr int k = 6; __VA_ARGS__ } break;                 \
+  case BASE + 7: if constexpr (7 < K) { constexpr int k = 7; __VA_ARGS__ } break;
+          SRHIP_K_CASES(H_PUSH0, { UNR for (int r = 0; r < R; ++r) S[k][r] = A[r]; })
+          SRHIP_K_CASES(H_FETCHS0, { UNR for (int r = 0; r < R; ++r) B[r] = S[k][r]; })
+
+#define SRHIP_SPEC_CASE(NAME, FN)                                                                  \
+  case h_spec(SB_##NAME, SPEC_AF):                                                                 \
+    if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
+      T xv[R];                                                                                     \
+      load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
+      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(A[r], xv[r]);                                   \
+      chk_update<R>(M, A);                                                                         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
+    }                                                                                              \
+    break;                                                                                         \
+  case h_spec(SB_##NAME, SPEC_FA):                                                                 \
+    if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
+      T xv[R];                                                                                     \
+      load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
+      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(xv[r], A[r]);                                   \
+      chk_update<R>(M, A);                                                                         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
+    }                                                                                              \
+    break;                                                                                         \
+  case h_spec(SB_##NAME, SPEC_AC):                                                                 \
+    if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
+      const T c = imm_as<T>(ins.imm);                                                              \
+      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(A[r], c);                                       \
+      chk_update<R>(M, A);                                                                         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
+    }                                                                                              \
+    break;                                                                                         \
+  case h_spec(SB_##NAME, SPEC_CA):                                                                 \
+    if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
+      const T c = imm_as<T>(ins.imm);                                                              \
+      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(c, A[r]);                                       \
+      chk_update<R>(M, A);                                                                         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
+    }                                                                                              \
+    break;                                                                                         \
+    SRHIP_K_CASES(h_spec(SB_##NAME, SPEC_SA0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
+      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(S[k][r], A[r]);                                 \
+      chk_update<R>(M, A);                                                                         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
+    })                                                                                             \
+    SRHIP_K_CASES(h_spec(SB_##NAME, SPEC_AS0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
+      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(A[r], S[k][r]);                                 \
+      chk_update<R>(M, A);                                                                         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
+    })
+          SRHIP_SPEC_BINOPS(SRHIP_SPEC_CASE)
+#undef SRHIP_SPEC_CASE
+
+#define SRHIP_HEAVY_CASE(NAME, FN)                                               \
+  case h_heavy(HB_##NAME, false):                                                \
+    if constexpr (hb_ok<T>(HB_##NAME)) {                                         \
+      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(A[r], B[r]);                  \
+      chk_update<R>(M, A);                                                       \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0); \
+    }                                                                            \
+    break;                                                                       \
+  case h_heavy(HB_##NAME, true):                                                 \
+    if constexpr (hb_ok<T>(HB_##NAME)) {                                         \
+      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(B[r], A[r]);                  \
+      chk_update<R>(M, A);                                                       \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0); \
+    }                                                                            \
+    break;
+          SRHIP_HEAVY_BINOPS(SRHIP_HEAVY_CASE)
+#undef SRHIP_HEAVY_CASE
+
+#define SRHIP_UN_CASE(NAME, FN)                                                  \
+  case h_un(UN_##NAME):                                                          \
+    if constexpr (un_ok<T>(UN_##NAME)) {                                         \
+      UNR for (int r = 0; r < R; ++r) { A[r] = O::FN(A[r]); SRHIP_ROW_FENCE(); } \
+      chk_update<R>(M, A);                                                       \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0); \
+    }                                                                            \
+    break;
+          SRHIP_UNOPS(SRHIP_UN_CASE)
+#undef SRHIP_UN_CASE
+#undef SRHIP_K_CASES
+          default: break;
+        }
+      }
+    done:
+      if constexpr (MODE == MODE_LOSS) {
+        loss_tile<T, R>(p, A, ysrc + (int64_t)tile * TILE, wsrc + (int64_t)tile * TILE, lane, row0, lacc);
+      } else if constexpr (MODE == MODE_PRED) {
+        store_pred<T, R>(p, A, tree, lane, row0);
+      }
+    }
+    // ---- wave reduction, one partial per (tree, row block) ----
+    if constexpr (MODE == MODE_LOSS) {
+      lacc = wave_sum(lacc);
+      if (lane == 0) reinterpret_cast<LAccT<T>*>(p.slab_loss)[(int64_t)tree * p.nrb + rb] = lacc;
+    }
+    if constexpr (!kIsInt<T> && MODE != MODE_PRECISE) {
+      M = wave_chk(M);
+      if (lane == 0) reinterpret_cast<CT*>(p.slab_chk)[(int64_t)tree * p.nrb + rb] = M;
+    }
+  }
+}
+
+// Per-tree reduction of the (tree, row block) partials, fixed order (deterministic).
+// One wavefront per tree.
+template <typename LT, typename CT, bool CHK_MAX>
+__global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab_loss, const CT* __restrict__ slab_chk,
+                                                     int nrb, int ntrees, LT* __restrict__ out_loss,
+                                                     CT* __restrict__ out_chk) {
+  const int lane = threadIdx.x & 63;
+  const int tree = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (tree >= ntrees) return;
+  LT s = 0;
+  CT m = 0;
+  for (int i = lane; i < nrb; i += 64) {
+    if (slab_loss) s += slab_loss[(int64_t)tree * nrb + i];
+    if (slab_chk) {
+      const CT v = slab_chk[(int64_t)tree * nrb + i];
+      if constexpr (CHK_MAX) m = __builtin_elementwise_maximum(m, v); else m += v;
+    }
+  }
+  UNR for (int o = 32; o > 0; o >>= 1) {
+    if (slab_loss) s += __shfl_xor(s, o);
+    if constexpr (CHK_MAX) m = __builtin_elementwise_maximum(m, __shfl_xor(m, o));
+    else m += __shfl_xor(m, o);
+  }
+  if (lane == 0) {
+    if (out_loss) out_loss[tree] = s;
+    if (out_chk) out_chk[tree] = m;
+  }
+}
+
+// View of a dataset through row indices (batching: src/LossFunctions.jl:36-42,114-127):
+// dst[f][i] = src[f][idx[i]] for i < m; rows m..ld_dst-1 replicate row idx[m-1]; w pad = 0.
+template <typename T>
+__global__ void gather_kernel(const T* __restrict__ X, const T* __restrict__ y, const T* __restrict__ w, int64_t ld_src,
+                              int nfeat, const int64_t* __restrict__ idx, int64_t m, int64_t ld_dst, T* __restrict__ Xd,
+                              T* __restrict__ yd, T* __restrict__ wd) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ld_dst) return;
+  const bool pad = i >= m;
+  const int64_t j = idx[pad ? m - 1 : i];
+  for (int f = 0; f < nfeat; ++f) Xd[(int64_t)f * ld_dst + i] = X[(int64_t)f * ld_src + j];
+  if (y) yd[i] = y[j];
+  if (w) wd[i] = pad ? T(0) : w[j];
+}
+
+// Per-feature statistics over the first m rows, for DynamicExpressions' feature-array checks
+// (isfinite(sum(X[f, :]))): count of non-finite entries and the f64 sum (Float64 data: sum of
+// x * 2^-64 so that it cannot overflow).  One block per feature.
+template <typename T>
+__global__ __launch_bounds__(256) void feature_stats_kernel(const T* __restrict__ X, int64_t ld, int64_t m,
+                                                            FeatStat* __restrict__ out) {
+  const int f = blockIdx.x;
+  const T* col = X + (int64_t)f * ld;
+  double s = 0.0;
+  unsigned long long bad = 0;
+  for (int64_t i = threadIdx.x; i < m; i += blockDim.x) {
+    const T v = col[i];
+    if (!m_isfinite(v)) bad++;
+    else s += sizeof(T) == 8 ? (double)v * 0x1p-64 : (double)v;
+  }
+  __shared__ double ss[256];
+  __shared__ unsigned long long sb[256];
+  ss[threadIdx.x] = s;
+  sb[threadIdx.x] = bad;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      ss[threadIdx.x] += ss[threadIdx.x + o];
+      sb[threadIdx.x] += sb[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[f].sum = ss[0];
+    out[f].nonfinite = (long long)sb[0];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host-side launchers (called from srhip_host.cpp)
+// ------------------------------------------------------------------------------------------------
+template <typename T, int R, int K, int MODE, bool XLDS>
+static hipError_t launch_eval_t(const EvalArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+  auto kern = eval_kernel<T, R, K, MODE, XLDS>;
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(kern, grid, dim3(64 * EVAL_WAVES), lds, s, a);
+  return hipGetLastError();
+}
+
+template <typename T, int R, int MODE, bool XLDS>
+static hipError_t launch_eval_k(const EvalArgs& a, int K, dim3 grid, size_t lds, hipStream_t s) {
+  if (K <= 4) return launch_eval_t<T, R, 4, MODE, XLDS>(a, grid, lds, s);
+  return launch_eval_t<T, R, 8, MODE, XLDS>(a, grid, lds, s);
+}
+
+template <typename T, int R>
+static hipError_t launch_eval_m(const EvalArgs& a, int K, int mode, bool xlds, dim3 grid, size_t lds, hipStream_t s) {
+  if (mode == MODE_LOSS)
+    return xlds ? launch_eval_k<T, R, MODE_LOSS, true>(a, K, grid, lds, s)
+                : launch_eval_k<T, R, MODE_LOSS, false>(a, K, grid, lds, s);
+  if (mode == MODE_PRED)
+    return xlds ? launch_eval_k<T, R, MODE_PRED, true>(a, K, grid, lds, s)
+                : launch_eval_k<T, R, MODE_PRED, false>(a, K, grid, lds, s);
+  if constexpr (!kIsInt<T>) {
+    // precise mode: rare path, K_MAX stack, global feature reads
+    (void)xlds;
+    return launch_eval_t<T, R, K_MAX, MODE_PRECISE, false>(a, grid, lds, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+int rows_per_lane(int dtype) { return dtype == SRHIP_F64 ? R_F64 : R_F32; }
+
+hipError_t launch_eval(int dtype, const EvalArgs& a, int K, int mode, bool xlds, dim3 grid, size_t lds,
+                       hipStream_t s) {
+  switch (dtype) {
+    case SRHIP_F32: return launch_eval_m<float, R_F32>(a, K, mode, xlds, grid, lds, s);
+    case SRHIP_F64: return launch_eval_m<double, R_F64>(a, K, mode, xlds, grid, lds, s);
+    case SRHIP_I32: return launch_eval_m<int32_t, R_F32>(a, K, mode, xlds, grid, lds, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_reduce(int dtype, const void* slab_loss, const void* slab_chk, int nrb, int ntrees, void* out_loss,
+                         void* out_chk, hipStream_t s) {
+  dim3 grid((ntrees + 3) / 4), block(256);
+  switch (dtype) {
+    case SRHIP_F32:
+      hipLaunchKernelGGL((reduce_kernel<double, float, true>), grid, block, 0, s, (const double*)slab_loss,
+                         (const float*)slab_chk, nrb, ntrees, (double*)out_loss, (float*)out_chk);
+      break;
+    case SRHIP_F64:
+      hipLaunchKernelGGL((reduce_kernel<double, double, false>), grid, block, 0, s, (const double*)slab_loss,
+                         (const double*)slab_chk, nrb, ntrees, (double*)out_loss, (double*)out_chk);
+      break;
+    case SRHIP_I32:
+      hipLaunchKernelGGL((reduce_kernel<long long, float, true>), grid, block, 0, s, (const long long*)slab_loss,
+                         (const float*)nullptr, nrb, ntrees, (long long*)out_loss, (float*)nullptr);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_gather(int dtype, const void* X, const void* y, const void* w, int64_t ld_src, int nfeat,
+                         const int64_t* idx, int64_t m, int64_t ld_dst, void* Xd, void* yd, void* wd, hipStream_t s) {
+  dim3 block(256), grid((unsigned)((ld_dst + 255) / 256));
+  switch (dtype) {
+    case SRHIP_F32:
+      hipLaunchKernelGGL(gather_kernel<float>, grid, block, 0, s, (const float*)X, (const float*)y, (const float*)w,
+                         ld_src, nfeat, idx, m, ld_dst, (float*)Xd, (float*)yd, (float*)wd);
+      break;
+    case SRHIP_F64:
+      hipLaunchKernelGGL(gather_kernel<double>, grid, block, 0, s, (const double*)X, (const double*)y,
+                         (const double*)w, ld_src, nfeat, idx, m, ld_dst, (double*)Xd, (double*)yd, (double*)wd);
+      break;
+    case SRHIP_I32:
+      hipLaunchKernelGGL(gather_kernel<int32_t>, grid, block, 0, s, (const int32_t*)X, (const int32_t*)y,
+                         (const int32_t*)w, ld_src, nfeat, idx, m, ld_dst, (int32_t*)Xd, (int32_t*)yd, (int32_t*)wd);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_feature_stats(int dtype, const void* X, int64_t ld, int64_t m, int nfeat, FeatStat* out,
+                                hipStream_t s) {
+  if (nfeat <= 0) return hipSuccess;
+  switch (dtype) {
+    case SRHIP_F32:
+      hipLaunchKernelGGL(feature_stats_kernel<float>, dim3(nfeat), dim3(256), 0, s, (const float*)X, ld, m, out);
+      break;
+    case SRHIP_F64:
+      hipLaunchKernelGGL(feature_stats_kernel<double>, dim3(nfeat), dim3(256), 0, s, (const double*)X, ld, m, out);
+      break;
+    default: return hipSuccess;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace srhip

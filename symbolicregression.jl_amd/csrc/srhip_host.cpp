@@ -1,0 +1,1093 @@
+// srhip_host.cpp — host side of libsrhip.so: the tree compiler (Node{T} -> bytecode), device
+// datasets, and the C ABI declared in include/srhip.h.
+//
+// The compiler restates, per tree, the host-decidable half of DynamicExpressions v0.16's
+// eval_tree_array (external dependency; behaviour pinned by the reference's
+// test/test_evaluation.jl, test/test_nan_detection.jl):
+//   * constant subtrees are evaluated once as scalars (_eval_constant_tree): any non-finite
+//     operator output => did_succeed = false; the folded value c is then a fill(c, n) array whose
+//     isfinite(sum) is checked by its parent (or by the final root check);
+//   * a non-finite constant leaf under a non-constant parent fails (@return_on_check);
+//   * a feature leaf evaluated as a child array (child of a non-fused unary node, or the root)
+//     gets its column's isfinite(sum) checked;
+//   * every remaining operator node is emitted as bytecode; the device checks its outputs.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "../../include/srhip.h"
+#include "srhip_isa.h"
+#include "srhip_kernels.h"
+#include "srhip_ops.h"
+
+using namespace srhip;
+
+// ---------------------------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                             \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess) return fail(SRHIP_ERR_DEVICE, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+  } while (0)
+
+static size_t dtype_size(int dtype) { return dtype == SRHIP_F64 ? 8 : 4; }
+
+// overflow thresholds of an exact sum rounded to T: 2^128 - 2^103 and 2^1024 - 2^970
+static long double ovf_threshold(int dtype) {
+  return dtype == SRHIP_F64 ? (ldexpl(1.0L, 1024) - ldexpl(1.0L, 970)) : (ldexpl(1.0L, 128) - ldexpl(1.0L, 103));
+}
+
+// ---------------------------------------------------------------------------------------------
+// device buffers
+// ---------------------------------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  hipError_t ensure(size_t n) {
+    if (n <= bytes && p) return hipSuccess;
+    release();
+    size_t want = n < 256 ? 256 : n;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) bytes = want;
+    return e;
+  }
+};
+struct HostBuf {  // pinned staging
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~HostBuf() { release(); }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  hipError_t ensure(size_t n) {
+    if (n <= bytes && p) return hipSuccess;
+    release();
+    size_t want = n < 256 ? 256 : n;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) bytes = want;
+    return e;
+  }
+};
+
+struct srhip_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  int num_cu = 256;
+  DevBuf slab_loss, slab_chk, red_loss, red_chk, slab_prec, order_prec;
+  DevBuf vX, vy, vw, vidx, vstats;  // gathered views (batching idx)
+  HostBuf h_loss, h_chk, h_stats, h_prec;
+};
+
+struct srhip_dataset {
+  srhip_ctx* ctx = nullptr;
+  int dtype = SRHIP_F32;
+  int64_t nfeat = 0, n = 0, ld = 0;
+  bool has_y = false, weighted = false;
+  double sum_w = 0.0;
+  DevBuf X, y, w, stats;
+  std::vector<FeatStat> hstats;  // feature stats over all n rows
+};
+
+struct TreeInfo {
+  bool static_fail = false;
+  std::vector<double> fill_consts;  // |c| * m >= OVF  => fail
+  std::vector<int> feat_checks;     // column checks (0-based features)
+  std::vector<uint8_t> op_sumcheck; // per emitted operator node: 1 = isfinite(sum) check, 0 = elementwise only
+  int32_t nconst = 0, nnodes = 0, nops = 0, need = 0;
+  int32_t code_begin = 0, code_len = 0;
+  double cost = 0.0;
+};
+
+struct srhip_program {
+  srhip_ctx* ctx = nullptr;
+  int dtype = SRHIP_F32;
+  int32_t ntrees = 0;
+  std::vector<srhip_node> nodes;
+  std::vector<int64_t> offsets;
+  std::vector<int32_t> binops, unaops;
+  std::vector<TreeInfo> info;
+  std::vector<Ins> code;
+  std::vector<int32_t> prog_off;
+  int32_t kmax = 0, max_ops = 0;
+  int64_t total_nodes = 0, total_ops = 0;
+  DevBuf d_code, d_off;
+};
+
+// ---------------------------------------------------------------------------------------------
+// tree compiler
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+template <typename T> struct HostVal {
+  static T from(double v) { return (T)v; }
+  static uint64_t bits(T v) {
+    if constexpr (sizeof(T) == 8) {
+      uint64_t b;
+      memcpy(&b, &v, 8);
+      return b;
+    } else {
+      uint32_t b;
+      memcpy(&b, &v, 4);
+      return b;
+    }
+  }
+};
+
+static double op_cost(uint32_t h) {
+  if (h == H_END) return 0.0;
+  if (h < H_BIN0) return 1.0;
+  if (h < H_HEAVY0) {
+    const int sb = (h - H_BIN0) / SPEC_STRIDE;
+    return sb == SB_DIV ? 10.0 : 2.0;
+  }
+  if (h < H_UN0) return 120.0;
+  const int u = h - H_UN0;
+  switch (u) {
+    case UN_NEG: case UN_SQUARE: case UN_CUBE: case UN_ABS: case UN_RELU: case UN_SIGN:
+    case UN_ROUND: case UN_FLOOR: case UN_CEIL:
+      return 2.0;
+    case UN_EXP: case UN_EXP2: case UN_SQRT: case UN_LOG: case UN_LOG2: case UN_LOG10:
+      return 14.0;
+    case UN_COS: case UN_SIN:
+      return 30.0;
+    default:
+      return 60.0;
+  }
+}
+
+template <typename T> class TreeCompiler {
+ public:
+  TreeCompiler(const srhip_node* nodes, int64_t nn, const srhip_program& prog, int nfeat_hint)
+      : nd_(nodes), nn_(nn), prog_(prog), nfeat_hint_(nfeat_hint) {}
+
+  // returns SRHIP_OK or an error (g_err set); fills info and appends to code
+  int compile(TreeInfo& info, std::vector<Ins>& code) {
+    info = TreeInfo();
+    if (nn_ <= 0) return fail(SRHIP_ERR_INVALID, "empty tree");
+    memo_const_.assign(nn_, -1);
+    state_.assign(nn_, 0);
+    int rc = validate(0, 0);
+    if (rc) return rc;
+    info.nnodes = count_nodes(0);
+    info.nconst = count_constants(0);
+    // host-decided checks (reference semantics, see header comment)
+    static_checks(0, -1, info);
+    info.code_begin = (int32_t)code.size();
+    if (!info.static_fail) {
+      info.need = need(0);
+      if (info.need > K_MAX)
+        return fail(SRHIP_ERR_UNSUPPORTED, "tree needs %d stack slots (> %d)", info.need, K_MAX);
+      code_ = &code;
+      info_ = &info;
+      emit(0, 0, -1);
+      Ins end{H_END, 0, 0};
+      code.push_back(end);
+      for (int64_t i = info.code_begin; i < (int64_t)code.size(); ++i) info.cost += op_cost(code[i].h);
+    } else {
+      Ins end{H_END, 0, 0};
+      code.push_back(end);
+    }
+    info.code_len = (int32_t)code.size() - info.code_begin;
+    return SRHIP_OK;
+  }
+
+ private:
+  const srhip_node* nd_;
+  int64_t nn_;
+  const srhip_program& prog_;
+  int nfeat_hint_;
+  std::vector<int8_t> memo_const_;
+  std::vector<uint8_t> state_;
+  std::vector<Ins>* code_ = nullptr;
+  TreeInfo* info_ = nullptr;
+
+  int validate(int64_t i, int depth) {
+    if (i < 0 || i >= nn_) return fail(SRHIP_ERR_INVALID, "child index %lld out of range", (long long)i);
+    if (depth > 100000) return fail(SRHIP_ERR_INVALID, "tree too deep");
+    if (state_[i] == 1) return fail(SRHIP_ERR_INVALID, "cycle in tree at node %lld", (long long)i);
+    if (state_[i] == 2) return SRHIP_OK;  // shared subtree (GraphNode) already validated
+    state_[i] = 1;
+    const srhip_node& n = nd_[i];
+    int rc = SRHIP_OK;
+    if (n.degree == 0) {
+      if (!n.constant) {
+        if (n.feature < 1) rc = fail(SRHIP_ERR_INVALID, "feature index %d < 1", (int)n.feature);
+        else if (nfeat_hint_ > 0 && n.feature > nfeat_hint_)
+          rc = fail(SRHIP_ERR_INVALID, "feature index %d > nfeatures %d", (int)n.feature, nfeat_hint_);
+      }
+    } else if (n.degree == 1) {
+      if (n.op < 1 || n.op > prog_.unaops.size())
+        rc = fail(SRHIP_ERR_INVALID, "unary op index %d out of range", (int)n.op);
+      else if (std::is_same<T, int32_t>::value && !int_unop_ok(unaop(i)))
+        rc = fail(SRHIP_ERR_UNSUPPORTED, "unary op code %d is not defined for Int32", unaop(i));
+      else rc = validate(n.l, depth + 1);
+    } else if (n.degree == 2) {
+      if (n.op < 1 || n.op > prog_.binops.size())
+        rc = fail(SRHIP_ERR_INVALID, "binary op index %d out of range", (int)n.op);
+      else if (std::is_same<T, int32_t>::value && !int_binop_ok(binop(i)))
+        rc = fail(SRHIP_ERR_UNSUPPORTED, "binary op code %d is not defined for Int32", binop(i));
+      else {
+        rc = validate(n.l, depth + 1);
+        if (!rc) rc = validate(n.r, depth + 1);
+      }
+    } else {
+      rc = fail(SRHIP_ERR_INVALID, "bad degree %d", (int)n.degree);
+    }
+    state_[i] = 2;
+    return rc;
+  }
+
+  int32_t count_nodes(int64_t i) const {
+    const srhip_node& n = nd_[i];
+    if (n.degree == 0) return 1;
+    if (n.degree == 1) return 1 + count_nodes(n.l);
+    return 1 + count_nodes(n.l) + count_nodes(n.r);
+  }
+  int32_t count_constants(int64_t i) const {
+    const srhip_node& n = nd_[i];
+    if (n.degree == 0) return n.constant ? 1 : 0;
+    if (n.degree == 1) return count_constants(n.l);
+    return count_constants(n.l) + count_constants(n.r);
+  }
+  bool is_const(int64_t i) {
+    if (memo_const_[i] >= 0) return memo_const_[i];
+    const srhip_node& n = nd_[i];
+    bool c;
+    if (n.degree == 0) c = n.constant;
+    else if (n.degree == 1) c = is_const(n.l);
+    else c = is_const(n.l) && is_const(n.r);
+    memo_const_[i] = c;
+    return c;
+  }
+  bool is_leaf(int64_t i) const { return nd_[i].degree == 0; }
+  bool leafish(int64_t i) { return is_leaf(i) || is_const(i); }
+  int binop(int64_t i) const { return prog_.binops[nd_[i].op - 1]; }
+  int unaop(int64_t i) const { return prog_.unaops[nd_[i].op - 1]; }
+
+  // scalar semantics for constant folding (DynamicExpressions _eval_constant_tree)
+  static T apply_bin(int code, T a, T b) {
+    if constexpr (std::is_same<T, int32_t>::value) {
+      switch (code) {
+        case SRHIP_OP_ADD: return IOps::add(a, b);
+        case SRHIP_OP_SUB: return IOps::sub(a, b);
+        case SRHIP_OP_MUL: return IOps::mul(a, b);
+        case SRHIP_OP_GREATER: return IOps::greater(a, b);
+        case SRHIP_OP_COND: return IOps::cond(a, b);
+        case SRHIP_OP_LOGICAL_OR: return IOps::logical_or(a, b);
+        case SRHIP_OP_LOGICAL_AND: return IOps::logical_and(a, b);
+        case SRHIP_OP_MAX: return IOps::max(a, b);
+        case SRHIP_OP_MIN: return IOps::min(a, b);
+        default: return 0;
+      }
+    } else {
+      using O = FOps<T>;
+      switch (code) {
+#define X_(NAME, FN) case SRHIP_OP_##NAME: return O::FN(a, b);
+        SRHIP_SPEC_BINOPS(X_)
+        SRHIP_HEAVY_BINOPS(X_)
+#undef X_
+        default: return FP<T>::nan();
+      }
+    }
+  }
+  static T apply_un(int code, T a) {
+    if constexpr (std::is_same<T, int32_t>::value) {
+      switch (code) {
+        case SRHIP_OP_NEG: return IOps::neg(a);
+        case SRHIP_OP_SQUARE: return IOps::square(a);
+        case SRHIP_OP_CUBE: return IOps::cube(a);
+        case SRHIP_OP_ABS: return IOps::abs(a);
+        case SRHIP_OP_RELU: return IOps::relu(a);
+        case SRHIP_OP_SIGN: return IOps::sign(a);
+        default: return 0;
+      }
+    } else {
+      using O = FOps<T>;
+      switch (code) {
+#define X_(NAME, FN) case SRHIP_OP_##NAME: return O::FN(a);
+        SRHIP_UNOPS(X_)
+#undef X_
+        default: return FP<T>::nan();
+      }
+    }
+  }
+  // returns ok; value in *v
+  bool eval_const(int64_t i, T* v) {
+    const srhip_node& n = nd_[i];
+    if (n.degree == 0) {  // deg0_eval_constant: no check on the leaf itself
+      *v = HostVal<T>::from(n.val);
+      return true;
+    }
+    if (n.degree == 1) {
+      T a;
+      if (!eval_const(n.l, &a)) return false;
+      *v = apply_un(unaop(i), a);
+      return m_isfinite(*v);
+    }
+    T a, b;
+    if (!eval_const(n.l, &a)) return false;
+    if (!eval_const(n.r, &b)) return false;
+    *v = apply_bin(binop(i), a, b);
+    return m_isfinite(*v);
+  }
+
+  // Reference fusion: node C is evaluated inline (per element, no isfinite(sum)) by its deg-1
+  // parent in DynamicExpressions' deg1_l2_ll0_lr0 / deg1_l1_ll0 kernels.
+  bool fused_inner(int64_t c, int64_t parent) const {
+    if (parent < 0 || nd_[parent].degree != 1) return false;
+    const srhip_node& n = nd_[c];
+    if (n.degree == 2) return is_leaf(n.l) && is_leaf(n.r);
+    if (n.degree == 1) return is_leaf(n.l);
+    return false;
+  }
+
+  void static_checks(int64_t i, int64_t parent, TreeInfo& info) {
+    const srhip_node& n = nd_[i];
+    const bool root = parent < 0;
+    if (is_const(i)) {
+      // constant subtree (or constant leaf): scalar path, fill(c, n) array then checked
+      if (n.degree == 0) {
+        if (root) info.fill_consts.push_back(n.val);
+        else if (!m_isfinite(HostVal<T>::from(n.val))) info.static_fail = true;  // @return_on_check
+        return;
+      }
+      T v;
+      if (!eval_const(i, &v)) {
+        info.static_fail = true;
+        return;
+      }
+      info.fill_consts.push_back((double)v);
+      return;
+    }
+    if (n.degree == 0) {  // feature leaf
+      if (root) info.feat_checks.push_back(n.feature - 1);
+      return;
+    }
+    if (n.degree == 1) {
+      const int64_t c = n.l;
+      // a feature leaf under a non-fused unary node is evaluated as an array and checked
+      if (is_leaf(c) && !nd_[c].constant && !fused_inner(i, parent)) info.feat_checks.push_back(nd_[c].feature - 1);
+      static_checks(c, i, info);
+      return;
+    }
+    static_checks(n.l, i, info);
+    static_checks(n.r, i, info);
+  }
+
+  int need(int64_t i) {
+    if (leafish(i)) return 0;
+    const srhip_node& n = nd_[i];
+    if (n.degree == 1) return need(n.l);
+    const bool ll = leafish(n.l), rl = leafish(n.r);
+    if (ll && rl) return 0;
+    if (rl) return need(n.l);
+    if (ll) return need(n.r);
+    const int a = need(n.l), b = need(n.r);
+    return a == b ? a + 1 : std::max(a, b);
+  }
+
+  void push_ins(uint32_t h, uint32_t a, uint64_t imm) { code_->push_back(Ins{h, a, imm}); }
+  // operator instruction: a = (op ordinal + 1) << 16 | operand
+  void push_op(uint32_t h, uint32_t operand, uint64_t imm, int64_t node, int64_t parent) {
+    info_->op_sumcheck.push_back((parent < 0 || !fused_inner(node, parent)) ? 1 : 0);
+    const uint32_t ord = (uint32_t)info_->op_sumcheck.size();
+    push_ins(h, (ord << 16) | (operand & 0xffff), imm);
+  }
+  uint64_t leaf_imm(int64_t i) {
+    if (nd_[i].degree == 0) return HostVal<T>::bits(HostVal<T>::from(nd_[i].val));
+    T v;
+    eval_const(i, &v);  // folded constant subtree (ok: checked in static_checks)
+    return HostVal<T>::bits(v);
+  }
+  bool leaf_is_feature(int64_t i) const { return nd_[i].degree == 0 && !nd_[i].constant; }
+
+  void emit_leaf(int64_t i) {
+    if (leaf_is_feature(i)) push_ins(H_LOADF, nd_[i].feature - 1, 0);
+    else push_ins(H_LOADC, 0, leaf_imm(i));
+  }
+
+  void emit(int64_t i, int base, int64_t parent) {
+    if (leafish(i)) {
+      emit_leaf(i);
+      return;
+    }
+    const srhip_node& n = nd_[i];
+    if (n.degree == 1) {
+      emit(n.l, base, i);
+      push_op(h_un(classify_unop(unaop(i))), 0, 0, i, parent);
+      return;
+    }
+    int sb, hb;
+    classify_binop(binop(i), &sb, &hb);
+    const int64_t L = n.l, Rr = n.r;
+    const bool ll = leafish(L), rl = leafish(Rr);
+    if (sb >= 0) {
+      if (rl) {
+        emit(L, base, i);
+        if (leaf_is_feature(Rr)) push_op(h_spec(sb, SPEC_AF), nd_[Rr].feature - 1, 0, i, parent);
+        else push_op(h_spec(sb, SPEC_AC), 0, leaf_imm(Rr), i, parent);
+      } else if (ll) {
+        emit(Rr, base, i);
+        if (leaf_is_feature(L)) push_op(h_spec(sb, SPEC_FA), nd_[L].feature - 1, 0, i, parent);
+        else push_op(h_spec(sb, SPEC_CA), 0, leaf_imm(L), i, parent);
+      } else if (need(L) >= need(Rr)) {
+        emit(L, base, i);
+        push_ins(H_PUSH0 + base, 0, 0);
+        emit(Rr, base + 1, i);
+        push_op(h_spec(sb, SPEC_SA0 + base), 0, 0, i, parent);
+      } else {
+        emit(Rr, base, i);
+        push_ins(H_PUSH0 + base, 0, 0);
+        emit(L, base + 1, i);
+        push_op(h_spec(sb, SPEC_AS0 + base), 0, 0, i, parent);
+      }
+      return;
+    }
+    // heavy binary op: operand in B
+    if (rl) {
+      emit(L, base, i);
+      if (leaf_is_feature(Rr)) push_ins(H_FETCHF, nd_[Rr].feature - 1, 0);
+      else push_ins(H_FETCHC, 0, leaf_imm(Rr));
+      push_op(h_heavy(hb, false), 0, 0, i, parent);  // A = A op B
+    } else if (ll) {
+      emit(Rr, base, i);
+      if (leaf_is_feature(L)) push_ins(H_FETCHF, nd_[L].feature - 1, 0);
+      else push_ins(H_FETCHC, 0, leaf_imm(L));
+      push_op(h_heavy(hb, true), 0, 0, i, parent);   // A = B op A
+    } else if (need(L) >= need(Rr)) {
+      emit(L, base, i);
+      push_ins(H_PUSH0 + base, 0, 0);
+      emit(Rr, base + 1, i);
+      push_ins(H_FETCHS0 + base, 0, 0);
+      push_op(h_heavy(hb, true), 0, 0, i, parent);   // A = S op A
+    } else {
+      emit(Rr, base, i);
+      push_ins(H_PUSH0 + base, 0, 0);
+      emit(L, base + 1, i);
+      push_ins(H_FETCHS0 + base, 0, 0);
+      push_op(h_heavy(hb, false), 0, 0, i, parent);  // A = A op S
+    }
+  }
+};
+
+template <typename T>
+int compile_program_t(srhip_program& P) {
+  P.code.clear();
+  P.prog_off.assign(P.ntrees, 0);
+  P.info.assign(P.ntrees, TreeInfo());
+  P.kmax = 0;
+  P.max_ops = 0;
+  P.total_nodes = 0;
+  P.total_ops = 0;
+  for (int32_t t = 0; t < P.ntrees; ++t) {
+    const int64_t b = P.offsets[t], e = P.offsets[t + 1];
+    TreeCompiler<T> tc(P.nodes.data() + b, e - b, P, 0);
+    int rc = tc.compile(P.info[t], P.code);
+    if (rc) return fail(rc, "tree %d: %s", (int)t, g_err.c_str());
+    P.prog_off[t] = P.info[t].code_begin;
+    P.kmax = std::max(P.kmax, P.info[t].need);
+    P.max_ops = std::max(P.max_ops, (int32_t)P.info[t].op_sumcheck.size());
+    P.total_nodes += P.info[t].nnodes;
+  }
+  // operator-node count (degree >= 1), from the node tables
+  for (int32_t t = 0; t < P.ntrees; ++t)
+    for (int64_t i = P.offsets[t]; i < P.offsets[t + 1]; ++i) P.total_ops += P.nodes[i].degree > 0;
+  return SRHIP_OK;
+}
+
+int compile_program(srhip_program& P) {
+  switch (P.dtype) {
+    case SRHIP_F32: return compile_program_t<float>(P);
+    case SRHIP_F64: return compile_program_t<double>(P);
+    case SRHIP_I32: return compile_program_t<int32_t>(P);
+    default: return fail(SRHIP_ERR_INVALID, "bad dtype %d", P.dtype);
+  }
+}
+
+int upload_program(srhip_program& P) {
+  HIP_TRY(hipSetDevice(P.ctx->device));
+  HIP_TRY(P.d_code.ensure(P.code.size() * sizeof(Ins)));
+  HIP_TRY(P.d_off.ensure(std::max<size_t>(1, P.prog_off.size()) * sizeof(int32_t)));
+  HIP_TRY(hipMemcpyAsync(P.d_code.p, P.code.data(), P.code.size() * sizeof(Ins), hipMemcpyHostToDevice, P.ctx->stream));
+  if (!P.prog_off.empty())
+    HIP_TRY(hipMemcpyAsync(P.d_off.p, P.prog_off.data(), P.prog_off.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                           P.ctx->stream));
+  HIP_TRY(hipStreamSynchronize(P.ctx->stream));
+  return SRHIP_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// evaluation driver
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+struct View {
+  const void* X;
+  const void* y;
+  const void* w;
+  int64_t ld, m;
+  const FeatStat* stats;  // host
+  double sum_w;
+};
+
+int make_view(srhip_ctx* ctx, const srhip_dataset* ds, const int64_t* idx, int64_t nidx, bool need_y, View& v) {
+  if (need_y && !ds->has_y) return fail(SRHIP_ERR_INVALID, "dataset has no y");
+  if (!idx) {
+    v.X = ds->X.p;
+    v.y = ds->y.p;
+    v.w = ds->weighted ? ds->w.p : nullptr;
+    v.ld = ds->ld;
+    v.m = ds->n;
+    v.stats = ds->hstats.data();
+    v.sum_w = ds->sum_w;
+    return SRHIP_OK;
+  }
+  if (nidx <= 0) return fail(SRHIP_ERR_INVALID, "empty idx");
+  for (int64_t i = 0; i < nidx; ++i)
+    if (idx[i] < 0 || idx[i] >= ds->n) return fail(SRHIP_ERR_INVALID, "idx[%lld] = %lld out of range", (long long)i, (long long)idx[i]);
+  const size_t es = dtype_size(ds->dtype);
+  const int64_t ld = (nidx + ROW_ALIGN - 1) / ROW_ALIGN * ROW_ALIGN;
+  HIP_TRY(ctx->vX.ensure((size_t)std::max<int64_t>(1, ds->nfeat) * ld * es));
+  HIP_TRY(ctx->vy.ensure((size_t)ld * es));
+  HIP_TRY(ctx->vw.ensure((size_t)ld * es));
+  HIP_TRY(ctx->vidx.ensure((size_t)nidx * sizeof(int64_t)));
+  HIP_TRY(ctx->vstats.ensure((size_t)std::max<int64_t>(1, ds->nfeat) * sizeof(FeatStat)));
+  HIP_TRY(ctx->h_stats.ensure((size_t)std::max<int64_t>(1, ds->nfeat) * sizeof(FeatStat)));
+  HIP_TRY(hipMemcpyAsync(ctx->vidx.p, idx, (size_t)nidx * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(launch_gather(ds->dtype, ds->X.p, ds->has_y ? ds->y.p : nullptr, ds->weighted ? ds->w.p : nullptr, ds->ld,
+                        (int)ds->nfeat, (const int64_t*)ctx->vidx.p, nidx, ld, ctx->vX.p,
+                        ds->has_y ? ctx->vy.p : nullptr, ds->weighted ? ctx->vw.p : nullptr, ctx->stream));
+  HIP_TRY(launch_feature_stats(ds->dtype, ctx->vX.p, ld, nidx, (int)ds->nfeat, (FeatStat*)ctx->vstats.p, ctx->stream));
+  if (ds->dtype != SRHIP_I32 && ds->nfeat > 0)
+    HIP_TRY(hipMemcpyAsync(ctx->h_stats.p, ctx->vstats.p, (size_t)ds->nfeat * sizeof(FeatStat), hipMemcpyDeviceToHost,
+                           ctx->stream));
+  double sw = 0.0;
+  if (ds->weighted) {
+    // sum of gathered weights, from the host copy kept at upload
+    // (computed below by the caller from the device buffer would need a sync; weights are small)
+  }
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  v.X = ctx->vX.p;
+  v.y = ds->has_y ? ctx->vy.p : nullptr;
+  v.w = ds->weighted ? ctx->vw.p : nullptr;
+  v.ld = ld;
+  v.m = nidx;
+  v.stats = (const FeatStat*)ctx->h_stats.p;
+  v.sum_w = sw;
+  return SRHIP_OK;
+}
+
+struct LaunchPlan {
+  int rb_rows, nrb, groups, tpg;
+  bool xlds;
+  size_t lds;
+};
+
+LaunchPlan plan_launch(const srhip_ctx* ctx, int dtype, int64_t nfeat, bool weighted, bool with_y, int64_t m,
+                       int32_t ntrees) {
+  LaunchPlan L;
+  const int R = rows_per_lane(dtype);
+  const int tile = 64 * R;
+  const size_t es = dtype_size(dtype);
+  const int ncols = (int)nfeat + (with_y ? 1 : 0) + (weighted ? 1 : 0);
+  const size_t budget = 64 * 1024 - 64;
+  int rb = ROW_ALIGN;
+  while (rb > tile && (size_t)ncols * rb * es > budget) rb /= 2;
+  // do not make blocks much larger than the data
+  while (rb > tile && rb / 2 >= m) rb /= 2;
+  L.rb_rows = rb;
+  L.xlds = (size_t)ncols * rb * es <= budget;
+  L.lds = (L.xlds ? (size_t)ncols * rb * es : 0) + 16;
+  L.nrb = (int)((m + rb - 1) / rb);
+  const int target_blocks = 4 * ctx->num_cu;
+  int g = (target_blocks + L.nrb - 1) / L.nrb;
+  const int max_g = std::max(1, ntrees / (2 * EVAL_WAVES));
+  g = std::max(1, std::min(g, max_g));
+  L.groups = g;
+  L.tpg = (ntrees + g - 1) / g;
+  L.groups = (ntrees + L.tpg - 1) / L.tpg;
+  return L;
+}
+
+// trees sorted by estimated cost (desc), dealt round-robin to groups; returns order [ntrees]
+std::vector<int32_t> make_order(const srhip_program& P, const std::vector<int32_t>& trees, int groups, int tpg) {
+  std::vector<int32_t> s(trees);
+  std::stable_sort(s.begin(), s.end(), [&](int32_t a, int32_t b) { return P.info[a].cost > P.info[b].cost; });
+  const int n = (int)s.size();
+  std::vector<int32_t> order(s.size());
+  std::vector<int> fill(groups, 0), cap(groups, 0);
+  for (int g = 0; g < groups; ++g) cap[g] = std::max(0, std::min(tpg, n - g * tpg));
+  int g = 0;
+  for (int i = 0; i < n; ++i) {
+    while (fill[g] >= cap[g]) g = (g + 1) % groups;  // the last group may be shorter
+    order[(size_t)g * tpg + fill[g]++] = s[i];
+    g = (g + 1) % groups;
+  }
+  return order;
+}
+
+// Host decision from the device partials.  Returns 0 ok, 1 fail, 2 uncertain (needs precise pass)
+int decide(const srhip_program& P, int32_t t, int dtype, const View& v, double chk) {
+  const TreeInfo& I = P.info[t];
+  if (I.static_fail) return 1;
+  if (dtype == SRHIP_I32) return 0;
+  const long double ovf = ovf_threshold(dtype);
+  for (double c : I.fill_consts)
+    if ((long double)fabs(c) * (long double)v.m >= ovf) return 1;
+  for (int f : I.feat_checks) {
+    const FeatStat& s = v.stats[f];
+    if (s.nonfinite > 0) return 1;
+    const long double sum = dtype == SRHIP_F64 ? ldexpl((long double)s.sum, 64) : (long double)s.sum;
+    if (fabsl(sum) >= ovf) return 1;
+  }
+  if (I.op_sumcheck.empty()) return 0;
+  if (!isfinite(chk)) return 1;  // a NaN / Inf operator output
+  long double bound;
+  if (dtype == SRHIP_F64) bound = ldexpl((long double)chk, 512);     // sum |v|
+  else bound = (long double)chk * (long double)v.m;                   // m * max |v|
+  if (bound * 2.0L >= ovf) return 2;
+  return 0;
+}
+
+}  // namespace
+
+static int run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
+                    const int64_t* idx, int64_t nidx, double* out_loss, void* out_pred, uint8_t* out_ok) {
+  if (!ctx || !ds || !P) return fail(SRHIP_ERR_INVALID, "null handle");
+  if (ds->dtype != P->dtype) return fail(SRHIP_ERR_INVALID, "dataset dtype %d != program dtype %d", ds->dtype, P->dtype);
+  if (ds->ctx != ctx || P->ctx != ctx) return fail(SRHIP_ERR_INVALID, "handles belong to a different context");
+  // feature range check against this dataset
+  for (const srhip_node& n : P->nodes)
+    if (n.degree == 0 && !n.constant && n.feature > ds->nfeat)
+      return fail(SRHIP_ERR_INVALID, "tree uses feature %d but dataset has %lld features", (int)n.feature, (long long)ds->nfeat);
+  const int dtype = P->dtype;
+  if (mode == MODE_LOSS) {
+    if (!loss) return fail(SRHIP_ERR_INVALID, "null loss");
+    if (dtype == SRHIP_I32 && loss->kind != SRHIP_LOSS_L2 && loss->kind != SRHIP_LOSS_L1)
+      return fail(SRHIP_ERR_UNSUPPORTED, "Int32 datasets support L2/L1 losses only");
+    if (loss->kind < SRHIP_LOSS_L2 || loss->kind > SRHIP_LOSS_QUANTILE)
+      return fail(SRHIP_ERR_UNSUPPORTED, "loss kind %d", loss->kind);
+  }
+  HIP_TRY(hipSetDevice(ctx->device));
+  View v;
+  int rc = make_view(ctx, ds, idx, nidx, mode == MODE_LOSS, v);
+  if (rc) return rc;
+  if (idx && ds->weighted && mode == MODE_LOSS) {
+    // sum of gathered weights from the device copy (deterministic host sum)
+    std::vector<unsigned char> wbuf((size_t)nidx * dtype_size(dtype));
+    HIP_TRY(hipMemcpy(wbuf.data(), ctx->vw.p, wbuf.size(), hipMemcpyDeviceToHost));
+    double s = 0.0;
+    for (int64_t i = 0; i < nidx; ++i)
+      s += dtype == SRHIP_F64 ? ((double*)wbuf.data())[i] : (double)((float*)wbuf.data())[i];
+    v.sum_w = s;
+  }
+  const int32_t nt = P->ntrees;
+  for (int32_t t = 0; t < nt; ++t) {
+    if (out_ok) out_ok[t] = 0;
+    if (out_loss) out_loss[t] = INFINITY;
+  }
+  if (nt == 0) return SRHIP_OK;
+  const bool weighted = ds->weighted && mode == MODE_LOSS;
+  std::vector<int32_t> live;
+  live.reserve(nt);
+  for (int32_t t = 0; t < nt; ++t)
+    if (!P->info[t].static_fail) live.push_back(t);
+  std::vector<uint8_t> status(nt, 1);
+  std::vector<double> lsum(nt, 0.0), chk(nt, 0.0);
+  const size_t es = dtype_size(dtype);
+  LaunchPlan L = plan_launch(ctx, dtype, ds->nfeat, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size());
+  if (!live.empty()) {
+    const int nl = (int)live.size();
+    std::vector<int32_t> order = make_order(*P, live, L.groups, L.tpg);
+    // order buffer + slabs (indexed by tree id)
+    HIP_TRY(ctx->order_prec.ensure(order.size() * sizeof(int32_t)));
+    HIP_TRY(hipMemcpyAsync(ctx->order_prec.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                           ctx->stream));
+    HIP_TRY(ctx->slab_loss.ensure((size_t)nt * L.nrb * 8));
+    HIP_TRY(ctx->slab_chk.ensure((size_t)nt * L.nrb * 8));
+    HIP_TRY(ctx->red_loss.ensure((size_t)nt * 8));
+    HIP_TRY(ctx->red_chk.ensure((size_t)nt * 8));
+    HIP_TRY(ctx->h_loss.ensure((size_t)nt * 8));
+    HIP_TRY(ctx->h_chk.ensure((size_t)nt * 8));
+    EvalArgs a{};
+    a.code = (const Ins*)P->d_code.p;
+    a.prog_off = (const int32_t*)P->d_off.p;
+    a.order = (const int32_t*)ctx->order_prec.p;
+    a.X = v.X;
+    a.y = v.y;
+    a.w = weighted ? v.w : nullptr;
+    a.slab_loss = ctx->slab_loss.p;
+    a.slab_chk = ctx->slab_chk.p;
+    a.ld = v.ld;
+    a.nvalid = v.m;
+    a.ntrees = nl;
+    a.nfeat = (int32_t)ds->nfeat;
+    a.rb_rows = L.rb_rows;
+    a.nrb = L.nrb;
+    a.trees_per_group = L.tpg;
+    a.loss_kind = loss ? loss->kind : 0;
+    a.loss_p0 = loss ? loss->p0 : 0.0;
+    a.weighted = weighted ? 1 : 0;
+    a.has_y = mode == MODE_LOSS ? 1 : 0;
+    DevBuf pred;
+    if (mode == MODE_PRED) {
+      HIP_TRY(pred.ensure((size_t)nt * v.m * es));
+      a.out_pred = pred.p;
+    }
+    const int K = P->kmax <= 4 ? 4 : 8;
+    dim3 grid(L.nrb, L.groups);
+    HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+    HIP_TRY(launch_eval(dtype, a, K, mode, L.xlds, grid, L.lds, ctx->stream));
+    HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+    ctx->timed = true;
+    HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p,
+                          L.nrb, nt, mode == MODE_LOSS ? ctx->red_loss.p : nullptr,
+                          dtype == SRHIP_I32 ? nullptr : ctx->red_chk.p, ctx->stream));
+    if (mode == MODE_LOSS)
+      HIP_TRY(hipMemcpyAsync(ctx->h_loss.p, ctx->red_loss.p, (size_t)nt * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (dtype != SRHIP_I32)
+      HIP_TRY(hipMemcpyAsync(ctx->h_chk.p, ctx->red_chk.p, (size_t)nt * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (mode == MODE_PRED)
+      HIP_TRY(hipMemcpyAsync(out_pred, pred.p, (size_t)nt * v.m * es, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (int32_t t : live) {
+      if (mode == MODE_LOSS) {
+        if (dtype == SRHIP_I32) lsum[t] = (double)((long long*)ctx->h_loss.p)[t];
+        else lsum[t] = ((double*)ctx->h_loss.p)[t];
+      }
+      if (dtype == SRHIP_F32) chk[t] = ((float*)ctx->h_chk.p)[t];
+      else if (dtype == SRHIP_F64) chk[t] = ((double*)ctx->h_chk.p)[t];
+    }
+  }
+  // decisions
+  std::vector<int32_t> unc;
+  for (int32_t t = 0; t < nt; ++t) {
+    status[t] = (uint8_t)decide(*P, t, dtype, v, chk[t]);
+    if (status[t] == 2) unc.push_back(t);
+  }
+  // precise pass for undecided trees: exact per-operator-node sums over the evaluated rows
+  if (!unc.empty()) {
+    const int nu = (int)unc.size();
+    const int stride = std::max(1, P->max_ops);
+    LaunchPlan Lp = plan_launch(ctx, dtype, ds->nfeat, false, false, v.m, nu);
+    Lp.groups = 1;
+    Lp.tpg = nu;
+    const size_t slab_bytes = (size_t)nu * stride * Lp.nrb * sizeof(double);
+    HIP_TRY(ctx->slab_prec.ensure(slab_bytes));
+    HIP_TRY(hipMemsetAsync(ctx->slab_prec.p, 0, slab_bytes, ctx->stream));
+    HIP_TRY(ctx->order_prec.ensure((size_t)nu * sizeof(int32_t)));
+    HIP_TRY(hipMemcpyAsync(ctx->order_prec.p, unc.data(), (size_t)nu * sizeof(int32_t), hipMemcpyHostToDevice,
+                           ctx->stream));
+    EvalArgs a{};
+    a.code = (const Ins*)P->d_code.p;
+    a.prog_off = (const int32_t*)P->d_off.p;
+    a.order = (const int32_t*)ctx->order_prec.p;
+    a.X = v.X;
+    a.ld = v.ld;
+    a.nvalid = v.m;
+    a.ntrees = nu;
+    a.nfeat = (int32_t)ds->nfeat;
+    a.rb_rows = Lp.rb_rows;
+    a.nrb = Lp.nrb;
+    a.trees_per_group = nu;
+    a.slab_prec = ctx->slab_prec.p;
+    a.prec_stride = stride;
+    HIP_TRY(launch_eval(dtype, a, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, 1), 16, ctx->stream));
+    HIP_TRY(ctx->h_prec.ensure(slab_bytes));
+    HIP_TRY(hipMemcpyAsync(ctx->h_prec.p, ctx->slab_prec.p, slab_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    const double* hp = (const double*)ctx->h_prec.p;
+    const long double ovf = ovf_threshold(dtype);
+    for (int u = 0; u < nu; ++u) {
+      const int32_t t = unc[u];
+      const TreeInfo& I = P->info[t];
+      int st = 0;
+      for (size_t k = 0; k < I.op_sumcheck.size() && !st; ++k) {
+        long double s = 0.0L;
+        for (int b = 0; b < Lp.nrb; ++b) s += hp[((size_t)u * stride + k) * Lp.nrb + b];
+        if (!isfinite((double)s)) st = 1;
+        else if (I.op_sumcheck[k]) {
+          const long double S = dtype == SRHIP_F64 ? ldexpl(s, 64) : s;
+          if (fabsl(S) >= ovf) st = 1;
+        }
+      }
+      status[t] = (uint8_t)st;
+    }
+  }
+  for (int32_t t = 0; t < nt; ++t) {
+    const bool ok = status[t] == 0;
+    if (out_ok) out_ok[t] = ok ? 1 : 0;
+    if (out_loss) {
+      if (!ok) out_loss[t] = INFINITY;
+      else if (weighted) out_loss[t] = lsum[t] / v.sum_w;
+      else out_loss[t] = lsum[t] / (double)v.m;
+    }
+  }
+  return SRHIP_OK;
+}
+
+template <typename T>
+static void pack_column(const void* src, int64_t f, int64_t n, int64_t sf, int64_t sr, int64_t ld, T* dst) {
+  const T* s = (const T*)src;
+  for (int64_t j = 0; j < n; ++j) dst[j] = s[f * sf + j * sr];
+  for (int64_t j = n; j < ld; ++j) dst[j] = dst[n - 1];
+}
+
+// ---------------------------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------------------------
+extern "C" {
+
+const char* srhip_last_error(void) { return g_err.c_str(); }
+const char* srhip_version(void) { return "srhip 0.1.0 gfx950"; }
+
+int srhip_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int srhip_ctx_create(int device, srhip_ctx** out) {
+  if (!out) return fail(SRHIP_ERR_INVALID, "null out");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(SRHIP_ERR_DEVICE, "no HIP device available");
+  if (device < 0 || device >= n) return fail(SRHIP_ERR_INVALID, "device %d out of range (%d devices)", device, n);
+  std::unique_ptr<srhip_ctx> c(new srhip_ctx());
+  c->device = device;
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  c->num_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(SRHIP_ERR_UNSUPPORTED, "device %d is %s; libsrhip is built for gfx950 only", device, prop.gcnArchName);
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreate(&c->ev0));
+  HIP_TRY(hipEventCreate(&c->ev1));
+  *out = c.release();
+  return SRHIP_OK;
+}
+
+void srhip_ctx_destroy(srhip_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int srhip_ctx_synchronize(srhip_ctx* ctx) {
+  if (!ctx) return fail(SRHIP_ERR_INVALID, "null ctx");
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return SRHIP_OK;
+}
+
+int srhip_dataset_create(srhip_ctx* ctx, int dtype, const void* X, int64_t nfeat, int64_t n, int64_t sf, int64_t sr,
+                         const void* y, const void* w, srhip_dataset** out) {
+  if (!ctx || !out) return fail(SRHIP_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (dtype != SRHIP_F32 && dtype != SRHIP_F64 && dtype != SRHIP_I32) return fail(SRHIP_ERR_UNSUPPORTED, "dtype %d", dtype);
+  if (n <= 0) return fail(SRHIP_ERR_INVALID, "dataset needs n >= 1 rows");
+  if (nfeat < 0 || nfeat > 65535) return fail(SRHIP_ERR_INVALID, "nfeatures %lld out of range", (long long)nfeat);
+  if (nfeat > 0 && !X) return fail(SRHIP_ERR_INVALID, "null X");
+  if (dtype == SRHIP_I32 && w) return fail(SRHIP_ERR_UNSUPPORTED, "weights on Int32 datasets");
+  HIP_TRY(hipSetDevice(ctx->device));
+  std::unique_ptr<srhip_dataset> d(new srhip_dataset());
+  d->ctx = ctx;
+  d->dtype = dtype;
+  d->nfeat = nfeat;
+  d->n = n;
+  d->ld = (n + ROW_ALIGN - 1) / ROW_ALIGN * ROW_ALIGN;
+  d->has_y = y != nullptr;
+  d->weighted = w != nullptr;
+  const size_t es = dtype_size(dtype);
+  const size_t colb = (size_t)d->ld * es;
+  HIP_TRY(d->X.ensure(std::max<size_t>(1, (size_t)nfeat) * colb));
+  HostBuf stage;
+  HIP_TRY(stage.ensure(colb));
+  for (int64_t f = 0; f < nfeat; ++f) {
+    if (dtype == SRHIP_F64) pack_column<uint64_t>(X, f, n, sf, sr, d->ld, (uint64_t*)stage.p);
+    else pack_column<uint32_t>(X, f, n, sf, sr, d->ld, (uint32_t*)stage.p);  // bit copy
+    HIP_TRY(hipMemcpy((char*)d->X.p + f * colb, stage.p, colb, hipMemcpyHostToDevice));
+  }
+  if (y) {
+    HIP_TRY(d->y.ensure(colb));
+    if (dtype == SRHIP_F64) pack_column<uint64_t>(y, 0, n, 0, 1, d->ld, (uint64_t*)stage.p);
+    else pack_column<uint32_t>(y, 0, n, 0, 1, d->ld, (uint32_t*)stage.p);
+    HIP_TRY(hipMemcpy(d->y.p, stage.p, colb, hipMemcpyHostToDevice));
+  }
+  if (w) {
+    HIP_TRY(d->w.ensure(colb));
+    double s = 0.0;
+    if (dtype == SRHIP_F64) {
+      double* st = (double*)stage.p;
+      for (int64_t j = 0; j < d->ld; ++j) st[j] = j < n ? ((const double*)w)[j] : 0.0;
+      for (int64_t j = 0; j < n; ++j) s += st[j];
+    } else {
+      float* st = (float*)stage.p;
+      for (int64_t j = 0; j < d->ld; ++j) st[j] = j < n ? ((const float*)w)[j] : 0.0f;
+      for (int64_t j = 0; j < n; ++j) s += st[j];
+    }
+    d->sum_w = s;
+    HIP_TRY(hipMemcpy(d->w.p, stage.p, colb, hipMemcpyHostToDevice));
+  }
+  d->hstats.assign(std::max<int64_t>(1, nfeat), FeatStat{0.0, 0});
+  if (dtype != SRHIP_I32 && nfeat > 0) {
+    HIP_TRY(d->stats.ensure((size_t)nfeat * sizeof(FeatStat)));
+    HIP_TRY(launch_feature_stats(dtype, d->X.p, d->ld, n, (int)nfeat, (FeatStat*)d->stats.p, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(d->hstats.data(), d->stats.p, (size_t)nfeat * sizeof(FeatStat), hipMemcpyDeviceToHost,
+                           ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+  }
+  *out = d.release();
+  return SRHIP_OK;
+}
+
+void srhip_dataset_destroy(srhip_dataset* ds) {
+  if (!ds) return;
+  (void)hipSetDevice(ds->ctx->device);
+  delete ds;
+}
+
+int srhip_program_create(srhip_ctx* ctx, int dtype, const srhip_node* nodes, const int64_t* offsets, int32_t ntrees,
+                         const srhip_operators* ops, srhip_program** out) {
+  if (!ctx || !out || !ops || (!offsets && ntrees > 0)) return fail(SRHIP_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (ntrees < 0) return fail(SRHIP_ERR_INVALID, "ntrees < 0");
+  if (dtype != SRHIP_F32 && dtype != SRHIP_F64 && dtype != SRHIP_I32) return fail(SRHIP_ERR_UNSUPPORTED, "dtype %d", dtype);
+  std::unique_ptr<srhip_program> P(new srhip_program());
+  P->ctx = ctx;
+  P->dtype = dtype;
+  P->ntrees = ntrees;
+  for (int i = 0; i < ops->nbin; ++i) {
+    int sb, hb;
+    if (!classify_binop(ops->binops[i], &sb, &hb)) return fail(SRHIP_ERR_UNSUPPORTED, "binary op code %d", ops->binops[i]);
+    P->binops.push_back(ops->binops[i]);
+  }
+  for (int i = 0; i < ops->nuna; ++i) {
+    if (classify_unop(ops->unaops[i]) < 0) return fail(SRHIP_ERR_UNSUPPORTED, "unary op code %d", ops->unaops[i]);
+    P->unaops.push_back(ops->unaops[i]);
+  }
+  P->offsets.assign(offsets, offsets + ntrees + 1);
+  if (ntrees > 0) {
+    if (P->offsets[0] != 0) return fail(SRHIP_ERR_INVALID, "tree_offsets[0] must be 0");
+    for (int32_t t = 0; t < ntrees; ++t)
+      if (P->offsets[t + 1] <= P->offsets[t]) return fail(SRHIP_ERR_INVALID, "tree %d is empty", (int)t);
+    P->nodes.assign(nodes, nodes + P->offsets[ntrees]);
+  }
+  int rc = compile_program(*P);
+  if (rc) return rc;
+  rc = upload_program(*P);
+  if (rc) return rc;
+  *out = P.release();
+  return SRHIP_OK;
+}
+
+void srhip_program_destroy(srhip_program* P) {
+  if (!P) return;
+  (void)hipSetDevice(P->ctx->device);
+  delete P;
+}
+
+int srhip_program_num_constants(const srhip_program* P, int32_t* out) {
+  if (!P || !out) return fail(SRHIP_ERR_INVALID, "null argument");
+  for (int32_t t = 0; t < P->ntrees; ++t) out[t] = P->info[t].nconst;
+  return SRHIP_OK;
+}
+
+static void set_consts_rec(std::vector<srhip_node>& nodes, int64_t base, int64_t i, const double*& c) {
+  srhip_node& n = nodes[base + i];
+  if (n.degree == 0) {
+    if (n.constant) n.val = *c++;
+    return;
+  }
+  set_consts_rec(nodes, base, n.l, c);
+  if (n.degree == 2) set_consts_rec(nodes, base, n.r, c);
+}
+
+int srhip_program_set_constants(srhip_program* P, const double* consts) {
+  if (!P || (!consts && P->ntrees > 0)) return fail(SRHIP_ERR_INVALID, "null argument");
+  const double* c = consts;
+  for (int32_t t = 0; t < P->ntrees; ++t) set_consts_rec(P->nodes, P->offsets[t], 0, c);
+  int rc = compile_program(*P);
+  if (rc) return rc;
+  return upload_program(*P);
+}
+
+int srhip_eval_loss(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* prog, const srhip_loss* loss,
+                    const int64_t* idx, int64_t nidx, double* out_loss, uint8_t* out_ok) {
+  if (!out_loss || !out_ok) return fail(SRHIP_ERR_INVALID, "null output");
+  return run_eval(ctx, ds, prog, MODE_LOSS, loss, idx, nidx, out_loss, nullptr, out_ok);
+}
+
+int srhip_eval_predict(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* prog, const int64_t* idx,
+                       int64_t nidx, void* out_pred, uint8_t* out_ok) {
+  if (!out_pred || !out_ok) return fail(SRHIP_ERR_INVALID, "null output");
+  return run_eval(ctx, ds, prog, MODE_PRED, nullptr, idx, nidx, nullptr, out_pred, out_ok);
+}
+
+int srhip_eval_loss_batch(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_node* nodes, const int64_t* offsets,
+                          int32_t ntrees, const srhip_operators* ops, const srhip_loss* loss, const int64_t* idx,
+                          int64_t nidx, double* out_loss, uint8_t* out_ok) {
+  if (!ds) return fail(SRHIP_ERR_INVALID, "null dataset");
+  srhip_program* P = nullptr;
+  int rc = srhip_program_create(ctx, ds->dtype, nodes, offsets, ntrees, ops, &P);
+  if (rc) return rc;
+  rc = srhip_eval_loss(ctx, ds, P, loss, idx, nidx, out_loss, out_ok);
+  srhip_program_destroy(P);
+  return rc;
+}
+
+double srhip_last_kernel_ms(const srhip_ctx* ctx) {
+  if (!ctx || !ctx->timed) return -1.0;
+  float ms = -1.0f;
+  if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) != hipSuccess) return -1.0;
+  return (double)ms;
+}
+
+int srhip_program_stats(const srhip_program* P, int64_t* total_nodes, int64_t* total_opnodes, int32_t* max_stack) {
+  if (!P) return fail(SRHIP_ERR_INVALID, "null program");
+  if (total_nodes) *total_nodes = P->total_nodes;
+  if (total_opnodes) *total_opnodes = P->total_ops;
+  if (max_stack) *max_stack = P->kmax;
+  return SRHIP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,128 @@
+// srhip_isa.h — the device bytecode ("postfix accumulator/stack machine") shared by the host
+// compiler (srhip_compile.cpp) and the gfx950 interpreter (srhip_eval.hip).
+//
+// Machine model (one wavefront, R rows per lane, all state in VGPRs):
+//   A      accumulator: the value of the subexpression being evaluated (R values per lane)
+//   S[k]   stack slots k < K (Sethi-Ullman ordering keeps K = Strahler number - 1 small)
+//   B      operand register for "heavy" binary ops (pow, mod, atan2)
+//   X[f]   feature f of the current row tile, read from LDS
+// Every operator instruction also folds max|A| (NaN-propagating) into the tree's check
+// accumulator: that is the device side of DynamicExpressions' did_succeed checks (see
+// DESIGN.md "did_succeed"). Instruction = 16 bytes, read with one s_load_dwordx4 (wave-uniform).
+#pragma once
+#include <stdint.h>
+
+#include "../../include/srhip.h"
+
+namespace srhip {
+
+constexpr int K_MAX = 8;  // stack slots in the largest kernel variant
+
+// Binary operators specialised for every operand form (cheap or very common).
+#define SRHIP_SPEC_BINOPS(X)                                                                \
+  X(ADD, add) X(SUB, sub) X(MUL, mul) X(DIV, div) X(GREATER, greater) X(COND, cond)           \
+  X(LOGICAL_OR, logical_or) X(LOGICAL_AND, logical_and) X(MAX, max) X(MIN, min)
+// Binary operators with large bodies: only A = A op B / A = B op A (B loaded by FETCH*).
+#define SRHIP_HEAVY_BINOPS(X) X(POW, pow) X(MOD, mod) X(ATAN2, atan2)
+#define SRHIP_UNOPS(X)                                                                         \
+  X(NEG, neg) X(SQUARE, square) X(CUBE, cube) X(ABS, abs) X(RELU, relu) X(COS, cos) X(SIN, sin) \
+  X(TAN, tan) X(EXP, exp) X(LOG, log) X(LOG2, log2) X(LOG10, log10) X(LOG1P, log1p)            \
+  X(SQRT, sqrt) X(ACOSH, acosh) X(ATANH_CLIP, atanh_clip) X(SINH, sinh) X(COSH, cosh)          \
+  X(TANH, tanh) X(ASIN, asin) X(ACOS, acos) X(ATAN, atan) X(ASINH, asinh) X(ERF, erf)          \
+  X(ERFC, erfc) X(GAMMA, gamma) X(ROUND, round) X(FLOOR, floor) X(CEIL, ceil) X(SIGN, sign)    \
+  X(EXP2, exp2) X(EXPM1, expm1) X(CBRT, cbrt)
+
+enum SpecBin : int {
+#define X_(n, f) SB_##n,
+  SRHIP_SPEC_BINOPS(X_)
+#undef X_
+  NUM_SPEC_BIN
+};
+enum HeavyBin : int {
+#define X_(n, f) HB_##n,
+  SRHIP_HEAVY_BINOPS(X_)
+#undef X_
+  NUM_HEAVY_BIN
+};
+enum Unop : int {
+#define X_(n, f) UN_##n,
+  SRHIP_UNOPS(X_)
+#undef X_
+  NUM_UNOP
+};
+
+// ---- handler ids -----------------------------------------------------------------------------
+enum : uint32_t {
+  H_END = 0,
+  H_LOADF = 1,  // A = X[a]
+  H_LOADC = 2,  // A = imm
+  H_FETCHF = 3, // B = X[a]
+  H_FETCHC = 4, // B = imm
+  H_PUSH0 = 5,  // S[k] = A           (k < K_MAX)
+  H_FETCHS0 = H_PUSH0 + K_MAX,        // B = S[k]
+  H_BIN0 = H_FETCHS0 + K_MAX,         // specialised binary ops, SPEC_STRIDE handlers each
+};
+constexpr uint32_t SPEC_AF = 0, SPEC_FA = 1, SPEC_AC = 2, SPEC_CA = 3, SPEC_SA0 = 4,
+                   SPEC_AS0 = 4 + K_MAX, SPEC_STRIDE = 4 + 2 * K_MAX;
+constexpr uint32_t H_HEAVY0 = H_BIN0 + NUM_SPEC_BIN * SPEC_STRIDE;  // +0 AB (A=A op B), +1 BA
+constexpr uint32_t H_UN0 = H_HEAVY0 + 2 * NUM_HEAVY_BIN;
+constexpr uint32_t H_COUNT = H_UN0 + NUM_UNOP;
+
+constexpr uint32_t h_spec(int sb, uint32_t form) { return H_BIN0 + uint32_t(sb) * SPEC_STRIDE + form; }
+constexpr uint32_t h_heavy(int hb, bool ba) { return H_HEAVY0 + uint32_t(hb) * 2 + (ba ? 1u : 0u); }
+constexpr uint32_t h_un(int u) { return H_UN0 + uint32_t(u); }
+
+struct __attribute__((aligned(16))) Ins {
+  uint32_t h;    // handler id
+  uint32_t a;    // feature index (0-based) or stack slot
+  uint64_t imm;  // constant bits: f32/i32 in the low word, f64 full
+};
+static_assert(sizeof(Ins) == 16, "Ins must be 16 bytes");
+
+// Map public SRHIP_OP_* codes to the internal categories; returns false if unknown.
+inline bool classify_binop(int code, int* spec, int* heavy) {
+  *spec = -1;
+  *heavy = -1;
+  switch (code) {
+#define X_(n, f) \
+  case SRHIP_OP_##n: *spec = SB_##n; return true;
+    SRHIP_SPEC_BINOPS(X_)
+#undef X_
+#define X_(n, f) \
+  case SRHIP_OP_##n: *heavy = HB_##n; return true;
+    SRHIP_HEAVY_BINOPS(X_)
+#undef X_
+    default: return false;
+  }
+}
+inline int classify_unop(int code) {
+  switch (code) {
+#define X_(n, f) \
+  case SRHIP_OP_##n: return UN_##n;
+    SRHIP_UNOPS(X_)
+#undef X_
+    default: return -1;
+  }
+}
+
+// Integer-typed trees (Node{Int32}) support only wrap-around ring ops and comparisons
+// (Julia Int32 semantics; `/` on Int32 returns Float64 in Julia and is rejected).
+inline bool int_binop_ok(int code) {
+  switch (code) {
+    case SRHIP_OP_ADD: case SRHIP_OP_SUB: case SRHIP_OP_MUL: case SRHIP_OP_GREATER:
+    case SRHIP_OP_COND: case SRHIP_OP_LOGICAL_OR: case SRHIP_OP_LOGICAL_AND:
+    case SRHIP_OP_MAX: case SRHIP_OP_MIN:
+      return true;
+    default: return false;
+  }
+}
+inline bool int_unop_ok(int code) {
+  switch (code) {
+    case SRHIP_OP_NEG: case SRHIP_OP_SQUARE: case SRHIP_OP_CUBE: case SRHIP_OP_ABS:
+    case SRHIP_OP_RELU: case SRHIP_OP_SIGN:
+      return true;
+    default: return false;
+  }
+}
+
+}  // namespace srhip

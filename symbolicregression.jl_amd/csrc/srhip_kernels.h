@@ -1,0 +1,57 @@
+// srhip_kernels.h — kernel argument blocks and launcher declarations (host <-> srhip_eval.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "srhip_isa.h"
+
+namespace srhip {
+
+constexpr int EVAL_WAVES = 8;  // wavefronts per workgroup of the interpreter kernel
+constexpr int R_F32 = 8;       // rows per lane per dispatch, 4-byte types
+constexpr int R_F64 = 4;       // rows per lane per dispatch, Float64
+constexpr int ROW_ALIGN = 4096;  // device datasets are padded to a multiple of this many rows
+constexpr int MODE_LOSS = 0, MODE_PRED = 1, MODE_PRECISE = 2;
+
+struct FeatStat {
+  double sum;           // f64 sum (Float64 data: sum of x * 2^-64)
+  long long nonfinite;  // count of Inf/NaN entries
+};
+
+struct EvalArgs {
+  const Ins* code;          // all trees' bytecode
+  const int32_t* prog_off;  // [ntrees] first instruction of each tree
+  const int32_t* order;     // [ntrees] processing order (grouped, cost-sorted)
+  const void* X;            // [nfeat][ld] SoA, padded
+  const void* y;            // [ld] (nullptr for prediction-only)
+  const void* w;            // [ld] or nullptr
+  void* slab_loss;          // [ntrees][nrb] loss partials (double; int64 for Int32)
+  void* slab_chk;           // [ntrees][nrb] check partials (float max|v| / double sum|v|*2^-512)
+  void* out_pred;           // [ntrees][nvalid] (MODE_PRED)
+  void* slab_prec;          // [n][prec_stride][nrb] double (MODE_PRECISE)
+  int64_t ld;               // padded rows of X / y / w
+  int64_t nvalid;           // rows evaluated
+  int32_t ntrees;
+  int32_t nfeat;
+  int32_t rb_rows;          // rows per workgroup (multiple of 64*R)
+  int32_t nrb;              // row blocks
+  int32_t trees_per_group;  // trees per grid.y group
+  int32_t loss_kind;
+  double loss_p0;
+  int32_t weighted;
+  int32_t prec_stride;      // operator nodes per tree slot in slab_prec
+  int32_t has_y;            // stage y into LDS (MODE_LOSS)
+  int32_t pad_;
+};
+
+int rows_per_lane(int dtype);
+hipError_t launch_eval(int dtype, const EvalArgs& a, int K, int mode, bool xlds, dim3 grid, size_t lds,
+                       hipStream_t s);
+hipError_t launch_reduce(int dtype, const void* slab_loss, const void* slab_chk, int nrb, int ntrees, void* out_loss,
+                         void* out_chk, hipStream_t s);
+hipError_t launch_gather(int dtype, const void* X, const void* y, const void* w, int64_t ld_src, int nfeat,
+                         const int64_t* idx, int64_t m, int64_t ld_dst, void* Xd, void* yd, void* wd, hipStream_t s);
+hipError_t launch_feature_stats(int dtype, const void* X, int64_t ld, int64_t m, int nfeat, FeatStat* out,
+                                hipStream_t s);
+
+}  // namespace srhip

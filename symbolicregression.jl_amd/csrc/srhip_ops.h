@@ -1,0 +1,226 @@
+// srhip_ops.h — scalar operator and elementwise-loss semantics, host+device.
+//
+// Restated from the reference (src/Operators.jl) and the Julia Base functions it aliases
+// (src/Options.jl:92-150 binopmap/unaopmap), including Julia's Bool "strong zero"
+// (false * x == copysign(0, x)) used by relu/cond/greater/logical_* (src/Operators.jl:79-96).
+// The same source is compiled for the device (OCML math) and for the host compiler's constant
+// folding (libm), so folded constant subtrees follow the reference's scalar path
+// (DynamicExpressions _eval_constant_tree) with the same formulas.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#define SRHIP_HD __host__ __device__ __attribute__((always_inline)) inline
+
+namespace srhip {
+
+// ---- small generic helpers -------------------------------------------------------------------
+template <typename T> struct FP;
+template <> struct FP<float> {
+  static SRHIP_HD float nan() { return __builtin_nanf(""); }
+  static SRHIP_HD float inf() { return __builtin_inff(); }
+  // |x| at or above this rounds to Inf when summed exactly: 2^128 - 2^103
+  static constexpr double OVF = 3.4028235677973366e38;
+};
+template <> struct FP<double> {
+  static SRHIP_HD double nan() { return __builtin_nan(""); }
+  static SRHIP_HD double inf() { return __builtin_inf(); }
+  static constexpr double OVF = 1.7976931348623157e308;  // DBL_MAX (2^1024 - 2^970 is not representable)
+};
+
+SRHIP_HD float m_copysign(float a, float b) { return __builtin_copysignf(a, b); }
+SRHIP_HD double m_copysign(double a, double b) { return __builtin_copysign(a, b); }
+SRHIP_HD float m_abs(float a) { return __builtin_fabsf(a); }
+SRHIP_HD double m_abs(double a) { return __builtin_fabs(a); }
+SRHIP_HD bool m_isfinite(float a) { return __builtin_isfinite(a); }
+SRHIP_HD bool m_isfinite(double a) { return __builtin_isfinite(a); }
+SRHIP_HD bool m_isfinite(int32_t) { return true; }
+SRHIP_HD bool m_isinf(float a) { return __builtin_isinf(a); }
+SRHIP_HD bool m_isinf(double a) { return __builtin_isinf(a); }
+
+// Julia max/min on floats: NaN-propagating, -0.0 < +0.0 (IEEE 754-2019 maximum/minimum).
+SRHIP_HD float m_max(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+SRHIP_HD double m_max(double a, double b) { return __builtin_elementwise_maximum(a, b); }
+SRHIP_HD float m_min(float a, float b) { return __builtin_elementwise_minimum(a, b); }
+SRHIP_HD double m_min(double a, double b) { return __builtin_elementwise_minimum(a, b); }
+
+// ---- libm wrappers (float and double) ----------------------------------------------------------
+#define SRHIP_WRAP1(name, ff, df)                      \
+  SRHIP_HD float m_##name(float x) { return ff(x); }   \
+  SRHIP_HD double m_##name(double x) { return df(x); }
+SRHIP_WRAP1(cos, cosf, cos)
+SRHIP_WRAP1(sin, sinf, sin)
+SRHIP_WRAP1(tan, tanf, tan)
+SRHIP_WRAP1(exp, expf, exp)
+SRHIP_WRAP1(log, logf, log)
+SRHIP_WRAP1(log2, log2f, log2)
+SRHIP_WRAP1(log10, log10f, log10)
+SRHIP_WRAP1(log1p, log1pf, log1p)
+SRHIP_WRAP1(sqrt, sqrtf, sqrt)
+SRHIP_WRAP1(acosh, acoshf, acosh)
+SRHIP_WRAP1(atanh, atanhf, atanh)
+SRHIP_WRAP1(sinh, sinhf, sinh)
+SRHIP_WRAP1(cosh, coshf, cosh)
+SRHIP_WRAP1(tanh, tanhf, tanh)
+SRHIP_WRAP1(asin, asinf, asin)
+SRHIP_WRAP1(acos, acosf, acos)
+SRHIP_WRAP1(atan, atanf, atan)
+SRHIP_WRAP1(asinh, asinhf, asinh)
+SRHIP_WRAP1(erf, erff, erf)
+SRHIP_WRAP1(erfc, erfcf, erfc)
+SRHIP_WRAP1(tgamma, tgammaf, tgamma)
+SRHIP_WRAP1(rint, rintf, rint)
+SRHIP_WRAP1(floor, floorf, floor)
+SRHIP_WRAP1(ceil, ceilf, ceil)
+SRHIP_WRAP1(exp2, exp2f, exp2)
+SRHIP_WRAP1(expm1, expm1f, expm1)
+SRHIP_WRAP1(cbrt, cbrtf, cbrt)
+SRHIP_WRAP1(trunc, truncf, trunc)
+#undef SRHIP_WRAP1
+SRHIP_HD float m_fmod(float a, float b) { return fmodf(a, b); }
+SRHIP_HD double m_fmod(double a, double b) { return fmod(a, b); }
+SRHIP_HD float m_atan2(float a, float b) { return atan2f(a, b); }
+SRHIP_HD double m_atan2(double a, double b) { return atan2(a, b); }
+// Julia's Float32 ^ Float32 is evaluated by widening to Float64 (base/math.jl); same here.
+SRHIP_HD float m_pow(float a, float b) { return (float)pow((double)a, (double)b); }
+SRHIP_HD double m_pow(double a, double b) { return pow(a, b); }
+
+// ---- operator semantics, floating point T ------------------------------------------------------
+template <typename T> struct FOps {
+  // binary (Julia Base + src/Operators.jl)
+  static SRHIP_HD T add(T a, T b) { return a + b; }
+  static SRHIP_HD T sub(T a, T b) { return a - b; }
+  static SRHIP_HD T mul(T a, T b) { return a * b; }
+  static SRHIP_HD T div(T a, T b) { return a / b; }
+  // src/Operators.jl:82-84  greater(x, y) = (x > y) * one(x)
+  static SRHIP_HD T greater(T a, T b) { return (a > b) ? T(1) : T(0); }
+  // src/Operators.jl:85-87  cond(x, y) = (x > zero(x)) * y
+  static SRHIP_HD T cond(T a, T b) { return (a > T(0)) ? b : m_copysign(T(0), b); }
+  // src/Operators.jl:91-96
+  static SRHIP_HD T logical_or(T a, T b) { return ((a > T(0)) | (b > T(0))) ? T(1) : T(0); }
+  static SRHIP_HD T logical_and(T a, T b) { return ((a > T(0)) & (b > T(0))) ? T(1) : T(0); }
+  static SRHIP_HD T max(T a, T b) { return m_max(a, b); }
+  static SRHIP_HD T min(T a, T b) { return m_min(a, b); }
+  // src/Operators.jl:28-36  safe_pow
+  static SRHIP_HD T pow(T x, T y) {
+    const bool yint = (y - m_trunc(y)) == T(0);  // isinteger(y): false for Inf/NaN
+    if (yint) {
+      if (y < T(0) && x == T(0)) return FP<T>::nan();
+    } else {
+      if (y > T(0) && x < T(0)) return FP<T>::nan();
+      if (y < T(0) && x <= T(0)) return FP<T>::nan();
+    }
+    return m_pow(x, y);
+  }
+  // Julia Base mod(x::T, y::T) for floats: r = rem(x, y); r == 0 ? copysign(r, y) :
+  // ((r > 0) xor (y > 0)) ? r + y : r
+  static SRHIP_HD T mod(T x, T y) {
+    const T r = m_fmod(x, y);
+    if (r == T(0)) return m_copysign(r, y);
+    if ((r > T(0)) != (y > T(0))) return r + y;
+    return r;
+  }
+  static SRHIP_HD T atan2(T a, T b) { return m_atan2(a, b); }
+
+  // unary
+  static SRHIP_HD T neg(T x) { return -x; }
+  static SRHIP_HD T square(T x) { return x * x; }        // src/Operators.jl:65
+  static SRHIP_HD T cube(T x) { return (x * x) * x; }    // src/Operators.jl:66
+  static SRHIP_HD T abs(T x) { return m_abs(x); }
+  static SRHIP_HD T relu(T x) { return (x > T(0)) ? x : m_copysign(T(0), x); }  // :88-90
+  static SRHIP_HD T cos(T x) { return m_cos(x); }
+  static SRHIP_HD T sin(T x) { return m_sin(x); }
+  static SRHIP_HD T tan(T x) { return m_tan(x); }
+  static SRHIP_HD T exp(T x) { return m_exp(x); }
+  // src/Operators.jl:37-60 safe_log*, safe_log1p, safe_acosh, safe_sqrt
+  static SRHIP_HD T log(T x) { return (x <= T(0)) ? FP<T>::nan() : m_log(x); }
+  static SRHIP_HD T log2(T x) { return (x <= T(0)) ? FP<T>::nan() : m_log2(x); }
+  static SRHIP_HD T log10(T x) { return (x <= T(0)) ? FP<T>::nan() : m_log10(x); }
+  static SRHIP_HD T log1p(T x) { return (x <= T(-1)) ? FP<T>::nan() : m_log1p(x); }
+  static SRHIP_HD T sqrt(T x) { return (x < T(0)) ? FP<T>::nan() : m_sqrt(x); }
+  static SRHIP_HD T acosh(T x) { return (x < T(1)) ? FP<T>::nan() : m_acosh(x); }
+  // src/Operators.jl:17 atanh_clip(x) = atanh(mod(x + 1, 2) - 1)
+  static SRHIP_HD T atanh_clip(T x) { return m_atanh(mod(x + T(1), T(2)) - T(1)); }
+  static SRHIP_HD T sinh(T x) { return m_sinh(x); }
+  static SRHIP_HD T cosh(T x) { return m_cosh(x); }
+  static SRHIP_HD T tanh(T x) { return m_tanh(x); }
+  // Julia throws DomainError for |x| > 1; the device returns NaN (-> did_succeed = false).
+  static SRHIP_HD T asin(T x) { return m_asin(x); }
+  static SRHIP_HD T acos(T x) { return m_acos(x); }
+  static SRHIP_HD T atan(T x) { return m_atan(x); }
+  static SRHIP_HD T asinh(T x) { return m_asinh(x); }
+  static SRHIP_HD T erf(T x) { return m_erf(x); }
+  static SRHIP_HD T erfc(T x) { return m_erfc(x); }
+  // src/Operators.jl:11-15  gamma(x) = isinf(out) ? NaN : out
+  static SRHIP_HD T gamma(T x) {
+    const T g = m_tgamma(x);
+    return m_isinf(g) ? FP<T>::nan() : g;
+  }
+  static SRHIP_HD T round(T x) { return m_rint(x); }  // Julia round: RoundNearest (ties even)
+  static SRHIP_HD T floor(T x) { return m_floor(x); }
+  static SRHIP_HD T ceil(T x) { return m_ceil(x); }
+  // Julia sign: -1 / +1, keeps ±0, NaN -> NaN
+  static SRHIP_HD T sign(T x) { return (x < T(0)) ? T(-1) : ((x > T(0)) ? T(1) : x); }
+  static SRHIP_HD T exp2(T x) { return m_exp2(x); }
+  static SRHIP_HD T expm1(T x) { return m_expm1(x); }
+  static SRHIP_HD T cbrt(T x) { return m_cbrt(x); }
+};
+
+// ---- Int32 semantics: Julia Int32 wrap-around arithmetic (two's complement) ---------------------
+struct IOps {
+  using T = int32_t;
+  static SRHIP_HD T w(uint32_t v) { return (T)v; }
+  static SRHIP_HD T add(T a, T b) { return w((uint32_t)a + (uint32_t)b); }
+  static SRHIP_HD T sub(T a, T b) { return w((uint32_t)a - (uint32_t)b); }
+  static SRHIP_HD T mul(T a, T b) { return w((uint32_t)a * (uint32_t)b); }
+  static SRHIP_HD T greater(T a, T b) { return a > b ? 1 : 0; }
+  static SRHIP_HD T cond(T a, T b) { return a > 0 ? b : 0; }
+  static SRHIP_HD T logical_or(T a, T b) { return ((a > 0) | (b > 0)) ? 1 : 0; }
+  static SRHIP_HD T logical_and(T a, T b) { return ((a > 0) & (b > 0)) ? 1 : 0; }
+  static SRHIP_HD T max(T a, T b) { return a > b ? a : b; }
+  static SRHIP_HD T min(T a, T b) { return a < b ? a : b; }
+  static SRHIP_HD T neg(T x) { return w(0u - (uint32_t)x); }
+  static SRHIP_HD T square(T x) { return mul(x, x); }
+  static SRHIP_HD T cube(T x) { return mul(mul(x, x), x); }
+  static SRHIP_HD T abs(T x) { return x < 0 ? neg(x) : x; }
+  static SRHIP_HD T relu(T x) { return x > 0 ? x : 0; }
+  static SRHIP_HD T sign(T x) { return x > 0 ? 1 : (x < 0 ? -1 : 0); }
+};
+
+// ---- elementwise losses (LossFunctions.jl 0.10/0.11 distance losses, diff = output - target) ---
+// Restated; the package is not in the container (see DESIGN.md "oracle").
+template <typename T>
+SRHIP_HD T loss_elem(int kind, T diff, T p0) {
+  switch (kind) {
+    case SRHIP_LOSS_L2: return diff * diff;                 // abs2(diff)
+    case SRHIP_LOSS_L1: return m_abs(diff);
+    case SRHIP_LOSS_LP: return m_pow(m_abs(diff), p0);      // abs(diff)^P
+    case SRHIP_LOSS_HUBER: {                                // HuberLoss(d)
+      const T a = m_abs(diff);
+      return (a <= p0) ? T(0.5) * (diff * diff) : p0 * (a - T(0.5) * p0);
+    }
+    case SRHIP_LOSS_L1_EPS_INS: return m_max(T(0), m_abs(diff) - p0);
+    case SRHIP_LOSS_L2_EPS_INS: { const T e = m_max(T(0), m_abs(diff) - p0); return e * e; }
+    case SRHIP_LOSS_LOGIT_DIST: {                           // -log(4 e^d / (1 + e^d)^2)
+      const T er = m_exp(diff);
+      const T den = T(1) + er;
+      return -m_log(T(4) * er / (den * den));
+    }
+    case SRHIP_LOSS_PERIODIC:                               // 1 - cos(2 pi diff / c)
+      return T(1) - m_cos(diff * (T(2) * T(3.14159265358979323846)) / p0);
+    case SRHIP_LOSS_QUANTILE:                               // diff * (tau - (diff < 0))
+      return diff * (p0 - ((diff < T(0)) ? T(1) : T(0)));
+    default: return FP<T>::nan();
+  }
+}
+// Int32 datasets: the elementwise loss is computed in Int32 wrap arithmetic and summed in Int64.
+SRHIP_HD int32_t loss_elem_int(int kind, int32_t diff) {
+  switch (kind) {
+    case SRHIP_LOSS_L2: return IOps::mul(diff, diff);
+    case SRHIP_LOSS_L1: return IOps::abs(diff);
+    default: return 0;
+  }
+}
+
+}  // namespace srhip

@@ -1,0 +1,207 @@
+"""The reference's hot-path API, backed by libsrhip:
+
+  eval_tree_array(tree, X, options)        src/InterfaceDynamicExpressions.jl:56-63
+  eval_loss(tree, dataset, options; ...)   src/LossFunctions.jl:97-112 (-> _eval_loss :45-75)
+  eval_loss_batched / batch_sample         src/LossFunctions.jl:114-127
+  loss_to_score                            src/LossFunctions.jl:138-158
+  score_func / score_func_batched          src/LossFunctions.jl:161-194
+  update_baseline_loss!                    src/LossFunctions.jl:201-215
+  compute_complexity                       src/Complexity.jl:17-50
+
+plus the batched entry points the device is built for (one launch per population):
+  eval_tree_array_batch, eval_loss_batch, score_func_batch.
+Same argument meaning and error behaviour as the reference; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import inspect
+
+import numpy as np
+
+from .dataset import Dataset
+from .device import Program, get_context
+from .losses import is_device_loss
+from .node import Node, count_nodes, flatten
+
+
+def _ctx(options):
+    return get_context(getattr(options, "device", 0))
+
+
+def _as_trees(trees):
+    if isinstance(trees, Node):
+        return [trees]
+    return [t.tree if hasattr(t, "tree") else t for t in trees]
+
+
+def compile_trees(trees, options, dtype) -> Program:
+    nodes, offsets = flatten(_as_trees(trees), options, dtype)
+    return Program(_ctx(options), nodes, offsets, options, dtype)
+
+
+# ---- eval_tree_array ---------------------------------------------------------------------------
+def eval_tree_array_batch(trees, X, options, idx=None):
+    """Evaluate many trees over X: returns (out[ntrees, n] in T, ok[ntrees])."""
+    ctx = _ctx(options)
+    if isinstance(X, Dataset):
+        ds = X
+    else:
+        ds = Dataset(np.asarray(X))
+    prog = compile_trees(trees, options, ds.X.dtype)
+    try:
+        return prog.eval_predict(ds.device(ctx), idx)
+    finally:
+        prog.close()
+
+
+def eval_tree_array(tree, X, options, **kws):
+    """(output::Vector{T}, complete::Bool) for one tree (src/InterfaceDynamicExpressions.jl:56-63)."""
+    out, ok = eval_tree_array_batch([tree], X, options)
+    return out[0], bool(ok[0])
+
+
+# ---- losses ------------------------------------------------------------------------------------
+def _host_elementwise_loss(pred, y, w, loss):
+    """User-defined elementwise loss (a Julia function in the reference): evaluated on the host
+    over device predictions, with _loss / _weighted_loss's normalisation (src/LossFunctions.jl:13-33)."""
+    T = pred.dtype.type
+    if w is None:
+        vals = np.array([loss(pred[i], y[i]) for i in range(len(pred))], dtype=pred.dtype)
+        return float(np.sum(vals.astype(np.float64)) / len(pred))
+    vals = np.array([loss(pred[i], y[i], w[i]) for i in range(len(pred))], dtype=pred.dtype)
+    return float(np.sum(vals.astype(np.float64)) / np.sum(w.astype(np.float64)))
+
+
+def eval_loss_batch(trees, dataset: Dataset, options, regularization: bool = True, idx=None):
+    """_eval_loss for every tree in one device launch: returns (loss[ntrees] float64, ok[ntrees]).
+
+    Loss is +Inf where did_succeed is false (L(Inf), src/LossFunctions.jl:55-57)."""
+    trees = _as_trees(trees)
+    if options.loss_function is not None:
+        out = np.array([eval_loss(t, dataset, options, regularization=regularization, idx=idx) for t in trees],
+                       dtype=np.float64)
+        return out, np.isfinite(out)
+    ctx = _ctx(options)
+    loss = options.elementwise_loss
+    prog = compile_trees(trees, options, dataset.X.dtype)
+    try:
+        if is_device_loss(loss):
+            return prog.eval_loss(dataset.device(ctx), loss, idx)
+        pred, ok = prog.eval_predict(dataset.device(ctx), idx)
+        y = dataset.y if idx is None else dataset.y[np.asarray(idx)]
+        w = None if not dataset.weighted else (dataset.weights if idx is None else dataset.weights[np.asarray(idx)])
+        out = np.full(len(trees), np.inf)
+        for t in range(len(trees)):
+            if ok[t]:
+                out[t] = _host_elementwise_loss(pred[t], y, w, loss)
+        return out, ok
+    finally:
+        prog.close()
+
+
+def _evaluator(f, tree, dataset, options, idx):
+    """src/LossFunctions.jl:78-94: user loss_function dispatch on whether it accepts idx."""
+    try:
+        nparams = len(inspect.signature(f).parameters)
+    except (TypeError, ValueError):
+        nparams = 4
+    if nparams >= 4:
+        return f(tree, dataset, options, idx)
+    if options.batching:
+        raise RuntimeError(
+            "User-defined loss function must accept batching indices if `options.batching == true`. "
+            "For example, `f(tree, dataset, options, idx)`, where `idx` is `nothing` if full dataset is "
+            "to be used, and a vector of indices otherwise.")
+    return f(tree, dataset, options)
+
+
+def eval_loss(tree, dataset: Dataset, options, regularization: bool = True, idx=None):
+    """src/LossFunctions.jl:97-112. Returns a scalar of the dataset's loss type L."""
+    L = dataset.loss_type.type
+    if options.loss_function is not None:
+        return L(_evaluator(options.loss_function, tree, dataset, options, idx))
+    loss, _ = eval_loss_batch([tree], dataset, options, regularization=regularization, idx=idx)
+    # dimensional_regularization (units) is out of scope for the device path: no units -> 0
+    return L(loss[0])
+
+
+def batch_sample(dataset: Dataset, options, rng=None):
+    """StatsBase.sample(1:n, batch_size; replace=true) (src/LossFunctions.jl:125-127), 0-based."""
+    rng = np.random.default_rng() if rng is None else rng
+    return rng.integers(0, dataset.n, size=options.batch_size)
+
+
+def eval_loss_batched(tree, dataset, options, regularization=True, idx=None, rng=None):
+    _idx = batch_sample(dataset, options, rng) if idx is None else idx
+    return eval_loss(tree, dataset, options, regularization=regularization, idx=_idx)
+
+
+# ---- complexity / scoring ----------------------------------------------------------------------
+def compute_complexity(tree: Node, options) -> int:
+    """count_nodes, or the custom complexity mapping (src/Complexity.jl:17-50)."""
+    cm = options.complexity_mapping
+    if not cm.use:
+        return count_nodes(tree)
+    total = 0.0
+    for n in tree:
+        if n.degree == 0:
+            if n.constant:
+                total += cm.constant_complexity
+            else:
+                vc = cm.variable_complexity
+                total += vc[n.feature - 1] if isinstance(vc, (list, tuple, np.ndarray)) else vc
+        elif n.degree == 1:
+            total += cm.unaop_complexities[options.unary_index(n.op) - 1]
+        else:
+            total += cm.binop_complexities[options.binary_index(n.op) - 1]
+    return int(round(total))
+
+
+def loss_to_score(loss, use_baseline, baseline, member, options, complexity=None):
+    """src/LossFunctions.jl:138-158."""
+    L = type(loss) if isinstance(loss, np.floating) else np.float64
+    normalization = baseline if (baseline >= L(0.01) and use_baseline) else L(0.01)
+    loss_val = L(loss) / L(normalization)
+    size = compute_complexity(member.tree if hasattr(member, "tree") else member, options) \
+        if complexity is None else complexity
+    parsimony_term = size * options.parsimony
+    return L(loss_val + L(parsimony_term))
+
+
+def score_func(dataset: Dataset, member, options, complexity=None):
+    """(score, loss) — src/LossFunctions.jl:161-174."""
+    tree = member.tree if hasattr(member, "tree") else member
+    result_loss = eval_loss(tree, dataset, options)
+    score = loss_to_score(result_loss, dataset.use_baseline, dataset.baseline_loss, member, options, complexity)
+    return score, result_loss
+
+
+def score_func_batched(dataset, member, options, complexity=None, idx=None, rng=None):
+    """src/LossFunctions.jl:177-194."""
+    tree = member.tree if hasattr(member, "tree") else member
+    result_loss = eval_loss_batched(tree, dataset, options, idx=idx, rng=rng)
+    score = loss_to_score(result_loss, dataset.use_baseline, dataset.baseline_loss, member, options, complexity)
+    return score, result_loss
+
+
+def score_func_batch(dataset: Dataset, members, options, idx=None):
+    """score_func over a whole population in one device launch: (scores, losses) arrays in L."""
+    trees = _as_trees(members)
+    L = dataset.loss_type.type
+    losses, _ = eval_loss_batch(trees, dataset, options, idx=idx)
+    losses = losses.astype(dataset.loss_type)
+    scores = np.array([loss_to_score(L(l), dataset.use_baseline, dataset.baseline_loss, t, options)
+                       for l, t in zip(losses, trees)], dtype=dataset.loss_type)
+    return scores, losses
+
+
+def update_baseline_loss(dataset: Dataset, options) -> None:
+    """update_baseline_loss! (src/LossFunctions.jl:201-215): loss of the constant tree avg_y."""
+    example_tree = Node(val=dataset.avg_y)
+    baseline_loss = eval_loss(example_tree, dataset, options)
+    if np.isfinite(baseline_loss):
+        dataset.baseline_loss = baseline_loss
+        dataset.use_baseline = True
+    else:
+        dataset.baseline_loss = dataset.loss_type.type(1)
+        dataset.use_baseline = False

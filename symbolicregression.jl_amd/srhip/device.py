@@ -1,0 +1,162 @@
+"""Handles over libsrhip objects: Context (device + stream), DeviceDataset, Program.
+
+One Context per (host thread, device): libsrhip contexts are not thread-safe, which matches
+the reference's concurrency model (one task per population, src/SearchUtils.jl:108-127).
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ptr
+
+
+class Context:
+    def __init__(self, device: int = 0):
+        lib = _lib.load()
+        h = ctypes.c_void_p()
+        check(lib.srhip_ctx_create(int(device), ctypes.byref(h)))
+        self.handle = h
+        self.device = int(device)
+        self._lib = lib
+
+    def synchronize(self):
+        check(self._lib.srhip_ctx_synchronize(self.handle))
+
+    def last_kernel_ms(self) -> float:
+        return float(self._lib.srhip_last_kernel_ms(self.handle))
+
+    def close(self):
+        if self.handle:
+            self._lib.srhip_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_tls = threading.local()
+
+
+def get_context(device: int = 0) -> Context:
+    """The calling thread's context for `device` (created on first use)."""
+    cache = getattr(_tls, "ctxs", None)
+    if cache is None:
+        cache = _tls.ctxs = {}
+    ctx = cache.get(device)
+    if ctx is None:
+        ctx = cache[device] = Context(device)
+    return ctx
+
+
+def device_count() -> int:
+    try:
+        return int(_lib.load().srhip_device_count())
+    except _lib.SrhipError:
+        return 0
+
+
+class DeviceDataset:
+    """A dataset uploaded to HBM (X as [nfeatures][n] padded SoA, y, weights)."""
+
+    def __init__(self, ctx: Context, X: np.ndarray, y=None, weights=None):
+        X = np.asarray(X)
+        if X.ndim != 2:
+            raise ValueError("X must be (nfeatures, n)")
+        self.dtype = X.dtype
+        code = _lib.dtype_code(X.dtype)
+        nfeat, n = X.shape
+        # element (f, j) at X[f*sf + j*sr] in elements
+        es = X.itemsize
+        sf, sr = X.strides[0] // es, X.strides[1] // es
+        if X.strides[0] % es or X.strides[1] % es:
+            X = np.ascontiguousarray(X)
+            sf, sr = n, 1
+        yv = None if y is None else np.ascontiguousarray(y, dtype=X.dtype)
+        wv = None if weights is None else np.ascontiguousarray(weights, dtype=X.dtype)
+        h = ctypes.c_void_p()
+        check(_lib.load().srhip_dataset_create(ctx.handle, code, ptr(X), nfeat, n, sf, sr, ptr(yv), ptr(wv),
+                                               ctypes.byref(h)))
+        self.handle = h
+        self.ctx = ctx
+        self.nfeatures = nfeat
+        self.n = n
+        self.weighted = weights is not None
+
+    def close(self):
+        if self.handle:
+            _lib.load().srhip_dataset_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Program:
+    """A compiled batch of trees (bytecode resident on the device)."""
+
+    def __init__(self, ctx: Context, nodes: np.ndarray, offsets: np.ndarray, options, dtype):
+        self.ctx = ctx
+        self.nodes = np.ascontiguousarray(nodes)
+        self.offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        self.ntrees = len(self.offsets) - 1
+        self.options = options
+        self.dtype = np.dtype(dtype)
+        h = ctypes.c_void_p()
+        self._ops = options.c_operators()
+        check(_lib.load().srhip_program_create(ctx.handle, _lib.dtype_code(dtype), ptr(self.nodes),
+                                               ptr(self.offsets), self.ntrees, ctypes.byref(self._ops),
+                                               ctypes.byref(h)))
+        self.handle = h
+
+    def num_constants(self) -> np.ndarray:
+        out = np.zeros(self.ntrees, dtype=np.int32)
+        check(_lib.load().srhip_program_num_constants(self.handle, ptr(out)))
+        return out
+
+    def set_constants(self, consts: np.ndarray) -> None:
+        c = np.ascontiguousarray(consts, dtype=np.float64)
+        check(_lib.load().srhip_program_set_constants(self.handle, ptr(c)))
+
+    def stats(self):
+        a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
+        check(_lib.load().srhip_program_stats(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return dict(total_nodes=a.value, total_opnodes=b.value, max_stack=c.value)
+
+    def eval_loss(self, ds: DeviceDataset, loss, idx=None):
+        out = np.empty(self.ntrees, dtype=np.float64)
+        ok = np.empty(self.ntrees, dtype=np.uint8)
+        ls = loss.c_struct()
+        idxa = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        check(_lib.load().srhip_eval_loss(self.ctx.handle, ds.handle, self.handle, ctypes.byref(ls), ptr(idxa),
+                                          0 if idxa is None else len(idxa), ptr(out), ptr(ok)))
+        return out, ok.astype(bool)
+
+    def eval_predict(self, ds: DeviceDataset, idx=None):
+        idxa = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        m = ds.n if idxa is None else len(idxa)
+        out = np.empty((self.ntrees, m), dtype=self.dtype)
+        ok = np.empty(self.ntrees, dtype=np.uint8)
+        check(_lib.load().srhip_eval_predict(self.ctx.handle, ds.handle, self.handle, ptr(idxa),
+                                             0 if idxa is None else len(idxa), ptr(out), ptr(ok)))
+        return out, ok.astype(bool)
+
+    def close(self):
+        if self.handle:
+            _lib.load().srhip_program_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
