@@ -22,6 +22,19 @@
 #include "srhip_ops.h"
 
 #define UNR _Pragma("unroll")
+// SRHIP_KDEBUG builds (diagnostic only): lane 0 of wave 0 of block (0,0) printfs its progress.
+#ifdef SRHIP_KDEBUG
+#define KDBG(...) do { if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) printf(__VA_ARGS__); } while (0)
+#else
+#define KDBG(...) do { } while (0)
+#endif
+// Progress words for SRHIP_TRACE runs: lane 0 of wave 0 of block (0,0) stores (slot, value) to
+// host-coherent memory with system scope, so the host can read them while the kernel runs.
+#define KMARK(slot, val)                                                                       \
+  do {                                                                                         \
+    if (p.dbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                      \
+      __hip_atomic_store(p.dbg + (slot), (int32_t)(val), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
+  } while (0)
 #ifndef SRHIP_ROW_FENCE
 #define SRHIP_ROW_FENCE() __builtin_amdgcn_sched_barrier(0)
 #endif
@@ -202,6 +215,8 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
   using O = OpsT<T>;
   using CT = typename Chk<T>::type;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  KMARK(0, 1);
+  if (p.debug_stop == 1) return;
   constexpr int TILE = 64 * R;
   const int lane = threadIdx.x & 63;
   const int rb = blockIdx.x;
@@ -213,7 +228,6 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
   const T* ysrc;
   const T* wsrc;
   int64_t xstride;
-  int* counter;
   if constexpr (XLDS) {
     T* lx = reinterpret_cast<T*>(smem);
     const int rbb = p.rb_rows;
@@ -230,31 +244,35 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
       const T* src = c < p.nfeat ? gX + (int64_t)c * p.ld : (c == p.nfeat ? gy : gw);
       reinterpret_cast<V*>(lx + (int64_t)c * rbb)[v] = reinterpret_cast<const V*>(src + row_base)[v];
     }
-    counter = reinterpret_cast<int*>(smem + (size_t)ncols * rbb * sizeof(T));
     xsrc = lx;
     ysrc = lx + (int64_t)p.nfeat * rbb;
     wsrc = lx + (int64_t)(p.nfeat + 1) * rbb;
     xstride = rbb;
   } else {
-    counter = reinterpret_cast<int*>(smem);
     xsrc = reinterpret_cast<const T*>(p.X) + row_base;
     ysrc = reinterpret_cast<const T*>(p.y) + row_base;
     wsrc = reinterpret_cast<const T*>(p.w) + row_base;
     xstride = p.ld;
   }
-  if (threadIdx.x == 0) *counter = 0;
+  KDBG("[k] staged, ntiles=%d rb_rows=%d nvalid=%ld max_steps=%d\n", ntiles, p.rb_rows, (long)p.nvalid, p.max_steps);
   __syncthreads();
+  KMARK(0, 2);
+  if (p.debug_stop == 2) return;
 
   const int group_base = blockIdx.y * p.trees_per_group;
   const int group_n = min(p.trees_per_group, p.ntrees - group_base);
 
-  for (;;) {
-    int ti = 0;
-    if (lane == 0) ti = atomicAdd(counter, 1);
-    ti = __builtin_amdgcn_readfirstlane(__shfl(ti, 0));
-    if (ti >= group_n) break;
+  // static assignment: the host deals cost-sorted trees round-robin, wave w takes w, w+WAVES, ...
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  KMARK(8 + wave, 10);
+  for (int ti = wave; ti < group_n; ti += EVAL_WAVES) {
+    KMARK(8 + wave, 11);
     const int tree = __builtin_amdgcn_readfirstlane(p.order[group_base + ti]);
     const int pc0 = __builtin_amdgcn_readfirstlane(p.prog_off[tree]);
+    KDBG("[k] ti=%d tree=%d pc0=%d group_n=%d\n", ti, tree, pc0, group_n);
+    KMARK(0, 3);
+    KMARK(1, tree);
+    if (p.debug_stop == 3) continue;
 
     LAccT<T> lacc = 0;
     CT M = 0;
@@ -266,11 +284,17 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
       UNR for (int r = 0; r < R; ++r) { A[r] = T(0); B[r] = T(0); }
       UNR for (int k = 0; k < K; ++k) UNR for (int r = 0; r < R; ++r) S[k][r] = T(0);
       int pc = pc0;
-      for (;;) {
+      // bounded: a malformed program ends after max_steps instructions instead of hanging
+      for (int step = 0; step < p.max_steps; ++step) {
         const Ins ins = p.code[pc];
+        KDBG("[k]   tile=%d step=%d pc=%d h=%u a=%u\n", tile, step, pc, ins.h, ins.a);
+        KMARK(2, tile);
+        KMARK(3, step);
+        KMARK(4, pc);
+        KMARK(5, ins.h);
         ++pc;
+        if (ins.h == H_END) break;
         switch (ins.h) {
-          case H_END: goto done;
           case H_LOADF: load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A); break;
           case H_LOADC: { const T c = imm_as<T>(ins.imm); UNR for (int r = 0; r < R; ++r) A[r] = c; break; }
           case H_FETCHF: load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, B); break;
@@ -367,13 +391,17 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
           default: break;
         }
       }
-    done:
+      KDBG("[k]   tile %d done\n", tile);
+      KMARK(0, 4);
       if constexpr (MODE == MODE_LOSS) {
         loss_tile<T, R>(p, A, ysrc + (int64_t)tile * TILE, wsrc + (int64_t)tile * TILE, lane, row0, lacc);
       } else if constexpr (MODE == MODE_PRED) {
         store_pred<T, R>(p, A, tree, lane, row0);
       }
     }
+    KDBG("[k] tree %d tiles done\n", tree);
+    KMARK(0, 5);
+    KMARK(8 + wave, 12);
     // ---- wave reduction, one partial per (tree, row block) ----
     if constexpr (MODE == MODE_LOSS) {
       lacc = wave_sum(lacc);
@@ -383,7 +411,9 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
       M = wave_chk(M);
       if (lane == 0) reinterpret_cast<CT*>(p.slab_chk)[(int64_t)tree * p.nrb + rb] = M;
     }
+    KMARK(8 + wave, 13);
   }
+  KMARK(8 + wave, 14);
 }
 
 // Per-tree reduction of the (tree, row block) partials, fixed order (deterministic).

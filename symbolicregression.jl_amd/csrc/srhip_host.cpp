@@ -16,7 +16,9 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <memory>
@@ -47,9 +49,21 @@ static int fail(int code, const char* fmt, ...) {
   return code;
 }
 
+// SRHIP_TRACE=1 in the environment prints every HIP call of the library (before and after) to
+// stderr, flushed: a GPU hang then names the call it happened in.
+static bool trace_on() {
+  static const int on = [] { const char* e = getenv("SRHIP_TRACE"); return e && *e && *e != '0'; }();
+  return on != 0;
+}
+static int debug_stop() {
+  static const int v = [] { const char* e = getenv("SRHIP_DEBUG_STOP"); return e ? atoi(e) : 0; }();
+  return v;
+}
 #define HIP_TRY(expr)                                                                             \
   do {                                                                                            \
+    if (trace_on()) { fprintf(stderr, "[srhip] %s:%d %s\n", __FILE__, __LINE__, #expr); fflush(stderr); } \
     hipError_t e_ = (expr);                                                                       \
+    if (trace_on()) { fprintf(stderr, "[srhip]   -> %d\n", (int)e_); fflush(stderr); }          \
     if (e_ != hipSuccess) return fail(SRHIP_ERR_DEVICE, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
   } while (0)
 
@@ -90,11 +104,11 @@ struct HostBuf {  // pinned staging
     p = nullptr;
     bytes = 0;
   }
-  hipError_t ensure(size_t n) {
+  hipError_t ensure(size_t n, unsigned flags = hipHostMallocDefault) {
     if (n <= bytes && p) return hipSuccess;
     release();
     size_t want = n < 256 ? 256 : n;
-    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&p, want, flags);
     if (e == hipSuccess) bytes = want;
     return e;
   }
@@ -108,7 +122,7 @@ struct srhip_ctx {
   int num_cu = 256;
   DevBuf slab_loss, slab_chk, red_loss, red_chk, slab_prec, order_prec;
   DevBuf vX, vy, vw, vidx, vstats;  // gathered views (batching idx)
-  HostBuf h_loss, h_chk, h_stats, h_prec;
+  HostBuf h_loss, h_chk, h_stats, h_prec, h_dbg;
 };
 
 struct srhip_dataset {
@@ -141,7 +155,7 @@ struct srhip_program {
   std::vector<TreeInfo> info;
   std::vector<Ins> code;
   std::vector<int32_t> prog_off;
-  int32_t kmax = 0, max_ops = 0;
+  int32_t kmax = 0, max_ops = 0, max_len = 0;
   int64_t total_nodes = 0, total_ops = 0;
   DevBuf d_code, d_off;
 };
@@ -510,6 +524,7 @@ int compile_program_t(srhip_program& P) {
   P.info.assign(P.ntrees, TreeInfo());
   P.kmax = 0;
   P.max_ops = 0;
+  P.max_len = 0;
   P.total_nodes = 0;
   P.total_ops = 0;
   for (int32_t t = 0; t < P.ntrees; ++t) {
@@ -520,6 +535,7 @@ int compile_program_t(srhip_program& P) {
     P.prog_off[t] = P.info[t].code_begin;
     P.kmax = std::max(P.kmax, P.info[t].need);
     P.max_ops = std::max(P.max_ops, (int32_t)P.info[t].op_sumcheck.size());
+    P.max_len = std::max(P.max_len, P.info[t].code_len);
     P.total_nodes += P.info[t].nnodes;
   }
   // operator-node count (degree >= 1), from the node tables
@@ -621,6 +637,8 @@ struct LaunchPlan {
 LaunchPlan plan_launch(const srhip_ctx* ctx, int dtype, int64_t nfeat, bool weighted, bool with_y, int64_t m,
                        int32_t ntrees) {
   LaunchPlan L;
+  ntrees = std::max<int32_t>(1, ntrees);  // every tree may have failed statically
+  m = std::max<int64_t>(1, m);
   const int R = rows_per_lane(dtype);
   const int tile = 64 * R;
   const size_t es = dtype_size(dtype);
@@ -764,6 +782,13 @@ static int run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program
     a.loss_p0 = loss ? loss->p0 : 0.0;
     a.weighted = weighted ? 1 : 0;
     a.has_y = mode == MODE_LOSS ? 1 : 0;
+    a.max_steps = P->max_len;
+    a.debug_stop = debug_stop();
+    if (trace_on()) {
+      HIP_TRY(ctx->h_dbg.ensure(64 * sizeof(int32_t), hipHostMallocCoherent));
+      memset(ctx->h_dbg.p, 0xff, 64 * sizeof(int32_t));
+      a.dbg = (int32_t*)ctx->h_dbg.p;
+    }
     DevBuf pred;
     if (mode == MODE_PRED) {
       HIP_TRY(pred.ensure((size_t)nt * v.m * es));
@@ -775,6 +800,31 @@ static int run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program
     HIP_TRY(launch_eval(dtype, a, K, mode, L.xlds, grid, L.lds, ctx->stream));
     HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
     ctx->timed = true;
+    if (trace_on()) {  // poll the kernel's progress words for up to 10 s, then abort loudly
+      const volatile int32_t* d = (const volatile int32_t*)ctx->h_dbg.p;
+      int32_t last[16];
+      for (int i = 0; i < 16; ++i) last[i] = -2;
+      for (int it = 0; it < 10000; ++it) {
+        hipError_t q = hipStreamQuery(ctx->stream);
+        bool changed = false;
+        for (int i = 0; i < 16; ++i) changed |= d[i] != last[i];
+        if (changed) {
+          for (int i = 0; i < 16; ++i) last[i] = d[i];
+          fprintf(stderr, "[srhip] kernel progress: stage=%d tree=%d tile=%d step=%d pc=%d h=%d waves=%d,%d,%d,%d,%d,%d,%d,%d\n",
+                  last[0], last[1], last[2], last[3], last[4], last[5], last[8], last[9], last[10], last[11], last[12],
+                  last[13], last[14], last[15]);
+          fflush(stderr);
+        }
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) HIP_TRY(q);
+        usleep(1000);
+        if (it == 9999) {
+          fprintf(stderr, "[srhip] kernel did not finish in 10 s; aborting\n");
+          fflush(stderr);
+          abort();
+        }
+      }
+    }
     HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p,
                           L.nrb, nt, mode == MODE_LOSS ? ctx->red_loss.p : nullptr,
                           dtype == SRHIP_I32 ? nullptr : ctx->red_chk.p, ctx->stream));
@@ -827,6 +877,7 @@ static int run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program
     a.trees_per_group = nu;
     a.slab_prec = ctx->slab_prec.p;
     a.prec_stride = stride;
+    a.max_steps = P->max_len;
     HIP_TRY(launch_eval(dtype, a, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, 1), 16, ctx->stream));
     HIP_TRY(ctx->h_prec.ensure(slab_bytes));
     HIP_TRY(hipMemcpyAsync(ctx->h_prec.p, ctx->slab_prec.p, slab_bytes, hipMemcpyDeviceToHost, ctx->stream));

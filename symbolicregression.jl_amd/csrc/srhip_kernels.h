@@ -41,7 +41,10 @@ struct EvalArgs {
   int32_t weighted;
   int32_t prec_stride;      // operator nodes per tree slot in slab_prec
   int32_t has_y;            // stage y into LDS (MODE_LOSS)
+  int32_t max_steps;        // longest tree program (instructions): bounds every interpreter loop
+  int32_t debug_stop;       // diagnostic early exits (SRHIP_DEBUG_STOP); 0 in normal runs
   int32_t pad_;
+  int32_t* dbg;             // SRHIP_TRACE: host-coherent progress words of block (0,0) wave 0, else nullptr
 };
 
 int rows_per_lane(int dtype);
