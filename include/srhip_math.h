@@ -1,0 +1,292 @@
+/*
+ * srhip_math.h — the scalar libm of the srhip evaluator: exp, log, sin, cos (and tan) in Float64,
+ * written with IEEE-754 basic operations and fma only, so that the gfx950 kernels (hipcc) and the
+ * CPU parity oracle (gcc) compute bit-identical values from this one source.
+ *
+ * Why it exists.  The reference evaluates operators with Julia Base.Math (pure-Julia libm derived
+ * from FreeBSD msun / fdlibm).  Vendor libms (OCML on the device, glibc on the host) are each
+ * within ~1 ULP of it but not bit-identical, and symbolic-regression trees routinely amplify a
+ * 1-ULP difference chaotically (cos(exp(x) * c) at large arguments), so parity at 1e-6 / 1e-12
+ * relative loss needs the device and the oracle to share the function values.  This file restates
+ * the fdlibm algorithms (e_exp.c reduction, e_log.c, k_sin.c, k_cos.c, e_rem_pio2.c, with a
+ * Payne-Hanek reduction written for 64-bit limbs); every constant is the fdlibm one (reduction
+ * constants regenerated with mpmath and checked bit-for-bit, see tests/test_math_accuracy.py,
+ * which also pins every function against glibc: <= 1 ULP in Float64, and Float32 values that are
+ * the correctly rounded results in all but double-rounding cases).
+ *
+ * Float32 evaluation widens to Float64 and rounds once (srm_*f below), as Julia does for Float32
+ * trigonometry (DoubleFloat32 kernels) and for Float32 `^`.
+ *
+ * Usable from C99 (oracle, gcc) and HIP C++ (host and device).  Compile WITHOUT fp contraction
+ * (-ffp-contract=off): the explicit fma() calls are the only fused operations.
+ */
+#ifndef SRHIP_MATH_H
+#define SRHIP_MATH_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define SRM_FN __host__ __device__ static inline __attribute__((always_inline))
+#define SRM_NOINLINE __host__ __device__ static __attribute__((noinline))
+#else
+#define SRM_FN static inline
+#define SRM_NOINLINE static
+#endif
+
+/* ---- bit helpers ---------------------------------------------------------------------------- */
+SRM_FN uint64_t srm_bits(double x) { uint64_t u; __builtin_memcpy(&u, &x, 8); return u; }
+SRM_FN double srm_from_bits(uint64_t u) { double x; __builtin_memcpy(&x, &u, 8); return x; }
+SRM_FN double srm_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+SRM_FN double srm_rint(double x) { return __builtin_rint(x); }
+SRM_FN double srm_inf(void) { return __builtin_inf(); }
+SRM_FN double srm_nan(void) { return __builtin_nan(""); }
+
+/* ---- exp ------------------------------------------------------------------------------------ */
+/* fdlibm e_exp.c argument reduction x = k ln2 + r, |r| <= ln2/2, with ln2 split so that k*ln2HI is
+ * exact; e^r by a degree-13 Taylor polynomial (truncation < 2^-57 on |r| <= 0.3466) instead of
+ * fdlibm's rational form, which would need a division (a ~10-instruction sequence on gfx950). */
+SRM_FN double srm_exp(double x) {
+  const double o_threshold = 7.09782712893383973096e+02;  /* 0x40862E42 FEFA39EF */
+  const double u_threshold = -7.45133219101941108420e+02; /* 0xc0874910 D52D3051 */
+  const double invln2 = 1.44269504088896338700e+00;
+  const double ln2HI = 6.93147180369123816490e-01; /* 0x3fe62e42 fee00000 */
+  const double ln2LO = 1.90821492927058770002e-10; /* 0x3dea39ef 35793c76 */
+  if (!(x == x)) return x + x;
+  if (x > o_threshold) return srm_inf();
+  if (x < u_threshold) return 0.0;
+  const double k = srm_rint(x * invln2);
+  const double hi = srm_fma(-k, ln2HI, x); /* exact product, one rounding (== fdlibm x - k*ln2HI) */
+  const double lo = k * ln2LO;
+  const double r = hi - lo;
+  /* q = sum_{n=2}^{13} r^(n-2) / n! */
+  double q = 1.6059043836821613e-10;          /* 1/13! */
+  q = srm_fma(q, r, 2.08767569878681e-09);  /* 1/12! */
+  q = srm_fma(q, r, 2.505210838544172e-08);  /* 1/11! */
+  q = srm_fma(q, r, 2.755731922398589e-07);  /* 1/10! */
+  q = srm_fma(q, r, 2.7557319223985893e-06);  /* 1/9!  */
+  q = srm_fma(q, r, 2.48015873015873e-05);  /* 1/8!  */
+  q = srm_fma(q, r, 1.984126984126984e-04);  /* 1/7!  */
+  q = srm_fma(q, r, 1.388888888888889e-03);  /* 1/6!  */
+  q = srm_fma(q, r, 8.333333333333333e-03);  /* 1/5!  */
+  q = srm_fma(q, r, 4.1666666666666664e-02);  /* 1/4!  */
+  q = srm_fma(q, r, 1.6666666666666666e-01);  /* 1/3!  */
+  q = srm_fma(q, r, 0.5);                         /* 1/2!  */
+  /* r as hi - lo: e^r = 1 + (hi - lo) + r^2 q, with the lo correction kept out of the rounding of r */
+  const double s = srm_fma(r * r, q, -lo) + hi;
+  const double y = 1.0 + s;
+  const int ki = (int)k;
+  if (ki >= -1021 && ki <= 1023) return y * srm_from_bits((uint64_t)(ki + 1023) << 52);
+  if (ki > 1023) return y * 2.0 * srm_from_bits((uint64_t)(ki - 1 + 1023) << 52);
+  /* deep underflow: scale in two steps (gradual underflow rounds once at the end) */
+  return (y * srm_from_bits((uint64_t)(ki + 54 + 1023) << 52)) * 5.55111512312578270212e-17; /* 2^-54 */
+}
+
+/* ---- log ------------------------------------------------------------------------------------ */
+/* fdlibm e_log.c: x = 2^k (1+f), 1+f in [sqrt(2)/2, sqrt(2)); s = f/(2+f); log(1+f) = f - hfsq +
+ * s (hfsq + R(s^2)) with fdlibm's Lg1..Lg7.  Caller handles the reference's safe_log domain. */
+SRM_FN double srm_log(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+               Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+               Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+               Lg7 = 1.479819860511658591e-01;
+  uint64_t u = srm_bits(x);
+  int32_t hx = (int32_t)(u >> 32);
+  int k = 0;
+  if (hx < 0x00100000) {                                   /* x < 2^-1022 (or negative) */
+    if ((u & 0x7fffffffffffffffULL) == 0) return -srm_inf(); /* log(+-0) = -inf */
+    if (hx < 0) return srm_nan();                            /* log(-x) = NaN */
+    k -= 54;
+    x *= 1.80143985094819840000e+16;                         /* 2^54: subnormal, scale up */
+    u = srm_bits(x);
+    hx = (int32_t)(u >> 32);
+  }
+  if (hx >= 0x7ff00000) return x + x; /* Inf or NaN */
+  k += (hx >> 20) - 1023;
+  hx &= 0x000fffff;
+  const int32_t i = (hx + 0x95f64) & 0x100000;
+  x = srm_from_bits(((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (u & 0xffffffffULL)); /* x or x/2 */
+  k += (i >> 20);
+  const double f = x - 1.0;
+  const double dk = (double)k;
+  const double s = f / (2.0 + f);
+  const double z = s * s;
+  const double w = z * z;
+  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  const double R = t2 + t1;
+  const int32_t ii = (hx - 0x6147a) | (0x6b851 - hx);
+  if (f == 0.0) return dk * ln2_hi + dk * ln2_lo;
+  if (ii > 0) {
+    const double hfsq = 0.5 * f * f;
+    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+  }
+  return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+/* ---- sin / cos kernels on [-pi/4, pi/4] (fdlibm k_sin.c / k_cos.c), x + y the reduced arg ---- */
+SRM_FN double srm_ksin(double x, double y) {
+  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+               S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+               S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+  const double z = x * x;
+  const double w = z * z;
+  const double r = S2 + z * (S3 + z * S4) + z * w * (S5 + z * S6);
+  const double v = z * x;
+  return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+}
+SRM_FN double srm_kcos(double x, double y) {
+  const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+               C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+               C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+  const double z = x * x;
+  double w = z * z;
+  const double r = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
+  const double hz = 0.5 * z;
+  w = 1.0 - hz;
+  return w + (((1.0 - w) - hz) + (z * r - x * y));
+}
+
+/* ---- argument reduction x = n pi/2 + (y0 + y1) ------------------------------------------------ */
+/* 2/pi, 64 bits per word, most significant first (regenerated with mpmath in tests). */
+#define SRM_TWO_OVER_PI_WORDS                                                                     \
+  {0xA2F9836E4E441529ULL, 0xFC2757D1F534DDC0ULL, 0xDB6295993C439041ULL, 0xFE5163ABDEBBC561ULL,    \
+   0xB7246E3A424DD2E0ULL, 0x06492EEA09D1921CULL, 0xFE1DEB1CB129A73EULL, 0xE88235F52EBB4484ULL,    \
+   0xE99C7026B45F7E41ULL, 0x3991D639835339F4ULL, 0x9C845F8BBDF9283BULL, 0x1FF897FFDE05980FULL,    \
+   0xEF2F118B5A0A6D1FULL, 0x6D367ECF27CB09B7ULL, 0x4F463F669E5FEA2DULL, 0x7527BAC7EBE5F17BULL,    \
+   0x3D0739F78A5292EAULL, 0x6BFB5FB11F8D5D08ULL, 0x56033046FC7B6BABULL, 0xF0CFBC209AF4361DULL}
+#if defined(__HIPCC__)
+__device__ __constant__ static const uint64_t srm_2opi_dev[20] = SRM_TWO_OVER_PI_WORDS;
+#endif
+static const uint64_t srm_2opi_host[20] = SRM_TWO_OVER_PI_WORDS;
+
+/* 64 bits of 2/pi starting at fraction bit `pos` (1 = the first bit after the binary point);
+ * bits at positions <= 0 are zero (2/pi < 1). */
+SRM_FN uint64_t srm_2opi_bits(int pos) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint64_t* T = srm_2opi_dev;
+#else
+  const uint64_t* T = srm_2opi_host;
+#endif
+  const int b = pos - 1;
+  if (b <= -64) return 0;
+  if (b < 0) return T[0] >> (-b);
+  const int k = b >> 6, sh = b & 63;
+  return sh ? ((T[k] << sh) | (T[k + 1] >> (64 - sh))) : T[k];
+}
+
+/* Payne-Hanek for |x| >= 2^20 pi/2: x = M 2^E (M the 53-bit significand); x 2/pi mod 4 from a
+ * 192-bit window of 2/pi starting at fraction bit E-1 (bits of weight >= 4 dropped), as a
+ * 192-bit fixed-point product; the fraction is rounded to the nearest quadrant. */
+SRM_NOINLINE int srm_rem_pio2_large(double x, double* y0, double* y1) {
+  const uint64_t u = srm_bits(x);
+  const int e = (int)((u >> 52) & 0x7ff) - 1023;
+  const uint64_t M = (u & 0x000fffffffffffffULL) | 0x0010000000000000ULL;
+  const int E = e - 52;
+  const uint64_t w2 = srm_2opi_bits(E - 1), w1 = srm_2opi_bits(E - 1 + 64), w0 = srm_2opi_bits(E - 1 + 128);
+  /* P = M * [w2:w1:w0] mod 2^192 */
+  const unsigned __int128 q0 = (unsigned __int128)M * w0;
+  const unsigned __int128 q1 = (unsigned __int128)M * w1 + (uint64_t)(q0 >> 64);
+  const uint64_t p0 = (uint64_t)q0, p1 = (uint64_t)q1;
+  const uint64_t p2 = (uint64_t)M * w2 + (uint64_t)(q1 >> 64);
+  /* value = P 2^-190: quadrant = bits 190..191, fraction = bits 0..189 */
+  int n = (int)(p2 >> 62);
+  const uint64_t T1 = (p2 << 2) | (p1 >> 62); /* top 64 fraction bits */
+  const uint64_t T2 = (p1 << 2) | (p0 >> 62); /* next 64 */
+  const int64_t Ts = (int64_t)T1;             /* fraction >= 1/2 reads negative: f - 1 */
+  if (Ts < 0) n += 1;
+  /* f = Ts 2^-64 + T2 2^-128, split into a 53-bit head and a tail */
+  const double fhi = (double)(Ts >> 11) * 1.1102230246251565404e-16;                      /* 2^-53 */
+  const double flo = (double)(T1 & 0x7ff) * 5.42101086242752217004e-20                     /* 2^-64 */
+                     + (double)T2 * 2.93873587705571876992e-39;                            /* 2^-128 */
+  const double pio2_hi = 1.57079632679489655800e+00, pio2_lo = 6.12323399573676603587e-17;
+  const double rhi = fhi * pio2_hi;
+  const double rlo = srm_fma(fhi, pio2_hi, -rhi) + (fhi * pio2_lo + flo * pio2_hi);
+  const double s = rhi + rlo;
+  *y0 = (x < 0.0) ? -s : s;
+  const double t = rlo - (s - rhi);
+  *y1 = (x < 0.0) ? -t : t;
+  return (x < 0.0) ? -n : n;
+}
+
+/* fdlibm e_rem_pio2.c for |x| < 2^20 pi/2 (three Cody-Waite rounds with 33-bit pieces of pi/2). */
+SRM_FN int srm_rem_pio2(double x, double* y0, double* y1) {
+  const double invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
+               pio2_1t = 6.07710050650619224932e-11, pio2_2 = 6.07710050630396597660e-11,
+               pio2_2t = 2.02226624879595063154e-21, pio2_3 = 2.02226624871116645580e-21,
+               pio2_3t = 8.47842766036889956997e-32;
+  const uint32_t ix = (uint32_t)(srm_bits(x) >> 32) & 0x7fffffff;
+  if (ix <= 0x3fe921fb) { /* |x| ~<= pi/4 */
+    *y0 = x;
+    *y1 = 0.0;
+    return 0;
+  }
+  if (ix >= 0x413921fb) return srm_rem_pio2_large(x, y0, y1);
+  const double fn = srm_rint(x * invpio2);
+  const int n = (int)fn;
+  double r = x - fn * pio2_1;
+  double w = fn * pio2_1t;
+  const int j = (int)(ix >> 20);
+  double yy = r - w;
+  int i = j - (int)((srm_bits(yy) >> 52) & 0x7ff);
+  if (i > 16) { /* 2nd round, good to 118 bits */
+    double t = r;
+    w = fn * pio2_2;
+    r = t - w;
+    w = fn * pio2_2t - ((t - r) - w);
+    yy = r - w;
+    i = j - (int)((srm_bits(yy) >> 52) & 0x7ff);
+    if (i > 49) { /* 3rd round, good to 151 bits */
+      t = r;
+      w = fn * pio2_3;
+      r = t - w;
+      w = fn * pio2_3t - ((t - r) - w);
+      yy = r - w;
+    }
+  }
+  *y0 = yy;
+  *y1 = (r - yy) - w;
+  return n;
+}
+
+SRM_FN double srm_cos(double x) {
+  if (!(x - x == 0.0)) return srm_nan(); /* Inf or NaN */
+  double y0, y1;
+  const int n = srm_rem_pio2(x, &y0, &y1);
+  const double c = srm_kcos(y0, y1), s = srm_ksin(y0, y1);
+  switch (n & 3) {
+    case 0: return c;
+    case 1: return -s;
+    case 2: return -c;
+    default: return s;
+  }
+}
+SRM_FN double srm_sin(double x) {
+  if (!(x - x == 0.0)) return srm_nan();
+  double y0, y1;
+  const int n = srm_rem_pio2(x, &y0, &y1);
+  const double c = srm_kcos(y0, y1), s = srm_ksin(y0, y1);
+  switch (n & 3) {
+    case 0: return s;
+    case 1: return c;
+    case 2: return -s;
+    default: return -c;
+  }
+}
+/* tan = sin/cos over one shared reduction (<= ~1.5 ULP; fdlibm's k_tan is not restated) */
+SRM_FN double srm_tan(double x) {
+  if (!(x - x == 0.0)) return srm_nan();
+  double y0, y1;
+  const int n = srm_rem_pio2(x, &y0, &y1);
+  const double c = srm_kcos(y0, y1), s = srm_ksin(y0, y1);
+  return (n & 1) ? -c / s : s / c;
+}
+
+/* ---- Float32: widen, evaluate in Float64, round once ---------------------------------------- */
+SRM_FN float srm_expf(float x) { return (float)srm_exp((double)x); }
+SRM_FN float srm_logf(float x) { return (float)srm_log((double)x); }
+SRM_FN float srm_cosf(float x) { return (float)srm_cos((double)x); }
+SRM_FN float srm_sinf(float x) { return (float)srm_sin((double)x); }
+SRM_FN float srm_tanf(float x) { return (float)srm_tan((double)x); }
+
+#endif /* SRHIP_MATH_H */

@@ -24,11 +24,16 @@
 #endif
 
 #include "../include/srhip.h"
+#include "../include/srhip_math.h"
 
 #define CAT_(a, b) a##b
 #define CAT(a, b) CAT_(a, b)
 
-/* ---------------- Float32 ---------------- */
+/* ---------------- Float32 ----------------
+ * Transcendentals widen to Float64 and round once (Julia evaluates Float32 trig through Float64
+ * kernels, and Float32 ^ by widening): exp/log/sin/cos/tan from the shared include/srhip_math.h
+ * (fdlibm restatement, pinned against glibc in tests/test_math_accuracy.py), the rest from glibc. */
+#define W1(fn, x) ((float)fn((double)(x)))
 static float julia_modf32(float x, float y) {
   const float r = fmodf(x, y);
   if (r == 0.0f) return copysignf(r, y);
@@ -64,7 +69,7 @@ static float bin_f32(int op, float a, float b) {
       if (a == b) return signbit(a) ? a : b;
       return a < b ? a : b;
     case SRHIP_OP_MOD: return julia_modf32(a, b);
-    case SRHIP_OP_ATAN2: return atan2f(a, b);
+    case SRHIP_OP_ATAN2: return (float)atan2((double)a, (double)b);
     default: return NAN;
   }
 }
@@ -75,34 +80,34 @@ static float un_f32(int op, float x) {
     case SRHIP_OP_CUBE: return x * x * x;
     case SRHIP_OP_ABS: return fabsf(x);
     case SRHIP_OP_RELU: return x > 0.0f ? x : copysignf(0.0f, x);
-    case SRHIP_OP_COS: return cosf(x);
-    case SRHIP_OP_SIN: return sinf(x);
-    case SRHIP_OP_TAN: return tanf(x);
-    case SRHIP_OP_EXP: return expf(x);
-    case SRHIP_OP_LOG: return x <= 0.0f ? NAN : logf(x);
-    case SRHIP_OP_LOG2: return x <= 0.0f ? NAN : log2f(x);
-    case SRHIP_OP_LOG10: return x <= 0.0f ? NAN : log10f(x);
-    case SRHIP_OP_LOG1P: return x <= -1.0f ? NAN : log1pf(x);
+    case SRHIP_OP_COS: return srm_cosf(x);
+    case SRHIP_OP_SIN: return srm_sinf(x);
+    case SRHIP_OP_TAN: return srm_tanf(x);
+    case SRHIP_OP_EXP: return srm_expf(x);
+    case SRHIP_OP_LOG: return x <= 0.0f ? NAN : srm_logf(x);
+    case SRHIP_OP_LOG2: return x <= 0.0f ? NAN : W1(log2, x);
+    case SRHIP_OP_LOG10: return x <= 0.0f ? NAN : W1(log10, x);
+    case SRHIP_OP_LOG1P: return x <= -1.0f ? NAN : W1(log1p, x);
     case SRHIP_OP_SQRT: return x < 0.0f ? NAN : sqrtf(x);
-    case SRHIP_OP_ACOSH: return x < 1.0f ? NAN : acoshf(x);
-    case SRHIP_OP_ATANH_CLIP: return atanhf(julia_modf32(x + 1.0f, 2.0f) - 1.0f);
-    case SRHIP_OP_SINH: return sinhf(x);
-    case SRHIP_OP_COSH: return coshf(x);
-    case SRHIP_OP_TANH: return tanhf(x);
-    case SRHIP_OP_ASIN: return asinf(x);
-    case SRHIP_OP_ACOS: return acosf(x);
-    case SRHIP_OP_ATAN: return atanf(x);
-    case SRHIP_OP_ASINH: return asinhf(x);
-    case SRHIP_OP_ERF: return erff(x);
-    case SRHIP_OP_ERFC: return erfcf(x);
-    case SRHIP_OP_GAMMA: { const float g = tgammaf(x); return isinf(g) ? NAN : g; }
+    case SRHIP_OP_ACOSH: return x < 1.0f ? NAN : W1(acosh, x);
+    case SRHIP_OP_ATANH_CLIP: return W1(atanh, julia_modf32(x + 1.0f, 2.0f) - 1.0f);
+    case SRHIP_OP_SINH: return W1(sinh, x);
+    case SRHIP_OP_COSH: return W1(cosh, x);
+    case SRHIP_OP_TANH: return W1(tanh, x);
+    case SRHIP_OP_ASIN: return W1(asin, x);
+    case SRHIP_OP_ACOS: return W1(acos, x);
+    case SRHIP_OP_ATAN: return W1(atan, x);
+    case SRHIP_OP_ASINH: return W1(asinh, x);
+    case SRHIP_OP_ERF: return W1(erf, x);
+    case SRHIP_OP_ERFC: return W1(erfc, x);
+    case SRHIP_OP_GAMMA: { const float g = W1(tgamma, x); return isinf(g) ? NAN : g; }
     case SRHIP_OP_ROUND: return rintf(x);
     case SRHIP_OP_FLOOR: return floorf(x);
     case SRHIP_OP_CEIL: return ceilf(x);
     case SRHIP_OP_SIGN: return x < 0.0f ? -1.0f : (x > 0.0f ? 1.0f : x);
-    case SRHIP_OP_EXP2: return exp2f(x);
-    case SRHIP_OP_EXPM1: return expm1f(x);
-    case SRHIP_OP_CBRT: return cbrtf(x);
+    case SRHIP_OP_EXP2: return W1(exp2, x);
+    case SRHIP_OP_EXPM1: return W1(expm1, x);
+    case SRHIP_OP_CBRT: return W1(cbrt, x);
     default: return NAN;
   }
 }
@@ -114,8 +119,8 @@ static float loss_f32(int kind, float d, float p0) {
     case SRHIP_LOSS_HUBER: { const float a = fabsf(d); return a <= p0 ? 0.5f * (d * d) : p0 * (a - 0.5f * p0); }
     case SRHIP_LOSS_L1_EPS_INS: { const float e = fabsf(d) - p0; return e > 0.0f ? e : 0.0f; }
     case SRHIP_LOSS_L2_EPS_INS: { const float e = fabsf(d) - p0; const float m = e > 0.0f ? e : 0.0f; return m * m; }
-    case SRHIP_LOSS_LOGIT_DIST: { const float er = expf(d); const float den = 1.0f + er; return -logf(4.0f * er / (den * den)); }
-    case SRHIP_LOSS_PERIODIC: return 1.0f - cosf(d * (2.0f * 3.14159265358979323846f) / p0);
+    case SRHIP_LOSS_LOGIT_DIST: { const float er = srm_expf(d); const float den = 1.0f + er; return -srm_logf(4.0f * er / (den * den)); }
+    case SRHIP_LOSS_PERIODIC: return 1.0f - srm_cosf(d * (2.0f * 3.14159265358979323846f) / p0);
     case SRHIP_LOSS_QUANTILE: return d * (p0 - (d < 0.0f ? 1.0f : 0.0f));
     default: return NAN;
   }
@@ -168,11 +173,11 @@ static double un_f64(int op, double x) {
     case SRHIP_OP_CUBE: return x * x * x;
     case SRHIP_OP_ABS: return fabs(x);
     case SRHIP_OP_RELU: return x > 0.0 ? x : copysign(0.0, x);
-    case SRHIP_OP_COS: return cos(x);
-    case SRHIP_OP_SIN: return sin(x);
-    case SRHIP_OP_TAN: return tan(x);
-    case SRHIP_OP_EXP: return exp(x);
-    case SRHIP_OP_LOG: return x <= 0.0 ? NAN : log(x);
+    case SRHIP_OP_COS: return srm_cos(x);
+    case SRHIP_OP_SIN: return srm_sin(x);
+    case SRHIP_OP_TAN: return srm_tan(x);
+    case SRHIP_OP_EXP: return srm_exp(x);
+    case SRHIP_OP_LOG: return x <= 0.0 ? NAN : srm_log(x);
     case SRHIP_OP_LOG2: return x <= 0.0 ? NAN : log2(x);
     case SRHIP_OP_LOG10: return x <= 0.0 ? NAN : log10(x);
     case SRHIP_OP_LOG1P: return x <= -1.0 ? NAN : log1p(x);
@@ -207,8 +212,8 @@ static double loss_f64(int kind, double d, double p0) {
     case SRHIP_LOSS_HUBER: { const double a = fabs(d); return a <= p0 ? 0.5 * (d * d) : p0 * (a - 0.5 * p0); }
     case SRHIP_LOSS_L1_EPS_INS: { const double e = fabs(d) - p0; return e > 0.0 ? e : 0.0; }
     case SRHIP_LOSS_L2_EPS_INS: { const double e = fabs(d) - p0; const double m = e > 0.0 ? e : 0.0; return m * m; }
-    case SRHIP_LOSS_LOGIT_DIST: { const double er = exp(d); const double den = 1.0 + er; return -log(4.0 * er / (den * den)); }
-    case SRHIP_LOSS_PERIODIC: return 1.0 - cos(d * (2.0 * 3.14159265358979323846) / p0);
+    case SRHIP_LOSS_LOGIT_DIST: { const double er = srm_exp(d); const double den = 1.0 + er; return -srm_log(4.0 * er / (den * den)); }
+    case SRHIP_LOSS_PERIODIC: return 1.0 - srm_cos(d * (2.0 * 3.14159265358979323846) / p0);
     case SRHIP_LOSS_QUANTILE: return d * (p0 - (d < 0.0 ? 1.0 : 0.0));
     default: return NAN;
   }
@@ -244,6 +249,18 @@ static int32_t un_i32(int op, int32_t x) {
 
 /* scalar entry points (used by tests to check operator semantics one value at a time) */
 float oracle_bin_f32(int op, float a, float b) { return bin_f32(op, a, b); }
+/* the shared libm (include/srhip_math.h), vectorised for tests/test_math_accuracy.py */
+void oracle_srm_f64(int which, const double* x, double* y, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) {
+    switch (which) {
+      case 0: y[i] = srm_exp(x[i]); break;
+      case 1: y[i] = srm_log(x[i]); break;
+      case 2: y[i] = srm_sin(x[i]); break;
+      case 3: y[i] = srm_cos(x[i]); break;
+      default: y[i] = srm_tan(x[i]); break;
+    }
+  }
+}
 float oracle_un_f32(int op, float x) { return un_f32(op, x); }
 double oracle_bin_f64(int op, double a, double b) { return bin_f64(op, a, b); }
 double oracle_un_f64(int op, double x) { return un_f64(op, x); }

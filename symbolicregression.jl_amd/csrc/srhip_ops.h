@@ -11,6 +11,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "../../include/srhip_math.h"
+
 #define SRHIP_HD __host__ __device__ __attribute__((always_inline)) inline
 
 namespace srhip {
@@ -46,41 +48,56 @@ SRHIP_HD float m_min(float a, float b) { return __builtin_elementwise_minimum(a,
 SRHIP_HD double m_min(double a, double b) { return __builtin_elementwise_minimum(a, b); }
 
 // ---- libm wrappers (float and double) ----------------------------------------------------------
-#define SRHIP_WRAP1(name, ff, df)                      \
-  SRHIP_HD float m_##name(float x) { return ff(x); }   \
+// exp/log/sin/cos/tan come from the shared include/srhip_math.h (bit-identical on the device, in
+// the host constant folder and in the oracle).  Every Float32 transcendental widens to Float64
+// and rounds once (Julia's Float32 trig and ^ do the same), so the remaining vendor functions
+// (OCML here, glibc in the oracle) agree on Float32 results except in double-rounding cases.
+#define SRHIP_WRAP1(name, df)                                      \
+  SRHIP_HD float m_##name(float x) { return (float)df((double)x); } \
   SRHIP_HD double m_##name(double x) { return df(x); }
-SRHIP_WRAP1(cos, cosf, cos)
-SRHIP_WRAP1(sin, sinf, sin)
-SRHIP_WRAP1(tan, tanf, tan)
-SRHIP_WRAP1(exp, expf, exp)
-SRHIP_WRAP1(log, logf, log)
-SRHIP_WRAP1(log2, log2f, log2)
-SRHIP_WRAP1(log10, log10f, log10)
-SRHIP_WRAP1(log1p, log1pf, log1p)
-SRHIP_WRAP1(sqrt, sqrtf, sqrt)
-SRHIP_WRAP1(acosh, acoshf, acosh)
-SRHIP_WRAP1(atanh, atanhf, atanh)
-SRHIP_WRAP1(sinh, sinhf, sinh)
-SRHIP_WRAP1(cosh, coshf, cosh)
-SRHIP_WRAP1(tanh, tanhf, tanh)
-SRHIP_WRAP1(asin, asinf, asin)
-SRHIP_WRAP1(acos, acosf, acos)
-SRHIP_WRAP1(atan, atanf, atan)
-SRHIP_WRAP1(asinh, asinhf, asinh)
-SRHIP_WRAP1(erf, erff, erf)
-SRHIP_WRAP1(erfc, erfcf, erfc)
-SRHIP_WRAP1(tgamma, tgammaf, tgamma)
-SRHIP_WRAP1(rint, rintf, rint)
-SRHIP_WRAP1(floor, floorf, floor)
-SRHIP_WRAP1(ceil, ceilf, ceil)
-SRHIP_WRAP1(exp2, exp2f, exp2)
-SRHIP_WRAP1(expm1, expm1f, expm1)
-SRHIP_WRAP1(cbrt, cbrtf, cbrt)
-SRHIP_WRAP1(trunc, truncf, trunc)
+SRHIP_HD float m_cos(float x) { return srm_cosf(x); }
+SRHIP_HD double m_cos(double x) { return srm_cos(x); }
+SRHIP_HD float m_sin(float x) { return srm_sinf(x); }
+SRHIP_HD double m_sin(double x) { return srm_sin(x); }
+SRHIP_HD float m_tan(float x) { return srm_tanf(x); }
+SRHIP_HD double m_tan(double x) { return srm_tan(x); }
+SRHIP_HD float m_exp(float x) { return srm_expf(x); }
+SRHIP_HD double m_exp(double x) { return srm_exp(x); }
+SRHIP_HD float m_log(float x) { return srm_logf(x); }
+SRHIP_HD double m_log(double x) { return srm_log(x); }
+SRHIP_WRAP1(log2, log2)
+SRHIP_WRAP1(log10, log10)
+SRHIP_WRAP1(log1p, log1p)
+SRHIP_WRAP1(acosh, acosh)
+SRHIP_WRAP1(atanh, atanh)
+SRHIP_WRAP1(sinh, sinh)
+SRHIP_WRAP1(cosh, cosh)
+SRHIP_WRAP1(tanh, tanh)
+SRHIP_WRAP1(asin, asin)
+SRHIP_WRAP1(acos, acos)
+SRHIP_WRAP1(atan, atan)
+SRHIP_WRAP1(asinh, asinh)
+SRHIP_WRAP1(erf, erf)
+SRHIP_WRAP1(erfc, erfc)
+SRHIP_WRAP1(tgamma, tgamma)
+SRHIP_WRAP1(exp2, exp2)
+SRHIP_WRAP1(expm1, expm1)
+SRHIP_WRAP1(cbrt, cbrt)
 #undef SRHIP_WRAP1
+// exact in any IEEE implementation: no widening needed
+SRHIP_HD float m_sqrt(float x) { return sqrtf(x); }
+SRHIP_HD double m_sqrt(double x) { return sqrt(x); }
+SRHIP_HD float m_rint(float x) { return rintf(x); }
+SRHIP_HD double m_rint(double x) { return rint(x); }
+SRHIP_HD float m_floor(float x) { return floorf(x); }
+SRHIP_HD double m_floor(double x) { return floor(x); }
+SRHIP_HD float m_ceil(float x) { return ceilf(x); }
+SRHIP_HD double m_ceil(double x) { return ceil(x); }
+SRHIP_HD float m_trunc(float x) { return truncf(x); }
+SRHIP_HD double m_trunc(double x) { return trunc(x); }
 SRHIP_HD float m_fmod(float a, float b) { return fmodf(a, b); }
 SRHIP_HD double m_fmod(double a, double b) { return fmod(a, b); }
-SRHIP_HD float m_atan2(float a, float b) { return atan2f(a, b); }
+SRHIP_HD float m_atan2(float a, float b) { return (float)atan2((double)a, (double)b); }
 SRHIP_HD double m_atan2(double a, double b) { return atan2(a, b); }
 // Julia's Float32 ^ Float32 is evaluated by widening to Float64 (base/math.jl); same here.
 SRHIP_HD float m_pow(float a, float b) { return (float)pow((double)a, (double)b); }

@@ -62,6 +62,8 @@ def _ds(ctx, X, y=None, w=None):
 
 
 def _rel(a, b):
+    if a == b or (math.isnan(a) and math.isnan(b)):  # equal infinities / both NaN
+        return 0.0
     return abs(a - b) / max(abs(b), 1e-300)
 
 
