@@ -74,11 +74,9 @@ SRM_FN double srm_exp(double x) {
   /* r as hi - lo: e^r = 1 + (hi - lo) + r^2 q, with the lo correction kept out of the rounding of r */
   const double s = srm_fma(r * r, q, -lo) + hi;
   const double y = 1.0 + s;
-  const int ki = (int)k;
-  if (ki >= -1021 && ki <= 1023) return y * srm_from_bits((uint64_t)(ki + 1023) << 52);
-  if (ki > 1023) return y * 2.0 * srm_from_bits((uint64_t)(ki - 1 + 1023) << 52);
-  /* deep underflow: scale in two steps (gradual underflow rounds once at the end) */
-  return (y * srm_from_bits((uint64_t)(ki + 54 + 1023) << 52)) * 5.55111512312578270212e-17; /* 2^-54 */
+  /* y 2^k in two exact steps (k1, k2 in the normal range); a subnormal result rounds once */
+  const int ki = (int)k, k1 = ki / 2, k2 = ki - k1;
+  return (y * srm_from_bits((uint64_t)(k1 + 1023) << 52)) * srm_from_bits((uint64_t)(k2 + 1023) << 52);
 }
 
 /* ---- log ------------------------------------------------------------------------------------ */
@@ -282,11 +280,95 @@ SRM_FN double srm_tan(double x) {
   return (n & 1) ? -c / s : s / c;
 }
 
-/* ---- Float32: widen, evaluate in Float64, round once ---------------------------------------- */
-SRM_FN float srm_expf(float x) { return (float)srm_exp((double)x); }
+/* ---- Float32 ---------------------------------------------------------------------------------
+ * Every Float32 function evaluates in Float64 and rounds once.
+ *   sinf/cosf/tanf: FreeBSD s_sinf.c / s_cosf.c / e_rem_pio2f.c, which Julia Base restates for
+ *     Float32 (DoubleFloat32 kernels): small multiples of pi/2 (|x| <= 9pi/4) reduced by
+ *     x - n*(pi/2 as a double), medium |x| < 2^28 pi/2 by two-term Cody-Waite with the 25-bit
+ *     pio2_1, huge |x| by the shared Payne-Hanek; kernels __kernel_cosdf / __kernel_sindf
+ *     (degree-4 double polynomials, |error| < 2^-34).  The case analysis of s_cosf.c is written
+ *     as one quadrant formula (n = rint(2x/pi)): the same kernels and reduced arguments, no
+ *     per-lane branches.
+ *   expf: x = k ln2 + r in Float64 (ln2 as a double pair, fma), degree-10 Taylor (< 2^-42).
+ *   logf: srm_log on the widened value (exact: every float is a normal double). */
+SRM_FN double srm_kcosdf(double x) {
+  const double C0 = -0.499999997251031, C1 = 0.04166662332373906, C2 = -0.001388676377460993,
+               C3 = 2.439044879627741e-05;
+  const double z = x * x, w = z * z, r = C2 + z * C3;
+  return ((1.0 + z * C0) + w * C1) + (w * z) * r;
+}
+SRM_FN double srm_ksindf(double x) {
+  const double S1 = -0.16666666641626524, S2 = 0.008333329385889463, S3 = -0.00019839334836096632,
+               S4 = 2.718311493989822e-06;
+  const double z = x * x, w = z * z, r = S3 + z * S4, s = z * x;
+  return (x + s * (S1 + z * S2)) + s * w * r;
+}
+/* returns n (quadrant), *y the reduced argument; x finite */
+SRM_FN int srm_rem_pio2f(float xf, double* y) {
+  const double x = (double)xf;
+  const double ax = x < 0.0 ? -x : x;
+  if (!(ax < 421657428.2663131)) { /* |x| >= 2^28 pi/2: Payne-Hanek (rare, one branch per wave) */
+    double y0, y1;
+    const int n = srm_rem_pio2_large(x, &y0, &y1);
+    *y = y0;
+    return n;
+  }
+  const double invpio2 = 6.36619772367581382433e-01, pio2 = 1.5707963267948966,
+               pio2_1 = 1.57079631090164184570e+00, pio2_1t = 1.58932547735281966916e-08;
+  const double fn = srm_rint(x * invpio2);
+  const double small = x - fn * pio2;                  /* |x| <= 9pi/4: x -/+ c{1,2,3,4}pio2 */
+  const double medium = (x - fn * pio2_1) - fn * pio2_1t; /* fn*pio2_1 exact (25-bit pio2_1) */
+  *y = (ax <= 7.0685834705770345) ? small : medium;
+  return (int)fn;
+}
+SRM_FN float srm_cosf(float x) {
+  if (!(x - x == 0.0f)) return x - x; /* Inf, NaN -> NaN */
+  double y;
+  const int n = srm_rem_pio2f(x, &y);
+  const double c = srm_kcosdf(y), s = srm_ksindf(y);
+  const double r = (n & 1) ? s : c;
+  return (float)(((n + 1) & 2) ? -r : r);
+}
+SRM_FN float srm_sinf(float x) {
+  if (!(x - x == 0.0f)) return x - x;
+  double y;
+  const int n = srm_rem_pio2f(x, &y);
+  const double c = srm_kcosdf(y), s = srm_ksindf(y);
+  const double r = (n & 1) ? c : s;
+  return (float)((n & 2) ? -r : r);
+}
+SRM_FN float srm_tanf(float x) {
+  if (!(x - x == 0.0f)) return x - x;
+  double y;
+  const int n = srm_rem_pio2f(x, &y);
+  const double c = srm_kcosdf(y), s = srm_ksindf(y);
+  return (float)((n & 1) ? -c / s : s / c);
+}
+SRM_FN float srm_expf(float xf) {
+  const double invln2 = 1.4426950408889634, ln2_hi = 0.6931471805599453, ln2_lo = 2.3190468138462996e-17;
+  double x = (double)xf;
+  /* clamp to where the float result is already 0 or Inf (also maps NaN to a finite value) */
+  x = (x <= 89.0) ? x : 89.0;
+  x = (x >= -104.0) ? x : -104.0;
+  const double k = srm_rint(x * invln2);
+  double r = srm_fma(-k, ln2_hi, x);
+  r = srm_fma(-k, ln2_lo, r);
+  double p = 2.505210838544172e-08;     /* 1/11! */
+  p = srm_fma(p, r, 2.755731922398589e-07);
+  p = srm_fma(p, r, 2.7557319223985893e-06);
+  p = srm_fma(p, r, 2.48015873015873e-05);
+  p = srm_fma(p, r, 1.984126984126984e-04);
+  p = srm_fma(p, r, 1.388888888888889e-03);
+  p = srm_fma(p, r, 8.333333333333333e-03);
+  p = srm_fma(p, r, 4.1666666666666664e-02);
+  p = srm_fma(p, r, 1.6666666666666666e-01);
+  p = srm_fma(p, r, 0.5);
+  p = srm_fma(p, r, 1.0);
+  p = srm_fma(p, r, 1.0);
+  const double sc = srm_from_bits((uint64_t)((int64_t)k + 1023) << 52);
+  const float res = (float)(p * sc);
+  return (xf == xf) ? res : xf;
+}
 SRM_FN float srm_logf(float x) { return (float)srm_log((double)x); }
-SRM_FN float srm_cosf(float x) { return (float)srm_cos((double)x); }
-SRM_FN float srm_sinf(float x) { return (float)srm_sin((double)x); }
-SRM_FN float srm_tanf(float x) { return (float)srm_tan((double)x); }
 
 #endif /* SRHIP_MATH_H */

@@ -118,3 +118,18 @@ def scalar_un(op, x, dtype):
     ct = {"f32": ctypes.c_float, "f64": ctypes.c_double, "i32": ctypes.c_int32}[sfx]
     fn = _setup(getattr(lib, f"oracle_un_{sfx}"), ct, [ctypes.c_int, ct])
     return np.dtype(dtype).type(fn(int(op), ct(x)))
+
+
+_SRM = {"exp": 0, "log": 1, "sin": 2, "cos": 3, "tan": 4}
+
+
+def srm(name, x):
+    """The shared libm (include/srhip_math.h) on an array: Float64 or Float32 by x's dtype."""
+    lib = load()
+    x = np.ascontiguousarray(x)
+    y = np.empty_like(x)
+    sfx = "f64" if x.dtype == np.float64 else "f32"
+    fn = _setup(getattr(lib, f"oracle_srm_{sfx}"), None,
+                [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64])
+    fn(_SRM[name], _p(x), _p(y), len(x))
+    return y

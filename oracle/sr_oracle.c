@@ -261,6 +261,17 @@ void oracle_srm_f64(int which, const double* x, double* y, int64_t n) {
     }
   }
 }
+void oracle_srm_f32(int which, const float* x, float* y, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) {
+    switch (which) {
+      case 0: y[i] = srm_expf(x[i]); break;
+      case 1: y[i] = srm_logf(x[i]); break;
+      case 2: y[i] = srm_sinf(x[i]); break;
+      case 3: y[i] = srm_cosf(x[i]); break;
+      default: y[i] = srm_tanf(x[i]); break;
+    }
+  }
+}
 float oracle_un_f32(int op, float x) { return un_f32(op, x); }
 double oracle_bin_f64(int op, double a, double b) { return bin_f64(op, a, b); }
 double oracle_un_f64(int op, double x) { return un_f64(op, x); }

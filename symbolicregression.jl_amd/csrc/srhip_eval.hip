@@ -83,6 +83,77 @@ template <typename T> __device__ __attribute__((always_inline)) inline T imm_as(
   }
 }
 
+// ---- heavy operators: one out-of-line body per (T, R, op), called by every kernel variant ----
+// Transcendentals are 20-60 VALU instructions per row; inlining them R times into every handler of
+// every kernel variant made a ~700k-instruction kernel whose hot loop thrashed the instruction
+// cache (SQ_IFETCH ~ 0.4 x SQ_INSTS).  Out of line, the dispatch loop and the cheap handlers stay
+// compact and each heavy body exists once; the R rows travel in VGPRs (vector argument/return).
+template <typename T, int R> struct RowVec { typedef T type __attribute__((ext_vector_type(R))); };
+template <typename T, int R> using RV = typename RowVec<T, R>::type;
+
+template <typename T, int R, int U>
+__device__ __attribute__((noinline)) RV<T, R> heavy_un(RV<T, R> v) {
+  using O = OpsT<T>;
+  UNR for (int r = 0; r < R; ++r) {
+    T x = v[r];
+    switch (U) {
+#define X_(NAME, FN) case UN_##NAME: if constexpr (un_ok<T>(UN_##NAME)) x = O::FN(x); break;
+      SRHIP_UNOPS(X_)
+#undef X_
+      default: break;
+    }
+    v[r] = x;
+  }
+  return v;
+}
+// heavy binary: a op b per row
+template <typename T, int R, int HB>
+__device__ __attribute__((noinline)) RV<T, R> heavy_bin(RV<T, R> a, RV<T, R> b) {
+  using O = OpsT<T>;
+  UNR for (int r = 0; r < R; ++r) {
+    T x = a[r];
+    switch (HB) {
+#define X_(NAME, FN) case HB_##NAME: if constexpr (hb_ok<T>(HB_##NAME)) x = O::FN(a[r], b[r]); break;
+      SRHIP_HEAVY_BINOPS(X_)
+#undef X_
+      default: break;
+    }
+    a[r] = x;
+  }
+  return a;
+}
+// unary operators cheap enough to inline into the handler (a few VALU instructions per row)
+template <int U> constexpr bool un_inline() {
+  return U == UN_NEG || U == UN_SQUARE || U == UN_CUBE || U == UN_ABS || U == UN_RELU || U == UN_SIGN ||
+         U == UN_ROUND || U == UN_FLOOR || U == UN_CEIL;
+}
+template <typename T, int R, int U>
+__device__ __attribute__((always_inline)) inline void apply_un(T (&A)[R]) {
+  if constexpr (un_inline<U>()) {
+    using O = OpsT<T>;
+    UNR for (int r = 0; r < R; ++r) {
+      switch (U) {
+#define X_(NAME, FN) case UN_##NAME: if constexpr (un_ok<T>(UN_##NAME)) A[r] = O::FN(A[r]); break;
+        SRHIP_UNOPS(X_)
+#undef X_
+        default: break;
+      }
+    }
+  } else {
+    RV<T, R> v;
+    UNR for (int r = 0; r < R; ++r) v[r] = A[r];
+    v = heavy_un<T, R, U>(v);
+    UNR for (int r = 0; r < R; ++r) A[r] = v[r];
+  }
+}
+template <typename T, int R, int HB>
+__device__ __attribute__((always_inline)) inline void apply_heavy(T (&A)[R], const T (&X)[R], const T (&Y)[R]) {
+  RV<T, R> a, b;
+  UNR for (int r = 0; r < R; ++r) { a[r] = X[r]; b[r] = Y[r]; }
+  a = heavy_bin<T, R, HB>(a, b);
+  UNR for (int r = 0; r < R; ++r) A[r] = a[r];
+}
+
 // Check accumulator: max |v| over every operator output (NaN-propagating, v_maximum3_f32) for
 // Float32; sum of |v| * 2^-512 for Float64 (Inf/NaN propagate, cannot overflow otherwise).
 template <typename T> struct Chk {
@@ -362,14 +433,14 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
 #define SRHIP_HEAVY_CASE(NAME, FN)                                               \
   case h_heavy(HB_##NAME, false):                                                \
     if constexpr (hb_ok<T>(HB_##NAME)) {                                         \
-      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(A[r], B[r]);                  \
+      apply_heavy<T, R, HB_##NAME>(A, A, B);                                     \
       chk_update<R>(M, A);                                                       \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0); \
     }                                                                            \
     break;                                                                       \
   case h_heavy(HB_##NAME, true):                                                 \
     if constexpr (hb_ok<T>(HB_##NAME)) {                                         \
-      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(B[r], A[r]);                  \
+      apply_heavy<T, R, HB_##NAME>(A, B, A);                                     \
       chk_update<R>(M, A);                                                       \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0); \
     }                                                                            \
@@ -380,7 +451,7 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
 #define SRHIP_UN_CASE(NAME, FN)                                                  \
   case h_un(UN_##NAME):                                                          \
     if constexpr (un_ok<T>(UN_##NAME)) {                                         \
-      UNR for (int r = 0; r < R; ++r) { A[r] = O::FN(A[r]); SRHIP_ROW_FENCE(); } \
+      apply_un<T, R, UN_##NAME>(A);                                              \
       chk_update<R>(M, A);                                                       \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0); \
     }                                                                            \

@@ -1,0 +1,144 @@
+"""Pins the shared scalar libm (include/srhip_math.h) that the device kernels and the oracle both
+use for exp / log / sin / cos / tan (see DESIGN.md "transcendentals").
+
+The reference evaluates these with Julia Base.Math (fdlibm / FreeBSD msun lineage; not available
+here), so the pin is accuracy, not bits: against glibc (Float64, <= 1 ULP; tan <= 2) and against
+the correctly rounded value (mpmath, 200 bits) for Float32 (<= 1 ULP, and equal to it for the
+overwhelming majority of inputs — FreeBSD's Float32 trig kernels, which Julia restates, are
+~2^-34 accurate before the final rounding).  The reduction constants are regenerated here.
+"""
+import math
+import struct
+
+import numpy as np
+import pytest
+
+mpmath = pytest.importorskip("mpmath")
+
+
+def _ulps64(a, b):
+    ai = a.view(np.int64).astype(object)
+    bi = b.view(np.int64).astype(object)
+    conv = lambda v: (-(1 << 63) - v) if v < 0 else v  # noqa: E731 - monotone integer map
+    return np.array([abs(conv(x) - conv(y)) for x, y in zip(ai, bi)])
+
+
+def _ulps32(a, b):
+    ai = a.view(np.int32).astype(np.int64)
+    bi = b.view(np.int32).astype(np.int64)
+    ai = np.where(ai < 0, -(1 << 31) - ai, ai)
+    bi = np.where(bi < 0, -(1 << 31) - bi, bi)
+    return np.abs(ai - bi)
+
+
+def _ulps64_fast(a, b):
+    ai = a.view(np.int64)
+    bi = b.view(np.int64)
+    ai = np.where(ai < 0, np.int64(-(2**63)) - ai, ai)
+    bi = np.where(bi < 0, np.int64(-(2**63)) - bi, bi)
+    return np.abs(ai - bi)
+
+
+def test_reduction_constants_match_fdlibm_bits():
+    mpmath.mp.prec = 400
+    pio2 = mpmath.pi / 2
+
+    def trunc_bits(x, nb):
+        e = int(mpmath.floor(mpmath.log(x, 2)))
+        s = mpmath.mpf(2) ** (nb - 1 - e)
+        return mpmath.floor(x * s) / s
+
+    hx = lambda d: struct.unpack("<Q", struct.pack("<d", float(d)))[0]  # noqa: E731
+    p1 = trunc_bits(pio2, 33)
+    assert hx(p1) == 0x3FF921FB54400000
+    assert hx(pio2 - p1) == 0x3DD0B4611A626331
+    p2 = trunc_bits(pio2 - p1, 33)
+    assert hx(p2) == 0x3DD0B4611A600000
+    assert hx(2 / mpmath.pi) == 0x3FE45F306DC9C883
+    # 2/pi words of the Payne-Hanek table (1280 bits)
+    mpmath.mp.prec = 2000
+    f = 2 / mpmath.pi
+    words = []
+    for _ in range(20):
+        f *= mpmath.mpf(2) ** 64
+        w = int(mpmath.floor(f))
+        words.append(w)
+        f -= w
+    src = open(__file__.replace("tests/test_math_accuracy.py", "include/srhip_math.h")).read()
+    for w in words:
+        assert f"0x{w:016X}ULL" in src
+
+
+RNG = np.random.default_rng(1234)
+F64_CASES = {
+    "exp": [RNG.uniform(-745, 709.7, 200_000), RNG.uniform(-1, 1, 200_000), np.array([0.0, -0.0, 1e-300, 709.78, -745.1])],
+    "log": [np.exp(RNG.uniform(-700, 700, 200_000)), RNG.uniform(0.9, 1.1, 200_000),
+            np.array([5e-324, 1e-310, 2.2250738585072014e-308, 1.0, 2.0, 1.7976931348623157e308])],
+    "sin": [RNG.uniform(-10, 10, 200_000), RNG.uniform(-2e6, 2e6, 100_000),
+            10 ** RNG.uniform(6, 300, 50_000) * RNG.choice([-1, 1], 50_000)],
+    "cos": [RNG.uniform(-10, 10, 200_000), RNG.uniform(-2e6, 2e6, 100_000),
+            10 ** RNG.uniform(6, 300, 50_000) * RNG.choice([-1, 1], 50_000)],
+    "tan": [RNG.uniform(-10, 10, 100_000), 10 ** RNG.uniform(6, 300, 20_000)],
+}
+
+
+@pytest.mark.parametrize("name", list(F64_CASES))
+def test_float64_within_one_ulp_of_glibc(oracle, name):
+    ref = getattr(np, name)
+    for x in F64_CASES[name]:
+        u = _ulps64_fast(oracle.srm(name, x), ref(x))
+        assert u.max() <= (2 if name == "tan" else 1), (name, x[np.argmax(u)])
+
+
+def test_float64_huge_arguments_vs_mpmath(oracle):
+    mpmath.mp.prec = 256
+    x = 10 ** RNG.uniform(6, 308, 200) * RNG.choice([-1, 1], 200)
+    for name in ("sin", "cos"):
+        cr = np.array([float(getattr(mpmath, name)(mpmath.mpf(float(v)))) for v in x])
+        assert _ulps64_fast(oracle.srm(name, x), cr).max() <= 1
+
+
+def test_specials(oracle):
+    inf, nan = np.inf, np.nan
+    e = oracle.srm("exp", np.array([inf, -inf, nan, 710.0, -746.0]))
+    assert e[0] == inf and e[1] == 0 and np.isnan(e[2]) and e[3] == inf and e[4] == 0
+    lg = oracle.srm("log", np.array([0.0, -1.0, inf, nan]))
+    assert lg[0] == -inf and np.isnan(lg[1]) and lg[2] == inf and np.isnan(lg[3])
+    for name in ("sin", "cos", "tan"):
+        assert np.all(np.isnan(oracle.srm(name, np.array([inf, -inf, nan]))))
+    e32 = oracle.srm("exp", np.array([np.inf, -np.inf, np.nan, 88.8, -104.0, 88.7], dtype=np.float32))
+    assert e32[0] == np.inf and e32[1] == 0 and np.isnan(e32[2]) and e32[3] == np.inf and e32[4] == 0
+    assert np.isfinite(e32[5])
+
+
+F32_CASES = {
+    "exp": lambda n: RNG.uniform(-104, 89, n),
+    "log": lambda n: np.exp(RNG.uniform(-100, 88, n)),
+    "sin": lambda n: np.concatenate([RNG.uniform(-8, 8, n // 2), RNG.uniform(-1e5, 1e5, n // 4),
+                                     10 ** RNG.uniform(5, 38, n // 4)]),
+    "cos": lambda n: np.concatenate([RNG.uniform(-8, 8, n // 2), RNG.uniform(-1e5, 1e5, n // 4),
+                                     10 ** RNG.uniform(5, 38, n // 4)]),
+    "tan": lambda n: RNG.uniform(-8, 8, n),
+}
+
+
+@pytest.mark.parametrize("name", list(F32_CASES))
+def test_float32_vs_correctly_rounded(oracle, name):
+    mpmath.mp.prec = 200
+    x = F32_CASES[name](3000).astype(np.float32)
+    got = oracle.srm(name, x)
+    fn = getattr(mpmath, name)
+    cr = np.array([float(fn(mpmath.mpf(float(v)))) for v in x]).astype(np.float32)
+    u = _ulps32(got, cr)
+    assert u.max() <= 1, (name, x[np.argmax(u)])
+    assert np.mean(u > 0) < 0.01, np.mean(u > 0)
+
+
+@pytest.mark.parametrize("name", list(F32_CASES))
+def test_float32_vs_glibc_widened_large_sample(oracle, name):
+    x = F32_CASES[name](400_000).astype(np.float32)
+    got = oracle.srm(name, x)
+    ref = getattr(np, name)(x.astype(np.float64)).astype(np.float32)
+    u = _ulps32(got, ref)
+    assert u.max() <= 1
+    assert np.mean(u > 0) < 0.01
