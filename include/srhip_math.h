@@ -282,66 +282,63 @@ SRM_FN double srm_tan(double x) {
 
 /* ---- Float32 ---------------------------------------------------------------------------------
  * Every Float32 function evaluates in Float64 and rounds once.
- *   sinf/cosf/tanf: FreeBSD s_sinf.c / s_cosf.c / e_rem_pio2f.c, which Julia Base restates for
- *     Float32 (DoubleFloat32 kernels): small multiples of pi/2 (|x| <= 9pi/4) reduced by
- *     x - n*(pi/2 as a double), medium |x| < 2^28 pi/2 by two-term Cody-Waite with the 25-bit
- *     pio2_1, huge |x| by the shared Payne-Hanek; kernels __kernel_cosdf / __kernel_sindf
- *     (degree-4 double polynomials, |error| < 2^-34).  The case analysis of s_cosf.c is written
- *     as one quadrant formula (n = rint(2x/pi)): the same kernels and reduced arguments, no
- *     per-lane branches.
+ *   sinf/cosf/tanf: the FreeBSD s_sinf.c / s_cosf.c scheme that Julia Base restates for Float32
+ *     (DoubleFloat32 kernels): reduction to [-pi/4, pi/4] in Float64, the degree-4 double
+ *     polynomials of __kernel_cosdf / __kernel_sindf (|error| < 2^-34), one rounding to Float32.
+ *     Written branch-free for a SIMD lane: one quadrant formula n = rint(2x/pi) instead of
+ *     s_cosf.c's case analysis, an fma reduction, and a single polynomial per row.
  *   expf: x = k ln2 + r in Float64 (ln2 as a double pair, fma), degree-10 Taylor (< 2^-42).
  *   logf: srm_log on the widened value (exact: every float is a normal double). */
-SRM_FN double srm_kcosdf(double x) {
-  const double C0 = -0.499999997251031, C1 = 0.04166662332373906, C2 = -0.001388676377460993,
-               C3 = 2.439044879627741e-05;
-  const double z = x * x, w = z * z, r = C2 + z * C3;
-  return ((1.0 + z * C0) + w * C1) + (w * z) * r;
+/* __kernel_cosdf / __kernel_sindf coefficients (FreeBSD k_cosf.c / k_sinf.c, |error| < 2^-34 on
+ * [-pi/4, pi/4]), evaluated as cos y = Q_C(z), sin y = y Q_S(z), z = y^2, Q_K(z) = 1 + K0 z + K1 z^2
+ * + K2 z^3 + K3 z^4 by fma Horner; one polynomial per row with per-row coefficients, since a SIMD
+ * lane would otherwise evaluate both kernels. */
+SRM_FN double srm_ksincosdf(double y, int odd) {
+  const double K0 = odd ? -0.16666666641626524 : -0.499999997251031;
+  const double K1 = odd ? 0.008333329385889463 : 0.04166662332373906;
+  const double K2 = odd ? -0.00019839334836096632 : -0.001388676377460993;
+  const double K3 = odd ? 2.718311493989822e-06 : 2.439044879627741e-05;
+  const double z = y * y;
+  const double q = srm_fma(z, srm_fma(z, srm_fma(z, srm_fma(z, K3, K2), K1), K0), 1.0);
+  return odd ? y * q : q;
 }
-SRM_FN double srm_ksindf(double x) {
-  const double S1 = -0.16666666641626524, S2 = 0.008333329385889463, S3 = -0.00019839334836096632,
-               S4 = 2.718311493989822e-06;
-  const double z = x * x, w = z * z, r = S3 + z * S4, s = z * x;
-  return (x + s * (S1 + z * S2)) + s * w * r;
-}
-/* returns n (quadrant), *y the reduced argument; x finite */
+/* returns n (quadrant), *y the reduced argument; x finite.  |x| < 2^28 pi/2: y = x - n (pi/2) with
+ * pi/2 as a double pair and two fmas (each one rounding; |y| error < 2^-50 relative for every
+ * float x in range); larger |x|: the shared Payne-Hanek (one rarely taken branch per wave). */
 SRM_FN int srm_rem_pio2f(float xf, double* y) {
   const double x = (double)xf;
   const double ax = x < 0.0 ? -x : x;
-  if (!(ax < 421657428.2663131)) { /* |x| >= 2^28 pi/2: Payne-Hanek (rare, one branch per wave) */
+  if (!(ax < 421657428.2663131)) {
     double y0, y1;
     const int n = srm_rem_pio2_large(x, &y0, &y1);
     *y = y0;
     return n;
   }
-  const double invpio2 = 6.36619772367581382433e-01, pio2 = 1.5707963267948966,
-               pio2_1 = 1.57079631090164184570e+00, pio2_1t = 1.58932547735281966916e-08;
+  const double invpio2 = 6.36619772367581382433e-01, pio2_hi = 1.5707963267948966,
+               pio2_lo = 6.123233995736766e-17;
   const double fn = srm_rint(x * invpio2);
-  const double small = x - fn * pio2;                  /* |x| <= 9pi/4: x -/+ c{1,2,3,4}pio2 */
-  const double medium = (x - fn * pio2_1) - fn * pio2_1t; /* fn*pio2_1 exact (25-bit pio2_1) */
-  *y = (ax <= 7.0685834705770345) ? small : medium;
+  *y = srm_fma(-fn, pio2_lo, srm_fma(-fn, pio2_hi, x));
   return (int)fn;
 }
 SRM_FN float srm_cosf(float x) {
   if (!(x - x == 0.0f)) return x - x; /* Inf, NaN -> NaN */
   double y;
   const int n = srm_rem_pio2f(x, &y);
-  const double c = srm_kcosdf(y), s = srm_ksindf(y);
-  const double r = (n & 1) ? s : c;
+  const double r = srm_ksincosdf(y, n & 1);
   return (float)(((n + 1) & 2) ? -r : r);
 }
 SRM_FN float srm_sinf(float x) {
   if (!(x - x == 0.0f)) return x - x;
   double y;
   const int n = srm_rem_pio2f(x, &y);
-  const double c = srm_kcosdf(y), s = srm_ksindf(y);
-  const double r = (n & 1) ? c : s;
+  const double r = srm_ksincosdf(y, (n & 1) ^ 1);
   return (float)((n & 2) ? -r : r);
 }
 SRM_FN float srm_tanf(float x) {
   if (!(x - x == 0.0f)) return x - x;
   double y;
   const int n = srm_rem_pio2f(x, &y);
-  const double c = srm_kcosdf(y), s = srm_ksindf(y);
+  const double c = srm_ksincosdf(y, 0), s = srm_ksincosdf(y, 1);
   return (float)((n & 1) ? -c / s : s / c);
 }
 SRM_FN float srm_expf(float xf) {
@@ -365,7 +362,7 @@ SRM_FN float srm_expf(float xf) {
   p = srm_fma(p, r, 0.5);
   p = srm_fma(p, r, 1.0);
   p = srm_fma(p, r, 1.0);
-  const double sc = srm_from_bits((uint64_t)((int64_t)k + 1023) << 52);
+  const double sc = srm_from_bits((uint64_t)(uint32_t)((int)k + 1023) << 52); /* |k| <= 151 */
   const float res = (float)(p * sc);
   return (xf == xf) ? res : xf;
 }

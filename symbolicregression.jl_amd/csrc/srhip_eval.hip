@@ -75,6 +75,12 @@ __device__ __attribute__((always_inline)) inline void load_rows(const T* base, i
   }
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(4))) Ins CIns;  // constant address space: scalar loads
+#else
+typedef const Ins CIns;
+#endif
+
 template <typename T> __device__ __attribute__((always_inline)) inline T imm_as(uint64_t bits) {
   if constexpr (sizeof(T) == 8) {
     return __builtin_bit_cast(T, bits);
@@ -335,11 +341,13 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
 
   // static assignment: the host deals cost-sorted trees round-robin, wave w takes w, w+WAVES, ...
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const CIns* code = (const CIns*)(uintptr_t)p.code;
   KMARK(8 + wave, 10);
   for (int ti = wave; ti < group_n; ti += EVAL_WAVES) {
     KMARK(8 + wave, 11);
     const int tree = __builtin_amdgcn_readfirstlane(p.order[group_base + ti]);
     const int pc0 = __builtin_amdgcn_readfirstlane(p.prog_off[tree]);
+    const int max_steps = __builtin_amdgcn_readfirstlane(p.max_steps);
     KDBG("[k] ti=%d tree=%d pc0=%d group_n=%d\n", ti, tree, pc0, group_n);
     KMARK(0, 3);
     KMARK(1, tree);
@@ -354,16 +362,15 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
       T A[R], B[R], S[K][R];
       UNR for (int r = 0; r < R; ++r) { A[r] = T(0); B[r] = T(0); }
       UNR for (int k = 0; k < K; ++k) UNR for (int r = 0; r < R; ++r) S[k][r] = T(0);
-      int pc = pc0;
+      // The program is read through the constant address space with a wave-uniform pc, so every
+      // instruction is one s_load_dwordx4 (scalar cache), prefetched one instruction ahead.
+      const CIns* prog = code + pc0;
+      Ins nxt = prog[0];
       // bounded: a malformed program ends after max_steps instructions instead of hanging
-      for (int step = 0; step < p.max_steps; ++step) {
-        const Ins ins = p.code[pc];
-        KDBG("[k]   tile=%d step=%d pc=%d h=%u a=%u\n", tile, step, pc, ins.h, ins.a);
-        KMARK(2, tile);
-        KMARK(3, step);
-        KMARK(4, pc);
-        KMARK(5, ins.h);
-        ++pc;
+      for (int step = 0; step < max_steps; ++step) {
+        const Ins ins = nxt;
+        nxt = prog[step + 1];
+        KDBG("[k]   tile=%d step=%d h=%u a=%u\n", tile, step, ins.h, ins.a);
         if (ins.h == H_END) break;
         switch (ins.h) {
           case H_LOADF: load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A); break;

@@ -8,7 +8,10 @@
 namespace srhip {
 
 constexpr int EVAL_WAVES = 8;  // wavefronts per workgroup of the interpreter kernel
-constexpr int R_F32 = 8;       // rows per lane per dispatch, 4-byte types
+#ifndef SRHIP_R_F32
+#define SRHIP_R_F32 8
+#endif
+constexpr int R_F32 = SRHIP_R_F32;  // rows per lane per dispatch, 4-byte types
 constexpr int R_F64 = 4;       // rows per lane per dispatch, Float64
 constexpr int ROW_ALIGN = 4096;  // device datasets are padded to a multiple of this many rows
 constexpr int MODE_LOSS = 0, MODE_PRED = 1, MODE_PRECISE = 2;
