@@ -138,7 +138,9 @@ int srhip_dataset_create(srhip_ctx* ctx, int dtype, const void* X, int64_t nfeat
                          const void* weights, srhip_dataset** out);
 void srhip_dataset_destroy(srhip_dataset* ds);
 
-/* Compile + upload a batch of trees (the population) for one operator table. */
+/* Compile + upload a batch of trees (the population) for one operator table.  ctx may be NULL:
+ * a host-only program (compiled, with its did_succeed metadata) usable by srhip_*_finalize and
+ * srhip_program_* queries but not by the evaluation calls. */
 int srhip_program_create(srhip_ctx* ctx, int dtype, const srhip_node* nodes,
                          const int64_t* tree_offsets /* [ntrees+1] into nodes */, int32_t ntrees,
                          const srhip_operators* ops, srhip_program** out);
@@ -164,6 +166,34 @@ int srhip_eval_loss_batch(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_n
                           const int64_t* tree_offsets, int32_t ntrees, const srhip_operators* ops,
                           const srhip_loss* loss, const int64_t* idx, int64_t nidx,
                           double* out_loss, uint8_t* out_ok);
+
+/* ---- row-sharded evaluation (several GPUs / processes, each holding a block of rows) -------
+ * Replaces nothing in the reference (it has no row parallelism): the reduction
+ * of src/LossFunctions.jl:13-33 and the did_succeed checks split into per-shard partials that
+ * combine by an all-reduce, then a decision every rank computes identically.
+ *   1. srhip_eval_loss_partials on each shard:
+ *        sums[2*T + 2*F + 1] (T trees, F features): per tree {sum of (w*)loss, sum of w (or rows)},
+ *        per feature {column sum (Float64 data: sum of x * 2^-64), non-finite count}, rows;
+ *        chk[T]: operator-output check statistic.
+ *   2. all-reduce: sums by SUM; chk by srhip_chk_reduce_op(dtype) (0 = MAX, 1 = SUM).
+ *   3. srhip_partials_finalize(prog, F, sums, chk, loss, ok, status): status 2 = undecided
+ *      (a near-overflow sum): then 4.
+ *   4. srhip_eval_precise_partials for the undecided trees on each shard -> opsums
+ *      [n_sel * srhip_program_max_ops(prog)], all-reduce SUM, srhip_precise_finalize -> ok.
+ * srhip_eval_loss runs exactly these steps on one device. */
+int srhip_eval_loss_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* prog,
+                             const srhip_loss* loss, const int64_t* idx, int64_t nidx,
+                             double* sums, double* chk);
+int srhip_partials_finalize(const srhip_program* prog, int64_t nfeatures, const double* sums,
+                            const double* chk, double* out_loss, uint8_t* out_ok,
+                            uint8_t* out_status);
+int srhip_eval_precise_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* prog,
+                                const int64_t* idx, int64_t nidx, const int32_t* trees,
+                                int32_t ntrees_sel, double* opsums);
+int srhip_precise_finalize(const srhip_program* prog, const int32_t* trees, int32_t ntrees_sel,
+                           const double* opsums, uint8_t* out_ok);
+int srhip_chk_reduce_op(int dtype);
+int32_t srhip_program_max_ops(const srhip_program* prog);
 
 /* ---- measurement hooks (bench / profiling) --------------------------------------------- */
 /* Device time (ms) of the last srhip_eval_loss/predict's main evaluation kernel, measured with

@@ -133,3 +133,25 @@ def srm(name, x):
                 [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64])
     fn(_SRM[name], _p(x), _p(y), len(x))
     return y
+
+
+def partials(nodes, offsets, binops, unaops, X, y, w=None, loss_kind=0, p0=0.0):
+    """One row shard's (sums, chk) in libsrhip's srhip_eval_loss_partials layout (row-wise)."""
+    lib = load()
+    X = np.ascontiguousarray(X)
+    sfx = _SFX[X.dtype]
+    nfeat, n = X.shape
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    T = len(offsets) - 1
+    sums = np.zeros(2 * T + 2 * nfeat + 1, dtype=np.float64)
+    chk = np.zeros(T, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=X.dtype)
+    w = None if w is None else np.ascontiguousarray(w, dtype=X.dtype)
+    fn = _setup(getattr(lib, f"oracle_partials_{sfx}"), None,
+                [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                 ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                 ctypes.c_int, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p])
+    fn(_p(np.ascontiguousarray(nodes)), _p(offsets), T, _p(np.ascontiguousarray(binops, dtype=np.int32)),
+       _p(np.ascontiguousarray(unaops, dtype=np.int32)), _p(X), nfeat, _p(y), _p(w), n, int(loss_kind),
+       float(p0), _p(sums), _p(chk))
+    return sums, chk

@@ -353,3 +353,85 @@ int CAT(oracle_eval_loss_batch_, SFX)(const srhip_node* nodes, const int64_t* of
 
 #undef INF_T
 #undef NONFINITE
+
+/* ---- row-shard partials (test infrastructure for the multi-GPU protocol, include/srhip.h) ----
+ * Row-wise restatement of what one shard contributes: per tree {sum (w*)loss, sum w (or rows)},
+ * per feature {column sum (Float64: x * 2^-64), non-finite count}, rows; chk[t] = max |v| (Float32,
+ * NaN-propagating) or sum |v| 2^-512 (Float64) over the outputs of every non-constant operator
+ * node (constant subtrees are scalars in the reference and on the device). */
+static T CAT(rowval_, SFX)(const CAT(Ctx, SFX) * c, int64_t i, int64_t j, double* chk, int* chk_nan) {
+  const srhip_node* n = &c->nd[i];
+  if (n->degree == 0) return CAT(leafrow_, SFX)(c, n, j);
+  if (CAT(is_const_, SFX)(c, i)) {
+    T v = 0;
+    CAT(eval_const_, SFX)(c, i, &v);
+    return v;
+  }
+  T v;
+  if (n->degree == 1) {
+    v = CAT(un_, SFX)(c->unaops[n->op - 1], CAT(rowval_, SFX)(c, n->l, j, chk, chk_nan));
+  } else {
+    const T a = CAT(rowval_, SFX)(c, n->l, j, chk, chk_nan);
+    const T b = CAT(rowval_, SFX)(c, n->r, j, chk, chk_nan);
+    v = CAT(bin_, SFX)(c->binops[n->op - 1], a, b);
+  }
+#if !IS_INT
+  if (v != v) *chk_nan = 1;
+  const double av = fabs((double)v);
+  if (sizeof(T) == 8) *chk += av * 0x1p-512;
+  else if (av > *chk) *chk = av;
+#endif
+  return v;
+}
+
+void CAT(oracle_partials_, SFX)(const srhip_node* nodes, const int64_t* offsets, int32_t ntrees, const int32_t* binops,
+                                const int32_t* unaops, const T* X, int64_t nfeat, const T* y, const T* w, int64_t n,
+                                int loss_kind, double p0, double* sums, double* chk) {
+  for (int32_t t = 0; t < ntrees; ++t) {
+    CAT(Ctx, SFX) c;
+    c.nd = nodes + offsets[t];
+    c.binops = binops;
+    c.unaops = unaops;
+    c.X = X;
+    c.n = n;
+    long double ls = 0.0L, ws = 0.0L;
+    double ck = 0.0;
+    int ck_nan = 0;
+    for (int64_t j = 0; j < n; ++j) {
+      const T pv = CAT(rowval_, SFX)(&c, 0, j, &ck, &ck_nan);
+#if IS_INT
+      const int32_t d = (int32_t)((uint32_t)pv - (uint32_t)y[j]);
+      ls += loss_kind == SRHIP_LOSS_L1 ? (d < 0 ? -(long double)d : (long double)d) : (long double)(int32_t)((uint32_t)d * (uint32_t)d);
+      ws += 1.0L;
+#else
+      const T l = CAT(loss_, SFX)(loss_kind, pv - y[j], (T)p0);
+      if (w) {
+        ls += (long double)(w[j] * l);
+        ws += (long double)w[j];
+      } else {
+        ls += (long double)l;
+        ws += 1.0L;
+      }
+#endif
+    }
+    sums[2 * t] = (double)ls;
+    sums[2 * t + 1] = (double)ws;
+    chk[t] = ck_nan ? (double)NAN : ck;
+  }
+  for (int64_t f = 0; f < nfeat; ++f) {
+    long double s = 0.0L;
+    double bad = 0;
+    for (int64_t j = 0; j < n; ++j) {
+      const T v = X[f * n + j];
+#if IS_INT
+      s += (long double)v;
+#else
+      if (!isfinite(v)) bad += 1;
+      else s += sizeof(T) == 8 ? (long double)v * 0x1p-64L : (long double)v;
+#endif
+    }
+    sums[2 * (int64_t)ntrees + 2 * f] = (double)s;
+    sums[2 * (int64_t)ntrees + 2 * f + 1] = bad;
+  }
+  sums[2 * (int64_t)ntrees + 2 * nfeat] = (double)n;
+}

@@ -679,235 +679,303 @@ std::vector<int32_t> make_order(const srhip_program& P, const std::vector<int32_
   return order;
 }
 
-// Host decision from the device partials.  Returns 0 ok, 1 fail, 2 uncertain (needs precise pass)
-int decide(const srhip_program& P, int32_t t, int dtype, const View& v, double chk) {
+// ---- the did_succeed decision, from (possibly all-reduced) partials ----------------------------
+// Partials layout (the C ABI's srhip_eval_loss_partials): sums[2t] = sum of (w *) l over the rows,
+// sums[2t+1] = sum of w (unweighted: the row count); sums[2T + 2f] = feature f column sum (Float64
+// data: sum of x * 2^-64), sums[2T + 2f + 1] = its non-finite count; sums[2T + 2F] = rows.  Every
+// entry combines across row shards by addition; chk[t] (the operator-output check statistic)
+// combines by max for Float32 (max |v|) and by addition for Float64 (sum of |v| 2^-512).
+static size_t sums_len(int32_t ntrees, int64_t nfeat) { return 2 * (size_t)ntrees + 2 * (size_t)nfeat + 1; }
+
+// Returns 0 ok, 1 fail, 2 undecided (needs the precise pass).
+static int decide(const srhip_program& P, int32_t t, int64_t nfeat, const double* sums, double chk) {
   const TreeInfo& I = P.info[t];
+  const int dtype = P.dtype;
   if (I.static_fail) return 1;
   if (dtype == SRHIP_I32) return 0;
+  const int32_t T = P.ntrees;
+  const long double m = (long double)sums[2 * (size_t)T + 2 * (size_t)nfeat];
   const long double ovf = ovf_threshold(dtype);
   for (double c : I.fill_consts)
-    if ((long double)fabs(c) * (long double)v.m >= ovf) return 1;
+    if ((long double)fabs(c) * m >= ovf) return 1;
   for (int f : I.feat_checks) {
-    const FeatStat& s = v.stats[f];
-    if (s.nonfinite > 0) return 1;
-    const long double sum = dtype == SRHIP_F64 ? ldexpl((long double)s.sum, 64) : (long double)s.sum;
-    if (fabsl(sum) >= ovf) return 1;
+    const double fsum = sums[2 * (size_t)T + 2 * (size_t)f], fbad = sums[2 * (size_t)T + 2 * (size_t)f + 1];
+    if (fbad > 0) return 1;
+    const long double sum = dtype == SRHIP_F64 ? ldexpl((long double)fsum, 64) : (long double)fsum;
+    if (!isfinite(fsum) || fabsl(sum) >= ovf) return 1;
   }
   if (I.op_sumcheck.empty()) return 0;
   if (!isfinite(chk)) return 1;  // a NaN / Inf operator output
   long double bound;
-  if (dtype == SRHIP_F64) bound = ldexpl((long double)chk, 512);     // sum |v|
-  else bound = (long double)chk * (long double)v.m;                   // m * max |v|
+  if (dtype == SRHIP_F64) bound = ldexpl((long double)chk, 512);  // sum |v|
+  else bound = (long double)chk * m;                              // m * max |v|
   if (bound * 2.0L >= ovf) return 2;
   return 0;
 }
 
+static void finalize(const srhip_program& P, int64_t nfeat, const double* sums, const double* chk, double* out_loss,
+                     uint8_t* out_ok, uint8_t* out_status) {
+  for (int32_t t = 0; t < P.ntrees; ++t) {
+    const int st = decide(P, t, nfeat, sums, chk ? chk[t] : 0.0);
+    if (out_status) out_status[t] = (uint8_t)st;
+    if (out_ok) out_ok[t] = st == 0 ? 1 : 0;
+    if (out_loss) out_loss[t] = st == 0 ? sums[2 * (size_t)t] / sums[2 * (size_t)t + 1] : INFINITY;
+  }
+}
+
+// opsums[u][k]: exact-ish (f64) sum over all rows of operator output k of tree trees[u]
+static void finalize_precise(const srhip_program& P, const int32_t* trees, int32_t nsel, const double* opsums,
+                             uint8_t* out_ok) {
+  const int stride = std::max(1, P.max_ops);
+  const long double ovf = ovf_threshold(P.dtype);
+  for (int u = 0; u < nsel; ++u) {
+    const TreeInfo& I = P.info[trees[u]];
+    int st = I.static_fail ? 1 : 0;
+    for (size_t k = 0; k < I.op_sumcheck.size() && !st; ++k) {
+      const double s = opsums[(size_t)u * stride + k];
+      if (!isfinite(s)) st = 1;
+      else if (I.op_sumcheck[k]) {
+        const long double S = P.dtype == SRHIP_F64 ? ldexpl((long double)s, 64) : (long double)s;
+        if (fabsl(S) >= ovf) st = 1;
+      }
+    }
+    out_ok[u] = st == 0 ? 1 : 0;
+  }
+}
+
 }  // namespace
 
-static int run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
-                    const int64_t* idx, int64_t nidx, double* out_loss, void* out_pred, uint8_t* out_ok) {
+static int check_eval_args(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode,
+                           const srhip_loss* loss) {
   if (!ctx || !ds || !P) return fail(SRHIP_ERR_INVALID, "null handle");
+  if (!P->ctx) return fail(SRHIP_ERR_INVALID, "host-only program (created without a context) cannot be evaluated");
   if (ds->dtype != P->dtype) return fail(SRHIP_ERR_INVALID, "dataset dtype %d != program dtype %d", ds->dtype, P->dtype);
   if (ds->ctx != ctx || P->ctx != ctx) return fail(SRHIP_ERR_INVALID, "handles belong to a different context");
-  // feature range check against this dataset
   for (const srhip_node& n : P->nodes)
     if (n.degree == 0 && !n.constant && n.feature > ds->nfeat)
       return fail(SRHIP_ERR_INVALID, "tree uses feature %d but dataset has %lld features", (int)n.feature, (long long)ds->nfeat);
-  const int dtype = P->dtype;
   if (mode == MODE_LOSS) {
     if (!loss) return fail(SRHIP_ERR_INVALID, "null loss");
-    if (dtype == SRHIP_I32 && loss->kind != SRHIP_LOSS_L2 && loss->kind != SRHIP_LOSS_L1)
+    if (P->dtype == SRHIP_I32 && loss->kind != SRHIP_LOSS_L2 && loss->kind != SRHIP_LOSS_L1)
       return fail(SRHIP_ERR_UNSUPPORTED, "Int32 datasets support L2/L1 losses only");
     if (loss->kind < SRHIP_LOSS_L2 || loss->kind > SRHIP_LOSS_QUANTILE)
       return fail(SRHIP_ERR_UNSUPPORTED, "loss kind %d", loss->kind);
   }
-  HIP_TRY(hipSetDevice(ctx->device));
-  View v;
-  int rc = make_view(ctx, ds, idx, nidx, mode == MODE_LOSS, v);
-  if (rc) return rc;
-  if (idx && ds->weighted && mode == MODE_LOSS) {
-    // sum of gathered weights from the device copy (deterministic host sum)
-    std::vector<unsigned char> wbuf((size_t)nidx * dtype_size(dtype));
-    HIP_TRY(hipMemcpy(wbuf.data(), ctx->vw.p, wbuf.size(), hipMemcpyDeviceToHost));
-    double s = 0.0;
-    for (int64_t i = 0; i < nidx; ++i)
-      s += dtype == SRHIP_F64 ? ((double*)wbuf.data())[i] : (double)((float*)wbuf.data())[i];
-    v.sum_w = s;
-  }
+  return SRHIP_OK;
+}
+
+// Device stage: one interpreter launch over the view + the per-tree reduction.  Fills the partials
+// (sums layout above; chk[T]) and, in MODE_PRED, out_pred.
+static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
+                         const View& v, void* out_pred, double* sums, double* chk) {
+  const int dtype = P->dtype;
   const int32_t nt = P->ntrees;
-  for (int32_t t = 0; t < nt; ++t) {
-    if (out_ok) out_ok[t] = 0;
-    if (out_loss) out_loss[t] = INFINITY;
-  }
-  if (nt == 0) return SRHIP_OK;
+  const int64_t nf = ds->nfeat;
   const bool weighted = ds->weighted && mode == MODE_LOSS;
+  for (size_t i = 0; i < sums_len(nt, nf); ++i) sums[i] = 0.0;
+  for (int32_t t = 0; t < nt; ++t) {
+    chk[t] = 0.0;
+    sums[2 * (size_t)t + 1] = weighted ? v.sum_w : (double)v.m;
+  }
+  for (int64_t f = 0; f < nf; ++f) {
+    sums[2 * (size_t)nt + 2 * f] = v.stats[f].sum;
+    sums[2 * (size_t)nt + 2 * f + 1] = (double)v.stats[f].nonfinite;
+  }
+  sums[2 * (size_t)nt + 2 * nf] = (double)v.m;
   std::vector<int32_t> live;
   live.reserve(nt);
   for (int32_t t = 0; t < nt; ++t)
     if (!P->info[t].static_fail) live.push_back(t);
-  std::vector<uint8_t> status(nt, 1);
-  std::vector<double> lsum(nt, 0.0), chk(nt, 0.0);
+  if (live.empty()) return SRHIP_OK;
   const size_t es = dtype_size(dtype);
-  LaunchPlan L = plan_launch(ctx, dtype, ds->nfeat, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size());
-  if (!live.empty()) {
-    const int nl = (int)live.size();
-    std::vector<int32_t> order = make_order(*P, live, L.groups, L.tpg);
-    // order buffer + slabs (indexed by tree id)
-    HIP_TRY(ctx->order_prec.ensure(order.size() * sizeof(int32_t)));
-    HIP_TRY(hipMemcpyAsync(ctx->order_prec.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                           ctx->stream));
-    HIP_TRY(ctx->slab_loss.ensure((size_t)nt * L.nrb * 8));
-    HIP_TRY(ctx->slab_chk.ensure((size_t)nt * L.nrb * 8));
-    HIP_TRY(ctx->red_loss.ensure((size_t)nt * 8));
-    HIP_TRY(ctx->red_chk.ensure((size_t)nt * 8));
-    HIP_TRY(ctx->h_loss.ensure((size_t)nt * 8));
-    HIP_TRY(ctx->h_chk.ensure((size_t)nt * 8));
-    EvalArgs a{};
-    a.code = (const Ins*)P->d_code.p;
-    a.prog_off = (const int32_t*)P->d_off.p;
-    a.order = (const int32_t*)ctx->order_prec.p;
-    a.X = v.X;
-    a.y = v.y;
-    a.w = weighted ? v.w : nullptr;
-    a.slab_loss = ctx->slab_loss.p;
-    a.slab_chk = ctx->slab_chk.p;
-    a.ld = v.ld;
-    a.nvalid = v.m;
-    a.ntrees = nl;
-    a.nfeat = (int32_t)ds->nfeat;
-    a.rb_rows = L.rb_rows;
-    a.nrb = L.nrb;
-    a.trees_per_group = L.tpg;
-    a.loss_kind = loss ? loss->kind : 0;
-    a.loss_p0 = loss ? loss->p0 : 0.0;
-    a.weighted = weighted ? 1 : 0;
-    a.has_y = mode == MODE_LOSS ? 1 : 0;
-    a.max_steps = P->max_len;
-    a.debug_stop = debug_stop();
-    if (trace_on()) {
-      HIP_TRY(ctx->h_dbg.ensure(64 * sizeof(int32_t), hipHostMallocCoherent));
-      memset(ctx->h_dbg.p, 0xff, 64 * sizeof(int32_t));
-      a.dbg = (int32_t*)ctx->h_dbg.p;
-    }
-    DevBuf pred;
-    if (mode == MODE_PRED) {
-      HIP_TRY(pred.ensure((size_t)nt * v.m * es));
-      a.out_pred = pred.p;
-    }
-    const int K = P->kmax <= 4 ? 4 : 8;
-    dim3 grid(L.nrb, L.groups);
-    HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
-    HIP_TRY(launch_eval(dtype, a, K, mode, L.xlds, grid, L.lds, ctx->stream));
-    HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
-    ctx->timed = true;
-    if (trace_on()) {  // poll the kernel's progress words for up to 10 s, then abort loudly
-      const volatile int32_t* d = (const volatile int32_t*)ctx->h_dbg.p;
-      int32_t last[16];
-      for (int i = 0; i < 16; ++i) last[i] = -2;
-      for (int it = 0; it < 10000; ++it) {
-        hipError_t q = hipStreamQuery(ctx->stream);
-        bool changed = false;
-        for (int i = 0; i < 16; ++i) changed |= d[i] != last[i];
-        if (changed) {
-          for (int i = 0; i < 16; ++i) last[i] = d[i];
-          fprintf(stderr, "[srhip] kernel progress: stage=%d tree=%d tile=%d step=%d pc=%d h=%d waves=%d,%d,%d,%d,%d,%d,%d,%d\n",
-                  last[0], last[1], last[2], last[3], last[4], last[5], last[8], last[9], last[10], last[11], last[12],
-                  last[13], last[14], last[15]);
-          fflush(stderr);
-        }
-        if (q == hipSuccess) break;
-        if (q != hipErrorNotReady) HIP_TRY(q);
-        usleep(1000);
-        if (it == 9999) {
-          fprintf(stderr, "[srhip] kernel did not finish in 10 s; aborting\n");
-          fflush(stderr);
-          abort();
-        }
+  LaunchPlan L = plan_launch(ctx, dtype, nf, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size());
+  const int nl = (int)live.size();
+  std::vector<int32_t> order = make_order(*P, live, L.groups, L.tpg);
+  HIP_TRY(ctx->order_prec.ensure(order.size() * sizeof(int32_t)));
+  HIP_TRY(hipMemcpyAsync(ctx->order_prec.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                         ctx->stream));
+  HIP_TRY(ctx->slab_loss.ensure((size_t)nt * L.nrb * 8));
+  HIP_TRY(ctx->slab_chk.ensure((size_t)nt * L.nrb * 8));
+  HIP_TRY(ctx->red_loss.ensure((size_t)nt * 8));
+  HIP_TRY(ctx->red_chk.ensure((size_t)nt * 8));
+  HIP_TRY(ctx->h_loss.ensure((size_t)nt * 8));
+  HIP_TRY(ctx->h_chk.ensure((size_t)nt * 8));
+  EvalArgs a{};
+  a.code = (const Ins*)P->d_code.p;
+  a.prog_off = (const int32_t*)P->d_off.p;
+  a.order = (const int32_t*)ctx->order_prec.p;
+  a.X = v.X;
+  a.y = v.y;
+  a.w = weighted ? v.w : nullptr;
+  a.slab_loss = ctx->slab_loss.p;
+  a.slab_chk = ctx->slab_chk.p;
+  a.ld = v.ld;
+  a.nvalid = v.m;
+  a.ntrees = nl;
+  a.nfeat = (int32_t)nf;
+  a.rb_rows = L.rb_rows;
+  a.nrb = L.nrb;
+  a.trees_per_group = L.tpg;
+  a.loss_kind = loss ? loss->kind : 0;
+  a.loss_p0 = loss ? loss->p0 : 0.0;
+  a.weighted = weighted ? 1 : 0;
+  a.has_y = mode == MODE_LOSS ? 1 : 0;
+  a.max_steps = P->max_len;
+  a.debug_stop = debug_stop();
+  if (trace_on()) {
+    HIP_TRY(ctx->h_dbg.ensure(64 * sizeof(int32_t), hipHostMallocCoherent));
+    memset(ctx->h_dbg.p, 0xff, 64 * sizeof(int32_t));
+    a.dbg = (int32_t*)ctx->h_dbg.p;
+  }
+  DevBuf pred;
+  if (mode == MODE_PRED) {
+    HIP_TRY(pred.ensure((size_t)nt * v.m * es));
+    a.out_pred = pred.p;
+  }
+  const int K = P->kmax <= 4 ? 4 : 8;
+  dim3 grid(L.nrb, L.groups);
+  HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+  HIP_TRY(launch_eval(dtype, a, K, mode, L.xlds, grid, L.lds, ctx->stream));
+  HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+  ctx->timed = true;
+  if (trace_on()) {  // poll the kernel's progress words for up to 10 s, then abort loudly
+    const volatile int32_t* d = (const volatile int32_t*)ctx->h_dbg.p;
+    int32_t last[16];
+    for (int i = 0; i < 16; ++i) last[i] = -2;
+    for (int it = 0; it < 10000; ++it) {
+      hipError_t q = hipStreamQuery(ctx->stream);
+      bool changed = false;
+      for (int i = 0; i < 16; ++i) changed |= d[i] != last[i];
+      if (changed) {
+        for (int i = 0; i < 16; ++i) last[i] = d[i];
+        fprintf(stderr, "[srhip] kernel progress: stage=%d tree=%d waves=%d,%d,%d,%d,%d,%d,%d,%d\n", last[0], last[1],
+                last[8], last[9], last[10], last[11], last[12], last[13], last[14], last[15]);
+        fflush(stderr);
+      }
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) HIP_TRY(q);
+      usleep(1000);
+      if (it == 9999) {
+        fprintf(stderr, "[srhip] kernel did not finish in 10 s; aborting\n");
+        fflush(stderr);
+        abort();
       }
     }
-    HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p,
-                          L.nrb, nt, mode == MODE_LOSS ? ctx->red_loss.p : nullptr,
-                          dtype == SRHIP_I32 ? nullptr : ctx->red_chk.p, ctx->stream));
+  }
+  HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p,
+                        L.nrb, nt, mode == MODE_LOSS ? ctx->red_loss.p : nullptr,
+                        dtype == SRHIP_I32 ? nullptr : ctx->red_chk.p, ctx->stream));
+  if (mode == MODE_LOSS)
+    HIP_TRY(hipMemcpyAsync(ctx->h_loss.p, ctx->red_loss.p, (size_t)nt * 8, hipMemcpyDeviceToHost, ctx->stream));
+  if (dtype != SRHIP_I32)
+    HIP_TRY(hipMemcpyAsync(ctx->h_chk.p, ctx->red_chk.p, (size_t)nt * 8, hipMemcpyDeviceToHost, ctx->stream));
+  if (mode == MODE_PRED)
+    HIP_TRY(hipMemcpyAsync(out_pred, pred.p, (size_t)nt * v.m * es, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  for (int32_t t : live) {
     if (mode == MODE_LOSS)
-      HIP_TRY(hipMemcpyAsync(ctx->h_loss.p, ctx->red_loss.p, (size_t)nt * 8, hipMemcpyDeviceToHost, ctx->stream));
-    if (dtype != SRHIP_I32)
-      HIP_TRY(hipMemcpyAsync(ctx->h_chk.p, ctx->red_chk.p, (size_t)nt * 8, hipMemcpyDeviceToHost, ctx->stream));
-    if (mode == MODE_PRED)
-      HIP_TRY(hipMemcpyAsync(out_pred, pred.p, (size_t)nt * v.m * es, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    for (int32_t t : live) {
-      if (mode == MODE_LOSS) {
-        if (dtype == SRHIP_I32) lsum[t] = (double)((long long*)ctx->h_loss.p)[t];
-        else lsum[t] = ((double*)ctx->h_loss.p)[t];
-      }
-      if (dtype == SRHIP_F32) chk[t] = ((float*)ctx->h_chk.p)[t];
-      else if (dtype == SRHIP_F64) chk[t] = ((double*)ctx->h_chk.p)[t];
-    }
+      sums[2 * (size_t)t] = dtype == SRHIP_I32 ? (double)((long long*)ctx->h_loss.p)[t] : ((double*)ctx->h_loss.p)[t];
+    if (dtype == SRHIP_F32) chk[t] = ((float*)ctx->h_chk.p)[t];
+    else if (dtype == SRHIP_F64) chk[t] = ((double*)ctx->h_chk.p)[t];
   }
-  // decisions
+  return SRHIP_OK;
+}
+
+// Precise stage: per-(tree, operator node) f64 sums over the view's rows for the selected trees;
+// opsums[u * max(1, max_ops) + k].
+static int eval_precise(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const View& v,
+                        const int32_t* trees, int32_t nu, double* opsums) {
+  const int dtype = P->dtype;
+  const int stride = std::max(1, P->max_ops);
+  for (size_t i = 0; i < (size_t)nu * stride; ++i) opsums[i] = 0.0;
+  if (nu == 0 || dtype == SRHIP_I32) return SRHIP_OK;
+  LaunchPlan Lp = plan_launch(ctx, dtype, ds->nfeat, false, false, v.m, nu);
+  Lp.groups = 1;
+  Lp.tpg = nu;
+  const size_t slab_bytes = (size_t)nu * stride * Lp.nrb * sizeof(double);
+  HIP_TRY(ctx->slab_prec.ensure(slab_bytes));
+  HIP_TRY(hipMemsetAsync(ctx->slab_prec.p, 0, slab_bytes, ctx->stream));
+  HIP_TRY(ctx->order_prec.ensure((size_t)nu * sizeof(int32_t)));
+  HIP_TRY(hipMemcpyAsync(ctx->order_prec.p, trees, (size_t)nu * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+  EvalArgs a{};
+  a.code = (const Ins*)P->d_code.p;
+  a.prog_off = (const int32_t*)P->d_off.p;
+  a.order = (const int32_t*)ctx->order_prec.p;
+  a.X = v.X;
+  a.ld = v.ld;
+  a.nvalid = v.m;
+  a.ntrees = nu;
+  a.nfeat = (int32_t)ds->nfeat;
+  a.rb_rows = Lp.rb_rows;
+  a.nrb = Lp.nrb;
+  a.trees_per_group = nu;
+  a.slab_prec = ctx->slab_prec.p;
+  a.prec_stride = stride;
+  a.max_steps = P->max_len;
+  HIP_TRY(launch_eval(dtype, a, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, 1), 16, ctx->stream));
+  HIP_TRY(ctx->h_prec.ensure(slab_bytes));
+  HIP_TRY(hipMemcpyAsync(ctx->h_prec.p, ctx->slab_prec.p, slab_bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  const double* hp = (const double*)ctx->h_prec.p;
+  for (int u = 0; u < nu; ++u)
+    for (int k = 0; k < stride; ++k) {
+      long double s = 0.0L;
+      for (int b = 0; b < Lp.nrb; ++b) s += hp[((size_t)u * stride + k) * Lp.nrb + b];
+      opsums[(size_t)u * stride + k] = (double)s;
+    }
+  return SRHIP_OK;
+}
+
+static int gathered_weight_sum(srhip_ctx* ctx, const srhip_dataset* ds, int64_t nidx, View& v) {
+  std::vector<unsigned char> wbuf((size_t)nidx * dtype_size(ds->dtype));
+  HIP_TRY(hipMemcpy(wbuf.data(), ctx->vw.p, wbuf.size(), hipMemcpyDeviceToHost));
+  double s = 0.0;
+  for (int64_t i = 0; i < nidx; ++i)
+    s += ds->dtype == SRHIP_F64 ? ((double*)wbuf.data())[i] : (double)((float*)wbuf.data())[i];
+  v.sum_w = s;
+  return SRHIP_OK;
+}
+
+// Single-device evaluation: partials -> decision -> precise pass for undecided trees.
+static int run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
+                    const int64_t* idx, int64_t nidx, double* out_loss, void* out_pred, uint8_t* out_ok) {
+  int rc = check_eval_args(ctx, ds, P, mode, loss);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(ctx->device));
+  View v;
+  rc = make_view(ctx, ds, idx, nidx, mode == MODE_LOSS, v);
+  if (rc) return rc;
+  if (idx && ds->weighted && mode == MODE_LOSS) {
+    rc = gathered_weight_sum(ctx, ds, nidx, v);
+    if (rc) return rc;
+  }
+  const int32_t nt = P->ntrees;
+  if (nt == 0) return SRHIP_OK;
+  std::vector<double> sums(sums_len(nt, ds->nfeat)), chk(nt);
+  rc = eval_partials(ctx, ds, P, mode, loss, v, out_pred, sums.data(), chk.data());
+  if (rc) return rc;
+  std::vector<uint8_t> status(nt), ok(nt);
+  std::vector<double> lossv(nt);
+  finalize(*P, ds->nfeat, sums.data(), chk.data(), lossv.data(), ok.data(), status.data());
   std::vector<int32_t> unc;
-  for (int32_t t = 0; t < nt; ++t) {
-    status[t] = (uint8_t)decide(*P, t, dtype, v, chk[t]);
+  for (int32_t t = 0; t < nt; ++t)
     if (status[t] == 2) unc.push_back(t);
-  }
-  // precise pass for undecided trees: exact per-operator-node sums over the evaluated rows
   if (!unc.empty()) {
-    const int nu = (int)unc.size();
     const int stride = std::max(1, P->max_ops);
-    LaunchPlan Lp = plan_launch(ctx, dtype, ds->nfeat, false, false, v.m, nu);
-    Lp.groups = 1;
-    Lp.tpg = nu;
-    const size_t slab_bytes = (size_t)nu * stride * Lp.nrb * sizeof(double);
-    HIP_TRY(ctx->slab_prec.ensure(slab_bytes));
-    HIP_TRY(hipMemsetAsync(ctx->slab_prec.p, 0, slab_bytes, ctx->stream));
-    HIP_TRY(ctx->order_prec.ensure((size_t)nu * sizeof(int32_t)));
-    HIP_TRY(hipMemcpyAsync(ctx->order_prec.p, unc.data(), (size_t)nu * sizeof(int32_t), hipMemcpyHostToDevice,
-                           ctx->stream));
-    EvalArgs a{};
-    a.code = (const Ins*)P->d_code.p;
-    a.prog_off = (const int32_t*)P->d_off.p;
-    a.order = (const int32_t*)ctx->order_prec.p;
-    a.X = v.X;
-    a.ld = v.ld;
-    a.nvalid = v.m;
-    a.ntrees = nu;
-    a.nfeat = (int32_t)ds->nfeat;
-    a.rb_rows = Lp.rb_rows;
-    a.nrb = Lp.nrb;
-    a.trees_per_group = nu;
-    a.slab_prec = ctx->slab_prec.p;
-    a.prec_stride = stride;
-    a.max_steps = P->max_len;
-    HIP_TRY(launch_eval(dtype, a, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, 1), 16, ctx->stream));
-    HIP_TRY(ctx->h_prec.ensure(slab_bytes));
-    HIP_TRY(hipMemcpyAsync(ctx->h_prec.p, ctx->slab_prec.p, slab_bytes, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    const double* hp = (const double*)ctx->h_prec.p;
-    const long double ovf = ovf_threshold(dtype);
-    for (int u = 0; u < nu; ++u) {
+    std::vector<double> opsums(unc.size() * stride);
+    rc = eval_precise(ctx, ds, P, v, unc.data(), (int32_t)unc.size(), opsums.data());
+    if (rc) return rc;
+    std::vector<uint8_t> uok(unc.size());
+    finalize_precise(*P, unc.data(), (int32_t)unc.size(), opsums.data(), uok.data());
+    for (size_t u = 0; u < unc.size(); ++u) {
       const int32_t t = unc[u];
-      const TreeInfo& I = P->info[t];
-      int st = 0;
-      for (size_t k = 0; k < I.op_sumcheck.size() && !st; ++k) {
-        long double s = 0.0L;
-        for (int b = 0; b < Lp.nrb; ++b) s += hp[((size_t)u * stride + k) * Lp.nrb + b];
-        if (!isfinite((double)s)) st = 1;
-        else if (I.op_sumcheck[k]) {
-          const long double S = dtype == SRHIP_F64 ? ldexpl(s, 64) : s;
-          if (fabsl(S) >= ovf) st = 1;
-        }
-      }
-      status[t] = (uint8_t)st;
+      ok[t] = uok[u];
+      lossv[t] = uok[u] ? sums[2 * (size_t)t] / sums[2 * (size_t)t + 1] : INFINITY;
     }
   }
   for (int32_t t = 0; t < nt; ++t) {
-    const bool ok = status[t] == 0;
-    if (out_ok) out_ok[t] = ok ? 1 : 0;
-    if (out_loss) {
-      if (!ok) out_loss[t] = INFINITY;
-      else if (weighted) out_loss[t] = lsum[t] / v.sum_w;
-      else out_loss[t] = lsum[t] / (double)v.m;
-    }
+    if (out_ok) out_ok[t] = ok[t];
+    if (out_loss) out_loss[t] = lossv[t];
   }
   return SRHIP_OK;
 }
@@ -1039,7 +1107,7 @@ void srhip_dataset_destroy(srhip_dataset* ds) {
 
 int srhip_program_create(srhip_ctx* ctx, int dtype, const srhip_node* nodes, const int64_t* offsets, int32_t ntrees,
                          const srhip_operators* ops, srhip_program** out) {
-  if (!ctx || !out || !ops || (!offsets && ntrees > 0)) return fail(SRHIP_ERR_INVALID, "null argument");
+  if (!out || !ops || (!offsets && ntrees > 0)) return fail(SRHIP_ERR_INVALID, "null argument");
   *out = nullptr;
   if (ntrees < 0) return fail(SRHIP_ERR_INVALID, "ntrees < 0");
   if (dtype != SRHIP_F32 && dtype != SRHIP_F64 && dtype != SRHIP_I32) return fail(SRHIP_ERR_UNSUPPORTED, "dtype %d", dtype);
@@ -1065,15 +1133,17 @@ int srhip_program_create(srhip_ctx* ctx, int dtype, const srhip_node* nodes, con
   }
   int rc = compile_program(*P);
   if (rc) return rc;
-  rc = upload_program(*P);
-  if (rc) return rc;
+  if (ctx) {  // ctx == NULL: host-only program (compile + did_succeed metadata, e.g. for finalize)
+    rc = upload_program(*P);
+    if (rc) return rc;
+  }
   *out = P.release();
   return SRHIP_OK;
 }
 
 void srhip_program_destroy(srhip_program* P) {
   if (!P) return;
-  (void)hipSetDevice(P->ctx->device);
+  if (P->ctx) (void)hipSetDevice(P->ctx->device);
   delete P;
 }
 
@@ -1099,7 +1169,7 @@ int srhip_program_set_constants(srhip_program* P, const double* consts) {
   for (int32_t t = 0; t < P->ntrees; ++t) set_consts_rec(P->nodes, P->offsets[t], 0, c);
   int rc = compile_program(*P);
   if (rc) return rc;
-  return upload_program(*P);
+  return P->ctx ? upload_program(*P) : SRHIP_OK;
 }
 
 int srhip_eval_loss(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* prog, const srhip_loss* loss,
@@ -1125,6 +1195,60 @@ int srhip_eval_loss_batch(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_n
   srhip_program_destroy(P);
   return rc;
 }
+
+int srhip_eval_loss_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const srhip_loss* loss,
+                             const int64_t* idx, int64_t nidx, double* sums, double* chk) {
+  if (!sums || !chk) return fail(SRHIP_ERR_INVALID, "null output");
+  int rc = check_eval_args(ctx, ds, P, MODE_LOSS, loss);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(ctx->device));
+  View v;
+  rc = make_view(ctx, ds, idx, nidx, true, v);
+  if (rc) return rc;
+  if (idx && ds->weighted) {
+    rc = gathered_weight_sum(ctx, ds, nidx, v);
+    if (rc) return rc;
+  }
+  return eval_partials(ctx, ds, P, MODE_LOSS, loss, v, nullptr, sums, chk);
+}
+
+int srhip_partials_finalize(const srhip_program* P, int64_t nfeatures, const double* sums, const double* chk,
+                            double* out_loss, uint8_t* out_ok, uint8_t* out_status) {
+  if (!P || !sums || (!chk && P->dtype != SRHIP_I32)) return fail(SRHIP_ERR_INVALID, "null argument");
+  if (nfeatures < 0) return fail(SRHIP_ERR_INVALID, "nfeatures < 0");
+  for (const TreeInfo& I : P->info)
+    for (int f : I.feat_checks)
+      if (f >= nfeatures) return fail(SRHIP_ERR_INVALID, "tree checks feature %d of %lld", f + 1, (long long)nfeatures);
+  finalize(*P, nfeatures, sums, chk, out_loss, out_ok, out_status);
+  return SRHIP_OK;
+}
+
+int srhip_eval_precise_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const int64_t* idx,
+                                int64_t nidx, const int32_t* trees, int32_t ntrees_sel, double* opsums) {
+  if (!opsums || (!trees && ntrees_sel > 0) || ntrees_sel < 0) return fail(SRHIP_ERR_INVALID, "null argument");
+  int rc = check_eval_args(ctx, ds, P, MODE_PRED, nullptr);
+  if (rc) return rc;
+  for (int32_t u = 0; u < ntrees_sel; ++u)
+    if (trees[u] < 0 || trees[u] >= P->ntrees) return fail(SRHIP_ERR_INVALID, "tree index %d out of range", trees[u]);
+  HIP_TRY(hipSetDevice(ctx->device));
+  View v;
+  rc = make_view(ctx, ds, idx, nidx, false, v);
+  if (rc) return rc;
+  return eval_precise(ctx, ds, P, v, trees, ntrees_sel, opsums);
+}
+
+int srhip_precise_finalize(const srhip_program* P, const int32_t* trees, int32_t ntrees_sel, const double* opsums,
+                           uint8_t* out_ok) {
+  if (!P || !opsums || !out_ok || (!trees && ntrees_sel > 0)) return fail(SRHIP_ERR_INVALID, "null argument");
+  for (int32_t u = 0; u < ntrees_sel; ++u)
+    if (trees[u] < 0 || trees[u] >= P->ntrees) return fail(SRHIP_ERR_INVALID, "tree index %d out of range", trees[u]);
+  finalize_precise(*P, trees, ntrees_sel, opsums, out_ok);
+  return SRHIP_OK;
+}
+
+int srhip_chk_reduce_op(int dtype) { return dtype == SRHIP_F32 ? 0 : 1; }
+
+int32_t srhip_program_max_ops(const srhip_program* P) { return P ? std::max(1, P->max_ops) : 0; }
 
 double srhip_last_kernel_ms(const srhip_ctx* ctx) {
   if (!ctx || !ctx->timed) return -1.0;

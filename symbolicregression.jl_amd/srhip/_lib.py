@@ -81,6 +81,12 @@ SIGNATURES = {
     "srhip_eval_predict": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     "srhip_eval_loss_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, ctypes.POINTER(Operators),
                                              ctypes.POINTER(Loss), _vp, _i64, _vp, _vp]),
+    "srhip_eval_loss_partials": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(Loss), _vp, _i64, _vp, _vp]),
+    "srhip_partials_finalize": (ctypes.c_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "srhip_eval_precise_partials": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp]),
+    "srhip_precise_finalize": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp]),
+    "srhip_chk_reduce_op": (ctypes.c_int, [ctypes.c_int]),
+    "srhip_program_max_ops": (_i32, [_vp]),
     "srhip_last_kernel_ms": (_dbl, [_vp]),
     "srhip_program_stats": (ctypes.c_int, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
                                            ctypes.POINTER(_i32)]),

@@ -102,9 +102,12 @@ class DeviceDataset:
 
 
 class Program:
-    """A compiled batch of trees (bytecode resident on the device)."""
+    """A compiled batch of trees (bytecode resident on the device).
 
-    def __init__(self, ctx: Context, nodes: np.ndarray, offsets: np.ndarray, options, dtype):
+    ctx=None makes a host-only program: compiled, with the did_succeed metadata that the
+    row-sharded finalize steps need, but not evaluable (no device is touched)."""
+
+    def __init__(self, ctx: Context | None, nodes: np.ndarray, offsets: np.ndarray, options, dtype):
         self.ctx = ctx
         self.nodes = np.ascontiguousarray(nodes)
         self.offsets = np.ascontiguousarray(offsets, dtype=np.int64)
@@ -113,7 +116,8 @@ class Program:
         self.dtype = np.dtype(dtype)
         h = ctypes.c_void_p()
         self._ops = options.c_operators()
-        check(_lib.load().srhip_program_create(ctx.handle, _lib.dtype_code(dtype), ptr(self.nodes),
+        check(_lib.load().srhip_program_create(None if ctx is None else ctx.handle, _lib.dtype_code(dtype),
+                                               ptr(self.nodes),
                                                ptr(self.offsets), self.ntrees, ctypes.byref(self._ops),
                                                ctypes.byref(h)))
         self.handle = h
@@ -149,6 +153,51 @@ class Program:
         check(_lib.load().srhip_eval_predict(self.ctx.handle, ds.handle, self.handle, ptr(idxa),
                                              0 if idxa is None else len(idxa), ptr(out), ptr(ok)))
         return out, ok.astype(bool)
+
+    # ---- row-sharded evaluation (include/srhip.h "row-sharded evaluation") ----------------------
+    def chk_reduce_op(self) -> str:
+        """How chk combines across shards: "max" (Float32) or "sum" (Float64 / Int32)."""
+        return "max" if _lib.load().srhip_chk_reduce_op(_lib.dtype_code(self.dtype)) == 0 else "sum"
+
+    def max_ops(self) -> int:
+        return int(_lib.load().srhip_program_max_ops(self.handle))
+
+    def eval_loss_partials(self, ds: DeviceDataset, loss, idx=None):
+        """This shard's (sums[2T + 2F + 1], chk[T]) — combine across shards, then finalize()."""
+        sums = np.empty(2 * self.ntrees + 2 * ds.nfeatures + 1, dtype=np.float64)
+        chk = np.empty(self.ntrees, dtype=np.float64)
+        ls = loss.c_struct()
+        idxa = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        check(_lib.load().srhip_eval_loss_partials(self.ctx.handle, ds.handle, self.handle, ctypes.byref(ls), ptr(idxa),
+                                                   0 if idxa is None else len(idxa), ptr(sums), ptr(chk)))
+        return sums, chk
+
+    def finalize(self, nfeatures: int, sums, chk):
+        """Decision from globally combined partials: (loss[T], ok[T], status[T]); status 2 = undecided."""
+        sums = np.ascontiguousarray(sums, dtype=np.float64)
+        chk = np.ascontiguousarray(chk, dtype=np.float64)
+        loss = np.empty(self.ntrees, dtype=np.float64)
+        ok = np.empty(self.ntrees, dtype=np.uint8)
+        st = np.empty(self.ntrees, dtype=np.uint8)
+        check(_lib.load().srhip_partials_finalize(self.handle, int(nfeatures), ptr(sums), ptr(chk), ptr(loss), ptr(ok),
+                                                  ptr(st)))
+        return loss, ok.astype(bool), st
+
+    def eval_precise_partials(self, ds: DeviceDataset, trees, idx=None):
+        trees = np.ascontiguousarray(trees, dtype=np.int32)
+        out = np.empty(len(trees) * self.max_ops(), dtype=np.float64)
+        idxa = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        check(_lib.load().srhip_eval_precise_partials(self.ctx.handle, ds.handle, self.handle, ptr(idxa),
+                                                      0 if idxa is None else len(idxa), ptr(trees), len(trees),
+                                                      ptr(out)))
+        return out
+
+    def precise_finalize(self, trees, opsums):
+        trees = np.ascontiguousarray(trees, dtype=np.int32)
+        opsums = np.ascontiguousarray(opsums, dtype=np.float64)
+        ok = np.empty(len(trees), dtype=np.uint8)
+        check(_lib.load().srhip_precise_finalize(self.handle, ptr(trees), len(trees), ptr(opsums), ptr(ok)))
+        return ok.astype(bool)
 
     def close(self):
         if self.handle:

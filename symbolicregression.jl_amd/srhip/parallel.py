@@ -1,0 +1,119 @@
+"""Multi-GPU layer: one process per GPU over torch.distributed (backend "nccl" = RCCL over xGMI
+on MI355X; "gloo" for the CPU tests).  SURVEY.md 8(e) names two partitions, both here:
+
+* islands (the default, as the reference partitions its populations over workers:
+  src/SymbolicRegression.jl:746-793, src/SearchUtils.jl:108-127): every rank holds a full
+  dataset replica and its own populations, so evaluation needs no collective at all.  The one
+  exchange is migration (src/Migration.jl:16-38 applied on the head node at
+  src/SymbolicRegression.jl:933-943): each rank's best members travel as node tables through
+  :func:`allgather_trees` (all-gather of a few KB; latency-bound on xGMI).
+* row shards (datasets too tall for one device): every rank evaluates every tree on its block
+  of rows; :func:`eval_loss_sharded` all-reduces the per-tree partials (sums by SUM, the check
+  statistic by MAX for Float32) and every rank takes the did_succeed decision identically
+  (include/srhip.h "row-sharded evaluation").  One fused all-reduce per population, plus one
+  more only when a tree's overflow check is undecided.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ._lib import NODE_DTYPE
+
+
+def _dist():
+    import torch.distributed as dist
+
+    return dist
+
+
+def world():
+    """(rank, world_size) of the default process group, (0, 1) when not initialised."""
+    try:
+        dist = _dist()
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank(), dist.get_world_size()
+    except ImportError:
+        pass
+    return 0, 1
+
+
+def shard_rows(n: int, rank: int, world_size: int):
+    """[lo, hi) of rank's contiguous block of n rows (sizes differ by at most one)."""
+    base, extra = divmod(n, world_size)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def _device(group=None):
+    import torch
+
+    dist = _dist()
+    backend = dist.get_backend(group)
+    if backend == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def allreduce_np(a: np.ndarray, op: str = "sum", group=None) -> np.ndarray:
+    """All-reduce of a float64 array in place semantics (returns the reduced copy)."""
+    import torch
+
+    dist = _dist()
+    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64).copy()).to(_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM, group=group)
+    return t.cpu().numpy()
+
+
+def eval_loss_sharded(prog, nfeatures: int, partials, precise=None, group=None):
+    """Row-sharded eval_loss for every tree of ``prog``.
+
+    partials(): this rank's (sums, chk) — ``prog.eval_loss_partials(shard, loss)`` on a GPU;
+    precise(trees): this rank's per-operator sums for undecided trees —
+    ``prog.eval_precise_partials(shard, trees)``.  Returns (loss[T], ok[T]) identical on all ranks.
+    """
+    sums, chk = partials()
+    sums = allreduce_np(sums, "sum", group)
+    chk = allreduce_np(chk, "max" if prog.chk_reduce_op() == "max" else "sum", group)
+    loss, ok, status = prog.finalize(nfeatures, sums, chk)
+    undecided = np.nonzero(status == 2)[0].astype(np.int32)
+    if len(undecided):
+        if precise is None:
+            raise RuntimeError("undecided overflow checks need the precise pass (pass precise=...)")
+        opsums = allreduce_np(precise(undecided), "sum", group)
+        uok = prog.precise_finalize(undecided, opsums)
+        ok[undecided] = uok
+        s, wsum = sums[2 * undecided], sums[2 * undecided + 1]
+        loss[undecided] = np.where(uok, s / wsum, np.inf)
+    return loss, ok
+
+
+def allgather_trees(nodes: np.ndarray, offsets: np.ndarray, group=None):
+    """Migration exchange: every rank's trees (srhip_node tables) -> list of (nodes, offsets) by rank."""
+    import torch
+
+    dist = _dist()
+    dev = _device(group)
+    ws = dist.get_world_size(group)
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    meta = torch.tensor([len(nodes), len(offsets)], dtype=torch.int64, device=dev)
+    metas = [torch.zeros_like(meta) for _ in range(ws)]
+    dist.all_gather(metas, meta, group=group)
+    metas = [m.cpu().numpy() for m in metas]
+    maxb = max(int(m[0]) for m in metas) * NODE_DTYPE.itemsize
+    maxo = max(int(m[1]) for m in metas)
+    buf = np.zeros(maxb + 8 * maxo, dtype=np.uint8)
+    raw = nodes.view(np.uint8)
+    buf[: len(raw)] = raw
+    buf[maxb: maxb + 8 * len(offsets)] = offsets.view(np.uint8)
+    t = torch.from_numpy(buf).to(dev)
+    outs = [torch.zeros_like(t) for _ in range(ws)]
+    dist.all_gather(outs, t, group=group)
+    result = []
+    for m, o in zip(metas, outs):
+        b = o.cpu().numpy()
+        nn, no = int(m[0]), int(m[1])
+        nd = b[: nn * NODE_DTYPE.itemsize].copy().view(NODE_DTYPE)
+        of = b[maxb: maxb + 8 * no].copy().view(np.int64)
+        result.append((nd, of))
+    return result

@@ -1,0 +1,125 @@
+"""The multi-GPU protocols of srhip.parallel on CPU (gloo, world_size 2).
+
+Row shards: each rank computes its shard's partials with the oracle (standing in for the device),
+the ranks all-reduce, and libsrhip's host-side finalize (a host-only program: no device touched)
+must reproduce the oracle's unsharded eval_loss (losses to 1e-12 relative, identical did_succeed).
+Islands: migration's all-gather of node tables returns every rank's trees intact.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OPS = dict(binary_operators=("+", "-", "*", "/"), unary_operators=("cos",))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _problem(dtype, n=1500, ntrees=48, seed=5):
+    import srhip
+
+    opts = srhip.Options(**OPS)
+    trees = srhip.random_population(ntrees, opts, 3, dtype, seed=seed, max_size=25)
+    nodes, offs = srhip.flatten(trees, opts, dtype)
+    rng = np.random.default_rng(seed + 1)
+    X = rng.standard_normal((3, n)).astype(dtype)
+    y = (np.cos(X[0]) * 2 + X[1] ** 2).astype(dtype)
+    w = rng.uniform(0.5, 2.0, n).astype(dtype)
+    return opts, nodes, offs, X, y, w
+
+
+def test_shard_rows_partition():
+    from srhip.parallel import shard_rows
+
+    for n in (0, 1, 7, 1000, 1001):
+        for ws in (1, 2, 3, 8):
+            blocks = [shard_rows(n, r, ws) for r in range(ws)]
+            assert blocks[0][0] == 0 and blocks[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(blocks, blocks[1:]))
+            sizes = [hi - lo for lo, hi in blocks]
+            assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_host_finalize_matches_oracle(oracle, dtype, weighted):
+    """Single process: oracle partials of the whole dataset -> libsrhip finalize == oracle eval_loss."""
+    import srhip
+
+    opts, nodes, offs, X, y, w = _problem(dtype)
+    w = w if weighted else None
+    prog = srhip.Program(None, nodes, offs, opts, dtype)
+    sums, chk = oracle.partials(nodes, offs, opts.binop_codes, opts.unaop_codes, X, y, w)
+    loss, ok, status = prog.finalize(X.shape[0], sums, chk)
+    assert not np.any(status == 2)
+    ol, _, ook, _ = oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, X, y, w, 0, 0.0)
+    assert np.array_equal(ok, ook)
+    np.testing.assert_allclose(loss[ook], ol[ook], rtol=1e-12)
+    assert np.all(np.isinf(loss[~ook]))
+
+
+def _rank_main(rank, world, port, dtype_name, q):
+    try:
+        sys.path[:0] = [os.path.join(ROOT, "symbolicregression.jl_amd"), os.path.join(ROOT, "oracle")]
+        import torch.distributed as dist
+
+        import oracle
+        import srhip
+        from srhip.parallel import allgather_trees, eval_loss_sharded, shard_rows
+
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        dtype = np.dtype(dtype_name).type
+        opts, nodes, offs, X, y, w = _problem(dtype)
+        lo, hi = shard_rows(X.shape[1], rank, world)
+        prog = srhip.Program(None, nodes, offs, opts, dtype)
+        part = lambda: oracle.partials(nodes, offs, opts.binop_codes, opts.unaop_codes,  # noqa: E731
+                                       X[:, lo:hi], y[lo:hi], w[lo:hi])
+        loss, ok = eval_loss_sharded(prog, X.shape[0], part)
+        # migration exchange: rank r contributes its own trees
+        mine = srhip.random_population(3 + rank, opts, 3, dtype, seed=100 + rank, max_size=12)
+        mn, mo = srhip.flatten(mine, opts, dtype)
+        got = allgather_trees(mn, mo)
+        q.put((rank, loss, ok, [(g[0].tobytes(), g[1]) for g in got]))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # surface the failure to the parent
+        q.put((rank, repr(e), None, None))
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_row_sharded_and_migration_gloo_world2(oracle, dtype):
+    import multiprocessing as mp
+
+    import srhip
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, np.dtype(dtype).name, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    res.sort(key=lambda r: r[0])
+    for r in res:
+        assert r[2] is not None, r[1]
+    opts, nodes, offs, X, y, w = _problem(dtype)
+    ol, _, ook, _ = oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, X, y, w, 0, 0.0)
+    for _, loss, ok, _ in res:
+        assert np.array_equal(ok, ook)
+        np.testing.assert_allclose(loss[ook], ol[ook], rtol=1e-12)
+    assert np.array_equal(res[0][1], res[1][1])  # identical decision on every rank
+    for rank in range(2):
+        mine = srhip.random_population(3 + rank, opts, 3, dtype, seed=100 + rank, max_size=12)
+        mn, mo = srhip.flatten(mine, opts, dtype)
+        for _, _, _, got in res:
+            assert got[rank][0] == mn.tobytes()
+            assert np.array_equal(got[rank][1], mo)

@@ -447,3 +447,38 @@ def test_reference_api_eval_loss_and_score(ctx):
                                              unary_operators=opts.unary_operators, parsimony=1.0))[0] > 1.0
     sr.update_baseline_loss(ds, opts)
     assert ds.use_baseline and ds.baseline_loss > 0
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_row_sharded_partials_match_single_device(ctx, oracle, dtype):
+    """Two row shards on one device, combined as srhip.parallel combines ranks (sum / max), equal the
+    unsharded evaluation; includes trees whose overflow check needs the precise pass."""
+    sr = _sr()
+    opts = sr.Options(binary_operators=("+", "-", "*", "/"), unary_operators=("cos", "exp"))
+    _, nodes, offs = _population(sr, opts, 96, 3, dtype, seed=77)
+    # near-overflow trees: exp(exp(x1)) * c and x1 * 1e37 (finite values whose sums may overflow)
+    x1 = sr.Node("x1")
+    big = 3e37 if dtype == np.float32 else 1e306
+    extra = [sr.exp(sr.exp(x1)) * sr.Node(val=1e30 if dtype == np.float32 else 1e300), x1 * sr.Node(val=big)]
+    en, eo = sr.flatten(extra, opts, dtype)
+    nodes = np.concatenate([nodes, en])
+    offs = np.concatenate([offs, eo[1:] + offs[-1]])
+    X, y, _ = _data(3, 5000, dtype, seed=3)
+    X[0, :] = np.abs(X[0, :]) + 1.0
+    prog = sr.Program(ctx, nodes, offs, opts, dtype)
+    full_l, full_ok = prog.eval_loss(_ds(ctx, X, y), sr.L2DistLoss())
+    parts = [prog.eval_loss_partials(_ds(ctx, X[:, a:b], y[a:b]), sr.L2DistLoss()) for a, b in ((0, 2100), (2100, 5000))]
+    sums = parts[0][0] + parts[1][0]
+    chk = np.maximum(parts[0][1], parts[1][1]) if prog.chk_reduce_op() == "max" else parts[0][1] + parts[1][1]
+    loss, ok, status = prog.finalize(3, sums, chk)
+    und = np.nonzero(status == 2)[0].astype(np.int32)
+    if len(und):
+        ops = sum(prog.eval_precise_partials(_ds(ctx, X[:, a:b], y[a:b]), und) for a, b in ((0, 2100), (2100, 5000)))
+        uok = prog.precise_finalize(und, ops)
+        ok[und] = uok
+        loss[und] = np.where(uok, sums[2 * und] / sums[2 * und + 1], np.inf)
+    assert np.array_equal(ok, full_ok)
+    ol, _, ook, _ = oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, X, y, None, 0, 0.0)
+    assert np.array_equal(ok, ook)
+    for t in np.nonzero(ok)[0]:
+        assert _rel(loss[t], full_l[t]) < 1e-12
