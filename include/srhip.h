@@ -150,6 +150,8 @@ int srhip_program_num_constants(const srhip_program* prog, int32_t* out_nconst /
 /* Replace constant leaves (depth-first, left-to-right = get_constants order), all trees:
  * consts holds sum(nconst) values, tree-major. Re-folds and re-uploads. */
 int srhip_program_set_constants(srhip_program* prog, const double* consts);
+/* Read the constants back (same layout), e.g. after srhip_optimize_constants. */
+int srhip_program_get_constants(const srhip_program* prog, double* consts);
 
 /* Fused evaluate + loss for every tree of prog on ds (rows = all, or idx[0..nidx) 0-based).
  * out_loss[t] = loss in double (L(Inf) = +Inf when !ok), out_ok[t] = did_succeed. */
@@ -194,6 +196,36 @@ int srhip_precise_finalize(const srhip_program* prog, const int32_t* trees, int3
                            const double* opsums, uint8_t* out_ok);
 int srhip_chk_reduce_op(int dtype);
 int32_t srhip_program_max_ops(const srhip_program* prog);
+
+/* ---- constant optimisation (src/ConstantOptimization.jl) ------------------------------------ */
+/* Loss and its exact gradient with respect to every tree's constants (forward-mode dual numbers
+ * on the device), for every tree of prog: out_loss[T] (+Inf where did_succeed fails),
+ * out_grad[sum nconst] in get_constants order per tree (srhip_program_num_constants), out_ok[T].
+ * Replaces the finite-difference gradient Optim derives from f(t) = eval_loss(t, dataset,
+ * options; regularization=false) (src/ConstantOptimization.jl:48-50); the counterpart of
+ * eval_grad_tree_array(tree, X, options; variable=false) (src/InterfaceDynamicExpressions.jl:118-124)
+ * reduced through the loss. */
+int srhip_eval_loss_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* prog,
+                         const srhip_loss* loss, const int64_t* idx, int64_t nidx,
+                         double* out_loss, double* out_grad, uint8_t* out_ok);
+
+typedef struct srhip_optim_options {
+  int32_t iterations;  /* BFGS iterations per start (Optim.Options(iterations=8), src/Options.jl:693) */
+  int32_t nrestarts;   /* perturbed restarts c * (1 + randn/2) (optimizer_nrestarts=2, src/Options.jl:432) */
+  uint64_t seed;       /* RNG seed of the restart perturbations */
+  double g_tol;        /* gradient infinity-norm tolerance (Optim default 1e-8; <= 0 -> 1e-8) */
+} srhip_optim_options;
+
+/* optimize_constants for every tree of prog at once (src/ConstantOptimization.jl:11-81): BFGS +
+ * BackTracking line search from the current constants and nrestarts perturbed starts; a tree's
+ * constants are replaced (in prog) only where the best minimum beats its baseline loss.
+ * out_loss[T]: the loss of the returned trees (eval_loss, regularization=false); out_improved[T];
+ * out_fcalls[T] (nullable): objective evaluations per tree (num_evals bookkeeping).  Trees whose
+ * constants need no optimisation (none, or a static did_succeed failure) are left unchanged. */
+int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* prog,
+                             const srhip_loss* loss, const int64_t* idx, int64_t nidx,
+                             const srhip_optim_options* opt, double* out_loss,
+                             uint8_t* out_improved, int64_t* out_fcalls);
 
 /* ---- measurement hooks (bench / profiling) --------------------------------------------- */
 /* Device time (ms) of the last srhip_eval_loss/predict's main evaluation kernel, measured with

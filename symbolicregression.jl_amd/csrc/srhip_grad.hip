@@ -1,0 +1,377 @@
+// srhip_grad.hip — batched forward-mode (dual-number) constant gradients for the constant optimizer.
+//
+// Replaces (reference): the objective of _optimize_constants (src/ConstantOptimization.jl:43-81),
+// f(c) = eval_loss(tree(c), dataset, options; regularization=false), whose gradient Optim obtains
+// by finite differences (no g! is passed, :50).  Here one launch returns, for every tree, the loss
+// and its exact gradient with respect to the tree's constants (get_constants order,
+// test/test_derivatives.jl:123-147), by carrying KT tangent components per value through the
+// same bytecode interpreter as the evaluator (the "gradient program": constants not folded, each
+// constant leaf tagged with its index).  A "chunk" is (tree, first constant c0): trees with more
+// than KT constants take several chunks.  One lane owns one row (R = 1); values and tangents
+// live in VGPRs.  Operator values are computed by the same functions as srhip_eval.hip, so the
+// loss equals srhip_eval_loss's.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "srhip_grad.h"
+#include "srhip_isa.h"
+#include "srhip_kernels.h"
+#include "srhip_ops.h"
+
+#define UNR _Pragma("unroll")
+#define DI __device__ __attribute__((always_inline)) inline
+
+namespace srhip {
+
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(4))) Ins GIns;  // bytecode through the scalar cache
+#else
+typedef const Ins GIns;
+#endif
+
+template <typename T> struct V2 { typedef T type __attribute__((ext_vector_type(2))); };
+template <typename T> struct V4 { typedef T type __attribute__((ext_vector_type(4))); };
+
+// ---- operator values and partial derivatives ------------------------------------------------
+template <int U> constexpr bool dun_inline() {
+  return U == UN_NEG || U == UN_SQUARE || U == UN_CUBE || U == UN_ABS || U == UN_RELU || U == UN_SIGN ||
+         U == UN_ROUND || U == UN_FLOOR || U == UN_CEIL;
+}
+
+// f(x) and f'(x) for a heavy unary operator U (one out-of-line body per (T, U))
+template <typename T, int U> __device__ __attribute__((noinline)) typename V2<T>::type dual_un_heavy(T x) {
+  using O = FOps<T>;
+  T f = T(0), df = T(0);
+  switch (U) {
+    case UN_COS: f = O::cos(x); df = -O::sin(x); break;
+    case UN_SIN: f = O::sin(x); df = O::cos(x); break;
+    case UN_TAN: f = O::tan(x); df = T(1) + f * f; break;
+    case UN_EXP: f = O::exp(x); df = f; break;
+    case UN_LOG: f = O::log(x); df = T(1) / x; break;
+    case UN_LOG2: f = O::log2(x); df = T(1) / (x * T(0.69314718055994530942)); break;
+    case UN_LOG10: f = O::log10(x); df = T(1) / (x * T(2.30258509299404568402)); break;
+    case UN_LOG1P: f = O::log1p(x); df = T(1) / (T(1) + x); break;
+    case UN_SQRT: f = O::sqrt(x); df = T(0.5) / f; break;
+    case UN_ACOSH: f = O::acosh(x); df = T(1) / m_sqrt(x * x - T(1)); break;
+    case UN_ATANH_CLIP: {
+      f = O::atanh_clip(x);
+      const T u = O::mod(x + T(1), T(2)) - T(1);
+      df = T(1) / (T(1) - u * u);
+      break;
+    }
+    case UN_SINH: f = O::sinh(x); df = O::cosh(x); break;
+    case UN_COSH: f = O::cosh(x); df = O::sinh(x); break;
+    case UN_TANH: f = O::tanh(x); df = T(1) - f * f; break;
+    case UN_ASIN: f = O::asin(x); df = T(1) / m_sqrt(T(1) - x * x); break;
+    case UN_ACOS: f = O::acos(x); df = -T(1) / m_sqrt(T(1) - x * x); break;
+    case UN_ATAN: f = O::atan(x); df = T(1) / (T(1) + x * x); break;
+    case UN_ASINH: f = O::asinh(x); df = T(1) / m_sqrt(x * x + T(1)); break;
+    case UN_ERF: f = O::erf(x); df = T(1.12837916709551257390) * O::exp(-x * x); break;
+    case UN_ERFC: f = O::erfc(x); df = -T(1.12837916709551257390) * O::exp(-x * x); break;
+    case UN_GAMMA: f = O::gamma(x); df = FP<T>::nan(); break;  // no digamma: no gradient (optimizer keeps c)
+    case UN_EXP2: f = O::exp2(x); df = f * T(0.69314718055994530942); break;
+    case UN_EXPM1: f = O::expm1(x); df = f + T(1); break;
+    case UN_CBRT: f = O::cbrt(x); df = T(1) / (T(3) * f * f); break;
+    default: f = FP<T>::nan(); df = FP<T>::nan(); break;
+  }
+  typename V2<T>::type r;
+  r[0] = f;
+  r[1] = df;
+  return r;
+}
+
+template <typename T, int U> DI void dual_un(T x, T& f, T& df) {
+  using O = FOps<T>;
+  if constexpr (dun_inline<U>()) {
+    switch (U) {
+      case UN_NEG: f = O::neg(x); df = T(-1); break;
+      case UN_SQUARE: f = O::square(x); df = T(2) * x; break;
+      case UN_CUBE: f = O::cube(x); df = T(3) * x * x; break;
+      case UN_ABS: f = O::abs(x); df = x > T(0) ? T(1) : (x < T(0) ? T(-1) : T(0)); break;
+      case UN_RELU: f = O::relu(x); df = x > T(0) ? T(1) : T(0); break;
+      case UN_SIGN: f = O::sign(x); df = T(0); break;
+      case UN_ROUND: f = O::round(x); df = T(0); break;
+      case UN_FLOOR: f = O::floor(x); df = T(0); break;
+      case UN_CEIL: f = O::ceil(x); df = T(0); break;
+      default: break;
+    }
+  } else {
+    const typename V2<T>::type r = dual_un_heavy<T, U>(x);
+    f = r[0];
+    df = r[1];
+  }
+}
+
+// f(a, b), df/da, df/db for a specialised (cheap) binary operator SB
+template <typename T, int SB> DI void dual_spec(T a, T b, T& f, T& fa, T& fb) {
+  using O = FOps<T>;
+  switch (SB) {
+    case SB_ADD: f = O::add(a, b); fa = T(1); fb = T(1); break;
+    case SB_SUB: f = O::sub(a, b); fa = T(1); fb = T(-1); break;
+    case SB_MUL: f = O::mul(a, b); fa = b; fb = a; break;
+    case SB_DIV: { f = O::div(a, b); const T ib = T(1) / b; fa = ib; fb = -f * ib; break; }
+    case SB_GREATER: f = O::greater(a, b); fa = T(0); fb = T(0); break;
+    case SB_COND: f = O::cond(a, b); fa = T(0); fb = a > T(0) ? T(1) : T(0); break;
+    case SB_LOGICAL_OR: f = O::logical_or(a, b); fa = T(0); fb = T(0); break;
+    case SB_LOGICAL_AND: f = O::logical_and(a, b); fa = T(0); fb = T(0); break;
+    case SB_MAX: f = O::max(a, b); fa = a > b ? T(1) : T(0); fb = a > b ? T(0) : T(1); break;
+    case SB_MIN: f = O::min(a, b); fa = a < b ? T(1) : T(0); fb = a < b ? T(0) : T(1); break;
+    default: f = FP<T>::nan(); fa = f; fb = f; break;
+  }
+}
+
+// heavy binary (pow, mod, atan2): out of line; returns (f, df/da, df/db, -)
+template <typename T, int HB> __device__ __attribute__((noinline)) typename V4<T>::type dual_heavy(T a, T b) {
+  using O = FOps<T>;
+  T f, fa, fb;
+  switch (HB) {
+    case HB_POW:
+      f = O::pow(a, b);
+      fa = b * O::pow(a, b - T(1));
+      fb = a > T(0) ? f * m_log(a) : T(0);
+      break;
+    case HB_MOD: f = O::mod(a, b); fa = T(1); fb = -m_floor(a / b); break;
+    case HB_ATAN2: { f = O::atan2(a, b); const T r = T(1) / (a * a + b * b); fa = b * r; fb = -a * r; break; }
+    default: f = FP<T>::nan(); fa = f; fb = f; break;
+  }
+  typename V4<T>::type r;
+  r[0] = f;
+  r[1] = fa;
+  r[2] = fb;
+  r[3] = T(0);
+  return r;
+}
+
+// d loss / d prediction for the distance losses of srhip_ops.h loss_elem (diff = pred - y)
+template <typename T> DI T dloss_elem(int kind, T d, T p0) {
+  const T sg = d > T(0) ? T(1) : (d < T(0) ? T(-1) : T(0));
+  switch (kind) {
+    case SRHIP_LOSS_L2: return T(2) * d;
+    case SRHIP_LOSS_L1: return sg;
+    case SRHIP_LOSS_LP: return p0 * m_pow(m_abs(d), p0 - T(1)) * sg;
+    case SRHIP_LOSS_HUBER: return m_abs(d) <= p0 ? d : p0 * sg;
+    case SRHIP_LOSS_L1_EPS_INS: return m_abs(d) > p0 ? sg : T(0);
+    case SRHIP_LOSS_L2_EPS_INS: return T(2) * m_max(T(0), m_abs(d) - p0) * sg;
+    case SRHIP_LOSS_LOGIT_DIST: { const T e = m_exp(d); return (e - T(1)) / (e + T(1)); }
+    case SRHIP_LOSS_PERIODIC: {
+      const T k = T(2) * T(3.14159265358979323846) / p0;
+      return k * m_sin(d * k);
+    }
+    case SRHIP_LOSS_QUANTILE: return p0 - (d < T(0) ? T(1) : T(0));
+    default: return FP<T>::nan();
+  }
+}
+
+// ---- the dual-number interpreter ----------------------------------------------------------------
+template <typename T> DI T imm_bits(uint64_t b) {
+  if constexpr (sizeof(T) == 8) return __builtin_bit_cast(T, b);
+  else return __builtin_bit_cast(T, (uint32_t)b);
+}
+
+template <typename T, int KT> struct Dual {
+  T v;
+  T d[KT];
+};
+
+template <typename T, int KT> DI void set_const(Dual<T, KT>& a, T c, int rel) {  // rel = cidx - c0
+  a.v = c;
+  UNR for (int j = 0; j < KT; ++j) a.d[j] = (rel == j) ? T(1) : T(0);
+}
+template <typename T, int KT> DI void set_feat(Dual<T, KT>& a, T x) {
+  a.v = x;
+  UNR for (int j = 0; j < KT; ++j) a.d[j] = T(0);
+}
+// out = f(l, r) with partials: out.d = fl * l.d + fr * r.d (out may alias l or r)
+template <typename T, int KT>
+DI void combine(Dual<T, KT>& out, const Dual<T, KT>& l, const Dual<T, KT>& r, T f, T fl, T fr) {
+  T d[KT];
+  UNR for (int j = 0; j < KT; ++j) d[j] = fl * l.d[j] + fr * r.d[j];
+  out.v = f;
+  UNR for (int j = 0; j < KT; ++j) out.d[j] = d[j];
+}
+
+// check statistic, as in the evaluator: max |v| (Float32, NaN-propagating) / sum |v| 2^-512 (Float64)
+DI void chk_fold(float& M, float v) { M = __builtin_elementwise_maximum(M, __builtin_fabsf(v)); }
+DI void chk_fold(double& M, double v) { M = __builtin_fma(__builtin_fabs(v), 0x1p-512, M); }
+
+template <typename T, int KT, int K>
+__global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
+  const int lane = threadIdx.x & 63;
+  const int rb = blockIdx.x;
+  const int64_t row_base = (int64_t)rb * p.rb_rows;
+  const int ntiles = p.rb_rows / 64;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int group_base = blockIdx.y * p.chunks_per_group;
+  const int group_n = min(p.chunks_per_group, p.nchunks - group_base);
+  const T* X = reinterpret_cast<const T*>(p.X);
+  const T* Y = reinterpret_cast<const T*>(p.y);
+  const T* W = reinterpret_cast<const T*>(p.w);
+  GIns* code = (GIns*)(uintptr_t)p.code;
+  const T p0 = (T)p.loss_p0;
+  const int max_steps = __builtin_amdgcn_readfirstlane(p.max_steps);
+  for (int ci = wave; ci < group_n; ci += GRAD_WAVES) {
+    const int chunk = group_base + ci;
+    const int tree = __builtin_amdgcn_readfirstlane(p.chunks[2 * chunk]);
+    const int c0 = __builtin_amdgcn_readfirstlane(p.chunks[2 * chunk + 1]);
+    const int pc0 = __builtin_amdgcn_readfirstlane(p.prog_off[tree]);
+    double lacc = 0.0;
+    double gacc[KT];
+    UNR for (int j = 0; j < KT; ++j) gacc[j] = 0.0;
+    T M = T(0);
+    for (int tile = 0; tile < ntiles; ++tile) {
+      const int64_t row0 = row_base + (int64_t)tile * 64;
+      if (row0 >= p.nvalid) break;
+      const int64_t row = row0 + lane;  // rows up to ld are finite replicas; masked at the loss
+      Dual<T, KT> A, B, S[K];
+      set_feat(A, T(0));
+      set_feat(B, T(0));
+      UNR for (int k = 0; k < K; ++k) set_feat(S[k], T(0));
+      GIns* prog = code + pc0;
+      Ins nxt = prog[0];
+      for (int step = 0; step < max_steps; ++step) {
+        const Ins ins = nxt;
+        nxt = prog[step + 1];
+        if (ins.h == H_END) break;
+        const int opnd = (int)(ins.a & 0xffff);
+        const T imm = imm_bits<T>(ins.imm);
+        switch (ins.h) {
+          case H_LOADF: set_feat(A, X[(int64_t)opnd * p.ld + row]); break;
+          case H_LOADC: set_const(A, imm, opnd - c0); break;
+          case H_FETCHF: set_feat(B, X[(int64_t)opnd * p.ld + row]); break;
+          case H_FETCHC: set_const(B, imm, opnd - c0); break;
+#define GK_CASES(BASE, ...)                                                                        \
+  case BASE + 0: if constexpr (0 < K) { constexpr int k = 0; __VA_ARGS__ } break;                \
+  case BASE + 1: if constexpr (1 < K) { constexpr int k = 1; __VA_ARGS__ } break;                \
+  case BASE + 2: if constexpr (2 < K) { constexpr int k = 2; __VA_ARGS__ } break;                \
+  case BASE + 3: if constexpr (3 < K) { constexpr int k = 3; __VA_ARGS__ } break;                \
+  case BASE + 4: if constexpr (4 < K) { constexpr int k = 4; __VA_ARGS__ } break;                \
+  case BASE + 5: if constexpr (5 < K) { constexpr int k = 5; __VA_ARGS__ } break;                \
+  case BASE + 6: if constexpr (6 < K) { constexpr int k = 6; __VA_ARGS__ } break;                \
+  case BASE + 7: if constexpr (7 < K) { constexpr int k = 7; __VA_ARGS__ } break;
+          GK_CASES(H_PUSH0, { S[k] = A; })
+          GK_CASES(H_FETCHS0, { B = S[k]; })
+#define GK_SPEC(NAME, FN)                                                                          \
+  case h_spec(SB_##NAME, SPEC_AF): {                                                               \
+    Dual<T, KT> o; set_feat(o, X[(int64_t)opnd * p.ld + row]);                                     \
+    T f, fl, fr; dual_spec<T, SB_##NAME>(A.v, o.v, f, fl, fr); combine(A, A, o, f, fl, fr);        \
+    chk_fold(M, A.v); break; }                                                                     \
+  case h_spec(SB_##NAME, SPEC_FA): {                                                               \
+    Dual<T, KT> o; set_feat(o, X[(int64_t)opnd * p.ld + row]);                                     \
+    T f, fl, fr; dual_spec<T, SB_##NAME>(o.v, A.v, f, fl, fr); combine(A, o, A, f, fl, fr);        \
+    chk_fold(M, A.v); break; }                                                                     \
+  case h_spec(SB_##NAME, SPEC_AC): {                                                               \
+    Dual<T, KT> o; set_const(o, imm, opnd - c0);                                                   \
+    T f, fl, fr; dual_spec<T, SB_##NAME>(A.v, o.v, f, fl, fr); combine(A, A, o, f, fl, fr);        \
+    chk_fold(M, A.v); break; }                                                                     \
+  case h_spec(SB_##NAME, SPEC_CA): {                                                               \
+    Dual<T, KT> o; set_const(o, imm, opnd - c0);                                                   \
+    T f, fl, fr; dual_spec<T, SB_##NAME>(o.v, A.v, f, fl, fr); combine(A, o, A, f, fl, fr);        \
+    chk_fold(M, A.v); break; }                                                                     \
+  GK_CASES(h_spec(SB_##NAME, SPEC_SA0), {                                                          \
+    T f, fl, fr; dual_spec<T, SB_##NAME>(S[k].v, A.v, f, fl, fr); combine(A, S[k], A, f, fl, fr);  \
+    chk_fold(M, A.v); })                                                                           \
+  GK_CASES(h_spec(SB_##NAME, SPEC_AS0), {                                                          \
+    T f, fl, fr; dual_spec<T, SB_##NAME>(A.v, S[k].v, f, fl, fr); combine(A, A, S[k], f, fl, fr);  \
+    chk_fold(M, A.v); })
+          SRHIP_SPEC_BINOPS(GK_SPEC)
+#undef GK_SPEC
+#define GK_HEAVY(NAME, FN)                                                                         \
+  case h_heavy(HB_##NAME, false): {                                                                \
+    const typename V4<T>::type r = dual_heavy<T, HB_##NAME>(A.v, B.v);                             \
+    combine(A, A, B, r[0], r[1], r[2]); chk_fold(M, A.v); break; }                                 \
+  case h_heavy(HB_##NAME, true): {                                                                 \
+    const typename V4<T>::type r = dual_heavy<T, HB_##NAME>(B.v, A.v);                             \
+    combine(A, B, A, r[0], r[1], r[2]); chk_fold(M, A.v); break; }
+          SRHIP_HEAVY_BINOPS(GK_HEAVY)
+#undef GK_HEAVY
+#define GK_UN(NAME, FN)                                                                            \
+  case h_un(UN_##NAME): {                                                                          \
+    T f, df; dual_un<T, UN_##NAME>(A.v, f, df);                                                    \
+    A.v = f;                                                                                       \
+    UNR for (int j = 0; j < KT; ++j) A.d[j] = df * A.d[j];                                         \
+    chk_fold(M, A.v); break; }
+          SRHIP_UNOPS(GK_UN)
+#undef GK_UN
+#undef GK_CASES
+          default: break;
+        }
+      }
+      if (row < p.nvalid) {
+        const T d = A.v - Y[row];
+        T l = loss_elem<T>(p.loss_kind, d, p0);
+        T dl = dloss_elem<T>(p.loss_kind, d, p0);
+        if (p.weighted) {
+          const T w = W[row];
+          l = w * l;
+          dl = w * dl;
+        }
+        lacc += (double)l;
+        UNR for (int j = 0; j < KT; ++j) gacc[j] += (double)(dl * A.d[j]);
+      }
+    }
+    // wave reductions, one slab entry per (chunk, row block)
+    UNR for (int o = 32; o > 0; o >>= 1) {
+      lacc += __shfl_xor(lacc, o);
+      UNR for (int j = 0; j < KT; ++j) gacc[j] += __shfl_xor(gacc[j], o);
+      if constexpr (sizeof(T) == 4) M = __builtin_elementwise_maximum(M, __shfl_xor(M, o));
+      else M += __shfl_xor(M, o);
+    }
+    if (lane == 0) {
+      double* out = p.slab + ((int64_t)chunk * p.nrb + rb) * (KT + 2);
+      out[0] = lacc;
+      UNR for (int j = 0; j < KT; ++j) out[1 + j] = gacc[j];
+      out[KT + 1] = (double)M;
+    }
+  }
+}
+
+// per-chunk fixed-order reduction over row blocks: one wave per chunk
+template <int KT, bool CHK_MAX>
+__global__ __launch_bounds__(256) void grad_reduce_kernel(const double* __restrict__ slab, int nrb, int nchunks,
+                                                          double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (chunk >= nchunks) return;
+  for (int e = 0; e < KT + 2; ++e) {
+    const bool is_max = CHK_MAX && e == KT + 1;
+    double s = 0.0;
+    for (int b = lane; b < nrb; b += 64) {
+      const double v = slab[((int64_t)chunk * nrb + b) * (KT + 2) + e];
+      s = is_max ? __builtin_elementwise_maximum(s, v) : s + v;
+    }
+    UNR for (int o = 32; o > 0; o >>= 1) {
+      const double t = __shfl_xor(s, o);
+      s = is_max ? __builtin_elementwise_maximum(s, t) : s + t;
+    }
+    if (lane == 0) out[(int64_t)chunk * (KT + 2) + e] = s;
+  }
+}
+
+template <typename T, int KT, int K>
+static hipError_t launch_grad_t(const GradArgs& a, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((grad_kernel<T, KT, K>), grid, dim3(64 * GRAD_WAVES), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_grad(int dtype, int K, const GradArgs& a, dim3 grid, hipStream_t s) {
+  switch (dtype) {
+    case SRHIP_F32:
+      return K <= 4 ? launch_grad_t<float, GRAD_KT, 4>(a, grid, s) : launch_grad_t<float, GRAD_KT, 8>(a, grid, s);
+    case SRHIP_F64:
+      return K <= 4 ? launch_grad_t<double, GRAD_KT, 4>(a, grid, s) : launch_grad_t<double, GRAD_KT, 8>(a, grid, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_grad_reduce(int dtype, const double* slab, int nrb, int nchunks, double* out, hipStream_t s) {
+  dim3 grid((nchunks + 3) / 4), block(256);
+  if (dtype == SRHIP_F32)
+    hipLaunchKernelGGL((grad_reduce_kernel<GRAD_KT, true>), grid, block, 0, s, slab, nrb, nchunks, out);
+  else
+    hipLaunchKernelGGL((grad_reduce_kernel<GRAD_KT, false>), grid, block, 0, s, slab, nrb, nchunks, out);
+  return hipGetLastError();
+}
+
+}  // namespace srhip

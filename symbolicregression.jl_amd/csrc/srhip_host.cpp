@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "../../include/srhip.h"
+#include "srhip_internal.h"
 #include "srhip_isa.h"
 #include "srhip_kernels.h"
 #include "srhip_ops.h"
@@ -39,7 +40,7 @@ using namespace srhip;
 // ---------------------------------------------------------------------------------------------
 static thread_local std::string g_err;
 
-static int fail(int code, const char* fmt, ...) {
+int srhip::fail(int code, const char* fmt, ...) {
   char buf[1024];
   va_list ap;
   va_start(ap, fmt);
@@ -48,117 +49,7 @@ static int fail(int code, const char* fmt, ...) {
   g_err = buf;
   return code;
 }
-
-// SRHIP_TRACE=1 in the environment prints every HIP call of the library (before and after) to
-// stderr, flushed: a GPU hang then names the call it happened in.
-static bool trace_on() {
-  static const int on = [] { const char* e = getenv("SRHIP_TRACE"); return e && *e && *e != '0'; }();
-  return on != 0;
-}
-static int debug_stop() {
-  static const int v = [] { const char* e = getenv("SRHIP_DEBUG_STOP"); return e ? atoi(e) : 0; }();
-  return v;
-}
-#define HIP_TRY(expr)                                                                             \
-  do {                                                                                            \
-    if (trace_on()) { fprintf(stderr, "[srhip] %s:%d %s\n", __FILE__, __LINE__, #expr); fflush(stderr); } \
-    hipError_t e_ = (expr);                                                                       \
-    if (trace_on()) { fprintf(stderr, "[srhip]   -> %d\n", (int)e_); fflush(stderr); }          \
-    if (e_ != hipSuccess) return fail(SRHIP_ERR_DEVICE, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
-  } while (0)
-
-static size_t dtype_size(int dtype) { return dtype == SRHIP_F64 ? 8 : 4; }
-
-// overflow thresholds of an exact sum rounded to T: 2^128 - 2^103 and 2^1024 - 2^970
-static long double ovf_threshold(int dtype) {
-  return dtype == SRHIP_F64 ? (ldexpl(1.0L, 1024) - ldexpl(1.0L, 970)) : (ldexpl(1.0L, 128) - ldexpl(1.0L, 103));
-}
-
-// ---------------------------------------------------------------------------------------------
-// device buffers
-// ---------------------------------------------------------------------------------------------
-struct DevBuf {
-  void* p = nullptr;
-  size_t bytes = 0;
-  ~DevBuf() { release(); }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    bytes = 0;
-  }
-  hipError_t ensure(size_t n) {
-    if (n <= bytes && p) return hipSuccess;
-    release();
-    size_t want = n < 256 ? 256 : n;
-    hipError_t e = hipMalloc(&p, want);
-    if (e == hipSuccess) bytes = want;
-    return e;
-  }
-};
-struct HostBuf {  // pinned staging
-  void* p = nullptr;
-  size_t bytes = 0;
-  ~HostBuf() { release(); }
-  void release() {
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    bytes = 0;
-  }
-  hipError_t ensure(size_t n, unsigned flags = hipHostMallocDefault) {
-    if (n <= bytes && p) return hipSuccess;
-    release();
-    size_t want = n < 256 ? 256 : n;
-    hipError_t e = hipHostMalloc(&p, want, flags);
-    if (e == hipSuccess) bytes = want;
-    return e;
-  }
-};
-
-struct srhip_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool timed = false;
-  int num_cu = 256;
-  DevBuf slab_loss, slab_chk, red_loss, red_chk, slab_prec, order_prec;
-  DevBuf vX, vy, vw, vidx, vstats;  // gathered views (batching idx)
-  HostBuf h_loss, h_chk, h_stats, h_prec, h_dbg;
-};
-
-struct srhip_dataset {
-  srhip_ctx* ctx = nullptr;
-  int dtype = SRHIP_F32;
-  int64_t nfeat = 0, n = 0, ld = 0;
-  bool has_y = false, weighted = false;
-  double sum_w = 0.0;
-  DevBuf X, y, w, stats;
-  std::vector<FeatStat> hstats;  // feature stats over all n rows
-};
-
-struct TreeInfo {
-  bool static_fail = false;
-  std::vector<double> fill_consts;  // |c| * m >= OVF  => fail
-  std::vector<int> feat_checks;     // column checks (0-based features)
-  std::vector<uint8_t> op_sumcheck; // per emitted operator node: 1 = isfinite(sum) check, 0 = elementwise only
-  int32_t nconst = 0, nnodes = 0, nops = 0, need = 0;
-  int32_t code_begin = 0, code_len = 0;
-  double cost = 0.0;
-};
-
-struct srhip_program {
-  srhip_ctx* ctx = nullptr;
-  int dtype = SRHIP_F32;
-  int32_t ntrees = 0;
-  std::vector<srhip_node> nodes;
-  std::vector<int64_t> offsets;
-  std::vector<int32_t> binops, unaops;
-  std::vector<TreeInfo> info;
-  std::vector<Ins> code;
-  std::vector<int32_t> prog_off;
-  int32_t kmax = 0, max_ops = 0, max_len = 0;
-  int64_t total_nodes = 0, total_ops = 0;
-  DevBuf d_code, d_off;
-};
+const char* srhip::last_error() { return g_err.c_str(); }
 
 // ---------------------------------------------------------------------------------------------
 // tree compiler
@@ -204,8 +95,11 @@ static double op_cost(uint32_t h) {
 
 template <typename T> class TreeCompiler {
  public:
-  TreeCompiler(const srhip_node* nodes, int64_t nn, const srhip_program& prog, int nfeat_hint)
-      : nd_(nodes), nn_(nn), prog_(prog), nfeat_hint_(nfeat_hint) {}
+  // grad = true: the constant-gradient program: constant subtrees are NOT folded (their
+  // constants need tangents) and every constant leaf carries its get_constants index (0-based,
+  // depth-first left-to-right) in the instruction's operand field.
+  TreeCompiler(const srhip_node* nodes, int64_t nn, const srhip_program& prog, int nfeat_hint, bool grad = false)
+      : nd_(nodes), nn_(nn), prog_(prog), nfeat_hint_(nfeat_hint), grad_(grad) {}
 
   // returns SRHIP_OK or an error (g_err set); fills info and appends to code
   int compile(TreeInfo& info, std::vector<Ins>& code) {
@@ -217,6 +111,9 @@ template <typename T> class TreeCompiler {
     if (rc) return rc;
     info.nnodes = count_nodes(0);
     info.nconst = count_constants(0);
+    cidx_.assign(nn_, -1);
+    int32_t nc = 0;
+    number_constants(0, nc);
     // host-decided checks (reference semantics, see header comment)
     static_checks(0, -1, info);
     info.code_begin = (int32_t)code.size();
@@ -243,6 +140,8 @@ template <typename T> class TreeCompiler {
   int64_t nn_;
   const srhip_program& prog_;
   int nfeat_hint_;
+  bool grad_;
+  std::vector<int32_t> cidx_;
   std::vector<int8_t> memo_const_;
   std::vector<uint8_t> state_;
   std::vector<Ins>* code_ = nullptr;
@@ -307,7 +206,18 @@ template <typename T> class TreeCompiler {
     return c;
   }
   bool is_leaf(int64_t i) const { return nd_[i].degree == 0; }
-  bool leafish(int64_t i) { return is_leaf(i) || is_const(i); }
+  bool leafish(int64_t i) { return is_leaf(i) || (!grad_ && is_const(i)); }
+  void number_constants(int64_t i, int32_t& k) {
+    const srhip_node& n = nd_[i];
+    if (n.degree == 0) {
+      if (n.constant) cidx_[i] = k++;
+      return;
+    }
+    number_constants(n.l, k);
+    if (n.degree == 2) number_constants(n.r, k);
+  }
+  // operand field of an instruction that consumes constant leaf i (gradient program only)
+  uint32_t cop(int64_t i) const { return grad_ && cidx_[i] >= 0 ? (uint32_t)cidx_[i] : 0u; }
   int binop(int64_t i) const { return prog_.binops[nd_[i].op - 1]; }
   int unaop(int64_t i) const { return prog_.unaops[nd_[i].op - 1]; }
 
@@ -450,7 +360,7 @@ template <typename T> class TreeCompiler {
 
   void emit_leaf(int64_t i) {
     if (leaf_is_feature(i)) push_ins(H_LOADF, nd_[i].feature - 1, 0);
-    else push_ins(H_LOADC, 0, leaf_imm(i));
+    else push_ins(H_LOADC, cop(i), leaf_imm(i));
   }
 
   void emit(int64_t i, int base, int64_t parent) {
@@ -472,11 +382,11 @@ template <typename T> class TreeCompiler {
       if (rl) {
         emit(L, base, i);
         if (leaf_is_feature(Rr)) push_op(h_spec(sb, SPEC_AF), nd_[Rr].feature - 1, 0, i, parent);
-        else push_op(h_spec(sb, SPEC_AC), 0, leaf_imm(Rr), i, parent);
+        else push_op(h_spec(sb, SPEC_AC), cop(Rr), leaf_imm(Rr), i, parent);
       } else if (ll) {
         emit(Rr, base, i);
         if (leaf_is_feature(L)) push_op(h_spec(sb, SPEC_FA), nd_[L].feature - 1, 0, i, parent);
-        else push_op(h_spec(sb, SPEC_CA), 0, leaf_imm(L), i, parent);
+        else push_op(h_spec(sb, SPEC_CA), cop(L), leaf_imm(L), i, parent);
       } else if (need(L) >= need(Rr)) {
         emit(L, base, i);
         push_ins(H_PUSH0 + base, 0, 0);
@@ -494,12 +404,12 @@ template <typename T> class TreeCompiler {
     if (rl) {
       emit(L, base, i);
       if (leaf_is_feature(Rr)) push_ins(H_FETCHF, nd_[Rr].feature - 1, 0);
-      else push_ins(H_FETCHC, 0, leaf_imm(Rr));
+      else push_ins(H_FETCHC, cop(Rr), leaf_imm(Rr));
       push_op(h_heavy(hb, false), 0, 0, i, parent);  // A = A op B
     } else if (ll) {
       emit(Rr, base, i);
       if (leaf_is_feature(L)) push_ins(H_FETCHF, nd_[L].feature - 1, 0);
-      else push_ins(H_FETCHC, 0, leaf_imm(L));
+      else push_ins(H_FETCHC, cop(L), leaf_imm(L));
       push_op(h_heavy(hb, true), 0, 0, i, parent);   // A = B op A
     } else if (need(L) >= need(Rr)) {
       emit(L, base, i);
@@ -544,7 +454,52 @@ int compile_program_t(srhip_program& P) {
   return SRHIP_OK;
 }
 
-int compile_program(srhip_program& P) {
+template <typename T>
+int compile_grad_t(srhip_program& P) {
+  P.gcode.clear();
+  P.gprog_off.assign(P.ntrees, 0);
+  P.ginfo.assign(P.ntrees, TreeInfo());
+  P.gkmax = 0;
+  P.gmax_len = 0;
+  for (int32_t t = 0; t < P.ntrees; ++t) {
+    const int64_t b = P.offsets[t], e = P.offsets[t + 1];
+    TreeCompiler<T> tc(P.nodes.data() + b, e - b, P, 0, true);
+    TreeInfo& gi = P.ginfo[t];
+    int rc = tc.compile(gi, P.gcode);
+    if (rc) return fail(rc, "tree %d (gradient program): %s", (int)t, g_err.c_str());
+    P.gprog_off[t] = gi.code_begin;
+    P.gkmax = std::max(P.gkmax, gi.need);
+    P.gmax_len = std::max(P.gmax_len, gi.code_len);
+  }
+  return SRHIP_OK;
+}
+
+}  // namespace
+
+int srhip::compile_grad_program(srhip_program& P) {
+  if (P.grad_ready) return SRHIP_OK;
+  int rc;
+  switch (P.dtype) {
+    case SRHIP_F32: rc = compile_grad_t<float>(P); break;
+    case SRHIP_F64: rc = compile_grad_t<double>(P); break;
+    default: return fail(SRHIP_ERR_UNSUPPORTED, "constant gradients need a Float32 or Float64 program");
+  }
+  if (rc) return rc;
+  if (!P.ctx) return fail(SRHIP_ERR_INVALID, "host-only program");
+  HIP_TRY(hipSetDevice(P.ctx->device));
+  HIP_TRY(P.d_gcode.ensure(P.gcode.size() * sizeof(Ins)));
+  HIP_TRY(P.d_goff.ensure(std::max<size_t>(1, P.gprog_off.size()) * sizeof(int32_t)));
+  HIP_TRY(hipMemcpyAsync(P.d_gcode.p, P.gcode.data(), P.gcode.size() * sizeof(Ins), hipMemcpyHostToDevice, P.ctx->stream));
+  if (!P.gprog_off.empty())
+    HIP_TRY(hipMemcpyAsync(P.d_goff.p, P.gprog_off.data(), P.gprog_off.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                           P.ctx->stream));
+  HIP_TRY(hipStreamSynchronize(P.ctx->stream));
+  P.grad_ready = true;
+  return SRHIP_OK;
+}
+
+int srhip::compile_program(srhip_program& P) {
+  P.grad_ready = false;
   switch (P.dtype) {
     case SRHIP_F32: return compile_program_t<float>(P);
     case SRHIP_F64: return compile_program_t<double>(P);
@@ -553,7 +508,7 @@ int compile_program(srhip_program& P) {
   }
 }
 
-int upload_program(srhip_program& P) {
+int srhip::upload_program(srhip_program& P) {
   HIP_TRY(hipSetDevice(P.ctx->device));
   HIP_TRY(P.d_code.ensure(P.code.size() * sizeof(Ins)));
   HIP_TRY(P.d_off.ensure(std::max<size_t>(1, P.prog_off.size()) * sizeof(int32_t)));
@@ -565,23 +520,15 @@ int upload_program(srhip_program& P) {
   return SRHIP_OK;
 }
 
-}  // namespace
 
 // ---------------------------------------------------------------------------------------------
 // evaluation driver
 // ---------------------------------------------------------------------------------------------
 namespace {
 
-struct View {
-  const void* X;
-  const void* y;
-  const void* w;
-  int64_t ld, m;
-  const FeatStat* stats;  // host
-  double sum_w;
-};
+}  // namespace
 
-int make_view(srhip_ctx* ctx, const srhip_dataset* ds, const int64_t* idx, int64_t nidx, bool need_y, View& v) {
+int srhip::make_view(srhip_ctx* ctx, const srhip_dataset* ds, const int64_t* idx, int64_t nidx, bool need_y, View& v) {
   if (need_y && !ds->has_y) return fail(SRHIP_ERR_INVALID, "dataset has no y");
   if (!idx) {
     v.X = ds->X.p;
@@ -628,19 +575,11 @@ int make_view(srhip_ctx* ctx, const srhip_dataset* ds, const int64_t* idx, int64
   return SRHIP_OK;
 }
 
-struct LaunchPlan {
-  int rb_rows, nrb, groups, tpg;
-  bool xlds;
-  size_t lds;
-};
-
-LaunchPlan plan_launch(const srhip_ctx* ctx, int dtype, int64_t nfeat, bool weighted, bool with_y, int64_t m,
-                       int32_t ntrees) {
+LaunchPlan srhip::plan_launch(const srhip_ctx* ctx, int dtype, int64_t nfeat, bool weighted, bool with_y, int64_t m,
+                              int32_t ntrees, int tile) {
   LaunchPlan L;
   ntrees = std::max<int32_t>(1, ntrees);  // every tree may have failed statically
   m = std::max<int64_t>(1, m);
-  const int R = rows_per_lane(dtype);
-  const int tile = 64 * R;
   const size_t es = dtype_size(dtype);
   const int ncols = (int)nfeat + (with_y ? 1 : 0) + (weighted ? 1 : 0);
   const size_t budget = 64 * 1024 - 64;
@@ -661,6 +600,8 @@ LaunchPlan plan_launch(const srhip_ctx* ctx, int dtype, int64_t nfeat, bool weig
   L.groups = (ntrees + L.tpg - 1) / L.tpg;
   return L;
 }
+
+namespace {
 
 // trees sorted by estimated cost (desc), dealt round-robin to groups; returns order [ntrees]
 std::vector<int32_t> make_order(const srhip_program& P, const std::vector<int32_t>& trees, int groups, int tpg) {
@@ -688,12 +629,9 @@ std::vector<int32_t> make_order(const srhip_program& P, const std::vector<int32_
 static size_t sums_len(int32_t ntrees, int64_t nfeat) { return 2 * (size_t)ntrees + 2 * (size_t)nfeat + 1; }
 
 // Returns 0 ok, 1 fail, 2 undecided (needs the precise pass).
-static int decide(const srhip_program& P, int32_t t, int64_t nfeat, const double* sums, double chk) {
-  const TreeInfo& I = P.info[t];
-  const int dtype = P.dtype;
+static int decide_info(const TreeInfo& I, int dtype, int32_t T, int64_t nfeat, const double* sums, double chk) {
   if (I.static_fail) return 1;
   if (dtype == SRHIP_I32) return 0;
-  const int32_t T = P.ntrees;
   const long double m = (long double)sums[2 * (size_t)T + 2 * (size_t)nfeat];
   const long double ovf = ovf_threshold(dtype);
   for (double c : I.fill_consts)
@@ -716,7 +654,7 @@ static int decide(const srhip_program& P, int32_t t, int64_t nfeat, const double
 static void finalize(const srhip_program& P, int64_t nfeat, const double* sums, const double* chk, double* out_loss,
                      uint8_t* out_ok, uint8_t* out_status) {
   for (int32_t t = 0; t < P.ntrees; ++t) {
-    const int st = decide(P, t, nfeat, sums, chk ? chk[t] : 0.0);
+    const int st = decide_info(P.info[t], P.dtype, P.ntrees, nfeat, sums, chk ? chk[t] : 0.0);
     if (out_status) out_status[t] = (uint8_t)st;
     if (out_ok) out_ok[t] = st == 0 ? 1 : 0;
     if (out_loss) out_loss[t] = st == 0 ? sums[2 * (size_t)t] / sums[2 * (size_t)t + 1] : INFINITY;
@@ -745,7 +683,11 @@ static void finalize_precise(const srhip_program& P, const int32_t* trees, int32
 
 }  // namespace
 
-static int check_eval_args(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode,
+int srhip::decide_tree(const TreeInfo& I, const srhip_program& P, int64_t nfeat, const double* sums, double chk) {
+  return decide_info(I, P.dtype, P.ntrees, nfeat, sums, chk);
+}
+
+int srhip::check_eval_args(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode,
                            const srhip_loss* loss) {
   if (!ctx || !ds || !P) return fail(SRHIP_ERR_INVALID, "null handle");
   if (!P->ctx) return fail(SRHIP_ERR_INVALID, "host-only program (created without a context) cannot be evaluated");
@@ -788,7 +730,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     if (!P->info[t].static_fail) live.push_back(t);
   if (live.empty()) return SRHIP_OK;
   const size_t es = dtype_size(dtype);
-  LaunchPlan L = plan_launch(ctx, dtype, nf, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size());
+  LaunchPlan L = plan_launch(ctx, dtype, nf, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * rows_per_lane(dtype));
   const int nl = (int)live.size();
   std::vector<int32_t> order = make_order(*P, live, L.groups, L.tpg);
   HIP_TRY(ctx->order_prec.ensure(order.size() * sizeof(int32_t)));
@@ -889,7 +831,7 @@ static int eval_precise(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pro
   const int stride = std::max(1, P->max_ops);
   for (size_t i = 0; i < (size_t)nu * stride; ++i) opsums[i] = 0.0;
   if (nu == 0 || dtype == SRHIP_I32) return SRHIP_OK;
-  LaunchPlan Lp = plan_launch(ctx, dtype, ds->nfeat, false, false, v.m, nu);
+  LaunchPlan Lp = plan_launch(ctx, dtype, ds->nfeat, false, false, v.m, nu, 64 * rows_per_lane(dtype));
   Lp.groups = 1;
   Lp.tpg = nu;
   const size_t slab_bytes = (size_t)nu * stride * Lp.nrb * sizeof(double);
@@ -926,7 +868,7 @@ static int eval_precise(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pro
   return SRHIP_OK;
 }
 
-static int gathered_weight_sum(srhip_ctx* ctx, const srhip_dataset* ds, int64_t nidx, View& v) {
+int srhip::gathered_weight_sum(srhip_ctx* ctx, const srhip_dataset* ds, int64_t nidx, View& v) {
   std::vector<unsigned char> wbuf((size_t)nidx * dtype_size(ds->dtype));
   HIP_TRY(hipMemcpy(wbuf.data(), ctx->vw.p, wbuf.size(), hipMemcpyDeviceToHost));
   double s = 0.0;
@@ -937,7 +879,7 @@ static int gathered_weight_sum(srhip_ctx* ctx, const srhip_dataset* ds, int64_t 
 }
 
 // Single-device evaluation: partials -> decision -> precise pass for undecided trees.
-static int run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
+int srhip::run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
                     const int64_t* idx, int64_t nidx, double* out_loss, void* out_pred, uint8_t* out_ok) {
   int rc = check_eval_args(ctx, ds, P, mode, loss);
   if (rc) return rc;
@@ -992,7 +934,7 @@ static void pack_column(const void* src, int64_t f, int64_t n, int64_t sf, int64
 // ---------------------------------------------------------------------------------------------
 extern "C" {
 
-const char* srhip_last_error(void) { return g_err.c_str(); }
+const char* srhip_last_error(void) { return srhip::last_error(); }
 const char* srhip_version(void) { return "srhip 0.1.0 gfx950"; }
 
 int srhip_device_count(void) {
@@ -1161,6 +1103,23 @@ static void set_consts_rec(std::vector<srhip_node>& nodes, int64_t base, int64_t
   }
   set_consts_rec(nodes, base, n.l, c);
   if (n.degree == 2) set_consts_rec(nodes, base, n.r, c);
+}
+
+static void get_consts_rec(const std::vector<srhip_node>& nodes, int64_t base, int64_t i, double*& c) {
+  const srhip_node& n = nodes[base + i];
+  if (n.degree == 0) {
+    if (n.constant) *c++ = n.val;
+    return;
+  }
+  get_consts_rec(nodes, base, n.l, c);
+  if (n.degree == 2) get_consts_rec(nodes, base, n.r, c);
+}
+
+int srhip_program_get_constants(const srhip_program* P, double* consts) {
+  if (!P || (!consts && P->ntrees > 0)) return fail(SRHIP_ERR_INVALID, "null argument");
+  double* c = consts;
+  for (int32_t t = 0; t < P->ntrees; ++t) get_consts_rec(P->nodes, P->offsets[t], 0, c);
+  return SRHIP_OK;
 }
 
 int srhip_program_set_constants(srhip_program* P, const double* consts) {

@@ -1,0 +1,184 @@
+// srhip_internal.h — library-internal declarations shared by the translation units of libsrhip.so
+// (srhip_host.cpp: compiler, datasets, evaluation driver, C ABI; srhip_optim.cpp: constant
+// gradients and the batched BFGS constant optimizer).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/srhip.h"
+#include "srhip_isa.h"
+#include "srhip_kernels.h"
+
+namespace srhip {
+
+// ---------------------------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------------------------
+// sets the thread-local message returned by srhip_last_error(); returns code
+int fail(int code, const char* fmt, ...);
+const char* last_error();
+
+// SRHIP_TRACE=1 in the environment prints every HIP call of the library (before and after) to
+// stderr, flushed: a GPU hang then names the call it happened in.
+inline bool trace_on() {
+  static const int on = [] { const char* e = getenv("SRHIP_TRACE"); return e && *e && *e != '0'; }();
+  return on != 0;
+}
+inline int debug_stop() {
+  static const int v = [] { const char* e = getenv("SRHIP_DEBUG_STOP"); return e ? atoi(e) : 0; }();
+  return v;
+}
+#define HIP_TRY(expr)                                                                             \
+  do {                                                                                            \
+    if (trace_on()) { fprintf(stderr, "[srhip] %s:%d %s\n", __FILE__, __LINE__, #expr); fflush(stderr); } \
+    hipError_t e_ = (expr);                                                                       \
+    if (trace_on()) { fprintf(stderr, "[srhip]   -> %d\n", (int)e_); fflush(stderr); }          \
+    if (e_ != hipSuccess) return fail(SRHIP_ERR_DEVICE, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+  } while (0)
+
+inline size_t dtype_size(int dtype) { return dtype == SRHIP_F64 ? 8 : 4; }
+
+// overflow thresholds of an exact sum rounded to T: 2^128 - 2^103 and 2^1024 - 2^970
+inline long double ovf_threshold(int dtype) {
+  return dtype == SRHIP_F64 ? (ldexpl(1.0L, 1024) - ldexpl(1.0L, 970)) : (ldexpl(1.0L, 128) - ldexpl(1.0L, 103));
+}
+
+// ---------------------------------------------------------------------------------------------
+// device buffers
+// ---------------------------------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  hipError_t ensure(size_t n) {
+    if (n <= bytes && p) return hipSuccess;
+    release();
+    size_t want = n < 256 ? 256 : n;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) bytes = want;
+    return e;
+  }
+};
+struct HostBuf {  // pinned staging
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~HostBuf() { release(); }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  hipError_t ensure(size_t n, unsigned flags = hipHostMallocDefault) {
+    if (n <= bytes && p) return hipSuccess;
+    release();
+    size_t want = n < 256 ? 256 : n;
+    hipError_t e = hipHostMalloc(&p, want, flags);
+    if (e == hipSuccess) bytes = want;
+    return e;
+  }
+};
+
+struct TreeInfo {
+  bool static_fail = false;
+  std::vector<double> fill_consts;  // |c| * m >= OVF  => fail
+  std::vector<int> feat_checks;     // column checks (0-based features)
+  std::vector<uint8_t> op_sumcheck; // per emitted operator node: 1 = isfinite(sum) check, 0 = elementwise only
+  int32_t nconst = 0, nnodes = 0, nops = 0, need = 0;
+  int32_t code_begin = 0, code_len = 0;
+  double cost = 0.0;
+};
+
+
+
+}  // namespace srhip
+
+// the opaque handles of include/srhip.h (global namespace, as declared there)
+struct srhip_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  int num_cu = 256;
+  srhip::DevBuf slab_loss, slab_chk, red_loss, red_chk, slab_prec, order_prec;
+  srhip::DevBuf vX, vy, vw, vidx, vstats;  // gathered views (batching idx)
+  srhip::DevBuf g_chunks, g_slab, g_red;   // constant-gradient launches
+  srhip::HostBuf h_loss, h_chk, h_stats, h_prec, h_dbg;
+};
+
+struct srhip_dataset {
+  srhip_ctx* ctx = nullptr;
+  int dtype = SRHIP_F32;
+  int64_t nfeat = 0, n = 0, ld = 0;
+  bool has_y = false, weighted = false;
+  double sum_w = 0.0;
+  srhip::DevBuf X, y, w, stats;
+  std::vector<srhip::FeatStat> hstats;  // feature stats over all n rows
+};
+
+struct srhip_program {
+  srhip_ctx* ctx = nullptr;
+  int dtype = SRHIP_F32;
+  int32_t ntrees = 0;
+  std::vector<srhip_node> nodes;
+  std::vector<int64_t> offsets;
+  std::vector<int32_t> binops, unaops;
+  std::vector<srhip::TreeInfo> info;
+  std::vector<srhip::Ins> code;
+  std::vector<int32_t> prog_off;
+  int32_t kmax = 0, max_ops = 0, max_len = 0;
+  int64_t total_nodes = 0, total_ops = 0;
+  srhip::DevBuf d_code, d_off;
+  // gradient program (constants not folded, constant leaves carry their get_constants index);
+  // compiled on first use by the constant-gradient path
+  bool grad_ready = false;
+  std::vector<srhip::Ins> gcode;
+  std::vector<int32_t> gprog_off;
+  std::vector<srhip::TreeInfo> ginfo;  // did_succeed metadata for the gradient program's constants
+  int32_t gkmax = 0, gmax_len = 0;
+  srhip::DevBuf d_gcode, d_goff;
+};
+
+namespace srhip {
+
+// ---- evaluation views and launch planning (srhip_host.cpp) ----------------------------------
+struct View {
+  const void* X;
+  const void* y;
+  const void* w;
+  int64_t ld, m;
+  const FeatStat* stats;  // host
+  double sum_w;
+};
+struct LaunchPlan {
+  int rb_rows, nrb, groups, tpg;
+  bool xlds;
+  size_t lds;
+};
+int compile_program(srhip_program& P);       // eval program (+ invalidates the gradient program)
+int compile_grad_program(srhip_program& P);  // gradient program, uploaded
+int upload_program(srhip_program& P);
+int make_view(srhip_ctx* ctx, const srhip_dataset* ds, const int64_t* idx, int64_t nidx, bool need_y, View& v);
+int gathered_weight_sum(srhip_ctx* ctx, const srhip_dataset* ds, int64_t nidx, View& v);
+LaunchPlan plan_launch(const srhip_ctx* ctx, int dtype, int64_t nfeat, bool weighted, bool with_y, int64_t m,
+                       int32_t ntrees, int rows_per_tile);
+// did_succeed decision of tree t from partials in the srhip_eval_loss_partials layout:
+// 0 ok, 1 fail, 2 undecided (only the sums' feature / row-count entries are read)
+int decide_tree(const TreeInfo& I, const srhip_program& P, int64_t nfeat, const double* sums, double chk);
+int check_eval_args(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss);
+int run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
+             const int64_t* idx, int64_t nidx, double* out_loss, void* out_pred, uint8_t* out_ok);
+
+}  // namespace srhip

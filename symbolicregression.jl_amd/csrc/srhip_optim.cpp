@@ -1,0 +1,402 @@
+// srhip_optim.cpp — constant gradients and the batched constant optimizer of libsrhip.so.
+//
+// srhip_eval_loss_grad: loss + exact d loss / d constants for every tree of a program (one launch of
+//   the dual-number kernel, srhip_grad.hip, over (tree, constant-chunk) pairs).
+// srhip_optimize_constants: optimize_constants / _optimize_constants (src/ConstantOptimization.jl:
+//   11-81) for a whole population at once: BFGS with LineSearches' BackTracking (order 3,
+//   c1 = 1e-4, rho in [0.1, 0.5]) from the current constants and from `nrestarts` perturbed starts
+//   x0 .* (1 + randn/2), `iterations` iterations each (Optim.Options(iterations = 8),
+//   src/Options.jl:691-705); a tree's constants are replaced only if the best minimum beats its
+//   baseline loss (:70-78).  All trees advance in lockstep, so every objective/gradient evaluation
+//   of the population is one kernel launch.  Differences from the reference, by design: exact
+//   (dual-number) gradients instead of Optim's finite differences, and BFGS also for one-constant
+//   trees (the reference uses Newton there) — parity is on the optimised loss, SURVEY.md 8(a) A13.
+#include <algorithm>
+#include <random>
+#include <vector>
+
+#include "srhip_grad.h"
+#include "srhip_internal.h"
+
+using namespace srhip;
+
+namespace {
+
+// constant offsets (get_constants order) of every tree: coff[t] .. coff[t+1]
+std::vector<int64_t> const_offsets(const srhip_program& P) {
+  std::vector<int64_t> c(P.ntrees + 1, 0);
+  for (int32_t t = 0; t < P.ntrees; ++t) c[t + 1] = c[t] + P.info[t].nconst;
+  return c;
+}
+
+void get_consts_rec(const srhip_node* nd, int64_t i, std::vector<double>& out) {
+  const srhip_node& n = nd[i];
+  if (n.degree == 0) {
+    if (n.constant) out.push_back(n.val);
+    return;
+  }
+  get_consts_rec(nd, n.l, out);
+  if (n.degree == 2) get_consts_rec(nd, n.r, out);
+}
+void set_consts_rec(srhip_node* nd, int64_t i, const double*& c) {
+  srhip_node& n = nd[i];
+  if (n.degree == 0) {
+    if (n.constant) n.val = *c++;
+    return;
+  }
+  set_consts_rec(nd, n.l, c);
+  if (n.degree == 2) set_consts_rec(nd, n.r, c);
+}
+std::vector<double> get_all_consts(const srhip_program& P) {
+  std::vector<double> out;
+  for (int32_t t = 0; t < P.ntrees; ++t) get_consts_rec(P.nodes.data() + P.offsets[t], 0, out);
+  return out;
+}
+void set_all_consts(srhip_program& P, const double* c) {
+  for (int32_t t = 0; t < P.ntrees; ++t) set_consts_rec(P.nodes.data() + P.offsets[t], 0, c);
+  P.grad_ready = false;
+}
+
+}  // namespace
+
+// Loss and gradient for `trees` (f[t] = +Inf where did_succeed fails or is undecided); gradients
+// land at g[coff[t] ..].  The gradient program must match the program's current constants.
+static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss, const View& v,
+                     const std::vector<int32_t>& trees, const std::vector<int64_t>& coff, double* f, double* g) {
+  int rc = compile_grad_program(*P);
+  if (rc) return rc;
+  const int dtype = P->dtype;
+  const bool weighted = ds->weighted;
+  const double wsum = weighted ? v.sum_w : (double)v.m;
+  std::vector<int32_t> chunks;
+  for (int32_t t : trees) {
+    f[t] = INFINITY;
+    for (int64_t k = coff[t]; k < coff[t + 1]; ++k) g[k] = 0.0;
+    if (P->ginfo[t].static_fail) continue;
+    const int nc = P->info[t].nconst;
+    for (int c0 = 0; c0 < std::max(nc, 1); c0 += GRAD_KT) {
+      chunks.push_back(t);
+      chunks.push_back(c0);
+    }
+  }
+  const int nch = (int)chunks.size() / 2;
+  if (nch == 0) return SRHIP_OK;
+  LaunchPlan L = plan_launch(ctx, dtype, ds->nfeat, weighted, true, v.m, nch, 64);
+  const int K = P->gkmax <= 4 ? 4 : 8;
+  HIP_TRY(ctx->g_chunks.ensure(chunks.size() * sizeof(int32_t)));
+  HIP_TRY(hipMemcpyAsync(ctx->g_chunks.p, chunks.data(), chunks.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                         ctx->stream));
+  const size_t slab_n = (size_t)nch * L.nrb * (GRAD_KT + 2);
+  HIP_TRY(ctx->g_slab.ensure(slab_n * sizeof(double)));
+  HIP_TRY(ctx->g_red.ensure((size_t)nch * (GRAD_KT + 2) * sizeof(double)));
+  GradArgs a{};
+  a.code = (const Ins*)P->d_gcode.p;
+  a.prog_off = (const int32_t*)P->d_goff.p;
+  a.chunks = (const int32_t*)ctx->g_chunks.p;
+  a.X = v.X;
+  a.y = v.y;
+  a.w = weighted ? v.w : nullptr;
+  a.slab = (double*)ctx->g_slab.p;
+  a.ld = v.ld;
+  a.nvalid = v.m;
+  a.nchunks = nch;
+  a.nfeat = (int32_t)ds->nfeat;
+  a.rb_rows = L.rb_rows;
+  a.nrb = L.nrb;
+  a.chunks_per_group = L.tpg;
+  a.loss_kind = loss->kind;
+  a.loss_p0 = loss->p0;
+  a.weighted = weighted ? 1 : 0;
+  a.max_steps = P->gmax_len;
+  HIP_TRY(launch_grad(dtype, K, a, dim3(L.nrb, L.groups), ctx->stream));
+  HIP_TRY(launch_grad_reduce(dtype, (const double*)ctx->g_slab.p, L.nrb, nch, (double*)ctx->g_red.p, ctx->stream));
+  std::vector<double> red((size_t)nch * (GRAD_KT + 2));
+  HIP_TRY(hipMemcpyAsync(red.data(), ctx->g_red.p, red.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  // decision inputs in the partials layout: only the feature statistics and the row count are read
+  std::vector<double> sums(2 * (size_t)P->ntrees + 2 * ds->nfeat + 1, 0.0);
+  for (int64_t fi = 0; fi < ds->nfeat; ++fi) {
+    sums[2 * (size_t)P->ntrees + 2 * fi] = v.stats[fi].sum;
+    sums[2 * (size_t)P->ntrees + 2 * fi + 1] = (double)v.stats[fi].nonfinite;
+  }
+  sums.back() = (double)v.m;
+  for (int c = 0; c < nch; ++c) {
+    const int32_t t = chunks[2 * c], c0 = chunks[2 * c + 1];
+    const double* r = red.data() + (size_t)c * (GRAD_KT + 2);
+    const int nc = P->info[t].nconst;
+    for (int j = 0; j < GRAD_KT && c0 + j < nc; ++j) g[coff[t] + c0 + j] = r[1 + j] / wsum;
+    if (c0 == 0) {
+      const int st = decide_tree(P->ginfo[t], *P, ds->nfeat, sums.data(), r[GRAD_KT + 1]);
+      f[t] = st == 0 ? r[0] / wsum : INFINITY;  // undecided counts as failed for the optimiser
+    }
+  }
+  return SRHIP_OK;
+}
+
+namespace {
+
+// LineSearches.jl BackTracking (order 3) state of one tree
+struct LineSearch {
+  double phi0, dphi0, a1, a2, phix0, phix1;
+  int iter = 0, iterfinite = 0;
+  bool accepted = false, stop = false;  // stop: line search failed or the tree converged
+};
+
+// next trial step after phi(a2) = phix1 failed the sufficient-decrease test
+double backtrack_step(LineSearch& s) {
+  const double rho_hi = 0.5, rho_lo = 0.1;
+  double a_tmp;
+  if (s.iter == 1) {
+    a_tmp = -(s.dphi0 * s.a2 * s.a2) / (2.0 * (s.phix1 - s.phi0 - s.dphi0 * s.a2));
+  } else {
+    const double div = 1.0 / (s.a1 * s.a1 * s.a2 * s.a2 * (s.a2 - s.a1));
+    const double e1 = s.phix1 - s.phi0 - s.dphi0 * s.a2, e0 = s.phix0 - s.phi0 - s.dphi0 * s.a1;
+    const double a = (s.a1 * s.a1 * e1 - s.a2 * s.a2 * e0) * div;
+    const double b = (-s.a1 * s.a1 * s.a1 * e1 + s.a2 * s.a2 * s.a2 * e0) * div;
+    if (fabs(a) <= 2.220446049250313e-16) a_tmp = s.dphi0 / (2.0 * b);
+    else a_tmp = (-b + sqrt(std::max(b * b - 3.0 * a * s.dphi0, 0.0))) / (3.0 * a);
+  }
+  s.a1 = s.a2;
+  a_tmp = std::isnan(a_tmp) ? s.a2 * rho_hi : std::min(a_tmp, s.a2 * rho_hi);  // NaNMath.min
+  return std::max(a_tmp, s.a2 * rho_lo);
+}
+
+}  // namespace
+
+// One BFGS run (lockstep over `trees`) from x (all constants; only `trees`' entries move).
+// On return x holds each tree's final point and f its objective value there.
+static int bfgs(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss, const View& v,
+                const std::vector<int32_t>& trees, const std::vector<int64_t>& coff, int iterations, double g_tol,
+                std::vector<double>& x, std::vector<double>& f, std::vector<int64_t>& fcalls) {
+  const size_t nall = x.size();
+  std::vector<double> g(nall), xt(nall), gt(nall), ft(P->ntrees), s(nall);
+  // per-tree inverse Hessian approximations (identity start, Optim's default)
+  std::vector<int64_t> hoff(P->ntrees + 1, 0);
+  for (int32_t t = 0; t < P->ntrees; ++t) {
+    const int64_t n = coff[t + 1] - coff[t];
+    hoff[t + 1] = hoff[t] + n * n;
+  }
+  std::vector<double> H(hoff.back(), 0.0);
+  for (int32_t t : trees)
+    for (int64_t i = 0; i < coff[t + 1] - coff[t]; ++i) H[hoff[t] + i * (coff[t + 1] - coff[t]) + i] = 1.0;
+  auto gnorm = [&](int32_t t, const std::vector<double>& gg) {
+    double m = 0.0;
+    for (int64_t k = coff[t]; k < coff[t + 1]; ++k) m = std::max(m, fabs(gg[k]));
+    return m;
+  };
+  set_all_consts(*P, x.data());
+  int rc = eval_grad(ctx, ds, P, loss, v, trees, coff, f.data(), g.data());
+  if (rc) return rc;
+  std::vector<int32_t> live;
+  for (int32_t t : trees) {
+    fcalls[t] += 1;
+    if (std::isfinite(f[t]) && !(gnorm(t, g) <= g_tol)) live.push_back(t);
+  }
+  std::vector<LineSearch> ls(P->ntrees);
+  for (int it = 0; it < iterations && !live.empty(); ++it) {
+    // search directions s = -H g (reset to steepest descent if not a descent direction)
+    for (int32_t t : live) {
+      const int64_t n = coff[t + 1] - coff[t], o = coff[t];
+      double dphi = 0.0;
+      for (int64_t i = 0; i < n; ++i) {
+        double acc = 0.0;
+        for (int64_t j = 0; j < n; ++j) acc += H[hoff[t] + i * n + j] * g[o + j];
+        s[o + i] = -acc;
+        dphi += g[o + i] * s[o + i];
+      }
+      if (!(dphi < 0.0)) {
+        dphi = 0.0;
+        for (int64_t i = 0; i < n; ++i) {
+          for (int64_t j = 0; j < n; ++j) H[hoff[t] + i * n + j] = i == j ? 1.0 : 0.0;
+          s[o + i] = -g[o + i];
+          dphi -= g[o + i] * g[o + i];
+        }
+      }
+      LineSearch& L = ls[t];
+      L = LineSearch();
+      L.phi0 = f[t];
+      L.dphi0 = dphi;
+      L.a1 = L.a2 = 1.0;
+      L.phix0 = L.phix1 = f[t];
+    }
+    // batched backtracking: every round evaluates all trees still searching in one launch
+    std::vector<int32_t> pending = live;
+    std::vector<uint8_t> first(P->ntrees, 1);
+    for (int round = 0; round < 60 && !pending.empty(); ++round) {
+      xt = x;
+      for (int32_t t : pending)
+        for (int64_t k = coff[t]; k < coff[t + 1]; ++k) xt[k] = x[k] + ls[t].a2 * s[k];
+      set_all_consts(*P, xt.data());
+      rc = eval_grad(ctx, ds, P, loss, v, pending, coff, ft.data(), gt.data());
+      if (rc) return rc;
+      std::vector<int32_t> next;
+      for (int32_t t : pending) {
+        fcalls[t] += 1;
+        LineSearch& L = ls[t];
+        const double phi = ft[t];
+        if (first[t]) {
+          first[t] = 0;
+          L.phix0 = L.phi0;
+        }
+        L.phix1 = phi;
+        bool accept = false;
+        if (!std::isfinite(phi)) {  // hard-coded halving until finite (iterfinitemax = 52)
+          if (++L.iterfinite >= 52) L.stop = true;
+          else {
+            L.a1 = L.a2;
+            L.a2 = L.a1 / 2.0;
+          }
+        } else if (phi > L.phi0 + 1e-4 * L.a2 * L.dphi0) {
+          if (++L.iter > 40) L.stop = true;
+          else {
+            const double a2 = backtrack_step(L);
+            L.phix0 = L.phix1;
+            L.a2 = a2;
+          }
+        } else {
+          accept = true;
+        }
+        if (accept) {
+          // BFGS update with dx = a s, dg = g_new - g (skipped unless dx'dg > 0, as Optim)
+          const int64_t n = coff[t + 1] - coff[t], o = coff[t];
+          std::vector<double> dx(n), dg(n), u(n);
+          double dxdg = 0.0;
+          for (int64_t i = 0; i < n; ++i) {
+            dx[i] = L.a2 * s[o + i];
+            dg[i] = gt[o + i] - g[o + i];
+            dxdg += dx[i] * dg[i];
+          }
+          if (dxdg > 0.0) {
+            double dgu = 0.0;
+            for (int64_t i = 0; i < n; ++i) {
+              double acc = 0.0;
+              for (int64_t j = 0; j < n; ++j) acc += H[hoff[t] + i * n + j] * dg[j];
+              u[i] = acc;
+              dgu += dg[i] * acc;
+            }
+            const double c1 = (dxdg + dgu) / (dxdg * dxdg), c2 = 1.0 / dxdg;
+            for (int64_t i = 0; i < n; ++i)
+              for (int64_t j = 0; j < n; ++j)
+                H[hoff[t] + i * n + j] += c1 * dx[i] * dx[j] - c2 * (u[i] * dx[j] + dx[i] * u[j]);
+          }
+          const double fold = f[t];
+          for (int64_t k = coff[t]; k < coff[t + 1]; ++k) {
+            x[k] = xt[k];
+            g[k] = gt[k];
+          }
+          f[t] = phi;
+          L.accepted = true;
+          // Optim's stopping rules with f_reltol = x_abstol = 0: no change, or |g| <= g_tol
+          if (phi == fold || gnorm(t, g) <= g_tol) L.stop = true;  // converged: leave the live set
+        } else if (!L.stop) {
+          next.push_back(t);
+        }
+      }
+      pending.swap(next);
+    }
+    std::vector<int32_t> still;
+    for (int32_t t : live)
+      if (ls[t].accepted && !ls[t].stop) still.push_back(t);
+    live.swap(still);
+  }
+  return SRHIP_OK;
+}
+
+extern "C" {
+
+int srhip_eval_loss_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
+                         const int64_t* idx, int64_t nidx, double* out_loss, double* out_grad, uint8_t* out_ok) {
+  if (!out_loss || !out_grad || !out_ok) return fail(SRHIP_ERR_INVALID, "null output");
+  int rc = check_eval_args(ctx, ds, P, MODE_LOSS, loss);
+  if (rc) return rc;
+  if (P->dtype == SRHIP_I32) return fail(SRHIP_ERR_UNSUPPORTED, "constant gradients need Float32 / Float64");
+  HIP_TRY(hipSetDevice(ctx->device));
+  View v;
+  rc = make_view(ctx, ds, idx, nidx, true, v);
+  if (rc) return rc;
+  if (idx && ds->weighted) {
+    rc = gathered_weight_sum(ctx, ds, nidx, v);
+    if (rc) return rc;
+  }
+  const std::vector<int64_t> coff = const_offsets(*P);
+  std::vector<int32_t> all(P->ntrees);
+  for (int32_t t = 0; t < P->ntrees; ++t) all[t] = t;
+  rc = eval_grad(ctx, ds, P, loss, v, all, coff, out_loss, out_grad);
+  if (rc) return rc;
+  for (int32_t t = 0; t < P->ntrees; ++t) out_ok[t] = std::isfinite(out_loss[t]) ? 1 : 0;
+  return SRHIP_OK;
+}
+
+int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
+                             const int64_t* idx, int64_t nidx, const srhip_optim_options* opt, double* out_loss,
+                             uint8_t* out_improved, int64_t* out_fcalls) {
+  if (!opt || !out_loss || !out_improved) return fail(SRHIP_ERR_INVALID, "null argument");
+  if (opt->iterations < 0 || opt->nrestarts < 0) return fail(SRHIP_ERR_INVALID, "negative iterations / restarts");
+  int rc = check_eval_args(ctx, ds, P, MODE_LOSS, loss);
+  if (rc) return rc;
+  if (P->dtype == SRHIP_I32) return fail(SRHIP_ERR_UNSUPPORTED, "constant optimisation needs Float32 / Float64");
+  HIP_TRY(hipSetDevice(ctx->device));
+  const int32_t nt = P->ntrees;
+  // baseline = f(tree) with the evaluator itself (src/ConstantOptimization.jl:49)
+  std::vector<double> base(nt);
+  std::vector<uint8_t> base_ok(nt);
+  rc = run_eval(ctx, ds, P, MODE_LOSS, loss, idx, nidx, base.data(), nullptr, base_ok.data());
+  if (rc) return rc;
+  View v;
+  rc = make_view(ctx, ds, idx, nidx, true, v);
+  if (rc) return rc;
+  if (idx && ds->weighted) {
+    rc = gathered_weight_sum(ctx, ds, nidx, v);
+    if (rc) return rc;
+  }
+  const std::vector<int64_t> coff = const_offsets(*P);
+  const std::vector<double> x0 = get_all_consts(*P);
+  std::vector<int32_t> trees;  // trees with constants (nconst == 0: nothing to optimise, :35)
+  for (int32_t t = 0; t < nt; ++t)
+    if (P->info[t].nconst > 0 && !P->info[t].static_fail) trees.push_back(t);
+  std::vector<double> best_x = x0, best_f(nt, INFINITY), x(x0.size()), f(nt);
+  std::vector<int64_t> fcalls(nt, 0);
+  std::mt19937_64 rng(opt->seed);
+  std::normal_distribution<double> randn(0.0, 1.0);
+  const double g_tol = opt->g_tol > 0 ? opt->g_tol : 1e-8;
+  for (int start = 0; start <= opt->nrestarts && !trees.empty(); ++start) {
+    x = x0;
+    if (start > 0)  // src/ConstantOptimization.jl:53-60: c * (1 + randn/2)
+      for (int32_t t : trees)
+        for (int64_t k = coff[t]; k < coff[t + 1]; ++k) x[k] = x0[k] * (1.0 + 0.5 * randn(rng));
+    rc = bfgs(ctx, ds, P, loss, v, trees, coff, opt->iterations, g_tol, x, f, fcalls);
+    if (rc) {
+      set_all_consts(*P, x0.data());
+      compile_program(*P);
+      upload_program(*P);
+      return rc;
+    }
+    for (int32_t t : trees)
+      if (f[t] < best_f[t]) {  // :62-64
+        best_f[t] = f[t];
+        for (int64_t k = coff[t]; k < coff[t + 1]; ++k) best_x[k] = x[k];
+      }
+  }
+  // accept where the best minimum beats the baseline (:70-78)
+  std::vector<double> final_x = x0;
+  for (int32_t t = 0; t < nt; ++t) {
+    const bool better = best_f[t] < base[t];
+    out_improved[t] = better ? 1 : 0;
+    if (better)
+      for (int64_t k = coff[t]; k < coff[t + 1]; ++k) final_x[k] = best_x[k];
+  }
+  set_all_consts(*P, final_x.data());
+  rc = compile_program(*P);
+  if (rc) return rc;
+  rc = upload_program(*P);
+  if (rc) return rc;
+  // the loss of the returned trees, by the evaluator (the reference re-scores accepted members)
+  std::vector<uint8_t> ok(nt);
+  rc = run_eval(ctx, ds, P, MODE_LOSS, loss, idx, nidx, out_loss, nullptr, ok.data());
+  if (rc) return rc;
+  if (out_fcalls)
+    for (int32_t t = 0; t < nt; ++t) out_fcalls[t] = fcalls[t] + 1;
+  return SRHIP_OK;
+}
+
+}  // extern "C"

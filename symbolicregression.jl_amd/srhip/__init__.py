@@ -12,7 +12,9 @@ from .api import (
     eval_loss_batch,
     eval_loss_batched,
     eval_tree_array,
+    eval_grad_loss_batch,
     eval_tree_array_batch,
+    optimize_constants,
     loss_to_score,
     score_func,
     score_func_batch,

@@ -52,6 +52,11 @@ class Loss(ctypes.Structure):
                 ("p0", ctypes.c_double), ("p1", ctypes.c_double)]
 
 
+class OptimOptions(ctypes.Structure):
+    _fields_ = [("iterations", ctypes.c_int32), ("nrestarts", ctypes.c_int32), ("seed", ctypes.c_uint64),
+                ("g_tol", ctypes.c_double)]
+
+
 class SrhipError(RuntimeError):
     """A nonzero status from libsrhip (message from srhip_last_error)."""
 
@@ -77,6 +82,7 @@ SIGNATURES = {
     "srhip_program_destroy": (None, [_vp]),
     "srhip_program_num_constants": (ctypes.c_int, [_vp, _vp]),
     "srhip_program_set_constants": (ctypes.c_int, [_vp, _vp]),
+    "srhip_program_get_constants": (ctypes.c_int, [_vp, _vp]),
     "srhip_eval_loss": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(Loss), _vp, _i64, _vp, _vp]),
     "srhip_eval_predict": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     "srhip_eval_loss_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, ctypes.POINTER(Operators),
@@ -87,6 +93,9 @@ SIGNATURES = {
     "srhip_precise_finalize": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp]),
     "srhip_chk_reduce_op": (ctypes.c_int, [ctypes.c_int]),
     "srhip_program_max_ops": (_i32, [_vp]),
+    "srhip_eval_loss_grad": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(Loss), _vp, _i64, _vp, _vp, _vp]),
+    "srhip_optimize_constants": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(Loss), _vp, _i64,
+                                                ctypes.POINTER(OptimOptions), _vp, _vp, _vp]),
     "srhip_last_kernel_ms": (_dbl, [_vp]),
     "srhip_program_stats": (ctypes.c_int, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
                                            ctypes.POINTER(_i32)]),

@@ -205,3 +205,53 @@ def update_baseline_loss(dataset: Dataset, options) -> None:
     else:
         dataset.baseline_loss = dataset.loss_type.type(1)
         dataset.use_baseline = False
+
+
+# ---- constant optimisation ---------------------------------------------------------------------
+def eval_grad_loss_batch(trees, dataset: Dataset, options, idx=None):
+    """Loss and its exact gradient w.r.t. each tree's constants (get_constants order), one launch:
+    (loss[T], [grad per tree], ok[T]).  The loss-level counterpart of eval_grad_tree_array
+    (src/InterfaceDynamicExpressions.jl:118-124, variable=false)."""
+    trees = _as_trees(trees)
+    prog = compile_trees(trees, options, dataset.X.dtype)
+    try:
+        return prog.eval_loss_grad(dataset.device(_ctx(options)), options.elementwise_loss, idx)
+    finally:
+        prog.close()
+
+
+def optimize_constants(dataset: Dataset, members, options, rng=None, idx=None):
+    """optimize_constants (src/ConstantOptimization.jl:11-81) for one member or a whole list at once.
+
+    Members are PopMember-like objects (``.tree``, ``.loss``, ``.score``) or bare Nodes.  Where the
+    optimised constants beat the member's baseline loss, its tree constants are replaced and loss and
+    score re-computed (:70-78).  Returns (members, num_evals) like the reference (num_evals summed)."""
+    from .node import get_constants, set_constants
+
+    single = not isinstance(members, (list, tuple))
+    mlist = [members] if single else list(members)
+    trees = [m.tree if hasattr(m, "tree") else m for m in mlist]
+    if options.loss_function is not None or not is_device_loss(options.elementwise_loss):
+        raise NotImplementedError("device constant optimisation needs a built-in elementwise loss")
+    if idx is None and options.batching:
+        idx = batch_sample(dataset, options, rng)
+    seed = int((rng or np.random.default_rng()).integers(0, 2**63 - 1))
+    prog = compile_trees(trees, options, dataset.X.dtype)
+    try:
+        losses, improved, fcalls = prog.optimize_constants(
+            dataset.device(_ctx(options)), options.elementwise_loss, iterations=options.optimizer_iterations,
+            nrestarts=options.optimizer_nrestarts, seed=seed, idx=idx)
+        consts = prog.get_constants()
+    finally:
+        prog.close()
+    eval_fraction = (options.batch_size / dataset.n) if options.batching else 1.0
+    L = dataset.loss_type.type
+    for m, t, ok, c, lo in zip(mlist, trees, improved, consts, losses):
+        if not ok:
+            continue
+        set_constants(t, c)
+        if hasattr(m, "tree"):
+            m.loss = L(lo)
+            m.score = loss_to_score(m.loss, dataset.use_baseline, dataset.baseline_loss, m, options)
+    num_evals = float(np.sum(fcalls)) * eval_fraction
+    return (mlist[0] if single else mlist), num_evals

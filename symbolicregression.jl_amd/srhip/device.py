@@ -154,6 +154,42 @@ class Program:
                                              0 if idxa is None else len(idxa), ptr(out), ptr(ok)))
         return out, ok.astype(bool)
 
+    # ---- constant optimisation (src/ConstantOptimization.jl) ---------------------------------
+    def get_constants(self) -> list:
+        """Per tree, its current constants in get_constants order."""
+        nconst = self.num_constants()
+        c = np.empty(int(nconst.sum()), dtype=np.float64)
+        check(_lib.load().srhip_program_get_constants(self.handle, ptr(c)))
+        return np.split(c, np.cumsum(nconst)[:-1])
+
+    def eval_loss_grad(self, ds: DeviceDataset, loss, idx=None):
+        """(loss[T], grads: list of per-tree arrays (get_constants order), ok[T])."""
+        nconst = self.num_constants()
+        out = np.empty(self.ntrees, dtype=np.float64)
+        grad = np.empty(int(nconst.sum()), dtype=np.float64)
+        ok = np.empty(self.ntrees, dtype=np.uint8)
+        ls = loss.c_struct()
+        idxa = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        check(_lib.load().srhip_eval_loss_grad(self.ctx.handle, ds.handle, self.handle, ctypes.byref(ls), ptr(idxa),
+                                               0 if idxa is None else len(idxa), ptr(out), ptr(grad), ptr(ok)))
+        splits = np.cumsum(nconst)[:-1]
+        return out, np.split(grad, splits), ok.astype(bool)
+
+    def optimize_constants(self, ds: DeviceDataset, loss, iterations=8, nrestarts=2, seed=0, g_tol=1e-8, idx=None):
+        """Batched optimize_constants; updates this program's constants in place.
+
+        Returns (loss[T] of the returned trees, improved[T], fcalls[T])."""
+        opt = _lib.OptimOptions(int(iterations), int(nrestarts), int(seed) & (2**64 - 1), float(g_tol))
+        out = np.empty(self.ntrees, dtype=np.float64)
+        imp = np.empty(self.ntrees, dtype=np.uint8)
+        fc = np.empty(self.ntrees, dtype=np.int64)
+        ls = loss.c_struct()
+        idxa = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        check(_lib.load().srhip_optimize_constants(self.ctx.handle, ds.handle, self.handle, ctypes.byref(ls), ptr(idxa),
+                                                   0 if idxa is None else len(idxa), ctypes.byref(opt), ptr(out),
+                                                   ptr(imp), ptr(fc)))
+        return out, imp.astype(bool), fc
+
     # ---- row-sharded evaluation (include/srhip.h "row-sharded evaluation") ----------------------
     def chk_reduce_op(self) -> str:
         """How chk combines across shards: "max" (Float32) or "sum" (Float64 / Int32)."""
