@@ -34,11 +34,15 @@ def parse():
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--config", default="c2", choices=("c2", "c4"),
+                    help="c2 (default, the headline metric) or c4: batched constant optimisation")
     return ap.parse_args()
 
 
 def main():
     args = parse()
+    if args.config == "c4":
+        return bench_c4(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -188,6 +192,70 @@ def cpu_baseline(nodes, offs, opts, X, y, target_s):
         "sample": f"all {len(offs) - 1} trees x first {m2} of the 1M rows ({dt:.1f} s), oracle/sr_oracle.c "
                   f"array-at-a-time restatement, OpenMP over trees",
     }
+
+
+def bench_c4(args):
+    """C4: optimize_constants (BFGS(8 iterations) + 2 restarts, src/ConstantOptimization.jl) on 512
+    fixed-size-20 trees with >= 2 constants over 5 x 100k Float64 rows, one MI355X.  A step = one
+    batched srhip_optimize_constants from the same initial constants.  Also reports the
+    dual-number gradient launch alone (node-row evals/s of the loss + gradient)."""
+    import numpy as np
+
+    import srhip
+
+    rows = 100_000 if args.rows == 1_000_000 else args.rows
+    ntrees = 512 if args.ntrees == 1024 else args.ntrees
+    opts = srhip.Options(binary_operators=("+", "-", "*", "/"), unary_operators=("cos", "exp"))
+    rng = np.random.default_rng(4)
+    trees = []
+    while len(trees) < ntrees:
+        t = srhip.gen_random_tree_fixed_size(20, opts, 5, np.float64, rng)
+        if srhip.count_constants(t) >= 2:
+            trees.append(t)
+    nodes, offs = srhip.flatten(trees, opts, np.float64)
+    X = rng.standard_normal((5, rows))
+    y = 2 * np.cos(X[3]) + X[0] ** 2 - 2 + 0.1 * rng.standard_normal(rows)
+    ctx = srhip.get_context(0)
+    ds = srhip.DeviceDataset(ctx, X, y)
+    prog = srhip.Program(ctx, nodes, offs, opts, np.float64)
+    x0 = np.concatenate(prog.get_constants())
+    loss = srhip.L2DistLoss()
+    base, ok = prog.eval_loss(ds, loss)
+
+    def step():
+        prog.set_constants(x0)
+        return prog.optimize_constants(ds, loss, iterations=8, nrestarts=2, seed=7)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out, improved, fcalls = step()
+    ctx.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    # gradient launch alone
+    st = prog.stats()
+    for _ in range(3):
+        prog.eval_loss_grad(ds, loss)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        prog.eval_loss_grad(ds, loss)
+    gdt = (time.perf_counter() - t0) / 10
+    fin = np.isfinite(base)
+    print(json.dumps({
+        "metric": "C4 batched constant optimisation: wall time per optimize_constants over the population",
+        "value": dt * 1e3, "unit": "ms", "higher_is_better": False, "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "dtype": "f64", "data": "synthetic (X ~ N(0,1) 5x100k; fixed-size-20 trees, >= 2 consts)",
+        "config": {"workload": f"C4: {ntrees} trees x {rows} rows Float64, BFGS(8) + 2 restarts",
+                   "ntrees": ntrees, "rows": rows, "nodes": int(st["total_nodes"])},
+        "objective_evals_per_s": float(np.sum(fcalls)) / dt,
+        "improved_trees": int(improved.sum()),
+        "mean_loss_before": float(np.mean(base[fin])), "mean_loss_after": float(np.mean(out[fin])),
+        "grad_launch_ms": gdt * 1e3,
+        "grad_node_row_evals_per_s": st["total_nodes"] * rows / gdt,
+    }))
 
 
 if __name__ == "__main__":

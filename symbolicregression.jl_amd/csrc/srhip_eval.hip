@@ -109,6 +109,7 @@ __device__ __attribute__((noinline)) RV<T, R> heavy_un(RV<T, R> v) {
       default: break;
     }
     v[r] = x;
+    SRHIP_ROW_FENCE();  // one row at a time: bounds the callee's registers (and so the kernel's)
   }
   return v;
 }
@@ -125,9 +126,16 @@ __device__ __attribute__((noinline)) RV<T, R> heavy_bin(RV<T, R> a, RV<T, R> b) 
       default: break;
     }
     a[r] = x;
+    SRHIP_ROW_FENCE();
   }
   return a;
 }
+// "Wide" unary operators: OCML bodies with ~70-100 live VGPRs.  A kernel's register budget is the
+// max over every callee it can reach, so only the K = K_MAX variant carries them; with them the
+// common variants would drop from 5 to 4 waves per SIMD.  Programs whose operator table has one
+// of them launch K_MAX (the host's variant choice).
+constexpr bool un_wide(int u) { return u == UN_ASIN || u == UN_ACOS || u == UN_ATANH_CLIP; }
+
 // unary operators cheap enough to inline into the handler (a few VALU instructions per row)
 template <int U> constexpr bool un_inline() {
   return U == UN_NEG || U == UN_SQUARE || U == UN_CUBE || U == UN_ABS || U == UN_RELU || U == UN_SIGN ||
@@ -359,8 +367,8 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
       const int64_t row0 = row_base + (int64_t)tile * TILE;
       if (row0 >= p.nvalid) break;  // whole tile is padding
       const T* xt = xsrc + (int64_t)tile * TILE;
-      T A[R], B[R], S[K][R];
-      UNR for (int r = 0; r < R; ++r) { A[r] = T(0); B[r] = T(0); }
+      T A[R], S[K][R];
+      UNR for (int r = 0; r < R; ++r) A[r] = T(0);
       UNR for (int k = 0; k < K; ++k) UNR for (int r = 0; r < R; ++r) S[k][r] = T(0);
       // The program is read through the constant address space with a wave-uniform pc, so every
       // instruction is one s_load_dwordx4 (scalar cache), prefetched one instruction ahead.
@@ -375,8 +383,6 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
         switch (ins.h) {
           case H_LOADF: load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A); break;
           case H_LOADC: { const T c = imm_as<T>(ins.imm); UNR for (int r = 0; r < R; ++r) A[r] = c; break; }
-          case H_FETCHF: load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, B); break;
-          case H_FETCHC: { const T c = imm_as<T>(ins.imm); UNR for (int r = 0; r < R; ++r) B[r] = c; break; }
 #define SRHIP_K_CASES(BASE, ...)                                                            \
   case BASE + 0: if constexpr (0 < K) { constexpr int k = 0; __VA_ARGS__ } break;                 \
   case BASE + 1: if constexpr (1 < K) { constexpr int k = 1; __VA_ARGS__ } break;                 \
@@ -387,7 +393,8 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
   case BASE + 6: if constexpr (6 < K) { constexpr int k = 6; __VA_ARGS__ } break;                 \
   case BASE + 7: if constexpr (7 < K) { constexpr int k = 7; __VA_ARGS__ } break;
           SRHIP_K_CASES(H_PUSH0, { UNR for (int r = 0; r < R; ++r) S[k][r] = A[r]; })
-          SRHIP_K_CASES(H_FETCHS0, { UNR for (int r = 0; r < R; ++r) B[r] = S[k][r]; })
+          SRHIP_K_CASES(H_SLOADF0, { load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, S[k]); })
+          SRHIP_K_CASES(H_SLOADC0, { const T c = imm_as<T>(ins.imm); UNR for (int r = 0; r < R; ++r) S[k][r] = c; })
 
 #define SRHIP_SPEC_CASE(NAME, FN)                                                                  \
   case h_spec(SB_##NAME, SPEC_AF):                                                                 \
@@ -437,27 +444,23 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
           SRHIP_SPEC_BINOPS(SRHIP_SPEC_CASE)
 #undef SRHIP_SPEC_CASE
 
-#define SRHIP_HEAVY_CASE(NAME, FN)                                               \
-  case h_heavy(HB_##NAME, false):                                                \
-    if constexpr (hb_ok<T>(HB_##NAME)) {                                         \
-      apply_heavy<T, R, HB_##NAME>(A, A, B);                                     \
-      chk_update<R>(M, A);                                                       \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0); \
-    }                                                                            \
-    break;                                                                       \
-  case h_heavy(HB_##NAME, true):                                                 \
-    if constexpr (hb_ok<T>(HB_##NAME)) {                                         \
-      apply_heavy<T, R, HB_##NAME>(A, B, A);                                     \
-      chk_update<R>(M, A);                                                       \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0); \
-    }                                                                            \
-    break;
+#define SRHIP_HEAVY_CASE(NAME, FN)                                                              \
+    SRHIP_K_CASES(h_heavy(HB_##NAME, HEAVY_SA0), if constexpr (hb_ok<T>(HB_##NAME)) {           \
+      apply_heavy<T, R, HB_##NAME>(A, S[k], A);                                                 \
+      chk_update<R>(M, A);                                                                      \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);  \
+    })                                                                                          \
+    SRHIP_K_CASES(h_heavy(HB_##NAME, HEAVY_AS0), if constexpr (hb_ok<T>(HB_##NAME)) {           \
+      apply_heavy<T, R, HB_##NAME>(A, A, S[k]);                                                 \
+      chk_update<R>(M, A);                                                                      \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);  \
+    })
           SRHIP_HEAVY_BINOPS(SRHIP_HEAVY_CASE)
 #undef SRHIP_HEAVY_CASE
 
 #define SRHIP_UN_CASE(NAME, FN)                                                  \
   case h_un(UN_##NAME):                                                          \
-    if constexpr (un_ok<T>(UN_##NAME)) {                                         \
+    if constexpr (un_ok<T>(UN_##NAME) && (K == K_MAX || !un_wide(UN_##NAME))) {  \
       apply_un<T, R, UN_##NAME>(A);                                              \
       chk_update<R>(M, A);                                                       \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0); \
@@ -587,6 +590,7 @@ static hipError_t launch_eval_t(const EvalArgs& a, dim3 grid, size_t lds, hipStr
 
 template <typename T, int R, int MODE, bool XLDS>
 static hipError_t launch_eval_k(const EvalArgs& a, int K, dim3 grid, size_t lds, hipStream_t s) {
+  if (K <= 2) return launch_eval_t<T, R, 2, MODE, XLDS>(a, grid, lds, s);
   if (K <= 4) return launch_eval_t<T, R, 4, MODE, XLDS>(a, grid, lds, s);
   return launch_eval_t<T, R, 8, MODE, XLDS>(a, grid, lds, s);
 }

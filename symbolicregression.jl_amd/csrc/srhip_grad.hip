@@ -224,9 +224,8 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
       const int64_t row0 = row_base + (int64_t)tile * 64;
       if (row0 >= p.nvalid) break;
       const int64_t row = row0 + lane;  // rows up to ld are finite replicas; masked at the loss
-      Dual<T, KT> A, B, S[K];
+      Dual<T, KT> A, S[K];
       set_feat(A, T(0));
-      set_feat(B, T(0));
       UNR for (int k = 0; k < K; ++k) set_feat(S[k], T(0));
       GIns* prog = code + pc0;
       Ins nxt = prog[0];
@@ -239,8 +238,6 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
         switch (ins.h) {
           case H_LOADF: set_feat(A, X[(int64_t)opnd * p.ld + row]); break;
           case H_LOADC: set_const(A, imm, opnd - c0); break;
-          case H_FETCHF: set_feat(B, X[(int64_t)opnd * p.ld + row]); break;
-          case H_FETCHC: set_const(B, imm, opnd - c0); break;
 #define GK_CASES(BASE, ...)                                                                        \
   case BASE + 0: if constexpr (0 < K) { constexpr int k = 0; __VA_ARGS__ } break;                \
   case BASE + 1: if constexpr (1 < K) { constexpr int k = 1; __VA_ARGS__ } break;                \
@@ -251,7 +248,8 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   case BASE + 6: if constexpr (6 < K) { constexpr int k = 6; __VA_ARGS__ } break;                \
   case BASE + 7: if constexpr (7 < K) { constexpr int k = 7; __VA_ARGS__ } break;
           GK_CASES(H_PUSH0, { S[k] = A; })
-          GK_CASES(H_FETCHS0, { B = S[k]; })
+          GK_CASES(H_SLOADF0, { set_feat(S[k], X[(int64_t)opnd * p.ld + row]); })
+          GK_CASES(H_SLOADC0, { set_const(S[k], imm, opnd - c0); })
 #define GK_SPEC(NAME, FN)                                                                          \
   case h_spec(SB_##NAME, SPEC_AF): {                                                               \
     Dual<T, KT> o; set_feat(o, X[(int64_t)opnd * p.ld + row]);                                     \
@@ -278,12 +276,12 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
           SRHIP_SPEC_BINOPS(GK_SPEC)
 #undef GK_SPEC
 #define GK_HEAVY(NAME, FN)                                                                         \
-  case h_heavy(HB_##NAME, false): {                                                                \
-    const typename V4<T>::type r = dual_heavy<T, HB_##NAME>(A.v, B.v);                             \
-    combine(A, A, B, r[0], r[1], r[2]); chk_fold(M, A.v); break; }                                 \
-  case h_heavy(HB_##NAME, true): {                                                                 \
-    const typename V4<T>::type r = dual_heavy<T, HB_##NAME>(B.v, A.v);                             \
-    combine(A, B, A, r[0], r[1], r[2]); chk_fold(M, A.v); break; }
+  GK_CASES(h_heavy(HB_##NAME, HEAVY_SA0), {                                                        \
+    const typename V4<T>::type r = dual_heavy<T, HB_##NAME>(S[k].v, A.v);                          \
+    combine(A, S[k], A, r[0], r[1], r[2]); chk_fold(M, A.v); })                                    \
+  GK_CASES(h_heavy(HB_##NAME, HEAVY_AS0), {                                                        \
+    const typename V4<T>::type r = dual_heavy<T, HB_##NAME>(A.v, S[k].v);                          \
+    combine(A, A, S[k], r[0], r[1], r[2]); chk_fold(M, A.v); })
           SRHIP_HEAVY_BINOPS(GK_HEAVY)
 #undef GK_HEAVY
 #define GK_UN(NAME, FN)                                                                            \

@@ -336,9 +336,12 @@ template <typename T> class TreeCompiler {
     const srhip_node& n = nd_[i];
     if (n.degree == 1) return need(n.l);
     const bool ll = leafish(n.l), rl = leafish(n.r);
-    if (ll && rl) return 0;
-    if (rl) return need(n.l);
-    if (ll) return need(n.r);
+    int sb, hb;
+    classify_binop(binop(i), &sb, &hb);
+    const int leaf_slot = hb >= 0 ? 1 : 0;  // a heavy op's leaf operand is loaded into a slot
+    if (ll && rl) return leaf_slot;
+    if (rl) return std::max(need(n.l), leaf_slot);
+    if (ll) return std::max(need(n.r), leaf_slot);
     const int a = need(n.l), b = need(n.r);
     return a == b ? a + 1 : std::max(a, b);
   }
@@ -400,29 +403,27 @@ template <typename T> class TreeCompiler {
       }
       return;
     }
-    // heavy binary op: operand in B
+    // heavy binary op (pow, mod, atan2): the second operand lives in stack slot `base`
     if (rl) {
       emit(L, base, i);
-      if (leaf_is_feature(Rr)) push_ins(H_FETCHF, nd_[Rr].feature - 1, 0);
-      else push_ins(H_FETCHC, cop(Rr), leaf_imm(Rr));
-      push_op(h_heavy(hb, false), 0, 0, i, parent);  // A = A op B
+      if (leaf_is_feature(Rr)) push_ins(H_SLOADF0 + base, nd_[Rr].feature - 1, 0);
+      else push_ins(H_SLOADC0 + base, cop(Rr), leaf_imm(Rr));
+      push_op(h_heavy(hb, HEAVY_AS0 + base), 0, 0, i, parent);  // A = A op S[base]
     } else if (ll) {
       emit(Rr, base, i);
-      if (leaf_is_feature(L)) push_ins(H_FETCHF, nd_[L].feature - 1, 0);
-      else push_ins(H_FETCHC, cop(L), leaf_imm(L));
-      push_op(h_heavy(hb, true), 0, 0, i, parent);   // A = B op A
+      if (leaf_is_feature(L)) push_ins(H_SLOADF0 + base, nd_[L].feature - 1, 0);
+      else push_ins(H_SLOADC0 + base, cop(L), leaf_imm(L));
+      push_op(h_heavy(hb, HEAVY_SA0 + base), 0, 0, i, parent);  // A = S[base] op A
     } else if (need(L) >= need(Rr)) {
       emit(L, base, i);
       push_ins(H_PUSH0 + base, 0, 0);
       emit(Rr, base + 1, i);
-      push_ins(H_FETCHS0 + base, 0, 0);
-      push_op(h_heavy(hb, true), 0, 0, i, parent);   // A = S op A
+      push_op(h_heavy(hb, HEAVY_SA0 + base), 0, 0, i, parent);  // A = S op A
     } else {
       emit(Rr, base, i);
       push_ins(H_PUSH0 + base, 0, 0);
       emit(L, base + 1, i);
-      push_ins(H_FETCHS0 + base, 0, 0);
-      push_op(h_heavy(hb, false), 0, 0, i, parent);  // A = A op S
+      push_op(h_heavy(hb, HEAVY_AS0 + base), 0, 0, i, parent);  // A = A op S
     }
   }
 };
@@ -774,7 +775,10 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     HIP_TRY(pred.ensure((size_t)nt * v.m * es));
     a.out_pred = pred.p;
   }
-  const int K = P->kmax <= 4 ? 4 : 8;
+  // stack slots of the kernel variant; the wide operators live only in the K_MAX variant
+  bool wide = false;
+  for (int32_t u : P->unaops) wide |= u == SRHIP_OP_ASIN || u == SRHIP_OP_ACOS || u == SRHIP_OP_ATANH_CLIP;
+  const int K = wide ? K_MAX : (P->kmax <= 2 ? 2 : (P->kmax <= 4 ? 4 : 8));
   dim3 grid(L.nrb, L.groups);
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
   HIP_TRY(launch_eval(dtype, a, K, mode, L.xlds, grid, L.lds, ctx->stream));

@@ -4,7 +4,6 @@
 // Machine model (one wavefront, R rows per lane, all state in VGPRs):
 //   A      accumulator: the value of the subexpression being evaluated (R values per lane)
 //   S[k]   stack slots k < K (Sethi-Ullman ordering keeps K = Strahler number - 1 small)
-//   B      operand register for "heavy" binary ops (pow, mod, atan2)
 //   X[f]   feature f of the current row tile, read from LDS
 // Every operator instruction also folds max|A| (NaN-propagating) into the tree's check
 // accumulator: that is the device side of DynamicExpressions' did_succeed checks (see
@@ -22,7 +21,7 @@ constexpr int K_MAX = 8;  // stack slots in the largest kernel variant
 #define SRHIP_SPEC_BINOPS(X)                                                                \
   X(ADD, add) X(SUB, sub) X(MUL, mul) X(DIV, div) X(GREATER, greater) X(COND, cond)           \
   X(LOGICAL_OR, logical_or) X(LOGICAL_AND, logical_and) X(MAX, max) X(MIN, min)
-// Binary operators with large bodies: only A = A op B / A = B op A (B loaded by FETCH*).
+// Binary operators with large bodies (out of line): A = S[k] op A or A = A op S[k].
 #define SRHIP_HEAVY_BINOPS(X) X(POW, pow) X(MOD, mod) X(ATAN2, atan2)
 #define SRHIP_UNOPS(X)                                                                         \
   X(NEG, neg) X(SQUARE, square) X(CUBE, cube) X(ABS, abs) X(RELU, relu) X(COS, cos) X(SIN, sin) \
@@ -54,22 +53,23 @@ enum Unop : int {
 // ---- handler ids -----------------------------------------------------------------------------
 enum : uint32_t {
   H_END = 0,
-  H_LOADF = 1,  // A = X[a]
-  H_LOADC = 2,  // A = imm
-  H_FETCHF = 3, // B = X[a]
-  H_FETCHC = 4, // B = imm
-  H_PUSH0 = 5,  // S[k] = A           (k < K_MAX)
-  H_FETCHS0 = H_PUSH0 + K_MAX,        // B = S[k]
-  H_BIN0 = H_FETCHS0 + K_MAX,         // specialised binary ops, SPEC_STRIDE handlers each
+  H_LOADF = 1,                        // A = X[a]
+  H_LOADC = 2,                        // A = imm
+  H_SLOADF0 = 3,                      // S[k] = X[a]   (operand of a heavy binary op)
+  H_SLOADC0 = H_SLOADF0 + K_MAX,      // S[k] = imm
+  H_PUSH0 = H_SLOADC0 + K_MAX,        // S[k] = A
+  H_BIN0 = H_PUSH0 + K_MAX,           // specialised binary ops, SPEC_STRIDE handlers each
 };
 constexpr uint32_t SPEC_AF = 0, SPEC_FA = 1, SPEC_AC = 2, SPEC_CA = 3, SPEC_SA0 = 4,
                    SPEC_AS0 = 4 + K_MAX, SPEC_STRIDE = 4 + 2 * K_MAX;
-constexpr uint32_t H_HEAVY0 = H_BIN0 + NUM_SPEC_BIN * SPEC_STRIDE;  // +0 AB (A=A op B), +1 BA
-constexpr uint32_t H_UN0 = H_HEAVY0 + 2 * NUM_HEAVY_BIN;
+// heavy binary ops take their second operand from a stack slot: A = S[k] op A, or A = A op S[k]
+constexpr uint32_t HEAVY_SA0 = 0, HEAVY_AS0 = K_MAX, HEAVY_STRIDE = 2 * K_MAX;
+constexpr uint32_t H_HEAVY0 = H_BIN0 + NUM_SPEC_BIN * SPEC_STRIDE;
+constexpr uint32_t H_UN0 = H_HEAVY0 + NUM_HEAVY_BIN * HEAVY_STRIDE;
 constexpr uint32_t H_COUNT = H_UN0 + NUM_UNOP;
 
 constexpr uint32_t h_spec(int sb, uint32_t form) { return H_BIN0 + uint32_t(sb) * SPEC_STRIDE + form; }
-constexpr uint32_t h_heavy(int hb, bool ba) { return H_HEAVY0 + uint32_t(hb) * 2 + (ba ? 1u : 0u); }
+constexpr uint32_t h_heavy(int hb, uint32_t form) { return H_HEAVY0 + uint32_t(hb) * HEAVY_STRIDE + form; }
 constexpr uint32_t h_un(int u) { return H_UN0 + uint32_t(u); }
 
 struct __attribute__((aligned(16))) Ins {
