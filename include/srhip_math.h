@@ -290,17 +290,16 @@ SRM_FN double srm_tan(double x) {
  *   expf: x = k ln2 + r in Float64 (ln2 as a double pair, fma), degree-10 Taylor (< 2^-42).
  *   logf: srm_log on the widened value (exact: every float is a normal double). */
 /* __kernel_cosdf / __kernel_sindf coefficients (FreeBSD k_cosf.c / k_sinf.c, |error| < 2^-34 on
- * [-pi/4, pi/4]), evaluated as cos y = Q_C(z), sin y = y Q_S(z), z = y^2, Q_K(z) = 1 + K0 z + K1 z^2
- * + K2 z^3 + K3 z^4 by fma Horner; one polynomial per row with per-row coefficients, since a SIMD
- * lane would otherwise evaluate both kernels. */
-SRM_FN double srm_ksincosdf(double y, int odd) {
-  const double K0 = odd ? -0.16666666641626524 : -0.499999997251031;
-  const double K1 = odd ? 0.008333329385889463 : 0.04166662332373906;
-  const double K2 = odd ? -0.00019839334836096632 : -0.001388676377460993;
-  const double K3 = odd ? 2.718311493989822e-06 : 2.439044879627741e-05;
-  const double z = y * y;
-  const double q = srm_fma(z, srm_fma(z, srm_fma(z, srm_fma(z, K3, K2), K1), K0), 1.0);
-  return odd ? y * q : q;
+ * [-pi/4, pi/4]), evaluated by fma Horner as cos y = Q_C(z), sin y = y Q_S(z), z = y^2,
+ * Q_K(z) = 1 + K0 z + K1 z^2 + K2 z^3 + K3 z^4.  Both polynomials are evaluated and the quadrant
+ * selects one: a SIMD lane would otherwise pay a per-row select for every coefficient. */
+SRM_FN double srm_qcos(double z) {
+  return srm_fma(z, srm_fma(z, srm_fma(z, srm_fma(z, 2.439044879627741e-05, -0.001388676377460993),
+                                       0.04166662332373906), -0.499999997251031), 1.0);
+}
+SRM_FN double srm_qsin(double z) {
+  return srm_fma(z, srm_fma(z, srm_fma(z, srm_fma(z, 2.718311493989822e-06, -0.00019839334836096632),
+                                       0.008333329385889463), -0.16666666641626524), 1.0);
 }
 /* returns n (quadrant), *y the reduced argument; x finite.  |x| < 2^28 pi/2: y = x - n (pi/2) with
  * pi/2 as a double pair and two fmas (each one rounding; |y| error < 2^-50 relative for every
@@ -321,25 +320,30 @@ SRM_FN int srm_rem_pio2f(float xf, double* y) {
   return (int)fn;
 }
 SRM_FN float srm_cosf(float x) {
-  if (!(x - x == 0.0f)) return x - x; /* Inf, NaN -> NaN */
+  const int fin = x - x == 0.0f; /* Inf / NaN -> NaN, selected at the end (no branch) */
   double y;
-  const int n = srm_rem_pio2f(x, &y);
-  const double r = srm_ksincosdf(y, n & 1);
-  return (float)(((n + 1) & 2) ? -r : r);
+  const int n = srm_rem_pio2f(fin ? x : 0.0f, &y);
+  const double z = y * y, c = srm_qcos(z), s = y * srm_qsin(z);
+  const double r = (n & 1) ? s : c;
+  const float res = (float)(((n + 1) & 2) ? -r : r);
+  return fin ? res : x - x;
 }
 SRM_FN float srm_sinf(float x) {
-  if (!(x - x == 0.0f)) return x - x;
+  const int fin = x - x == 0.0f;
   double y;
-  const int n = srm_rem_pio2f(x, &y);
-  const double r = srm_ksincosdf(y, (n & 1) ^ 1);
-  return (float)((n & 2) ? -r : r);
+  const int n = srm_rem_pio2f(fin ? x : 0.0f, &y);
+  const double z = y * y, c = srm_qcos(z), s = y * srm_qsin(z);
+  const double r = (n & 1) ? c : s;
+  const float res = (float)((n & 2) ? -r : r);
+  return fin ? res : x - x;
 }
 SRM_FN float srm_tanf(float x) {
-  if (!(x - x == 0.0f)) return x - x;
+  const int fin = x - x == 0.0f;
   double y;
-  const int n = srm_rem_pio2f(x, &y);
-  const double c = srm_ksincosdf(y, 0), s = srm_ksincosdf(y, 1);
-  return (float)((n & 1) ? -c / s : s / c);
+  const int n = srm_rem_pio2f(fin ? x : 0.0f, &y);
+  const double z = y * y, c = srm_qcos(z), s = y * srm_qsin(z);
+  const float res = (float)((n & 1) ? -c / s : s / c);
+  return fin ? res : x - x;
 }
 SRM_FN float srm_expf(float xf) {
   const double invln2 = 1.4426950408889634, ln2_hi = 0.6931471805599453, ln2_lo = 2.3190468138462996e-17;

@@ -588,6 +588,9 @@ LaunchPlan srhip::plan_launch(const srhip_ctx* ctx, int dtype, int64_t nfeat, bo
   while (rb > tile && (size_t)ncols * rb * es > budget) rb /= 2;
   // do not make blocks much larger than the data
   while (rb > tile && rb / 2 >= m) rb /= 2;
+  // diagnostic override (tuning runs): SRHIP_RB_ROWS = rows per workgroup, a power of two >= tile
+  static const int rb_env = [] { const char* e = getenv("SRHIP_RB_ROWS"); return e ? atoi(e) : 0; }();
+  if (rb_env >= tile && rb_env <= ROW_ALIGN && (rb_env & (rb_env - 1)) == 0 && rb_env < rb) rb = rb_env;
   L.rb_rows = rb;
   L.xlds = (size_t)ncols * rb * es <= budget;
   L.lds = (L.xlds ? (size_t)ncols * rb * es : 0) + 16;

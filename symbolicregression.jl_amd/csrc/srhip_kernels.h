@@ -7,7 +7,10 @@
 
 namespace srhip {
 
-constexpr int EVAL_WAVES = 8;  // wavefronts per workgroup of the interpreter kernel
+#ifndef SRHIP_EVAL_WAVES
+#define SRHIP_EVAL_WAVES 8
+#endif
+constexpr int EVAL_WAVES = SRHIP_EVAL_WAVES;  // wavefronts per workgroup of the interpreter kernel
 #ifndef SRHIP_R_F32
 #define SRHIP_R_F32 8
 #endif
