@@ -34,6 +34,8 @@ def parse():
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--binops", default="+,-,*,/", help="(tuning) binary operators of the C2 population")
+    ap.add_argument("--unaops", default="cos,exp", help="(tuning) unary operators of the C2 population")
     ap.add_argument("--config", default="c2", choices=("c2", "c4"),
                     help="c2 (default, the headline metric) or c4: batched constant optimisation")
     return ap.parse_args()
@@ -59,7 +61,8 @@ def main():
 
     import srhip
 
-    opts = srhip.Options(binary_operators=("+", "-", "*", "/"), unary_operators=("cos", "exp"))
+    opts = srhip.Options(binary_operators=tuple(o for o in args.binops.split(",") if o),
+                         unary_operators=tuple(o for o in args.unaops.split(",") if o))
     nfeat, n = 5, args.rows
     rng = np.random.default_rng(0 + 1000 * rank)
     X = rng.standard_normal((nfeat, n)).astype(np.float32)

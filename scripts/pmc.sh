@@ -15,10 +15,13 @@ while read -r counters; do
   rc=$?
   echo "  rc=$rc"
   [ $rc -eq 0 ] || exit $rc
-done <<'LIST'
+done <<LIST
+${PMC_LIST:-$(cat <<'DEFAULT'
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VMEM GRBM_GUI_ACTIVE
 SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_IFETCH SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE
 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_CVT
 FETCH_SIZE GRBM_GUI_ACTIVE
 WRITE_SIZE GRBM_GUI_ACTIVE
+DEFAULT
+)}
 LIST

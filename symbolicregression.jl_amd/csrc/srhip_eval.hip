@@ -35,6 +35,9 @@
     if (p.dbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                      \
       __hip_atomic_store(p.dbg + (slot), (int32_t)(val), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
   } while (0)
+#ifndef SRHIP_HEAVY_ILP
+#define SRHIP_HEAVY_ILP 1  // rows a heavy operator body may interleave
+#endif
 #ifndef SRHIP_ROW_FENCE
 #define SRHIP_ROW_FENCE() __builtin_amdgcn_sched_barrier(0)
 #endif
@@ -109,7 +112,7 @@ __device__ __attribute__((noinline)) RV<T, R> heavy_un(RV<T, R> v) {
       default: break;
     }
     v[r] = x;
-    SRHIP_ROW_FENCE();  // one row at a time: bounds the callee's registers (and so the kernel's)
+    if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();  // rows in groups: bounds the callee's registers
   }
   return v;
 }
@@ -126,7 +129,7 @@ __device__ __attribute__((noinline)) RV<T, R> heavy_bin(RV<T, R> a, RV<T, R> b) 
       default: break;
     }
     a[r] = x;
-    SRHIP_ROW_FENCE();
+    if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
   }
   return a;
 }
