@@ -301,56 +301,57 @@ SRM_FN double srm_qsin(double z) {
   return srm_fma(z, srm_fma(z, srm_fma(z, srm_fma(z, 2.718311493989822e-06, -0.00019839334836096632),
                                        0.008333329385889463), -0.16666666641626524), 1.0);
 }
-/* returns n (quadrant), *y the reduced argument; x finite.  |x| < 2^28 pi/2: y = x - n (pi/2) with
- * pi/2 as a double pair and two fmas (each one rounding; |y| error < 2^-50 relative for every
- * float x in range); larger |x|: the shared Payne-Hanek (one rarely taken branch per wave). */
-SRM_FN int srm_rem_pio2f(float xf, double* y) {
-  const double x = (double)xf;
-  const double ax = x < 0.0 ? -x : x;
-  if (!(ax < 421657428.2663131)) {
-    double y0, y1;
-    const int n = srm_rem_pio2_large(x, &y0, &y1);
-    *y = y0;
-    return n;
-  }
+/* Float32 trig in three shared pieces, so a batched caller (the device evaluates R rows per lane)
+ * can run the fast reduction for every row and the Payne-Hanek path only when some row needs it,
+ * and still produce bit-identical values:
+ *   srm_rem_pio2f_fast: |x| < SRM_PIO2F_BIG (2^28 pi/2): n = rint(x 2/pi), y = x - n (pi/2) with
+ *     pi/2 as a double pair and two fmas (each one rounding; |y| error < 2^-50 relative for every
+ *     float x in range);
+ *   srm_rem_pio2f_big: larger |x|, the shared Payne-Hanek;
+ *   srm_trigf_finish: quadrant selection of the two polynomials and the one rounding to Float32. */
+#define SRM_PIO2F_BIG 421657428.2663131
+SRM_FN int srm_rem_pio2f_fast(double x, double* y) {
   const double invpio2 = 6.36619772367581382433e-01, pio2_hi = 1.5707963267948966,
                pio2_lo = 6.123233995736766e-17;
   const double fn = srm_rint(x * invpio2);
   *y = srm_fma(-fn, pio2_lo, srm_fma(-fn, pio2_hi, x));
   return (int)fn;
 }
-SRM_FN float srm_cosf(float x) {
+SRM_FN int srm_rem_pio2f_big(double x, double* y) {
+  double y0, y1;
+  const int n = srm_rem_pio2_large(x, &y0, &y1);
+  *y = y0;
+  return n;
+}
+SRM_FN int srm_pio2f_is_big(double x) { return !(__builtin_fabs(x) < SRM_PIO2F_BIG); }
+/* returns n (quadrant), *y the reduced argument; x finite */
+SRM_FN int srm_rem_pio2f(float xf, double* y) {
+  const double x = (double)xf;
+  return srm_pio2f_is_big(x) ? srm_rem_pio2f_big(x, y) : srm_rem_pio2f_fast(x, y);
+}
+/* kind 0: cos, 1: sin, 2: tan of the reduced argument y in quadrant n */
+SRM_FN float srm_trigf_finish(int kind, int n, double y) {
+  const double z = y * y, c = srm_qcos(z), s = y * srm_qsin(z);
+  if (kind == 2) return (float)((n & 1) ? -c / s : s / c);
+  const int q = kind == 0 ? n + 1 : n;
+  const double r = ((n & 1) ^ kind) ? s : c;
+  return (float)((q & 2) ? -r : r);
+}
+SRM_FN float srm_trigf(int kind, float x) {
   const int fin = x - x == 0.0f; /* Inf / NaN -> NaN, selected at the end (no branch) */
   double y;
   const int n = srm_rem_pio2f(fin ? x : 0.0f, &y);
-  const double z = y * y, c = srm_qcos(z), s = y * srm_qsin(z);
-  const double r = (n & 1) ? s : c;
-  const float res = (float)(((n + 1) & 2) ? -r : r);
+  const float res = srm_trigf_finish(kind, n, y);
   return fin ? res : x - x;
 }
-SRM_FN float srm_sinf(float x) {
-  const int fin = x - x == 0.0f;
-  double y;
-  const int n = srm_rem_pio2f(fin ? x : 0.0f, &y);
-  const double z = y * y, c = srm_qcos(z), s = y * srm_qsin(z);
-  const double r = (n & 1) ? c : s;
-  const float res = (float)((n & 2) ? -r : r);
-  return fin ? res : x - x;
-}
-SRM_FN float srm_tanf(float x) {
-  const int fin = x - x == 0.0f;
-  double y;
-  const int n = srm_rem_pio2f(fin ? x : 0.0f, &y);
-  const double z = y * y, c = srm_qcos(z), s = y * srm_qsin(z);
-  const float res = (float)((n & 1) ? -c / s : s / c);
-  return fin ? res : x - x;
-}
+SRM_FN float srm_cosf(float x) { return srm_trigf(0, x); }
+SRM_FN float srm_sinf(float x) { return srm_trigf(1, x); }
+SRM_FN float srm_tanf(float x) { return srm_trigf(2, x); }
 SRM_FN float srm_expf(float xf) {
   const double invln2 = 1.4426950408889634, ln2_hi = 0.6931471805599453, ln2_lo = 2.3190468138462996e-17;
   double x = (double)xf;
   /* clamp to where the float result is already 0 or Inf (also maps NaN to a finite value) */
-  x = (x <= 89.0) ? x : 89.0;
-  x = (x >= -104.0) ? x : -104.0;
+  x = __builtin_fmin(__builtin_fmax(x, -104.0), 89.0);
   const double k = srm_rint(x * invln2);
   double r = srm_fma(-k, ln2_hi, x);
   r = srm_fma(-k, ln2_lo, r);

@@ -38,6 +38,9 @@
 #ifndef SRHIP_HEAVY_ILP
 #define SRHIP_HEAVY_ILP 1  // rows a heavy operator body may interleave
 #endif
+#ifndef SRHIP_TRIG_ROWS
+#define SRHIP_TRIG_ROWS 1  // Float32 cos/sin/tan batched over the rows (trigf_rows)
+#endif
 #ifndef SRHIP_ROW_FENCE
 #define SRHIP_ROW_FENCE() __builtin_amdgcn_sched_barrier(0)
 #endif
@@ -100,9 +103,42 @@ template <typename T> __device__ __attribute__((always_inline)) inline T imm_as(
 template <typename T, int R> struct RowVec { typedef T type __attribute__((ext_vector_type(R))); };
 template <typename T, int R> using RV = typename RowVec<T, R>::type;
 
+// Float32 cos/sin/tan over a lane's R rows: the fast reduction for every row, the Payne-Hanek
+// branch once per call (only if some row needs it), then the polynomials; the same pieces as the
+// scalar srm_trigf (include/srhip_math.h), so the values are bit-identical.
+// Rows with |x| >= 2^28 pi/2 redone by the scalar function (Payne-Hanek), out of line: a call in
+// the batched body would pin its live rows to callee-saved (high-numbered) VGPRs.
+template <int R, int KIND>
+__device__ __attribute__((noinline)) RV<float, R> trigf_fix(RV<float, R> v, RV<float, R> res) {
+  UNR for (int r = 0; r < R; ++r) {
+    const float x = v[r];
+    if (srm_pio2f_is_big((double)((x - x == 0.0f) ? x : 0.0f))) res[r] = srm_trigf(KIND, x);
+  }
+  return res;
+}
+template <int R, int KIND>
+__device__ __attribute__((always_inline)) inline RV<float, R> trigf_rows(RV<float, R> v) {
+  RV<float, R> res;
+  bool big = false;
+  UNR for (int r = 0; r < R; ++r) {
+    const float x = v[r];
+    const double xd = (double)((x - x == 0.0f) ? x : 0.0f);
+    const bool b = srm_pio2f_is_big(xd);
+    big |= b;
+    double y;
+    const int n = srm_rem_pio2f_fast(b ? 0.0 : xd, &y);
+    const float f = srm_trigf_finish(KIND, n, y);
+    res[r] = (x - x == 0.0f) ? f : x - x;
+  }
+  if (big) res = trigf_fix<R, KIND>(v, res);
+  return res;
+}
+
 template <typename T, int R, int U>
 __device__ __attribute__((noinline)) RV<T, R> heavy_un(RV<T, R> v) {
   using O = OpsT<T>;
+  if constexpr (SRHIP_TRIG_ROWS && std::is_same<T, float>::value && (U == UN_COS || U == UN_SIN || U == UN_TAN))
+    return trigf_rows<R, U == UN_COS ? 0 : (U == UN_SIN ? 1 : 2)>(v);
   UNR for (int r = 0; r < R; ++r) {
     T x = v[r];
     switch (U) {
