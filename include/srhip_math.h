@@ -281,13 +281,18 @@ SRM_FN double srm_tan(double x) {
 }
 
 /* ---- Float32 ---------------------------------------------------------------------------------
- * Every Float32 function evaluates in Float64 and rounds once.
- *   sinf/cosf/tanf: the FreeBSD s_sinf.c / s_cosf.c scheme that Julia Base restates for Float32
- *     (DoubleFloat32 kernels): reduction to [-pi/4, pi/4] in Float64, the degree-4 double
- *     polynomials of __kernel_cosdf / __kernel_sindf (|error| < 2^-34), one rounding to Float32.
- *     Written branch-free for a SIMD lane: one quadrant formula n = rint(2x/pi) instead of
- *     s_cosf.c's case analysis, an fma reduction, and a single polynomial per row.
- *   expf: x = k ln2 + r in Float64 (ln2 as a double pair, fma), degree-10 Taylor (< 2^-42).
+ * Every Float32 function evaluates in Float64 and rounds once (as Julia Base does for Float32
+ * sin/cos/exp: Float64 kernels, one rounding), so results are correctly rounded except when the
+ * Float64 value lies within ~2^-40 relative of a Float32 rounding boundary.
+ *   sinf/cosf, |x| < 2^28 pi/2: x = k pi + y with k an integer (sin) or half-integer (cos),
+ *     pi as a double pair and two fmas, |y| <= pi/2; then sin y = y P(y^2) with one degree-6
+ *     polynomial (relative error < 2^-43) and the sign of (-1)^k.  One polynomial and no quadrant
+ *     select: a SIMD lane pays for every branch of a per-row case analysis.
+ *   tanf, and sinf/cosf for |x| >= 2^28 pi/2: the FreeBSD s_tanf.c / s_cosf.c scheme (reduction to
+ *     [-pi/4, pi/4] by quadrant, Payne-Hanek when large, the degree-4 __kernel_cosdf/sindf
+ *     polynomials, |error| < 2^-34).
+ *   expf: x = k ln2 + r in Float64 (ln2 as a double pair, fma), degree-8 polynomial (< 2^-40),
+ *     exact scaling by 2^k, one rounding.
  *   logf: srm_log on the widened value (exact: every float is a normal double). */
 /* __kernel_cosdf / __kernel_sindf coefficients (FreeBSD k_cosf.c / k_sinf.c, |error| < 2^-34 on
  * [-pi/4, pi/4]), evaluated by fma Horner as cos y = Q_C(z), sin y = y Q_S(z), z = y^2,
@@ -337,12 +342,37 @@ SRM_FN float srm_trigf_finish(int kind, int n, double y) {
   const double r = ((n & 1) ^ kind) ? s : c;
   return (float)((q & 2) ? -r : r);
 }
+/* sin y / y = P(y^2) on |y| <= pi/2 (+1e-4): minimax on relative error, < 2^-43.5 */
+SRM_FN double srm_psin(double z) {
+  double p = 1.54087455323602e-10;
+  p = srm_fma(p, z, -2.503013916297275e-08);
+  p = srm_fma(p, z, 2.7556951471409603e-06);
+  p = srm_fma(p, z, -0.0001984126670887231);
+  p = srm_fma(p, z, 0.008333333320988472);
+  p = srm_fma(p, z, -0.16666666666503963);
+  return srm_fma(p, z, 1.0);
+}
+SRM_FN uint32_t srm_bitsf(float x) { uint32_t u; __builtin_memcpy(&u, &x, 4); return u; }
+SRM_FN float srm_from_bitsf(uint32_t u) { float x; __builtin_memcpy(&x, &u, 4); return x; }
+/* kind 0: cos, 1: sin of a finite x with |x| < SRM_PIO2F_BIG.
+ *   sin: k = rint(x/pi),       y = x - k pi, sin x = (-1)^k sin y
+ *   cos: k = rint(x/pi - 1/2), y = x - (k + 1/2) pi, cos x = (-1)^(k+1) sin y */
+SRM_FN float srm_sincosf_fast(int kind, double x) {
+  const double invpi = 0.3183098861837907, pi_hi = 3.141592653589793, pi_lo = 1.2246467991473532e-16;
+  double k = srm_rint(srm_fma(x, invpi, kind == 0 ? -0.5 : 0.0));
+  const int m = (int)k;
+  if (kind == 0) k += 0.5;
+  const double y = srm_fma(-k, pi_lo, srm_fma(-k, pi_hi, x));
+  const float r = (float)(y * srm_psin(y * y));
+  return srm_from_bitsf(srm_bitsf(r) ^ ((uint32_t)(m + (kind == 0)) << 31));
+}
 SRM_FN float srm_trigf(int kind, float x) {
-  const int fin = x - x == 0.0f; /* Inf / NaN -> NaN, selected at the end (no branch) */
+  if (!(x - x == 0.0f)) return x - x; /* Inf / NaN -> NaN */
+  const double xd = (double)x;
+  if (kind != 2 && !srm_pio2f_is_big(xd)) return srm_sincosf_fast(kind, xd);
   double y;
-  const int n = srm_rem_pio2f(fin ? x : 0.0f, &y);
-  const float res = srm_trigf_finish(kind, n, y);
-  return fin ? res : x - x;
+  const int n = srm_rem_pio2f(x, &y);
+  return srm_trigf_finish(kind, n, y);
 }
 SRM_FN float srm_cosf(float x) { return srm_trigf(0, x); }
 SRM_FN float srm_sinf(float x) { return srm_trigf(1, x); }
@@ -355,20 +385,18 @@ SRM_FN float srm_expf(float xf) {
   const double k = srm_rint(x * invln2);
   double r = srm_fma(-k, ln2_hi, x);
   r = srm_fma(-k, ln2_lo, r);
-  double p = 2.505210838544172e-08;     /* 1/11! */
-  p = srm_fma(p, r, 2.755731922398589e-07);
-  p = srm_fma(p, r, 2.7557319223985893e-06);
-  p = srm_fma(p, r, 2.48015873015873e-05);
-  p = srm_fma(p, r, 1.984126984126984e-04);
-  p = srm_fma(p, r, 1.388888888888889e-03);
-  p = srm_fma(p, r, 8.333333333333333e-03);
-  p = srm_fma(p, r, 4.1666666666666664e-02);
-  p = srm_fma(p, r, 1.6666666666666666e-01);
-  p = srm_fma(p, r, 0.5);
+  /* exp r = 1 + r Q(r) on |r| <= ln2/2 (+1e-4): minimax on relative error, < 2^-40 */
+  double p = 2.4736025668457734e-05;
+  p = srm_fma(p, r, 0.00019914637854529652);
+  p = srm_fma(p, r, 0.0013889148047310426);
+  p = srm_fma(p, r, 0.008333268860258102);
+  p = srm_fma(p, r, 0.04166666458462912);
+  p = srm_fma(p, r, 0.16666666872538483);
+  p = srm_fma(p, r, 0.5000000000448828);
+  p = srm_fma(p, r, 0.9999999999832456);
   p = srm_fma(p, r, 1.0);
-  p = srm_fma(p, r, 1.0);
-  const double sc = srm_from_bits((uint64_t)(uint32_t)((int)k + 1023) << 52); /* |k| <= 151 */
-  const float res = (float)(p * sc);
+  /* |k| <= 151: p 2^k is exact in Float64 (no rounding before the one to Float32) */
+  const float res = (float)__builtin_ldexp(p, (int)k);
   return (xf == xf) ? res : xf;
 }
 SRM_FN float srm_logf(float x) { return (float)srm_log((double)x); }

@@ -103,16 +103,16 @@ template <typename T> __device__ __attribute__((always_inline)) inline T imm_as(
 template <typename T, int R> struct RowVec { typedef T type __attribute__((ext_vector_type(R))); };
 template <typename T, int R> using RV = typename RowVec<T, R>::type;
 
-// Float32 cos/sin/tan over a lane's R rows: the fast reduction for every row, the Payne-Hanek
-// branch once per call (only if some row needs it), then the polynomials; the same pieces as the
+// Float32 cos/sin/tan over a lane's R rows.  Every row takes the fast path (|x| < 2^28 pi/2 after
+// mapping Inf/NaN and large |x| to 0); rows that are finite and large are redone by the scalar
+// srm_trigf out of line, once per call and only if some row needs it.  The same pieces as the
 // scalar srm_trigf (include/srhip_math.h), so the values are bit-identical.
-// Rows with |x| >= 2^28 pi/2 redone by the scalar function (Payne-Hanek), out of line: a call in
-// the batched body would pin its live rows to callee-saved (high-numbered) VGPRs.
+// (A call inside the batched body would pin its live rows to callee-saved, high-numbered VGPRs.)
 template <int R, int KIND>
 __device__ __attribute__((noinline)) RV<float, R> trigf_fix(RV<float, R> v, RV<float, R> res) {
   UNR for (int r = 0; r < R; ++r) {
     const float x = v[r];
-    if (srm_pio2f_is_big((double)((x - x == 0.0f) ? x : 0.0f))) res[r] = srm_trigf(KIND, x);
+    if (x - x == 0.0f && srm_pio2f_is_big((double)x)) res[r] = srm_trigf(KIND, x);
   }
   return res;
 }
@@ -122,13 +122,20 @@ __device__ __attribute__((always_inline)) inline RV<float, R> trigf_rows(RV<floa
   bool big = false;
   UNR for (int r = 0; r < R; ++r) {
     const float x = v[r];
-    const double xd = (double)((x - x == 0.0f) ? x : 0.0f);
-    const bool b = srm_pio2f_is_big(xd);
-    big |= b;
-    double y;
-    const int n = srm_rem_pio2f_fast(b ? 0.0 : xd, &y);
-    const float f = srm_trigf_finish(KIND, n, y);
-    res[r] = (x - x == 0.0f) ? f : x - x;
+    const bool fin = x - x == 0.0f;
+    const double xd = (double)x;
+    const bool b = srm_pio2f_is_big(xd);  // also true for Inf / NaN
+    big |= b && fin;
+    const double xs = b ? 0.0 : xd;
+    float f;
+    if constexpr (KIND == 2) {
+      double y;
+      const int n = srm_rem_pio2f_fast(xs, &y);
+      f = srm_trigf_finish(KIND, n, y);
+    } else {
+      f = srm_sincosf_fast(KIND, xs);
+    }
+    res[r] = fin ? f : x - x;
   }
   if (big) res = trigf_fix<R, KIND>(v, res);
   return res;
@@ -212,9 +219,11 @@ __device__ __attribute__((always_inline)) inline void apply_heavy(T (&A)[R], con
 template <typename T> struct Chk {
   using type = T;
 };
+// Float32: one v_maximum3_f32 per two rows, chained through M (the compiler's reassociation into
+// a pairwise tree costs R/2 + 2 instructions instead of R/2).
 template <int R> __device__ __attribute__((always_inline)) inline void chk_update(float& M, const float (&A)[R]) {
   UNR for (int r = 0; r < R; r += 2)
-    M = __builtin_elementwise_maximum(M, __builtin_elementwise_maximum(__builtin_fabsf(A[r]), __builtin_fabsf(A[r + 1])));
+    asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(M) : "v"(M), "v"(A[r]), "v"(A[r + 1]));
 }
 template <int R> __device__ __attribute__((always_inline)) inline void chk_update(double& M, const double (&A)[R]) {
   UNR for (int r = 0; r < R; ++r) M = __builtin_fma(__builtin_fabs(A[r]), 0x1p-512, M);
