@@ -661,8 +661,22 @@ static hipError_t launch_eval_m(const EvalArgs& a, int K, int mode, bool xlds, d
 
 int rows_per_lane(int dtype) { return dtype == SRHIP_F64 ? R_F64 : R_F32; }
 
-hipError_t launch_eval(int dtype, const EvalArgs& a, int K, int mode, bool xlds, dim3 grid, size_t lds,
+int pick_rows_per_lane(int dtype, int K, int mode, int64_t m) {
+  if (dtype == SRHIP_F32 && K <= 2 && mode != MODE_PRECISE && m >= WIDE_MIN_ROWS && R_F32_WIDE != R_F32)
+    return R_F32_WIDE;
+  return rows_per_lane(dtype);
+}
+
+hipError_t launch_eval(int dtype, const EvalArgs& a, int R, int K, int mode, bool xlds, dim3 grid, size_t lds,
                        hipStream_t s) {
+  if (R != pick_rows_per_lane(dtype, K, mode, a.nvalid)) return hipErrorInvalidValue;
+  if (R == R_F32_WIDE && R != R_F32) {  // Float32, K = 2, loss or prediction
+    if (mode == MODE_LOSS)
+      return xlds ? launch_eval_t<float, R_F32_WIDE, 2, MODE_LOSS, true>(a, grid, lds, s)
+                  : launch_eval_t<float, R_F32_WIDE, 2, MODE_LOSS, false>(a, grid, lds, s);
+    return xlds ? launch_eval_t<float, R_F32_WIDE, 2, MODE_PRED, true>(a, grid, lds, s)
+                : launch_eval_t<float, R_F32_WIDE, 2, MODE_PRED, false>(a, grid, lds, s);
+  }
   switch (dtype) {
     case SRHIP_F32: return launch_eval_m<float, R_F32>(a, K, mode, xlds, grid, lds, s);
     case SRHIP_F64: return launch_eval_m<double, R_F64>(a, K, mode, xlds, grid, lds, s);

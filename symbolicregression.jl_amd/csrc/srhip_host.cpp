@@ -734,7 +734,12 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     if (!P->info[t].static_fail) live.push_back(t);
   if (live.empty()) return SRHIP_OK;
   const size_t es = dtype_size(dtype);
-  LaunchPlan L = plan_launch(ctx, dtype, nf, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * rows_per_lane(dtype));
+  // stack slots of the kernel variant; the wide operators live only in the K_MAX variant
+  bool wide = false;
+  for (int32_t u : P->unaops) wide |= u == SRHIP_OP_ASIN || u == SRHIP_OP_ACOS || u == SRHIP_OP_ATANH_CLIP;
+  const int K = wide ? K_MAX : (P->kmax <= 2 ? 2 : (P->kmax <= 4 ? 4 : 8));
+  const int R = pick_rows_per_lane(dtype, K, mode, v.m);
+  LaunchPlan L = plan_launch(ctx, dtype, nf, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R);
   const int nl = (int)live.size();
   std::vector<int32_t> order = make_order(*P, live, L.groups, L.tpg);
   HIP_TRY(ctx->order_prec.ensure(order.size() * sizeof(int32_t)));
@@ -778,13 +783,9 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     HIP_TRY(pred.ensure((size_t)nt * v.m * es));
     a.out_pred = pred.p;
   }
-  // stack slots of the kernel variant; the wide operators live only in the K_MAX variant
-  bool wide = false;
-  for (int32_t u : P->unaops) wide |= u == SRHIP_OP_ASIN || u == SRHIP_OP_ACOS || u == SRHIP_OP_ATANH_CLIP;
-  const int K = wide ? K_MAX : (P->kmax <= 2 ? 2 : (P->kmax <= 4 ? 4 : 8));
   dim3 grid(L.nrb, L.groups);
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
-  HIP_TRY(launch_eval(dtype, a, K, mode, L.xlds, grid, L.lds, ctx->stream));
+  HIP_TRY(launch_eval(dtype, a, R, K, mode, L.xlds, grid, L.lds, ctx->stream));
   HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
   ctx->timed = true;
   if (trace_on()) {  // poll the kernel's progress words for up to 10 s, then abort loudly
@@ -838,7 +839,8 @@ static int eval_precise(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pro
   const int stride = std::max(1, P->max_ops);
   for (size_t i = 0; i < (size_t)nu * stride; ++i) opsums[i] = 0.0;
   if (nu == 0 || dtype == SRHIP_I32) return SRHIP_OK;
-  LaunchPlan Lp = plan_launch(ctx, dtype, ds->nfeat, false, false, v.m, nu, 64 * rows_per_lane(dtype));
+  const int R = pick_rows_per_lane(dtype, K_MAX, MODE_PRECISE, v.m);
+  LaunchPlan Lp = plan_launch(ctx, dtype, ds->nfeat, false, false, v.m, nu, 64 * R);
   Lp.groups = 1;
   Lp.tpg = nu;
   const size_t slab_bytes = (size_t)nu * stride * Lp.nrb * sizeof(double);
@@ -861,7 +863,7 @@ static int eval_precise(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pro
   a.slab_prec = ctx->slab_prec.p;
   a.prec_stride = stride;
   a.max_steps = P->max_len;
-  HIP_TRY(launch_eval(dtype, a, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, 1), 16, ctx->stream));
+  HIP_TRY(launch_eval(dtype, a, R, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, 1), 16, ctx->stream));
   HIP_TRY(ctx->h_prec.ensure(slab_bytes));
   HIP_TRY(hipMemcpyAsync(ctx->h_prec.p, ctx->slab_prec.p, slab_bytes, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));

@@ -16,6 +16,11 @@ constexpr int EVAL_WAVES = SRHIP_EVAL_WAVES;  // wavefronts per workgroup of the
 #endif
 constexpr int R_F32 = SRHIP_R_F32;  // rows per lane per dispatch, 4-byte types
 constexpr int R_F64 = 4;       // rows per lane per dispatch, Float64
+// Float32 trees whose stack fits K = 2 on datasets of at least WIDE_MIN_ROWS rows run with twice
+// the rows per lane: the per-instruction dispatch cost is paid once per 16 rows (121 VGPRs,
+// 4 waves per SIMD; the VALU-bound operators are unaffected, the cheap ones get ~20 % faster).
+constexpr int R_F32_WIDE = 16;
+constexpr int64_t WIDE_MIN_ROWS = 4096;
 constexpr int ROW_ALIGN = 4096;  // device datasets are padded to a multiple of this many rows
 constexpr int MODE_LOSS = 0, MODE_PRED = 1, MODE_PRECISE = 2;
 
@@ -54,7 +59,9 @@ struct EvalArgs {
 };
 
 int rows_per_lane(int dtype);
-hipError_t launch_eval(int dtype, const EvalArgs& a, int K, int mode, bool xlds, dim3 grid, size_t lds,
+// rows per lane of the kernel variant that evaluates a launch (K stack slots, mode, m rows)
+int pick_rows_per_lane(int dtype, int K, int mode, int64_t m);
+hipError_t launch_eval(int dtype, const EvalArgs& a, int R, int K, int mode, bool xlds, dim3 grid, size_t lds,
                        hipStream_t s);
 hipError_t launch_reduce(int dtype, const void* slab_loss, const void* slab_chk, int nrb, int ntrees, void* out_loss,
                          void* out_chk, hipStream_t s);
