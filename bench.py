@@ -123,6 +123,12 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(nodes, offs, opts, X, y, args.cpu_seconds)
 
+    # the kernel variant the library picks for this launch (csrc/srhip_eval.hip pick_rows_per_lane)
+    kst = 2 if st["max_stack"] <= 2 else (4 if st["max_stack"] <= 4 else 8)
+    rpl = 16 if (kst == 2 and n >= 4096) else 8
+    kname = f"srhip::eval_kernel<float, {rpl}, {kst}, 0, true>"
+    traffic, traffic_src = pmc_traffic(kname)
+
     if rank == 0:
         out = {
             "metric": "tree-node x row evals/sec (whole node), 1k trees x 1M rows f32; % VALU peak",
@@ -151,8 +157,9 @@ def main():
                 "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / PEAK_FP32_TFLOPS,
-                "traffic": None,
-                "kernel": "srhip::eval_kernel<float,8,K,0,true>",
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "kernel": kname,
                 "kernel_ms": kern_ms,
                 "flops_per_launch": int(flops),
             },
@@ -163,6 +170,26 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def pmc_traffic(kname):
+    """HBM bytes per launch of the eval kernel from the committed rocprofv3 --pmc summary of this
+    same command (scripts/pmc.sh + scripts/pmc_summary.py --json; separate counter passes, FETCH_SIZE
+    doubled per MI355X_MICROARCH.md).  None if no summary for this kernel variant is committed."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_c2*.json")))
+    if not files:
+        return None, None
+    try:
+        summ = json.load(open(files[-1]))
+    except (OSError, ValueError):
+        return None, None
+    want = kname.replace("srhip::", "").replace(" ", "")
+    for k, d in summ.items():
+        if want in k.replace(" ", "") and "hbm_bytes" in d:
+            return d["hbm_bytes"], os.path.relpath(files[-1], ROOT)
+    return None, None
 
 
 def cpu_baseline(nodes, offs, opts, X, y, target_s):
