@@ -235,6 +235,38 @@ double srhip_last_kernel_ms(const srhip_ctx* ctx);
 int srhip_program_stats(const srhip_program* prog, int64_t* total_nodes, int64_t* total_opnodes,
                         int32_t* max_stack);
 
+/* ---- Cross-population request coalescer (8(b) "Threading") ----------------
+ * The reference scores one tree per mutation from every population task concurrently
+ * (score_func in next_generation, src/Mutate.jl:268-274, under Threads.@spawn per population,
+ * src/SymbolicRegression.jl:964-987 / src/SearchUtils.jl:121-122).  A batcher owns one context
+ * and one device dataset; any number of threads submit single-tree score requests and block on
+ * their ticket; one worker thread flushes the queue as ONE program + ONE srhip_eval_loss launch
+ * when max_batch requests are queued, when every registered client is waiting (nclients > 0), or
+ * max_wait_us after the oldest request.  Requests with different row subsets (batching `idx`)
+ * go to separate launches of the same flush.  Results are exactly those of srhip_eval_loss on
+ * the single tree (the kernel's per-tree results do not depend on the batch).  Thread-safe; the
+ * context must not be used by other callers while the batcher lives. */
+typedef struct srhip_batcher srhip_batcher;
+int srhip_batcher_create(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_operators* ops,
+                         const srhip_loss* loss, int32_t max_batch, int32_t max_wait_us,
+                         srhip_batcher** out);
+/* expected number of concurrent clients (0 = unknown: flush on max_batch / max_wait_us only) */
+int srhip_batcher_set_clients(srhip_batcher* b, int32_t nclients);
+/* one tree (nodes[0] is its root); idx = optional 0-based row subset (copied) */
+int srhip_batcher_submit(srhip_batcher* b, const srhip_node* nodes, int64_t nnodes,
+                         const int64_t* idx, int64_t nidx, uint64_t* ticket);
+/* blocks until the ticket's batch ran; returns that request's status (errors carry the message
+ * of the failed compile / launch, readable with srhip_last_error on the waiting thread) */
+int srhip_batcher_wait(srhip_batcher* b, uint64_t ticket, double* out_loss, uint8_t* out_ok);
+/* submit + wait */
+int srhip_batcher_eval(srhip_batcher* b, const srhip_node* nodes, int64_t nnodes,
+                       const int64_t* idx, int64_t nidx, double* out_loss, uint8_t* out_ok);
+/* requests served, device launches, largest batch */
+int srhip_batcher_stats(const srhip_batcher* b, int64_t* nrequests, int64_t* nlaunches,
+                        int64_t* max_batch_seen);
+/* drains the queue (pending requests are evaluated), joins the worker */
+void srhip_batcher_destroy(srhip_batcher* b);
+
 #ifdef __cplusplus
 }
 #endif

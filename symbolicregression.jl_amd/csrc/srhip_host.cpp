@@ -981,6 +981,7 @@ void srhip_ctx_destroy(srhip_ctx* ctx) {
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
+  (void)hipGetLastError();
 }
 
 int srhip_ctx_synchronize(srhip_ctx* ctx) {
@@ -1001,6 +1002,7 @@ int srhip_dataset_create(srhip_ctx* ctx, int dtype, const void* X, int64_t nfeat
   HIP_TRY(hipSetDevice(ctx->device));
   std::unique_ptr<srhip_dataset> d(new srhip_dataset());
   d->ctx = ctx;
+  d->device = ctx->device;
   d->dtype = dtype;
   d->nfeat = nfeat;
   d->n = n;
@@ -1052,8 +1054,9 @@ int srhip_dataset_create(srhip_ctx* ctx, int dtype, const void* X, int64_t nfeat
 
 void srhip_dataset_destroy(srhip_dataset* ds) {
   if (!ds) return;
-  (void)hipSetDevice(ds->ctx->device);
+  (void)hipSetDevice(ds->device);
   delete ds;
+  (void)hipGetLastError();  // no sticky error from the ignored calls above
 }
 
 int srhip_program_create(srhip_ctx* ctx, int dtype, const srhip_node* nodes, const int64_t* offsets, int32_t ntrees,
@@ -1064,6 +1067,7 @@ int srhip_program_create(srhip_ctx* ctx, int dtype, const srhip_node* nodes, con
   if (dtype != SRHIP_F32 && dtype != SRHIP_F64 && dtype != SRHIP_I32) return fail(SRHIP_ERR_UNSUPPORTED, "dtype %d", dtype);
   std::unique_ptr<srhip_program> P(new srhip_program());
   P->ctx = ctx;
+  P->device = ctx ? ctx->device : -1;
   P->dtype = dtype;
   P->ntrees = ntrees;
   for (int i = 0; i < ops->nbin; ++i) {
@@ -1094,8 +1098,9 @@ int srhip_program_create(srhip_ctx* ctx, int dtype, const srhip_node* nodes, con
 
 void srhip_program_destroy(srhip_program* P) {
   if (!P) return;
-  if (P->ctx) (void)hipSetDevice(P->ctx->device);
+  if (P->device >= 0) (void)hipSetDevice(P->device);
   delete P;
+  (void)hipGetLastError();
 }
 
 int srhip_program_num_constants(const srhip_program* P, int32_t* out) {

@@ -120,6 +120,7 @@ struct srhip_ctx {
 
 struct srhip_dataset {
   srhip_ctx* ctx = nullptr;
+  int device = 0;  // own copy: a dataset may be destroyed after its context
   int dtype = SRHIP_F32;
   int64_t nfeat = 0, n = 0, ld = 0;
   bool has_y = false, weighted = false;
@@ -130,6 +131,7 @@ struct srhip_dataset {
 
 struct srhip_program {
   srhip_ctx* ctx = nullptr;
+  int device = -1;  // own copy (-1: host-only program)
   int dtype = SRHIP_F32;
   int32_t ntrees = 0;
   std::vector<srhip_node> nodes;

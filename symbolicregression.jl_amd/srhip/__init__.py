@@ -22,7 +22,7 @@ from .api import (
     update_baseline_loss,
 )
 from .dataset import Dataset
-from .device import Context, DeviceDataset, Program, device_count, get_context
+from .device import Coalescer, Context, DeviceDataset, Program, device_count, get_context
 from .losses import (
     HuberLoss,
     L1DistLoss,
@@ -65,5 +65,6 @@ from .operators import (
 )
 from .options import Options
 from .random_trees import gen_random_tree_fixed_size, random_population
+from .search import HallOfFame, MutationWeights, PopMember, SearchResult, equation_search
 
 __version__ = "0.1.0"

@@ -96,6 +96,15 @@ SIGNATURES = {
     "srhip_eval_loss_grad": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(Loss), _vp, _i64, _vp, _vp, _vp]),
     "srhip_optimize_constants": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(Loss), _vp, _i64,
                                                 ctypes.POINTER(OptimOptions), _vp, _vp, _vp]),
+    "srhip_batcher_create": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(Operators), ctypes.POINTER(Loss), _i32, _i32,
+                                            ctypes.POINTER(_vp)]),
+    "srhip_batcher_set_clients": (ctypes.c_int, [_vp, _i32]),
+    "srhip_batcher_submit": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, ctypes.POINTER(ctypes.c_uint64)]),
+    "srhip_batcher_wait": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.POINTER(_dbl), ctypes.POINTER(ctypes.c_uint8)]),
+    "srhip_batcher_eval": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, ctypes.POINTER(_dbl),
+                                          ctypes.POINTER(ctypes.c_uint8)]),
+    "srhip_batcher_stats": (ctypes.c_int, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
+    "srhip_batcher_destroy": (None, [_vp]),
     "srhip_last_kernel_ms": (_dbl, [_vp]),
     "srhip_program_stats": (ctypes.c_int, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
                                            ctypes.POINTER(_i32)]),

@@ -50,6 +50,16 @@ class Dataset:
 
         key = (id(ctx), ctx.device)
         d = self._dev.get(key)
+        # a cached copy keeps its Context object alive (so the id is not reused), but the
+        # context may have been closed explicitly: upload again then
+        if d is not None and (d.ctx is not ctx or d.handle is None or ctx.handle is None):
+            d = None
         if d is None:
             d = self._dev[key] = DeviceDataset(ctx, self.X, self.y, self.weights)
         return d
+
+    def release_device(self, ctx) -> None:
+        """Free the device copy held for `ctx` (before closing that context)."""
+        d = self._dev.pop((id(ctx), ctx.device), None)
+        if d is not None:
+            d.close()

@@ -245,3 +245,68 @@ class Program:
             self.close()
         except Exception:
             pass
+
+
+class Coalescer:
+    """Cross-population request coalescer over libsrhip's batcher (include/srhip.h,
+    SURVEY.md §8(f)-1).  Any number of threads call :meth:`score_loss` with ONE flattened tree;
+    a native worker thread batches concurrent requests into one launch.  The result equals
+    ``Program(ctx, tree).eval_loss(ds, loss)`` for that tree alone.  The context is owned by the
+    batcher for its lifetime (do not evaluate on it from other threads meanwhile)."""
+
+    def __init__(self, ctx: Context, ds: DeviceDataset, options, loss, max_batch: int = 256,
+                 max_wait_us: int = 200, nclients: int = 0):
+        self.ctx, self.ds, self.options, self.loss = ctx, ds, options, loss
+        self._ops = options.c_operators()
+        self._loss = loss.c_struct()
+        h = ctypes.c_void_p()
+        check(_lib.load().srhip_batcher_create(ctx.handle, ds.handle, ctypes.byref(self._ops),
+                                               ctypes.byref(self._loss), int(max_batch), int(max_wait_us),
+                                               ctypes.byref(h)))
+        self.handle = h
+        if nclients:
+            self.set_clients(nclients)
+
+    def set_clients(self, n: int) -> None:
+        check(_lib.load().srhip_batcher_set_clients(self.handle, int(n)))
+
+    def score_loss(self, nodes: np.ndarray, idx=None):
+        """(loss, did_succeed) of one tree given as a srhip_node run (root first).  Blocks; the
+        GIL is released while waiting (ctypes), so island threads overlap."""
+        nodes = np.ascontiguousarray(nodes)
+        idxa = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        loss, ok = ctypes.c_double(), ctypes.c_uint8()
+        check(_lib.load().srhip_batcher_eval(self.handle, ptr(nodes), len(nodes), ptr(idxa),
+                                             0 if idxa is None else len(idxa), ctypes.byref(loss),
+                                             ctypes.byref(ok)))
+        return float(loss.value), bool(ok.value)
+
+    def submit(self, nodes: np.ndarray, idx=None) -> int:
+        nodes = np.ascontiguousarray(nodes)
+        idxa = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        t = ctypes.c_uint64()
+        check(_lib.load().srhip_batcher_submit(self.handle, ptr(nodes), len(nodes), ptr(idxa),
+                                               0 if idxa is None else len(idxa), ctypes.byref(t)))
+        return int(t.value)
+
+    def wait(self, ticket: int):
+        loss, ok = ctypes.c_double(), ctypes.c_uint8()
+        check(_lib.load().srhip_batcher_wait(self.handle, ctypes.c_uint64(ticket), ctypes.byref(loss),
+                                             ctypes.byref(ok)))
+        return float(loss.value), bool(ok.value)
+
+    def stats(self) -> dict:
+        a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        check(_lib.load().srhip_batcher_stats(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return dict(requests=a.value, launches=b.value, max_batch=c.value)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.load().srhip_batcher_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

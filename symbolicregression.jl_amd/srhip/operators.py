@@ -150,3 +150,47 @@ logical_and = _binary_builder("logical_and", lambda x, y: 1.0 if (x > 0 and y > 
 plus = _binary_builder("+", lambda x, y: x + y)
 sub = _binary_builder("-", lambda x, y: x - y)
 mult = _binary_builder("*", lambda x, y: x * y)
+
+
+def _jl_mod(x, y):
+    """Julia mod: floored, sign of the divisor."""
+    r = np.fmod(x, y)
+    return r + y if (r != 0 and (r < 0) != (y < 0)) else r
+
+
+# Host scalar semantics by canonical name (src/Operators.jl; Julia Base): used by the search's
+# simplification (constant folding), never by evaluation — the device does that.
+_SCALAR_UNARY = {
+    "neg": lambda x: -x, "square": lambda x: x * x, "cube": lambda x: x * x * x, "abs": abs,
+    "relu": lambda x: x if x > 0 else x * 0, "cos": np.cos, "sin": np.sin, "tan": np.tan, "exp": np.exp,
+    "safe_log": lambda x: np.log(x) if x > 0 else math.nan, "safe_log2": lambda x: np.log2(x) if x > 0 else math.nan,
+    "safe_log10": lambda x: np.log10(x) if x > 0 else math.nan,
+    "safe_log1p": lambda x: np.log1p(x) if x > -1 else math.nan,
+    "safe_sqrt": lambda x: np.sqrt(x) if x >= 0 else math.nan,
+    "safe_acosh": lambda x: np.arccosh(x) if x >= 1 else math.nan,
+    "atanh_clip": lambda x: np.arctanh(_jl_mod(x + 1, type(x)(2)) - 1),
+    "sinh": np.sinh, "cosh": np.cosh, "tanh": np.tanh, "asin": np.arcsin, "acos": np.arccos, "atan": np.arctan,
+    "asinh": np.arcsinh, "erf": lambda x: type(x)(math.erf(x)), "erfc": lambda x: type(x)(math.erfc(x)),
+    "gamma": lambda x: type(x)(math.gamma(x)) if np.isfinite(x) and not (x <= 0 and x == int(x)) else math.nan,
+    "round": np.rint, "floor": np.floor, "ceil": np.ceil, "sign": np.sign, "exp2": np.exp2, "expm1": np.expm1,
+    "cbrt": np.cbrt,
+}
+_SCALAR_BINARY = {
+    "+": lambda x, y: x + y, "-": lambda x, y: x - y, "*": lambda x, y: x * y, "/": lambda x, y: x / y,
+    "^": _safe_pow, "greater": lambda x, y: type(x)(1) if x > y else type(x)(0),
+    "cond": lambda x, y: y if x > 0 else y * 0,
+    "logical_or": lambda x, y: type(x)(1) if (x > 0 or y > 0) else type(x)(0),
+    "logical_and": lambda x, y: type(x)(1) if (x > 0 and y > 0) else type(x)(0),
+    "max": lambda x, y: x if (x != x or x > y) else y, "min": lambda x, y: x if (x != x or x < y) else y,
+    "mod": _jl_mod, "atan2": np.arctan2,
+}
+
+
+def scalar_op(name: str, vals):
+    """Apply the operator `name` (canonical) to scalar NumPy values (host, for simplification)."""
+    try:
+        if len(vals) == 1:
+            return vals[0].dtype.type(_SCALAR_UNARY[name](vals[0]))
+        return vals[0].dtype.type(_SCALAR_BINARY[name](vals[0], vals[1]))
+    except (ValueError, OverflowError, ZeroDivisionError, KeyError):
+        return math.nan

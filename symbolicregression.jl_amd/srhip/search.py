@@ -1,0 +1,757 @@
+"""The search loop around the hot path: regularized evolution over islands, every score through
+the device (SURVEY.md §8(a) A12 scoring call sites, A14 ``s_r_cycle``, A15 migration; §8(f)-1
+cross-population request coalescer).
+
+Restated from the reference, file by file:
+  * ``s_r_cycle``                      src/SingleIteration.jl:24-98
+  * ``optimize_and_simplify_population`` src/SingleIteration.jl:100-127
+  * ``reg_evol_cycle``                 src/RegularizedEvolution.jl:13-111
+  * ``next_generation`` / ``crossover_generation`` / ``condition_mutation_weights!``
+                                       src/Mutate.jl:34-431
+  * mutation operators                 src/MutationFunctions.jl:33-318
+  * ``MutationWeights`` / ``sample_mutation``  src/MutationWeights.jl:42-66
+  * ``best_of_sample`` / ``best_sub_pop``      src/Population.jl:107-187
+  * ``RunningSearchStatistics``        src/AdaptiveParsimony.jl:22-97
+  * ``HallOfFame`` / ``calculate_pareto_frontier`` / ``update_hall_of_fame!``
+                                       src/HallOfFame.jl:30-96, src/SearchUtils.jl:513-531
+  * ``check_constraints`` (size, depth, per-operator complexity)  src/CheckConstraints.jl:69-97
+  * ``migrate!``                       src/Migration.jl:16-38
+  * ``get_cur_maxsize``                src/SearchUtils.jl:458-470
+  * the main loop (populations as concurrent tasks, results processed as they complete, HoF /
+    frequency / migration updates, re-dispatch)  src/SymbolicRegression.jl:870-1000, 1088-1129
+  * ``simplify_tree!`` / ``combine_operators``: DynamicExpressions v0.16 (external, absent from
+    the container; restated: constant folding of all-constant operator nodes, and merging of
+    constants through nested + and *) — parity unpinned.
+
+The reference scores ONE tree per mutation from every population task concurrently; here the
+island threads call :class:`srhip.Coalescer` (a native batcher in libsrhip), which turns the
+concurrent single-tree requests into one device launch.  NumPy Generators replace Julia's RNG:
+searches are statistically, not bit-, equivalent to the reference; with ``deterministic=True``
+a search is reproducible run to run (islands iterate in lock step, fixed processing order).
+"""
+from __future__ import annotations
+
+import itertools
+import math
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .api import compute_complexity, loss_to_score, optimize_constants, update_baseline_loss
+from .dataset import Dataset
+from .node import Node, count_constants, count_depth, count_nodes, flatten, string_tree
+from .random_trees import make_random_leaf
+
+MAX_DEGREE = 2
+
+# ---- search options (src/Options.jl:379-440 defaults) -------------------------------------------
+
+
+@dataclass
+class MutationWeights:
+    """src/MutationWeights.jl:42-55 (form/break_connection only apply to GraphNode: always 0 here)."""
+    mutate_constant: float = 0.048
+    mutate_operator: float = 0.47
+    swap_operands: float = 0.1
+    add_node: float = 0.79
+    insert_node: float = 5.1
+    delete_node: float = 1.7
+    simplify: float = 0.0020
+    randomize: float = 0.00023
+    do_nothing: float = 0.21
+    optimize: float = 0.0
+
+    def copy(self) -> "MutationWeights":
+        return MutationWeights(**self.__dict__)
+
+
+MUTATIONS = tuple(MutationWeights.__dataclass_fields__)
+
+SEARCH_DEFAULTS = dict(
+    populations=15, population_size=33, ncycles_per_iteration=550, tournament_selection_n=12,
+    tournament_selection_p=0.86, topn=12, alpha=0.1, perturbation_factor=0.076, annealing=False,
+    crossover_probability=0.066, warmup_maxsize_by=0.0, use_frequency=True, use_frequency_in_tournament=True,
+    adaptive_parsimony_scaling=20.0, fraction_replaced=0.00036, fraction_replaced_hof=0.035,
+    probability_negate_constant=0.01, maxdepth=None, migration=True, hof_migration=True, should_simplify=True,
+    should_optimize_constants=True, skip_mutation_failures=True, bin_constraints=None, una_constraints=None,
+    mutation_weights=None,
+)
+
+
+def search_option(options, name):
+    if hasattr(options, name):
+        return getattr(options, name)
+    return options.unused.get(name, SEARCH_DEFAULTS[name])
+
+
+def tournament_selection_weights(n: int, p: float) -> np.ndarray:
+    """src/Options.jl: weights p (1-p)^(k-1), k = 1..n, normalised."""
+    w = np.array([p * (1 - p) ** k for k in range(n)])
+    return w / w.sum()
+
+
+# ---- members, populations, statistics ------------------------------------------------------------
+_birth = itertools.count()
+_birth_lock = threading.Lock()
+
+
+def get_birth_order() -> int:
+    """src/Utils.jl get_birth_order (deterministic counter form)."""
+    with _birth_lock:
+        return next(_birth)
+
+
+@dataclass
+class PopMember:
+    """src/PopMember.jl:7-16."""
+    tree: Node
+    score: float
+    loss: float
+    birth: int = field(default_factory=get_birth_order)
+    complexity: int = -1
+    ref: int = -1
+    parent: int = -1
+
+    def copy(self) -> "PopMember":
+        return PopMember(self.tree.copy(), self.score, self.loss, self.birth, self.complexity, self.ref, self.parent)
+
+
+class RunningSearchStatistics:
+    """src/AdaptiveParsimony.jl:22-97."""
+
+    def __init__(self, options, window_size: int = 100000):
+        size = options.maxsize + MAX_DEGREE
+        self.window_size = window_size
+        self.frequencies = np.ones(size)
+        self.normalized_frequencies = self.frequencies / self.frequencies.sum()
+
+    def copy(self):
+        c = RunningSearchStatistics.__new__(RunningSearchStatistics)
+        c.window_size, c.frequencies, c.normalized_frequencies = (
+            self.window_size, self.frequencies.copy(), self.normalized_frequencies.copy())
+        return c
+
+    def update_frequencies(self, size: int) -> None:
+        if 0 < size <= len(self.frequencies):
+            self.frequencies[size - 1] += 1
+
+    def move_window(self) -> None:
+        smallest = 1.0
+        f = self.frequencies
+        total = f.sum()
+        if total <= self.window_size:
+            return
+        diff = total - self.window_size
+        for _ in range(1000):
+            if diff <= 0:
+                break
+            sel = f > smallest
+            nrem = int(sel.sum())
+            if nrem == 0:
+                break
+            amount = min(diff / nrem, f[sel].min() - smallest)
+            f[sel] -= amount
+            tot = amount * nrem
+            diff -= tot
+            if tot < 1e-6:
+                break
+
+    def normalize_frequencies(self) -> None:
+        self.normalized_frequencies = self.frequencies / self.frequencies.sum()
+
+
+class HallOfFame:
+    """src/HallOfFame.jl:30-60: best member per complexity."""
+
+    def __init__(self, options):
+        n = options.maxsize + MAX_DEGREE
+        self.members = [None] * n
+        self.exists = [False] * n
+
+    def update(self, members, options) -> None:
+        """update_hall_of_fame! (src/SearchUtils.jl:513-531)."""
+        for m in members:
+            size = compute_complexity(m.tree, options)
+            if not (0 < size < options.maxsize + MAX_DEGREE):
+                continue
+            if not self.exists[size - 1] or m.score < self.members[size - 1].score:
+                self.members[size - 1] = m.copy()
+                self.exists[size - 1] = True
+
+    def pareto_frontier(self):
+        """calculate_pareto_frontier (src/HallOfFame.jl:73-96)."""
+        dominating = []
+        for size, m in enumerate(self.members):
+            if not self.exists[size]:
+                continue
+            if all(not self.exists[i] or m.loss < self.members[i].loss for i in range(size)):
+                dominating.append(m.copy())
+        return dominating
+
+
+# ---- tree sampling and mutation operators (src/MutationFunctions.jl) ---------------------------
+def _sample(tree: Node, rng, pred=None):
+    """rand(NodeSampler(; tree, filter)): uniform over the (filtered) nodes."""
+    nodes = [n for n in tree if pred is None or pred(n)]
+    return nodes[int(rng.integers(0, len(nodes)))] if nodes else None
+
+
+def swap_operands(tree, rng):
+    node = _sample(tree, rng, lambda t: t.degree == 2)
+    if node is not None:
+        node.l, node.r = node.r, node.l
+    return tree
+
+
+def mutate_operator(tree, options, rng):
+    node = _sample(tree, rng, lambda t: t.degree != 0)
+    if node is None:
+        return tree
+    node.op = int(rng.integers(1, (options.nuna if node.degree == 1 else options.nbin) + 1))
+    return tree
+
+
+def mutate_constant(tree, temperature, options, dtype, rng):
+    """src/MutationFunctions.jl:63-92 (factor in T, negation with probability_negate_constant)."""
+    node = _sample(tree, rng, lambda t: t.degree == 0 and t.constant)
+    if node is None:
+        return tree
+    T = np.dtype(dtype).type
+    bottom = 0.1
+    max_change = search_option(options, "perturbation_factor") * temperature + 1 + bottom
+    factor = T(max_change ** T(rng.random()))
+    v = T(node.val)
+    v = v * factor if rng.random() < 0.5 else v / factor
+    if rng.random() > search_option(options, "probability_negate_constant"):
+        v = v * T(-1)
+    node.val = float(v)
+    return tree
+
+
+def _new_op(options, nfeatures, dtype, rng, left=None, make_bin=None):
+    if make_bin is None:
+        make_bin = rng.random() < options.nbin / (options.nuna + options.nbin)
+    if make_bin:
+        op = int(rng.integers(1, options.nbin + 1))
+        l = left if left is not None else make_random_leaf(nfeatures, dtype, rng)
+        return Node(op, l, make_random_leaf(nfeatures, dtype, rng))
+    op = int(rng.integers(1, options.nuna + 1))
+    return Node(op, left if left is not None else make_random_leaf(nfeatures, dtype, rng))
+
+
+def append_random_op(tree, options, nfeatures, dtype, rng, make_bin=None):
+    node = _sample(tree, rng, lambda t: t.degree == 0)
+    node.set_node(_new_op(options, nfeatures, dtype, rng, make_bin=make_bin))
+    return tree
+
+
+def insert_random_op(tree, options, nfeatures, dtype, rng):
+    node = _sample(tree, rng)
+    make_bin = rng.random() < options.nbin / (options.nuna + options.nbin)
+    node.set_node(_new_op(options, nfeatures, dtype, rng, left=node.copy(), make_bin=make_bin))
+    return tree
+
+
+def prepend_random_op(tree, options, nfeatures, dtype, rng):
+    make_bin = rng.random() < options.nbin / (options.nuna + options.nbin)
+    tree.set_node(_new_op(options, nfeatures, dtype, rng, left=tree.copy(), make_bin=make_bin))
+    return tree
+
+
+def random_node_and_parent(tree, rng):
+    if tree.degree == 0:
+        return tree, tree, "n"
+    parent = _sample(tree, rng, lambda t: t.degree != 0)
+    if parent.degree == 1 or rng.random() < 0.5:
+        return parent.l, parent, "l"
+    return parent.r, parent, "r"
+
+
+def delete_random_op(tree, options, nfeatures, dtype, rng):
+    node, parent, side = random_node_and_parent(tree, rng)
+    isroot = side == "n"
+    if node.degree == 0:
+        node.set_node(make_random_leaf(nfeatures, dtype, rng))
+        return tree
+    child = node.l if (node.degree == 1 or rng.random() < 0.5) else node.r
+    if isroot:
+        return child
+    if side == "l":
+        parent.l = child
+    else:
+        parent.r = child
+    return tree
+
+
+def gen_random_tree(length, options, nfeatures, dtype, rng):
+    """src/MutationFunctions.jl:227-240."""
+    tree = Node(val=1.0)
+    for _ in range(length):
+        tree = append_random_op(tree, options, nfeatures, dtype, rng)
+    return tree
+
+
+def gen_random_tree_fixed_size(node_count, options, nfeatures, dtype, rng):
+    from .random_trees import gen_random_tree_fixed_size as g
+
+    return g(node_count, options, nfeatures, dtype, rng)
+
+
+def crossover_trees(tree1, tree2, rng):
+    """src/MutationFunctions.jl:271-303."""
+    tree1, tree2 = tree1.copy(), tree2.copy()
+    node1, parent1, side1 = random_node_and_parent(tree1, rng)
+    node2, parent2, side2 = random_node_and_parent(tree2, rng)
+    node1 = node1.copy()
+    if side1 == "l":
+        parent1.l = node2.copy()
+    elif side1 == "r":
+        parent1.r = node2.copy()
+    else:
+        tree1 = node2.copy()
+    if side2 == "l":
+        parent2.l = node1
+    elif side2 == "r":
+        parent2.r = node1
+    else:
+        tree2 = node1
+    return tree1, tree2
+
+
+# ---- simplification (DynamicExpressions v0.16 simplify_tree! / combine_operators, restated) ------
+def _fold(name, vals, dtype):
+    from .operators import scalar_op
+
+    with np.errstate(all="ignore"):
+        out = scalar_op(name, [np.dtype(dtype).type(v) for v in vals])
+    return float(out) if np.isfinite(out) else None
+
+
+def simplify_tree(tree, options, dtype):
+    """Operator nodes whose children are all (finite) constants become the constant result
+    (kept only if finite), bottom-up."""
+    if tree.degree == 0:
+        return tree
+    tree.l = simplify_tree(tree.l, options, dtype)
+    if tree.degree == 2:
+        tree.r = simplify_tree(tree.r, options, dtype)
+    kids = [tree.l] if tree.degree == 1 else [tree.l, tree.r]
+    if all(k.degree == 0 and k.constant and math.isfinite(k.val) for k in kids):
+        names = options.unary_operators if tree.degree == 1 else options.binary_operators
+        name = names[(options.unary_index(tree.op) if tree.degree == 1 else options.binary_index(tree.op)) - 1]
+        v = _fold(name, [k.val for k in kids], dtype)
+        if v is not None:
+            return Node(val=v)
+    return tree
+
+
+def combine_operators(tree, options, dtype):
+    """Merge constants through nested + and *: (c1 op (c2 op x)) -> ((c1 op c2) op x) for
+    op in {+, *} (either operand order), bottom-up."""
+    if tree.degree == 0:
+        return tree
+    tree.l = combine_operators(tree.l, options, dtype)
+    if tree.degree == 2:
+        tree.r = combine_operators(tree.r, options, dtype)
+    if tree.degree != 2:
+        return tree
+    name = options.binary_operators[options.binary_index(tree.op) - 1]
+    if name not in ("+", "*"):
+        return tree
+    is_c = lambda n: n.degree == 0 and n.constant  # noqa: E731
+    for c, other in ((tree.l, tree.r), (tree.r, tree.l)):
+        if not is_c(c) or other.degree != 2:
+            continue
+        if options.binary_operators[options.binary_index(other.op) - 1] != name:
+            continue
+        for c2, x in ((other.l, other.r), (other.r, other.l)):
+            if is_c(c2):
+                v = _fold(name, [c.val, c2.val], dtype)
+                if v is None:
+                    return tree
+                return Node(tree.op, Node(val=v), x)
+    return tree
+
+
+# ---- constraints (src/CheckConstraints.jl) --------------------------------------------------------
+def check_constraints(tree, options, maxsize, cursize=None) -> bool:
+    size = compute_complexity(tree, options) if cursize is None else cursize
+    if size > maxsize:
+        return False
+    maxdepth = search_option(options, "maxdepth") or options.maxsize
+    if count_depth(tree) > maxdepth:
+        return False
+    bc = search_option(options, "bin_constraints")
+    uc = search_option(options, "una_constraints")
+    if bc or uc:
+        for n in tree:
+            if n.degree == 2 and bc:
+                cons = bc[options.binary_index(n.op) - 1]
+                if cons[0] > -1 and compute_complexity(n.l, options) > cons[0]:
+                    return False
+                if cons[1] > -1 and compute_complexity(n.r, options) > cons[1]:
+                    return False
+            elif n.degree == 1 and uc:
+                cons = uc[options.unary_index(n.op) - 1]
+                if cons > -1 and compute_complexity(n.l, options) > cons:
+                    return False
+    return True
+
+
+# ---- scoring through the device ----------------------------------------------------------------
+class DeviceScorer:
+    """score_func (src/LossFunctions.jl:161-174) for one tree at a time, served by the native
+    coalescer so concurrent islands share device launches."""
+
+    def __init__(self, dataset: Dataset, options, nclients: int = 0, max_batch: int = 256, max_wait_us: int = 300):
+        from .device import Coalescer, Context
+
+        self.dataset, self.options = dataset, options
+        self.ctx = Context(options.device)
+        self.ds = dataset.device(self.ctx)
+        self.coalescer = Coalescer(self.ctx, self.ds, options, options.elementwise_loss, max_batch=max_batch,
+                                   max_wait_us=max_wait_us, nclients=nclients)
+        self.L = dataset.loss_type.type
+        self.dtype = dataset.X.dtype
+
+    def score(self, tree, complexity=None, idx=None):
+        nodes, _ = flatten([tree], self.options, self.dtype)
+        loss, ok = self.coalescer.score_loss(nodes, idx)
+        loss = self.L(loss) if ok else self.L(np.inf)
+        score = loss_to_score(loss, self.dataset.use_baseline, self.dataset.baseline_loss, tree, self.options,
+                              complexity)
+        return score, loss
+
+    def close(self):
+        self.coalescer.close()
+        self.dataset.release_device(self.ctx)
+        self.ctx.close()
+
+
+# ---- one mutation / crossover (src/Mutate.jl) ----------------------------------------------------
+def condition_mutation_weights(w: MutationWeights, member: PopMember, options, curmaxsize) -> None:
+    """src/Mutate.jl:34-76."""
+    tree = member.tree
+    if tree.degree == 0:
+        w.mutate_operator = w.swap_operands = w.delete_node = w.simplify = 0.0
+        if not tree.constant:
+            w.optimize = 0.0
+            w.mutate_constant = 0.0
+        return
+    if not any(n.degree == 2 for n in tree):
+        w.swap_operands = 0.0
+    w.mutate_constant *= min(8, count_constants(tree)) / 8.0
+    if compute_complexity(tree, options) >= curmaxsize:
+        w.add_node = 0.0
+        w.insert_node = 0.0
+    if not search_option(options, "should_simplify"):
+        w.simplify = 0.0
+
+
+def sample_mutation(w: MutationWeights, rng) -> str:
+    p = np.array([getattr(w, k) for k in MUTATIONS])
+    return MUTATIONS[int(rng.choice(len(p), p=p / p.sum()))]
+
+
+class Island:
+    """One population and its evolution state (the body of a reference population task)."""
+
+    def __init__(self, k, dataset, options, scorer, rng, dtype):
+        self.k, self.dataset, self.options, self.scorer, self.rng, self.dtype = k, dataset, options, scorer, rng, dtype
+        self.nfeatures = dataset.nfeatures
+        self.num_evals = 0.0
+
+    # src/Mutate.jl:78-346
+    def next_generation(self, member, temperature, curmaxsize, stats):
+        o, rng = self.options, self.rng
+        before_score, before_loss = member.score, member.loss
+        w = (search_option(o, "mutation_weights") or MutationWeights()).copy()
+        condition_mutation_weights(w, member, o, curmaxsize)
+        choice = sample_mutation(w, rng)
+        successful = False
+        attempts = 0
+        tree = None
+        while not successful and attempts < 10:
+            tree = member.tree.copy()
+            successful = True
+            if choice == "mutate_constant":
+                tree = mutate_constant(tree, temperature, o, self.dtype, rng)
+            elif choice == "mutate_operator":
+                tree = mutate_operator(tree, o, rng)
+            elif choice == "swap_operands":
+                tree = swap_operands(tree, rng)
+            elif choice == "add_node":
+                if rng.random() < 0.5:
+                    tree = append_random_op(tree, o, self.nfeatures, self.dtype, rng)
+                else:
+                    tree = prepend_random_op(tree, o, self.nfeatures, self.dtype, rng)
+            elif choice == "insert_node":
+                tree = insert_random_op(tree, o, self.nfeatures, self.dtype, rng)
+            elif choice == "delete_node":
+                tree = delete_random_op(tree, o, self.nfeatures, self.dtype, rng)
+            elif choice == "simplify":
+                tree = combine_operators(simplify_tree(tree, o, self.dtype), o, self.dtype)
+                return PopMember(tree, before_score, before_loss, parent=member.ref), True
+            elif choice == "randomize":
+                size = int(rng.integers(1, curmaxsize + 1))
+                tree = gen_random_tree_fixed_size(size, o, self.nfeatures, self.dtype, rng)
+            elif choice == "optimize":
+                cur = PopMember(tree, before_score, before_loss, parent=member.ref)
+                cur, ne = optimize_constants(self.dataset, cur, o, rng=rng)
+                self.num_evals += ne
+                return cur, True
+            elif choice == "do_nothing":
+                return PopMember(tree, before_score, before_loss, parent=member.ref), True
+            successful = successful and check_constraints(tree, o, curmaxsize)
+            attempts += 1
+        if not successful:
+            return PopMember(member.tree.copy(), before_score, before_loss, parent=member.ref), False
+        after_score, after_loss = self.scorer.score(tree)
+        self.num_evals += 1
+        if math.isnan(after_score):
+            return PopMember(member.tree.copy(), before_score, before_loss, parent=member.ref), False
+        prob = 1.0
+        if search_option(o, "annealing"):
+            delta = after_score - before_score
+            prob *= math.exp(-delta / (temperature * search_option(o, "alpha")))
+        if search_option(o, "use_frequency"):
+            old_size = compute_complexity(member.tree, o)
+            new_size = compute_complexity(tree, o)
+            nf = stats.normalized_frequencies
+            old_f = nf[old_size - 1] if 0 < old_size <= o.maxsize else 1e-6
+            new_f = nf[new_size - 1] if 0 < new_size <= o.maxsize else 1e-6
+            prob *= old_f / new_f
+        if prob < rng.random():
+            return PopMember(member.tree.copy(), before_score, before_loss, parent=member.ref), False
+        return PopMember(tree, after_score, after_loss, parent=member.ref), True
+
+    # src/Mutate.jl:349-429
+    def crossover_generation(self, m1, m2, curmaxsize):
+        o = self.options
+        c1, c2 = crossover_trees(m1.tree, m2.tree, self.rng)
+        tries = 1
+        while True:
+            s1, s2 = compute_complexity(c1, o), compute_complexity(c2, o)
+            if check_constraints(c1, o, curmaxsize, s1) and check_constraints(c2, o, curmaxsize, s2):
+                break
+            if tries > 10:
+                return m1, m2, False
+            c1, c2 = crossover_trees(m1.tree, m2.tree, self.rng)
+            tries += 1
+        sc1, l1 = self.scorer.score(c1, s1)
+        sc2, l2 = self.scorer.score(c2, s2)
+        self.num_evals += 2
+        return PopMember(c1, sc1, l1, parent=m1.ref), PopMember(c2, sc2, l2, parent=m2.ref), True
+
+    # src/Population.jl:107-160
+    def best_of_sample(self, pop, stats):
+        o, rng = self.options, self.rng
+        n = search_option(o, "tournament_selection_n")
+        sample = [pop[i] for i in rng.choice(len(pop), size=min(n, len(pop)), replace=False)]
+        if search_option(o, "use_frequency_in_tournament"):
+            a = search_option(o, "adaptive_parsimony_scaling")
+            scores = []
+            for m in sample:
+                size = compute_complexity(m.tree, o)
+                freq = stats.normalized_frequencies[size - 1] if 0 < size <= o.maxsize else 0.0
+                scores.append(m.score * math.exp(a * freq))
+        else:
+            scores = [m.score for m in sample]
+        p = search_option(o, "tournament_selection_p")
+        if p == 1.0:
+            return sample[int(np.argmin(scores))]
+        w = tournament_selection_weights(len(sample), p)
+        k = int(rng.choice(len(w), p=w)) + 1
+        order = np.argsort(np.asarray(scores, dtype=np.float64), kind="stable")
+        return sample[int(order[k - 1])]
+
+    # src/RegularizedEvolution.jl:13-111
+    def reg_evol_cycle(self, pop, temperature, curmaxsize, stats):
+        o, rng = self.options, self.rng
+        n_cycles = math.ceil(len(pop) / search_option(o, "tournament_selection_n"))
+        skip = search_option(o, "skip_mutation_failures")
+        for _ in range(n_cycles):
+            if rng.random() > search_option(o, "crossover_probability"):
+                allstar = self.best_of_sample(pop, stats)
+                baby, accepted = self.next_generation(allstar, temperature, curmaxsize, stats)
+                if not accepted and skip:
+                    continue
+                oldest = min(range(len(pop)), key=lambda i: pop[i].birth)
+                pop[oldest] = baby
+            else:
+                a1, a2 = self.best_of_sample(pop, stats), self.best_of_sample(pop, stats)
+                b1, b2, accepted = self.crossover_generation(a1, a2, curmaxsize)
+                if not accepted and skip:
+                    continue
+                oldest = min(range(len(pop)), key=lambda i: pop[i].birth)
+                pop[oldest] = b1
+                oldest = min(range(len(pop)), key=lambda i: pop[i].birth)
+                pop[oldest] = b2
+        return pop
+
+    # src/SingleIteration.jl:24-98 (batching=false form: the member's own score)
+    def s_r_cycle(self, pop, ncycles, curmaxsize, stats):
+        o = self.options
+        max_temp, min_temp = 1.0, (0.0 if search_option(o, "annealing") else 1.0)
+        best_seen = HallOfFame(o)
+        for temperature in np.linspace(max_temp, min_temp, ncycles):
+            pop = self.reg_evol_cycle(pop, float(temperature), curmaxsize, stats)
+            for m in pop:
+                size = compute_complexity(m.tree, o)
+                if 0 < size <= o.maxsize and (not best_seen.exists[size - 1]
+                                              or m.score < best_seen.members[size - 1].score):
+                    best_seen.exists[size - 1] = True
+                    best_seen.members[size - 1] = m.copy()
+        return pop, best_seen
+
+    # src/SingleIteration.jl:100-127: simplify every member, optimise constants of a random 14 %
+    # (one batched device optimisation for the population instead of one per member)
+    def optimize_and_simplify_population(self, pop):
+        o, rng = self.options, self.rng
+        do_opt = rng.random(len(pop)) < o.optimizer_probability
+        if search_option(o, "should_simplify"):
+            for m in pop:
+                m.tree = combine_operators(simplify_tree(m.tree, o, self.dtype), o, self.dtype)
+        if search_option(o, "should_optimize_constants"):
+            chosen = [m for m, d in zip(pop, do_opt) if d and count_constants(m.tree) > 0]
+            if chosen:
+                _, ne = optimize_constants(self.dataset, chosen, o, rng=rng)
+                self.num_evals += ne
+        return pop
+
+    def run_iteration(self, pop, curmaxsize, stats):
+        """_dispatch_s_r_cycle (src/SymbolicRegression.jl:1088-1129)."""
+        stats = stats.copy()
+        stats.normalize_frequencies()
+        pop, best_seen = self.s_r_cycle(pop, search_option(self.options, "ncycles_per_iteration"), curmaxsize, stats)
+        pop = self.optimize_and_simplify_population(pop)
+        return pop, best_seen
+
+
+def migrate(candidates, pop, options, frac, rng) -> None:
+    """migrate! (src/Migration.jl:16-38)."""
+    n = len(pop)
+    num = int(rng.poisson(n * frac))
+    num = min(num, len(candidates), n)
+    if num == 0:
+        return
+    locs = rng.integers(0, n, size=num)
+    mig = rng.integers(0, len(candidates), size=num)
+    for i, j in zip(locs, mig):
+        m = candidates[int(j)].copy()
+        m.birth = get_birth_order()
+        pop[int(i)] = m
+
+
+def get_cur_maxsize(options, total_cycles, cycles_remaining) -> int:
+    """src/SearchUtils.jl:458-470."""
+    w = search_option(options, "warmup_maxsize_by")
+    frac = (total_cycles - cycles_remaining) / total_cycles
+    if w > 0 and frac <= w:
+        return 3 + int(math.floor((options.maxsize - 3) * frac / w))
+    return options.maxsize
+
+
+@dataclass
+class SearchResult:
+    hall_of_fame: HallOfFame
+    populations: list
+    num_evals: float
+    coalescer_stats: dict
+
+    def pareto_frontier(self):
+        return self.hall_of_fame.pareto_frontier()
+
+
+def equation_search(X, y, options, niterations: int = 10, weights=None, seed=None, scorer=None,
+                    verbosity: int = 0) -> SearchResult:
+    """equation_search (src/SymbolicRegression.jl:357-1000) for one output, populations as
+    concurrent island threads, every score through the device.  ``scorer`` (testing hook):
+    any object with ``score(tree, complexity=None) -> (score, loss)``; default: the device
+    coalescer."""
+    dataset = X if isinstance(X, Dataset) else Dataset(X, y, weights)
+    dtype = dataset.X.dtype
+    npops = search_option(options, "populations")
+    psize = search_option(options, "population_size")
+    det = bool(options.deterministic)
+    base_seed = options.seed if seed is None else seed
+    ss = np.random.SeedSequence(base_seed)
+    rngs = [np.random.default_rng(s) for s in ss.spawn(npops + 1)]
+    head_rng = rngs[-1]
+    own_scorer = scorer is None
+    if own_scorer:
+        update_baseline_loss(dataset, options)
+        scorer = DeviceScorer(dataset, options, nclients=npops)
+    try:
+        islands = [Island(k, dataset, options, scorer, rngs[k], dtype) for k in range(npops)]
+        # initial populations: gen_random_tree(3, ...) scored (src/Population.jl:40-63)
+        pops = []
+        for isl in islands:
+            trees = [gen_random_tree(3, options, dataset.nfeatures, dtype, isl.rng) for _ in range(psize)]
+            members = []
+            for t in trees:
+                sc, lo = scorer.score(t)
+                members.append(PopMember(t, sc, lo))
+            pops.append(members)
+        stats = RunningSearchStatistics(options)
+        hof = HallOfFame(options)
+        best_sub_pops = [[] for _ in range(npops)]
+        total_cycles = npops * niterations
+        cycles_remaining = total_cycles
+        curmaxsize = get_cur_maxsize(options, total_cycles, cycles_remaining)
+        num_evals = float(npops * psize)
+
+        def process(k, pop, best_seen):
+            nonlocal cycles_remaining, curmaxsize, num_evals
+            best_sub_pops[k] = [m for m in sorted(pop, key=lambda m: m.score)][:search_option(options, "topn")]
+            for m in pop:
+                stats.update_frequencies(compute_complexity(m.tree, options))
+            hof.update(pop, options)
+            hof.update([m for m, e in zip(best_seen.members, best_seen.exists) if e], options)
+            dominating = hof.pareto_frontier()
+            if search_option(options, "migration"):
+                cands = [m for sp in best_sub_pops for m in sp]
+                migrate(cands, pop, options, search_option(options, "fraction_replaced"), head_rng)
+            if search_option(options, "hof_migration") and dominating:
+                migrate(dominating, pop, options, search_option(options, "fraction_replaced_hof"), head_rng)
+            cycles_remaining -= 1
+            curmaxsize = get_cur_maxsize(options, total_cycles, cycles_remaining)
+            stats.move_window()
+            pops[k] = pop
+
+        with ThreadPoolExecutor(max_workers=npops) as ex:
+            if det:
+                for it in range(niterations):
+                    futs = [ex.submit(islands[k].run_iteration, pops[k], curmaxsize, stats) for k in range(npops)]
+                    for k, f in enumerate(futs):
+                        pop, best_seen = f.result()
+                        process(k, pop, best_seen)
+                    if verbosity:
+                        print(f"iteration {it + 1}/{niterations}: best loss "
+                              f"{min(m.loss for m in hof.pareto_frontier()):.4g}", flush=True)
+            else:
+                # asynchronous like the reference: a finished population is processed and re-dispatched
+                remaining = [niterations] * npops
+                running = {ex.submit(islands[k].run_iteration, pops[k], curmaxsize, stats): k for k in range(npops)}
+                from concurrent.futures import FIRST_COMPLETED, wait
+
+                while running:
+                    done, _ = wait(list(running), return_when=FIRST_COMPLETED)
+                    for f in done:
+                        k = running.pop(f)
+                        pop, best_seen = f.result()
+                        process(k, pop, best_seen)
+                        remaining[k] -= 1
+                        if remaining[k] > 0:
+                            running[ex.submit(islands[k].run_iteration, pops[k], curmaxsize, stats)] = k
+                        elif own_scorer:
+                            # one client fewer: the coalescer stops waiting for this island
+                            scorer.coalescer.set_clients(sum(1 for r in remaining if r > 0))
+        num_evals += sum(isl.num_evals for isl in islands)
+        cstats = scorer.coalescer.stats() if own_scorer else {}
+        return SearchResult(hof, pops, num_evals, cstats)
+    finally:
+        if own_scorer:
+            scorer.close()
