@@ -234,6 +234,11 @@ double srhip_last_kernel_ms(const srhip_ctx* ctx);
 /* Per-program work counters: sum over trees of count_nodes / operator nodes. */
 int srhip_program_stats(const srhip_program* prog, int64_t* total_nodes, int64_t* total_opnodes,
                         int32_t* max_stack);
+/* Derived columns of a program (heavy unary operators on feature leaves computed once per
+ * workgroup and shared by every tree): count, and if spec is non-null the first
+ * min(count, cap) entries as (device unary op << 16) | (feature - 1).  Set SRHIP_NO_DERIVE=1
+ * before srhip_program_create to compile without them. */
+int srhip_program_derived(const srhip_program* prog, int32_t* count, uint32_t* spec, int32_t cap);
 
 /* ---- Cross-population request coalescer (8(b) "Threading") ----------------
  * The reference scores one tree per mutation from every population task concurrently

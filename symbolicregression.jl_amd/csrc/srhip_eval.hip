@@ -180,13 +180,10 @@ __device__ __attribute__((noinline)) RV<T, R> heavy_bin(RV<T, R> a, RV<T, R> b) 
 // max over every callee it can reach, so only the K = K_MAX variant carries them; with them the
 // common variants would drop from 5 to 4 waves per SIMD.  Programs whose operator table has one
 // of them launch K_MAX (the host's variant choice).
-constexpr bool un_wide(int u) { return u == UN_ASIN || u == UN_ACOS || u == UN_ATANH_CLIP; }
+constexpr bool un_wide(int u) { return un_wide_op(u); }
 
 // unary operators cheap enough to inline into the handler (a few VALU instructions per row)
-template <int U> constexpr bool un_inline() {
-  return U == UN_NEG || U == UN_SQUARE || U == UN_CUBE || U == UN_ABS || U == UN_RELU || U == UN_SIGN ||
-         U == UN_ROUND || U == UN_FLOOR || U == UN_CEIL;
-}
+template <int U> constexpr bool un_inline() { return un_cheap(U); }
 template <typename T, int R, int U>
 __device__ __attribute__((always_inline)) inline void apply_un(T (&A)[R]) {
   if constexpr (un_inline<U>()) {
@@ -337,6 +334,63 @@ __device__ __attribute__((always_inline)) inline void store_pred(const EvalArgs&
   }
 }
 
+// Derived columns (srhip_isa.h): U(X[f]) for this workgroup's rows, computed once into LDS column
+// nfeat + d by the same out-of-line operator bodies the interpreter calls (rows are independent
+// and -ffp-contract=off, so the values are bit-identical to evaluating U inside a tree).  The
+// column's check statistic over the block's rows (max |v| for Float32, sum |v| 2^-512 for
+// Float64) lands in dchk[d]; a tree that reads the column folds it into its own statistic, exactly
+// as its U instruction would have.
+template <typename T, int R>
+__device__ __attribute__((noinline)) RV<T, R> derive_un(int u, RV<T, R> v) {
+  switch (u) {
+#define X_(NAME, FN)                                                                     \
+  case UN_##NAME:                                                                        \
+    if constexpr (un_ok<T>(UN_##NAME) && un_derivable(UN_##NAME)) return heavy_un<T, R, UN_##NAME>(v); \
+    break;
+    SRHIP_UNOPS(X_)
+#undef X_
+    default: break;
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __attribute__((always_inline)) inline void derive_columns(const EvalArgs& p, T* lx, int rbb,
+                                                                     typename Chk<T>::type* dchk) {
+  using CT = typename Chk<T>::type;
+  constexpr int VEC = 16 / sizeof(T);
+  __shared__ CT part[EVAL_WAVES];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int d = 0; d < p.nd; ++d) {
+    const uint32_t spec = __builtin_amdgcn_readfirstlane(p.dspec[d]);
+    const int u = (int)(spec >> 16), f = (int)(spec & 0xffff);
+    const T* src = lx + (int64_t)f * rbb;
+    T* dst = lx + (int64_t)(p.nfeat + d) * rbb;
+    CT m = 0;
+    for (int c = threadIdx.x; c < rbb / VEC; c += blockDim.x) {
+      RV<T, VEC> v = reinterpret_cast<const RV<T, VEC>*>(src)[c];
+      v = derive_un<T, VEC>(u, v);
+      reinterpret_cast<RV<T, VEC>*>(dst)[c] = v;
+      UNR for (int e = 0; e < VEC; ++e) {
+        if constexpr (sizeof(T) == 4) m = __builtin_elementwise_maximum(m, __builtin_fabsf(v[e]));
+        else m = __builtin_fma(__builtin_fabs(v[e]), 0x1p-512, m);
+      }
+    }
+    m = wave_chk(m);
+    if (lane == 0) part[wave] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      CT t = part[0];
+      for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+        if constexpr (sizeof(T) == 4) t = __builtin_elementwise_maximum(t, part[w]);
+        else t += part[w];
+      }
+      dchk[d] = t;
+    }
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // The interpreter kernel.
 //   grid.x = row blocks (RB rows each), grid.y = tree groups; block = WAVES wavefronts.
@@ -375,11 +429,12 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
       const int c = i / vec_per_col;
       const int v = i - c * vec_per_col;
       const T* src = c < p.nfeat ? gX + (int64_t)c * p.ld : (c == p.nfeat ? gy : gw);
-      reinterpret_cast<V*>(lx + (int64_t)c * rbb)[v] = reinterpret_cast<const V*>(src + row_base)[v];
+      const int lc = c < p.nfeat ? c : c + p.nd;  // LDS column: derived columns follow the features
+      reinterpret_cast<V*>(lx + (int64_t)lc * rbb)[v] = reinterpret_cast<const V*>(src + row_base)[v];
     }
     xsrc = lx;
-    ysrc = lx + (int64_t)p.nfeat * rbb;
-    wsrc = lx + (int64_t)(p.nfeat + 1) * rbb;
+    ysrc = lx + (int64_t)(p.nfeat + p.nd) * rbb;
+    wsrc = lx + (int64_t)(p.nfeat + p.nd + 1) * rbb;
     xstride = rbb;
   } else {
     xsrc = reinterpret_cast<const T*>(p.X) + row_base;
@@ -389,6 +444,11 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
   }
   KDBG("[k] staged, ntiles=%d rb_rows=%d nvalid=%ld max_steps=%d\n", ntiles, p.rb_rows, (long)p.nvalid, p.max_steps);
   __syncthreads();
+  constexpr bool DERIVED = XLDS && !kIsInt<T> && MODE != MODE_PRECISE;
+  __shared__ CT dchk[DERIVED ? DERIVE_MAX : 1];
+  if constexpr (DERIVED) {
+    if (p.nd > 0) derive_columns<T>(p, reinterpret_cast<T*>(smem), p.rb_rows, dchk);
+  }
   KMARK(0, 2);
   if (p.debug_stop == 2) return;
 
@@ -411,6 +471,19 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
 
     LAccT<T> lacc = 0;
     CT M = 0;
+    if constexpr (DERIVED) {
+      if (p.nd > 0) {  // check statistics of the derived columns this tree reads
+        uint64_t msk = p.dmask[tree];
+        msk = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(msk >> 32)) << 32) |
+              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)msk);
+        while (msk) {
+          const int d = __builtin_ctzll(msk);
+          msk &= msk - 1;
+          if constexpr (sizeof(T) == 4) M = __builtin_elementwise_maximum(M, dchk[d]);
+          else if (lane == 0) M += dchk[d];  // a wave sum follows: count the column once
+        }
+      }
+    }
     for (int tile = 0; tile < ntiles; ++tile) {
       const int64_t row0 = row_base + (int64_t)tile * TILE;
       if (row0 >= p.nvalid) break;  // whole tile is padding
@@ -524,6 +597,13 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
       KMARK(0, 4);
       if constexpr (MODE == MODE_LOSS) {
         loss_tile<T, R>(p, A, ysrc + (int64_t)tile * TILE, wsrc + (int64_t)tile * TILE, lane, row0, lacc);
+        constexpr int CH = sizeof(T) == 8 ? LOSS_CHUNK_8B : LOSS_CHUNK_4B;
+        static_assert(CH % TILE == 0, "a loss chunk is whole tiles");
+        if ((tile + 1) % (CH / TILE) == 0 || row0 + TILE >= p.nvalid) {  // chunk done (or last valid tile)
+          const LAccT<T> s = wave_sum(lacc);
+          if (lane == 0) reinterpret_cast<LAccT<T>*>(p.slab_loss)[(int64_t)tree * p.nch + row0 / CH] = s;
+          lacc = 0;
+        }
       } else if constexpr (MODE == MODE_PRED) {
         store_pred<T, R>(p, A, tree, lane, row0);
       }
@@ -532,10 +612,6 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
     KMARK(0, 5);
     KMARK(8 + wave, 12);
     // ---- wave reduction, one partial per (tree, row block) ----
-    if constexpr (MODE == MODE_LOSS) {
-      lacc = wave_sum(lacc);
-      if (lane == 0) reinterpret_cast<LAccT<T>*>(p.slab_loss)[(int64_t)tree * p.nrb + rb] = lacc;
-    }
     if constexpr (!kIsInt<T> && MODE != MODE_PRECISE) {
       M = wave_chk(M);
       if (lane == 0) reinterpret_cast<CT*>(p.slab_chk)[(int64_t)tree * p.nrb + rb] = M;
@@ -548,16 +624,17 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
 // Per-tree reduction of the (tree, row block) partials, fixed order (deterministic).
 // One wavefront per tree.
 template <typename LT, typename CT, bool CHK_MAX>
-__global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab_loss, const CT* __restrict__ slab_chk,
-                                                     int nrb, int ntrees, LT* __restrict__ out_loss,
-                                                     CT* __restrict__ out_chk) {
+__global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab_loss, int nch,
+                                                     const CT* __restrict__ slab_chk, int nrb, int ntrees,
+                                                     LT* __restrict__ out_loss, CT* __restrict__ out_chk) {
   const int lane = threadIdx.x & 63;
   const int tree = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (tree >= ntrees) return;
   LT s = 0;
   CT m = 0;
+  if (slab_loss)
+    for (int i = lane; i < nch; i += 64) s += slab_loss[(int64_t)tree * nch + i];
   for (int i = lane; i < nrb; i += 64) {
-    if (slab_loss) s += slab_loss[(int64_t)tree * nrb + i];
     if (slab_chk) {
       const CT v = slab_chk[(int64_t)tree * nrb + i];
       if constexpr (CHK_MAX) m = __builtin_elementwise_maximum(m, v); else m += v;
@@ -685,20 +762,20 @@ hipError_t launch_eval(int dtype, const EvalArgs& a, int R, int K, int mode, boo
   }
 }
 
-hipError_t launch_reduce(int dtype, const void* slab_loss, const void* slab_chk, int nrb, int ntrees, void* out_loss,
+hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, const void* slab_chk, int nrb, int ntrees, void* out_loss,
                          void* out_chk, hipStream_t s) {
   dim3 grid((ntrees + 3) / 4), block(256);
   switch (dtype) {
     case SRHIP_F32:
-      hipLaunchKernelGGL((reduce_kernel<double, float, true>), grid, block, 0, s, (const double*)slab_loss,
+      hipLaunchKernelGGL((reduce_kernel<double, float, true>), grid, block, 0, s, (const double*)slab_loss, nch,
                          (const float*)slab_chk, nrb, ntrees, (double*)out_loss, (float*)out_chk);
       break;
     case SRHIP_F64:
-      hipLaunchKernelGGL((reduce_kernel<double, double, false>), grid, block, 0, s, (const double*)slab_loss,
+      hipLaunchKernelGGL((reduce_kernel<double, double, false>), grid, block, 0, s, (const double*)slab_loss, nch,
                          (const double*)slab_chk, nrb, ntrees, (double*)out_loss, (double*)out_chk);
       break;
     case SRHIP_I32:
-      hipLaunchKernelGGL((reduce_kernel<long long, float, true>), grid, block, 0, s, (const long long*)slab_loss,
+      hipLaunchKernelGGL((reduce_kernel<long long, float, true>), grid, block, 0, s, (const long long*)slab_loss, nch,
                          (const float*)nullptr, nrb, ntrees, (long long*)out_loss, (float*)nullptr);
       break;
     default: return hipErrorInvalidValue;

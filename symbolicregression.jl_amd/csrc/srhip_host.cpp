@@ -106,12 +106,21 @@ template <typename T> class TreeCompiler {
     info = TreeInfo();
     if (nn_ <= 0) return fail(SRHIP_ERR_INVALID, "empty tree");
     memo_const_.assign(nn_, -1);
+    memo_need_.assign(nn_, -1);
     state_.assign(nn_, 0);
     int rc = validate(0, 0);
     if (rc) return rc;
     info.nnodes = count_nodes(0);
     info.nconst = count_constants(0);
     cidx_.assign(nn_, -1);
+    dcolv_.assign(dspec_ && !grad_ ? nn_ : 0, -1);
+    for (int64_t i = 0; i < (int64_t)dcolv_.size(); ++i) {
+      const srhip_node& n = nd_[i];
+      if (n.degree != 1 || !leaf_is_feature(n.l)) continue;
+      const uint32_t key = ((uint32_t)classify_unop(unaop(i)) << 16) | (uint32_t)(nd_[n.l].feature - 1);
+      for (size_t d = 0; d < dspec_->size(); ++d)
+        if ((*dspec_)[d] == key) dcolv_[i] = (int32_t)d;
+    }
     int32_t nc = 0;
     number_constants(0, nc);
     // host-decided checks (reference semantics, see header comment)
@@ -143,9 +152,24 @@ template <typename T> class TreeCompiler {
   bool grad_;
   std::vector<int32_t> cidx_;
   std::vector<int8_t> memo_const_;
+  std::vector<int16_t> memo_need_;
+  std::vector<int32_t> dcolv_;  // derived column per node, or -1
   std::vector<uint8_t> state_;
   std::vector<Ins>* code_ = nullptr;
   TreeInfo* info_ = nullptr;
+  const std::vector<uint32_t>* dspec_ = nullptr;  // derived columns (nullptr: plain program)
+  int dbase_ = 0;                                 // LDS column of derived column 0
+  uint64_t dmask_ = 0;
+
+ public:
+  // compile U(X[f]) nodes listed in dspec as reads of LDS column dbase + d (srhip_isa.h)
+  void set_derived(const std::vector<uint32_t>* dspec, int dbase) {
+    dspec_ = dspec;
+    dbase_ = dbase;
+  }
+  uint64_t dmask() const { return dmask_; }
+
+ private:
 
   int validate(int64_t i, int depth) {
     if (i < 0 || i >= nn_) return fail(SRHIP_ERR_INVALID, "child index %lld out of range", (long long)i);
@@ -206,7 +230,17 @@ template <typename T> class TreeCompiler {
     return c;
   }
   bool is_leaf(int64_t i) const { return nd_[i].degree == 0; }
-  bool leafish(int64_t i) { return is_leaf(i) || (!grad_ && is_const(i)); }
+  bool leafish(int64_t i) { return is_leaf(i) || (!grad_ && is_const(i)) || dcol(i) >= 0; }
+  // derived column of node i (a listed U applied to a feature leaf), or -1
+  int dcol(int64_t i) const { return dcolv_.empty() ? -1 : dcolv_[i]; }
+  // column a leaf-like operand is read from (feature or derived), or -1 for constants
+  int leaf_col(int64_t i) {
+    if (leaf_is_feature(i)) return nd_[i].feature - 1;
+    const int d = dcol(i);
+    if (d < 0) return -1;
+    dmask_ |= 1ull << d;
+    return dbase_ + d;
+  }
   void number_constants(int64_t i, int32_t& k) {
     const srhip_node& n = nd_[i];
     if (n.degree == 0) {
@@ -332,6 +366,10 @@ template <typename T> class TreeCompiler {
   }
 
   int need(int64_t i) {
+    if (memo_need_[i] < 0) memo_need_[i] = (int16_t)need_(i);
+    return memo_need_[i];
+  }
+  int need_(int64_t i) {
     if (leafish(i)) return 0;
     const srhip_node& n = nd_[i];
     if (n.degree == 1) return need(n.l);
@@ -362,7 +400,8 @@ template <typename T> class TreeCompiler {
   bool leaf_is_feature(int64_t i) const { return nd_[i].degree == 0 && !nd_[i].constant; }
 
   void emit_leaf(int64_t i) {
-    if (leaf_is_feature(i)) push_ins(H_LOADF, nd_[i].feature - 1, 0);
+    const int col = leaf_col(i);
+    if (col >= 0) push_ins(H_LOADF, (uint32_t)col, 0);
     else push_ins(H_LOADC, cop(i), leaf_imm(i));
   }
 
@@ -384,11 +423,11 @@ template <typename T> class TreeCompiler {
     if (sb >= 0) {
       if (rl) {
         emit(L, base, i);
-        if (leaf_is_feature(Rr)) push_op(h_spec(sb, SPEC_AF), nd_[Rr].feature - 1, 0, i, parent);
+        if (leaf_col(Rr) >= 0) push_op(h_spec(sb, SPEC_AF), leaf_col(Rr), 0, i, parent);
         else push_op(h_spec(sb, SPEC_AC), cop(Rr), leaf_imm(Rr), i, parent);
       } else if (ll) {
         emit(Rr, base, i);
-        if (leaf_is_feature(L)) push_op(h_spec(sb, SPEC_FA), nd_[L].feature - 1, 0, i, parent);
+        if (leaf_col(L) >= 0) push_op(h_spec(sb, SPEC_FA), leaf_col(L), 0, i, parent);
         else push_op(h_spec(sb, SPEC_CA), cop(L), leaf_imm(L), i, parent);
       } else if (need(L) >= need(Rr)) {
         emit(L, base, i);
@@ -406,12 +445,12 @@ template <typename T> class TreeCompiler {
     // heavy binary op (pow, mod, atan2): the second operand lives in stack slot `base`
     if (rl) {
       emit(L, base, i);
-      if (leaf_is_feature(Rr)) push_ins(H_SLOADF0 + base, nd_[Rr].feature - 1, 0);
+      if (leaf_col(Rr) >= 0) push_ins(H_SLOADF0 + base, leaf_col(Rr), 0);
       else push_ins(H_SLOADC0 + base, cop(Rr), leaf_imm(Rr));
       push_op(h_heavy(hb, HEAVY_AS0 + base), 0, 0, i, parent);  // A = A op S[base]
     } else if (ll) {
       emit(Rr, base, i);
-      if (leaf_is_feature(L)) push_ins(H_SLOADF0 + base, nd_[L].feature - 1, 0);
+      if (leaf_col(L) >= 0) push_ins(H_SLOADF0 + base, leaf_col(L), 0);
       else push_ins(H_SLOADC0 + base, cop(L), leaf_imm(L));
       push_op(h_heavy(hb, HEAVY_SA0 + base), 0, 0, i, parent);  // A = S[base] op A
     } else if (need(L) >= need(Rr)) {
@@ -427,6 +466,68 @@ template <typename T> class TreeCompiler {
     }
   }
 };
+
+// Derived-column program (srhip_isa.h): count the heavy U(X[f]) nodes reachable in the live trees,
+// keep the pairs used at least DERIVE_MIN_USES times (most used first, at most DERIVE_MAX) and
+// compile every tree again with those nodes as column reads.  SRHIP_NO_DERIVE=1 disables it.
+template <typename T>
+int compile_derived_t(srhip_program& P) {
+  P.dspec.clear();
+  P.dmask.assign(P.ntrees, 0);
+  P.dcode.clear();
+  P.dprog_off.assign(P.ntrees, 0);
+  P.dcost.assign(P.ntrees, 0.0);
+  P.dkmax = P.dmax_len = 0;
+  const char* env = getenv("SRHIP_NO_DERIVE");
+  const bool off = env && *env && *env != '0';
+  if (std::is_same<T, int32_t>::value || off) return SRHIP_OK;
+  std::vector<std::pair<uint32_t, int>> cnt;  // (key, uses)
+  std::vector<int64_t> stack;
+  for (int32_t t = 0; t < P.ntrees; ++t) {
+    if (P.info[t].static_fail) continue;
+    const srhip_node* nd = P.nodes.data() + P.offsets[t];
+    stack.assign(1, 0);
+    while (!stack.empty()) {
+      const int64_t i = stack.back();
+      stack.pop_back();
+      const srhip_node& n = nd[i];
+      if (n.degree == 0) continue;
+      stack.push_back(n.l);
+      if (n.degree == 2) {
+        stack.push_back(n.r);
+        continue;
+      }
+      const srhip_node& c = nd[n.l];
+      if (c.degree != 0 || c.constant) continue;
+      const int u = classify_unop(P.unaops[n.op - 1]);
+      if (!un_derivable(u)) continue;
+      const uint32_t key = ((uint32_t)u << 16) | (uint32_t)(c.feature - 1);
+      auto it = std::find_if(cnt.begin(), cnt.end(), [&](const std::pair<uint32_t, int>& e) { return e.first == key; });
+      if (it == cnt.end()) cnt.emplace_back(key, 1);
+      else ++it->second;
+    }
+  }
+  std::stable_sort(cnt.begin(), cnt.end(), [](const std::pair<uint32_t, int>& a, const std::pair<uint32_t, int>& b) {
+    return a.second > b.second;
+  });
+  for (const auto& e : cnt)
+    if (e.second >= DERIVE_MIN_USES && (int)P.dspec.size() < DERIVE_MAX) P.dspec.push_back(e.first);
+  if (P.dspec.empty()) return SRHIP_OK;
+  for (int32_t t = 0; t < P.ntrees; ++t) {
+    const int64_t b = P.offsets[t], e = P.offsets[t + 1];
+    TreeCompiler<T> tc(P.nodes.data() + b, e - b, P, 0);
+    tc.set_derived(&P.dspec, P.maxfeat);
+    TreeInfo ti;
+    int rc = tc.compile(ti, P.dcode);
+    if (rc) return fail(rc, "tree %d (derived program): %s", (int)t, g_err.c_str());
+    P.dprog_off[t] = ti.code_begin;
+    P.dmask[t] = tc.dmask();
+    P.dcost[t] = ti.cost;
+    P.dkmax = std::max(P.dkmax, ti.need);
+    P.dmax_len = std::max(P.dmax_len, ti.code_len);
+  }
+  return SRHIP_OK;
+}
 
 template <typename T>
 int compile_program_t(srhip_program& P) {
@@ -450,9 +551,13 @@ int compile_program_t(srhip_program& P) {
     P.total_nodes += P.info[t].nnodes;
   }
   // operator-node count (degree >= 1), from the node tables
+  P.maxfeat = 0;
   for (int32_t t = 0; t < P.ntrees; ++t)
-    for (int64_t i = P.offsets[t]; i < P.offsets[t + 1]; ++i) P.total_ops += P.nodes[i].degree > 0;
-  return SRHIP_OK;
+    for (int64_t i = P.offsets[t]; i < P.offsets[t + 1]; ++i) {
+      P.total_ops += P.nodes[i].degree > 0;
+      if (P.nodes[i].degree == 0 && !P.nodes[i].constant) P.maxfeat = std::max<int32_t>(P.maxfeat, P.nodes[i].feature);
+    }
+  return compile_derived_t<T>(P);
 }
 
 template <typename T>
@@ -517,6 +622,19 @@ int srhip::upload_program(srhip_program& P) {
   if (!P.prog_off.empty())
     HIP_TRY(hipMemcpyAsync(P.d_off.p, P.prog_off.data(), P.prog_off.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                            P.ctx->stream));
+  if (!P.dspec.empty()) {
+    HIP_TRY(P.d_dcode.ensure(P.dcode.size() * sizeof(Ins)));
+    HIP_TRY(P.d_doff.ensure(P.dprog_off.size() * sizeof(int32_t)));
+    HIP_TRY(P.d_dspec.ensure(P.dspec.size() * sizeof(uint32_t)));
+    HIP_TRY(P.d_dmask.ensure(P.dmask.size() * sizeof(uint64_t)));
+    HIP_TRY(hipMemcpyAsync(P.d_dcode.p, P.dcode.data(), P.dcode.size() * sizeof(Ins), hipMemcpyHostToDevice, P.ctx->stream));
+    HIP_TRY(hipMemcpyAsync(P.d_doff.p, P.dprog_off.data(), P.dprog_off.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                           P.ctx->stream));
+    HIP_TRY(hipMemcpyAsync(P.d_dspec.p, P.dspec.data(), P.dspec.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                           P.ctx->stream));
+    HIP_TRY(hipMemcpyAsync(P.d_dmask.p, P.dmask.data(), P.dmask.size() * sizeof(uint64_t), hipMemcpyHostToDevice,
+                           P.ctx->stream));
+  }
   HIP_TRY(hipStreamSynchronize(P.ctx->stream));
   return SRHIP_OK;
 }
@@ -576,21 +694,21 @@ int srhip::make_view(srhip_ctx* ctx, const srhip_dataset* ds, const int64_t* idx
   return SRHIP_OK;
 }
 
-LaunchPlan srhip::plan_launch(const srhip_ctx* ctx, int dtype, int64_t nfeat, bool weighted, bool with_y, int64_t m,
-                              int32_t ntrees, int tile) {
+LaunchPlan srhip::plan_launch(const srhip_ctx* ctx, int dtype, int64_t nxcols, bool weighted, bool with_y, int64_t m,
+                              int32_t ntrees, int tile, size_t budget) {
   LaunchPlan L;
   ntrees = std::max<int32_t>(1, ntrees);  // every tree may have failed statically
   m = std::max<int64_t>(1, m);
   const size_t es = dtype_size(dtype);
-  const int ncols = (int)nfeat + (with_y ? 1 : 0) + (weighted ? 1 : 0);
-  const size_t budget = 64 * 1024 - 64;
+  const int ncols = (int)nxcols + (with_y ? 1 : 0) + (weighted ? 1 : 0);
+  const int lo = std::max(tile, loss_chunk(dtype));  // row blocks are whole tiles and loss chunks
   int rb = ROW_ALIGN;
-  while (rb > tile && (size_t)ncols * rb * es > budget) rb /= 2;
+  while (rb > lo && (size_t)ncols * rb * es > budget) rb /= 2;
   // do not make blocks much larger than the data
-  while (rb > tile && rb / 2 >= m) rb /= 2;
+  while (rb > lo && rb / 2 >= m) rb /= 2;
   // diagnostic override (tuning runs): SRHIP_RB_ROWS = rows per workgroup, a power of two >= tile
   static const int rb_env = [] { const char* e = getenv("SRHIP_RB_ROWS"); return e ? atoi(e) : 0; }();
-  if (rb_env >= tile && rb_env <= ROW_ALIGN && (rb_env & (rb_env - 1)) == 0 && rb_env < rb) rb = rb_env;
+  if (rb_env >= lo && rb_env <= ROW_ALIGN && (rb_env & (rb_env - 1)) == 0 && rb_env < rb) rb = rb_env;
   L.rb_rows = rb;
   L.xlds = (size_t)ncols * rb * es <= budget;
   L.lds = (L.xlds ? (size_t)ncols * rb * es : 0) + 16;
@@ -608,9 +726,11 @@ LaunchPlan srhip::plan_launch(const srhip_ctx* ctx, int dtype, int64_t nfeat, bo
 namespace {
 
 // trees sorted by estimated cost (desc), dealt round-robin to groups; returns order [ntrees]
-std::vector<int32_t> make_order(const srhip_program& P, const std::vector<int32_t>& trees, int groups, int tpg) {
+std::vector<int32_t> make_order(const srhip_program& P, const std::vector<int32_t>& trees, int groups, int tpg,
+                                bool derived) {
   std::vector<int32_t> s(trees);
-  std::stable_sort(s.begin(), s.end(), [&](int32_t a, int32_t b) { return P.info[a].cost > P.info[b].cost; });
+  auto cost = [&](int32_t t) { return derived ? P.dcost[t] : P.info[t].cost; };
+  std::stable_sort(s.begin(), s.end(), [&](int32_t a, int32_t b) { return cost(a) > cost(b); });
   const int n = (int)s.size();
   std::vector<int32_t> order(s.size());
   std::vector<int> fill(groups, 0), cap(groups, 0);
@@ -737,24 +857,44 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   // stack slots of the kernel variant; the wide operators live only in the K_MAX variant
   bool wide = false;
   for (int32_t u : P->unaops) wide |= u == SRHIP_OP_ASIN || u == SRHIP_OP_ACOS || u == SRHIP_OP_ATANH_CLIP;
-  const int K = wide ? K_MAX : (P->kmax <= 2 ? 2 : (P->kmax <= 4 ? 4 : 8));
-  const int R = pick_rows_per_lane(dtype, K, mode, v.m);
-  LaunchPlan L = plan_launch(ctx, dtype, nf, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R);
+  auto kvariant = [&](int32_t kmax) { return wide ? K_MAX : (kmax <= 2 ? 2 : (kmax <= 4 ? 4 : 8)); };
+  // derived-column program when its staging fits LDS (the R = 16 variant runs 2 workgroups per CU,
+  // so it may use 80 KB); otherwise the plain program
+  const int nd = (int)P->dspec.size();
+  bool use_d = false;
+  int K = 0, R = 0;
+  LaunchPlan L{};
+  if (nd > 0 && mode != MODE_PRECISE) {
+    K = kvariant(P->dkmax);
+    R = pick_rows_per_lane(dtype, K, mode, v.m);
+    const size_t budget = (dtype == SRHIP_F32 && R == R_F32_WIDE) ? 80 * 1024 - 512 : 64 * 1024 - 512;
+    L = plan_launch(ctx, dtype, P->maxfeat + nd, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R, budget);
+    use_d = L.xlds;
+  }
+  if (!use_d) {
+    K = kvariant(P->kmax);
+    R = pick_rows_per_lane(dtype, K, mode, v.m);
+    L = plan_launch(ctx, dtype, P->maxfeat, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R);
+  }
   const int nl = (int)live.size();
-  std::vector<int32_t> order = make_order(*P, live, L.groups, L.tpg);
+  std::vector<int32_t> order = make_order(*P, live, L.groups, L.tpg, use_d);
   HIP_TRY(ctx->order_prec.ensure(order.size() * sizeof(int32_t)));
   HIP_TRY(hipMemcpyAsync(ctx->order_prec.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                          ctx->stream));
-  HIP_TRY(ctx->slab_loss.ensure((size_t)nt * L.nrb * 8));
+  const int nch = (int)((v.m + loss_chunk(dtype) - 1) / loss_chunk(dtype));
+  HIP_TRY(ctx->slab_loss.ensure((size_t)nt * nch * 8));
   HIP_TRY(ctx->slab_chk.ensure((size_t)nt * L.nrb * 8));
   HIP_TRY(ctx->red_loss.ensure((size_t)nt * 8));
   HIP_TRY(ctx->red_chk.ensure((size_t)nt * 8));
   HIP_TRY(ctx->h_loss.ensure((size_t)nt * 8));
   HIP_TRY(ctx->h_chk.ensure((size_t)nt * 8));
   EvalArgs a{};
-  a.code = (const Ins*)P->d_code.p;
-  a.prog_off = (const int32_t*)P->d_off.p;
+  a.code = (const Ins*)(use_d ? P->d_dcode.p : P->d_code.p);
+  a.prog_off = (const int32_t*)(use_d ? P->d_doff.p : P->d_off.p);
   a.order = (const int32_t*)ctx->order_prec.p;
+  a.nd = use_d ? nd : 0;
+  a.dspec = use_d ? (const uint32_t*)P->d_dspec.p : nullptr;
+  a.dmask = use_d ? (const uint64_t*)P->d_dmask.p : nullptr;
   a.X = v.X;
   a.y = v.y;
   a.w = weighted ? v.w : nullptr;
@@ -763,15 +903,16 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   a.ld = v.ld;
   a.nvalid = v.m;
   a.ntrees = nl;
-  a.nfeat = (int32_t)nf;
+  a.nfeat = P->maxfeat;  // staged feature columns
   a.rb_rows = L.rb_rows;
   a.nrb = L.nrb;
+  a.nch = nch;
   a.trees_per_group = L.tpg;
   a.loss_kind = loss ? loss->kind : 0;
   a.loss_p0 = loss ? loss->p0 : 0.0;
   a.weighted = weighted ? 1 : 0;
   a.has_y = mode == MODE_LOSS ? 1 : 0;
-  a.max_steps = P->max_len;
+  a.max_steps = use_d ? P->dmax_len : P->max_len;
   a.debug_stop = debug_stop();
   if (trace_on()) {
     HIP_TRY(ctx->h_dbg.ensure(64 * sizeof(int32_t), hipHostMallocCoherent));
@@ -812,7 +953,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       }
     }
   }
-  HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p,
+  HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, nch, dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p,
                         L.nrb, nt, mode == MODE_LOSS ? ctx->red_loss.p : nullptr,
                         dtype == SRHIP_I32 ? nullptr : ctx->red_chk.p, ctx->stream));
   if (mode == MODE_LOSS)
@@ -1235,6 +1376,13 @@ int srhip_program_stats(const srhip_program* P, int64_t* total_nodes, int64_t* t
   if (total_nodes) *total_nodes = P->total_nodes;
   if (total_opnodes) *total_opnodes = P->total_ops;
   if (max_stack) *max_stack = P->kmax;
+  return SRHIP_OK;
+}
+
+int srhip_program_derived(const srhip_program* P, int32_t* count, uint32_t* spec, int32_t cap) {
+  if (!P) return fail(SRHIP_ERR_INVALID, "null program");
+  if (count) *count = (int32_t)P->dspec.size();
+  for (int32_t d = 0; spec && d < cap && d < (int32_t)P->dspec.size(); ++d) spec[d] = P->dspec[d];
   return SRHIP_OK;
 }
 

@@ -142,7 +142,17 @@ struct srhip_program {
   std::vector<int32_t> prog_off;
   int32_t kmax = 0, max_ops = 0, max_len = 0;
   int64_t total_nodes = 0, total_ops = 0;
+  int32_t maxfeat = 0;  // largest feature index any tree reads (the columns a launch stages)
   srhip::DevBuf d_code, d_off;
+  // derived-column program (srhip_isa.h): the same trees with U(X[f]) leaves reading LDS columns;
+  // used by loss / prediction launches whose staging fits LDS, the plain program otherwise
+  std::vector<uint32_t> dspec;  // [nd] (U << 16) | (feature - 1)
+  std::vector<uint64_t> dmask;  // [ntrees]
+  std::vector<srhip::Ins> dcode;
+  std::vector<int32_t> dprog_off;
+  std::vector<double> dcost;
+  int32_t dkmax = 0, dmax_len = 0;
+  srhip::DevBuf d_dcode, d_doff, d_dspec, d_dmask;
   // gradient program (constants not folded, constant leaves carry their get_constants index);
   // compiled on first use by the constant-gradient path
   bool grad_ready = false;
@@ -174,8 +184,9 @@ int compile_grad_program(srhip_program& P);  // gradient program, uploaded
 int upload_program(srhip_program& P);
 int make_view(srhip_ctx* ctx, const srhip_dataset* ds, const int64_t* idx, int64_t nidx, bool need_y, View& v);
 int gathered_weight_sum(srhip_ctx* ctx, const srhip_dataset* ds, int64_t nidx, View& v);
-LaunchPlan plan_launch(const srhip_ctx* ctx, int dtype, int64_t nfeat, bool weighted, bool with_y, int64_t m,
-                       int32_t ntrees, int rows_per_tile);
+// ncols: feature (+ derived) columns staged; lds_budget: bytes of LDS a workgroup may use
+LaunchPlan plan_launch(const srhip_ctx* ctx, int dtype, int64_t ncols, bool weighted, bool with_y, int64_t m,
+                       int32_t ntrees, int rows_per_tile, size_t lds_budget = 64 * 1024 - 64);
 // did_succeed decision of tree t from partials in the srhip_eval_loss_partials layout:
 // 0 ok, 1 fail, 2 undecided (only the sums' feature / row-count entries are read)
 int decide_tree(const TreeInfo& I, const srhip_program& P, int64_t nfeat, const double* sums, double chk);

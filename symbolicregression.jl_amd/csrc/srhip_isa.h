@@ -50,6 +50,23 @@ enum Unop : int {
   NUM_UNOP
 };
 
+// Unary operators cheap enough to inline into their handler (a few VALU instructions per row).
+constexpr bool un_cheap(int u) {
+  return u == UN_NEG || u == UN_SQUARE || u == UN_CUBE || u == UN_ABS || u == UN_RELU || u == UN_SIGN ||
+         u == UN_ROUND || u == UN_FLOOR || u == UN_CEIL;
+}
+// "Wide" unary operators (OCML bodies with ~100 live VGPRs): only the K = K_MAX variant has them.
+constexpr bool un_wide_op(int u) { return u == UN_ASIN || u == UN_ACOS || u == UN_ATANH_CLIP; }
+
+// Derived columns: a heavy unary operator applied directly to a feature leaf, U(X[f]), has the same
+// value in every tree of a population.  The host lists the (U, f) pairs a program uses at least
+// DERIVE_MIN_USES times; each workgroup computes them once for its rows into LDS columns after the
+// staged features (same out-of-line operator bodies, so bit-identical values) and the trees read
+// them like features.  A derived column d is LDS column (staged features + d).
+constexpr int DERIVE_MAX = 16;
+constexpr int DERIVE_MIN_USES = 2;
+constexpr bool un_derivable(int u) { return u >= 0 && !un_cheap(u) && !un_wide_op(u); }
+
 // ---- handler ids -----------------------------------------------------------------------------
 enum : uint32_t {
   H_END = 0,

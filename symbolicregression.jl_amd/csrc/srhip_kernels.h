@@ -23,6 +23,12 @@ constexpr int R_F32_WIDE = 16;
 constexpr int64_t WIDE_MIN_ROWS = 4096;
 constexpr int ROW_ALIGN = 4096;  // device datasets are padded to a multiple of this many rows
 constexpr int MODE_LOSS = 0, MODE_PRED = 1, MODE_PRECISE = 2;
+// Loss partials are kept per fixed chunk of rows (not per workgroup row block): every lane adds
+// its rows of a chunk in the same order whatever R, K, row-block size or program (derived columns
+// or not) evaluates the tree, so a tree's loss on a dataset is one bit pattern in every launch.
+// Row blocks are whole chunks.
+constexpr int LOSS_CHUNK_4B = 1024, LOSS_CHUNK_8B = 256;
+inline int loss_chunk(int dtype) { return dtype == SRHIP_F64 ? LOSS_CHUNK_8B : LOSS_CHUNK_4B; }
 
 struct FeatStat {
   double sum;           // f64 sum (Float64 data: sum of x * 2^-64)
@@ -33,10 +39,10 @@ struct EvalArgs {
   const Ins* code;          // all trees' bytecode
   const int32_t* prog_off;  // [ntrees] first instruction of each tree
   const int32_t* order;     // [ntrees] processing order (grouped, cost-sorted)
-  const void* X;            // [nfeat][ld] SoA, padded
+  const void* X;            // [>= nfeat][ld] SoA, padded (the first nfeat columns are staged)
   const void* y;            // [ld] (nullptr for prediction-only)
   const void* w;            // [ld] or nullptr
-  void* slab_loss;          // [ntrees][nrb] loss partials (double; int64 for Int32)
+  void* slab_loss;          // [ntrees][nch] loss partials per row chunk (double; int64 for Int32)
   void* slab_chk;           // [ntrees][nrb] check partials (float max|v| / double sum|v|*2^-512)
   void* out_pred;           // [ntrees][nvalid] (MODE_PRED)
   void* slab_prec;          // [n][prec_stride][nrb] double (MODE_PRECISE)
@@ -46,6 +52,7 @@ struct EvalArgs {
   int32_t nfeat;
   int32_t rb_rows;          // rows per workgroup (multiple of 64*R)
   int32_t nrb;              // row blocks
+  int32_t nch;              // loss chunks: ceil(nvalid / loss_chunk)
   int32_t trees_per_group;  // trees per grid.y group
   int32_t loss_kind;
   double loss_p0;
@@ -54,7 +61,9 @@ struct EvalArgs {
   int32_t has_y;            // stage y into LDS (MODE_LOSS)
   int32_t max_steps;        // longest tree program (instructions): bounds every interpreter loop
   int32_t debug_stop;       // diagnostic early exits (SRHIP_DEBUG_STOP); 0 in normal runs
-  int32_t pad_;
+  int32_t nd;               // derived columns (LDS columns nfeat .. nfeat+nd-1); 0 unless XLDS
+  const uint32_t* dspec;    // [nd] (U << 16) | feature of each derived column
+  const uint64_t* dmask;    // [program trees] bit d: the tree reads derived column d
   int32_t* dbg;             // SRHIP_TRACE: host-coherent progress words of block (0,0) wave 0, else nullptr
 };
 
@@ -63,7 +72,7 @@ int rows_per_lane(int dtype);
 int pick_rows_per_lane(int dtype, int K, int mode, int64_t m);
 hipError_t launch_eval(int dtype, const EvalArgs& a, int R, int K, int mode, bool xlds, dim3 grid, size_t lds,
                        hipStream_t s);
-hipError_t launch_reduce(int dtype, const void* slab_loss, const void* slab_chk, int nrb, int ntrees, void* out_loss,
+hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, const void* slab_chk, int nrb, int ntrees, void* out_loss,
                          void* out_chk, hipStream_t s);
 hipError_t launch_gather(int dtype, const void* X, const void* y, const void* w, int64_t ld_src, int nfeat,
                          const int64_t* idx, int64_t m, int64_t ld_dst, void* Xd, void* yd, void* wd, hipStream_t s);

@@ -108,6 +108,7 @@ SIGNATURES = {
     "srhip_last_kernel_ms": (_dbl, [_vp]),
     "srhip_program_stats": (ctypes.c_int, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
                                            ctypes.POINTER(_i32)]),
+    "srhip_program_derived": (ctypes.c_int, [_vp, ctypes.POINTER(_i32), _vp, _i32]),
 }
 
 _lib = None

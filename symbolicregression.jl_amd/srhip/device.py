@@ -136,6 +136,13 @@ class Program:
         check(_lib.load().srhip_program_stats(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         return dict(total_nodes=a.value, total_opnodes=b.value, max_stack=c.value)
 
+    def derived_columns(self) -> list:
+        """[(device unary op, 0-based feature)] computed once per workgroup and shared by the trees."""
+        n = ctypes.c_int32()
+        spec = np.zeros(64, dtype=np.uint32)
+        check(_lib.load().srhip_program_derived(self.handle, ctypes.byref(n), ptr(spec), 64))
+        return [(int(s) >> 16, int(s) & 0xffff) for s in spec[:n.value]]
+
     def eval_loss(self, ds: DeviceDataset, loss, idx=None):
         out = np.empty(self.ntrees, dtype=np.float64)
         ok = np.empty(self.ntrees, dtype=np.uint8)
