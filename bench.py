@@ -36,8 +36,12 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--binops", default="+,-,*,/", help="(tuning) binary operators of the C2 population")
     ap.add_argument("--unaops", default="cos,exp", help="(tuning) unary operators of the C2 population")
-    ap.add_argument("--config", default="c2", choices=("c2", "c4"),
-                    help="c2 (default, the headline metric) or c4: batched constant optimisation")
+    ap.add_argument("--config", default="c2", choices=("c2", "c4", "c1", "c3"),
+                    help="c2 (default, the headline metric); c4: batched constant optimisation; c1 / c3: "
+                         "equation_search (README example / 10M x 10 islands over the ranks)")
+    ap.add_argument("--iterations", type=int, default=0,
+                    help="c1/c3: search iterations (default: c1 2 of the config's 40, c3 1)")
+    ap.add_argument("--ncycles", type=int, default=0, help="c1/c3: ncycles_per_iteration (default 550)")
     return ap.parse_args()
 
 
@@ -45,6 +49,8 @@ def main():
     args = parse()
     if args.config == "c4":
         return bench_c4(args)
+    if args.config in ("c1", "c3"):
+        return bench_search(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -286,6 +292,141 @@ def bench_c4(args):
         "grad_launch_ms": gdt * 1e3,
         "grad_node_row_evals_per_s": st["total_nodes"] * rows / gdt,
     }))
+
+
+def bench_search(args):
+    """C1 / C3: the full search (srhip.search.equation_search: regularized-evolution islands,
+    every score through the device coalescer, constants optimised on the device).
+      c1: README example, X = randn(2, 100) Float64, y = 2cos(x2) + x1^2 - 2, + * / - cos exp,
+          populations = 20 (the config's niterations = 40; default here a bounded 2).
+      c3: 10 x 10M Float32, populations = 15 per GPU, islands sharded over the ranks with the
+          per-iteration all-gather migration (RCCL under torch.distributed.run).
+    value = tree-node x row evaluations scored per second (all ranks), the search's wall time
+    bracketed by barriers, max over ranks.  cpu_baseline (rank 0, N = 1): the same search with
+    the oracle as scorer (c1), or the oracle's population-eval rate on a row sample (c3)."""
+    import numpy as np
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    import srhip
+    from srhip import search as S
+
+    c1 = args.config == "c1"
+    ops = dict(binary_operators=("+", "*", "/", "-"), unary_operators=("cos", "exp"))
+    if c1:
+        rng = np.random.default_rng(0)
+        X = rng.standard_normal((2, 100))
+        y = 2 * np.cos(X[1]) + X[0] ** 2 - 2
+        npops, iters = 20, args.iterations or 2
+    else:
+        n = 10_000_000 if args.rows == 1_000_000 else args.rows
+        rng = np.random.default_rng(0)  # same dataset on every rank (replicas)
+        X = rng.standard_normal((10, n)).astype(np.float32)
+        Xd = X.astype(np.float64)
+        y = (2 * np.cos(Xd[3]) + Xd[0] ** 2 - 2 + 0.5 * Xd[6] * Xd[2] - np.exp(Xd[9] / 4)).astype(np.float32)
+        del Xd
+        npops, iters = 15 * world, args.iterations or 1
+    kw = dict(populations=npops, deterministic=True, seed=1, device=local_rank, **ops)
+    if args.ncycles:
+        kw["ncycles_per_iteration"] = args.ncycles
+    opts = srhip.Options(**kw)
+    d = srhip.Dataset(X, y)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    res = S.equation_search(d, None, opts, niterations=iters)
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    front = res.pareto_frontier()
+    best = float(min(m.loss for m in front))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_search_baseline(args, c1, X, y, opts, iters, dt)
+    if rank == 0:
+        print(json.dumps({
+            "metric": ("C1 equation_search (README example)" if c1 else "C3 equation_search 10M x 10 F32 islands")
+                      + ": tree-node x row evals/s",
+            "value": res.node_rows / dt, "unit": "node-row evals/s", "higher_is_better": True,
+            "n_gpus": world, "steps": iters, "warmup": 0, "ms_per_step": dt * 1e3 / iters,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64" if c1 else "f32",
+            "data": "synthetic (README formula)" if c1 else "synthetic (X ~ N(0,1) 10x10M, fixed 10-feature formula)",
+            "config": {"workload": ("C1: X=randn(2,100) F64, + * / - cos exp, populations=20" if c1 else
+                                    f"C3: 10M rows x 10 features F32, {npops} populations ({npops // world} per GPU)"),
+                       "iterations": iters, "populations": npops, "ncycles_per_iteration": S.search_option(opts, "ncycles_per_iteration"),
+                       "parallelism": f"islands{world}" if world > 1 else "single"},
+            "search": {"wall_s": dt, "num_evals": res.num_evals, "evals_per_s": res.num_evals / dt,
+                       "node_rows": res.node_rows, "best_loss": best,
+                       "baseline_loss": float(np.mean((y.astype(np.float64) - y.mean()) ** 2)),
+                       "coalescer": res.coalescer_stats},
+            "cpu_baseline": cpu,
+        }))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_search_baseline(args, c1, X, y, opts, iters, gpu_dt):
+    """c1: the same search (same options and seed) with the oracle scorer on the host, bounded to
+    ~cpu_seconds of iterations; c3: the oracle's multithreaded population eval on a row sample."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    import srhip
+    from srhip import search as S
+
+    if c1:
+        class OracleScorer:
+            def __init__(self, d, o):
+                self.d, self.o, self.node_rows = d, o, 0
+
+            def score(self, tree, complexity=None, idx=None):
+                nodes, offs = srhip.flatten([tree], self.o, self.d.X.dtype)
+                le, _, ok, _ = oracle.eval_loss_batch(nodes, offs, self.o.binop_codes, self.o.unaop_codes,
+                                                      self.d.X, self.d.y, nthreads=1)
+                self.node_rows += len(nodes) * self.d.n
+                loss = float(le[0]) if ok[0] else float("inf")
+                return srhip.loss_to_score(loss, self.d.use_baseline, self.d.baseline_loss, tree, self.o,
+                                           complexity), loss
+
+        d = srhip.Dataset(X, y)
+        d.baseline_loss, d.use_baseline = float(np.mean((y - y.mean()) ** 2)), True
+        sc = OracleScorer(d, opts)
+        t0 = time.perf_counter()
+        S.equation_search(d, None, opts, niterations=1, scorer=sc)
+        dt = time.perf_counter() - t0
+        return {"value": sc.node_rows / dt, "unit": "node-row evals/s", "cores": 1, "kind": "port",
+                "sample": f"1 iteration of the same search (20 populations, Python islands) with the "
+                          f"oracle (oracle/sr_oracle.c) as scorer, {dt:.1f} s"}
+    rng = np.random.default_rng(5)
+    trees = srhip.random_population(64, opts, 10, np.float32, seed=6, max_size=20)
+    nodes, offs = srhip.flatten(trees, opts, np.float32)
+    threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1), os.cpu_count() or 1)
+    m = 100_000
+    t0 = time.perf_counter()
+    oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, X[:, :m].copy(), y[:m].copy(),
+                           nthreads=threads)
+    m = int(min(X.shape[1], max(m, m * args.cpu_seconds / max(time.perf_counter() - t0, 1e-6))))
+    t0 = time.perf_counter()
+    _, _, _, used = oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, X[:, :m].copy(),
+                                           y[:m].copy(), nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": int(offs[-1]) * m / dt, "unit": "node-row evals/s", "cores": int(used), "kind": "port",
+            "sample": f"oracle population eval: 64 random trees (size <= 20) x first {m} rows ({dt:.1f} s), "
+                      f"OpenMP over trees"}
 
 
 if __name__ == "__main__":

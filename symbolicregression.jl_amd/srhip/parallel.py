@@ -28,6 +28,10 @@ def _dist():
 
 def world():
     """(rank, world_size) of the default process group, (0, 1) when not initialised."""
+    import sys
+
+    if "torch" not in sys.modules:  # no process group can exist without torch loaded
+        return 0, 1
     try:
         dist = _dist()
         if dist.is_available() and dist.is_initialized():
@@ -117,3 +121,45 @@ def allgather_trees(nodes: np.ndarray, offsets: np.ndarray, group=None):
         of = b[maxb: maxb + 8 * no].copy().view(np.int64)
         result.append((nd, of))
     return result
+
+
+def allgather_f64(a: np.ndarray, group=None):
+    """Variable-length all-gather of a float64 vector -> list of arrays by rank."""
+    import torch
+
+    dist = _dist()
+    dev = _device(group)
+    ws = dist.get_world_size(group)
+    a = np.ascontiguousarray(a, dtype=np.float64).ravel()
+    meta = torch.tensor([len(a)], dtype=torch.int64, device=dev)
+    metas = [torch.zeros_like(meta) for _ in range(ws)]
+    dist.all_gather(metas, meta, group=group)
+    lens = [int(m.cpu().numpy()[0]) for m in metas]
+    buf = np.zeros(max(1, max(lens)), dtype=np.float64)
+    buf[: len(a)] = a
+    t = torch.from_numpy(buf).to(dev)
+    outs = [torch.zeros_like(t) for _ in range(ws)]
+    dist.all_gather(outs, t, group=group)
+    return [o.cpu().numpy()[:n].copy() for o, n in zip(outs, lens)]
+
+
+def exchange_members(trees, scores, losses, options, dtype, group=None):
+    """Migration exchange of the island search (src/Migration.jl:16-38 fed from every rank, as the
+    reference's head node sees every population's best_sub_pop and the hall of fame,
+    src/SymbolicRegression.jl:910-943): this rank's member trees travel as node tables plus
+    their (score, loss); returns [(tree, score, loss)] of all ranks in rank order."""
+    from .node import flatten, unflatten
+
+    if trees:
+        nodes, offs = flatten(trees, options, dtype)
+    else:
+        nodes, offs = np.zeros(0, dtype=NODE_DTYPE), np.zeros(1, dtype=np.int64)
+    sl = np.stack([np.asarray(scores, dtype=np.float64), np.asarray(losses, dtype=np.float64)], 1).ravel()
+    got = allgather_trees(nodes, offs, group)
+    vals = allgather_f64(sl, group)
+    out = []
+    for (nd, of), v in zip(got, vals):
+        ts = unflatten(nd, of, options) if len(of) > 1 else []
+        v = v.reshape(-1, 2)
+        out.extend((t, float(v[i, 0]), float(v[i, 1])) for i, t in enumerate(ts))
+    return out

@@ -117,6 +117,13 @@ class PopMember:
     def copy(self) -> "PopMember":
         return PopMember(self.tree.copy(), self.score, self.loss, self.birth, self.complexity, self.ref, self.parent)
 
+    def get_complexity(self, options) -> int:
+        """compute_complexity cached on the member, as the reference caches it in PopMember
+        (src/PopMember.jl:7-16, recompute_complexity!); reset to -1 whenever ``tree`` changes."""
+        if self.complexity < 0:
+            self.complexity = compute_complexity(self.tree, options)
+        return self.complexity
+
 
 class RunningSearchStatistics:
     """src/AdaptiveParsimony.jl:22-97."""
@@ -173,7 +180,7 @@ class HallOfFame:
     def update(self, members, options) -> None:
         """update_hall_of_fame! (src/SearchUtils.jl:513-531)."""
         for m in members:
-            size = compute_complexity(m.tree, options)
+            size = m.get_complexity(options)
             if not (0 < size < options.maxsize + MAX_DEGREE):
                 continue
             if not self.exists[size - 1] or m.score < self.members[size - 1].score:
@@ -415,10 +422,16 @@ class DeviceScorer:
                                    max_wait_us=max_wait_us, nclients=nclients)
         self.L = dataset.loss_type.type
         self.dtype = dataset.X.dtype
+        self._lock = threading.Lock()
+        self.trees_scored = 0
+        self.node_rows = 0
 
     def score(self, tree, complexity=None, idx=None):
         nodes, _ = flatten([tree], self.options, self.dtype)
         loss, ok = self.coalescer.score_loss(nodes, idx)
+        with self._lock:  # work counters (bench: node-row evaluations)
+            self.trees_scored += 1
+            self.node_rows += len(nodes) * (self.dataset.n if idx is None else len(idx))
         loss = self.L(loss) if ok else self.L(np.inf)
         score = loss_to_score(loss, self.dataset.use_baseline, self.dataset.baseline_loss, tree, self.options,
                               complexity)
@@ -507,24 +520,27 @@ class Island:
             successful = successful and check_constraints(tree, o, curmaxsize)
             attempts += 1
         if not successful:
-            return PopMember(member.tree.copy(), before_score, before_loss, parent=member.ref), False
+            return PopMember(member.tree.copy(), before_score, before_loss, complexity=member.complexity,
+                             parent=member.ref), False
         after_score, after_loss = self.scorer.score(tree)
         self.num_evals += 1
         if math.isnan(after_score):
-            return PopMember(member.tree.copy(), before_score, before_loss, parent=member.ref), False
+            return PopMember(member.tree.copy(), before_score, before_loss, complexity=member.complexity,
+                             parent=member.ref), False
         prob = 1.0
         if search_option(o, "annealing"):
             delta = after_score - before_score
             prob *= math.exp(-delta / (temperature * search_option(o, "alpha")))
         if search_option(o, "use_frequency"):
-            old_size = compute_complexity(member.tree, o)
+            old_size = member.get_complexity(o)
             new_size = compute_complexity(tree, o)
             nf = stats.normalized_frequencies
             old_f = nf[old_size - 1] if 0 < old_size <= o.maxsize else 1e-6
             new_f = nf[new_size - 1] if 0 < new_size <= o.maxsize else 1e-6
             prob *= old_f / new_f
         if prob < rng.random():
-            return PopMember(member.tree.copy(), before_score, before_loss, parent=member.ref), False
+            return PopMember(member.tree.copy(), before_score, before_loss, complexity=member.complexity,
+                             parent=member.ref), False
         return PopMember(tree, after_score, after_loss, parent=member.ref), True
 
     # src/Mutate.jl:349-429
@@ -554,7 +570,7 @@ class Island:
             a = search_option(o, "adaptive_parsimony_scaling")
             scores = []
             for m in sample:
-                size = compute_complexity(m.tree, o)
+                size = m.get_complexity(o)
                 freq = stats.normalized_frequencies[size - 1] if 0 < size <= o.maxsize else 0.0
                 scores.append(m.score * math.exp(a * freq))
         else:
@@ -599,7 +615,7 @@ class Island:
         for temperature in np.linspace(max_temp, min_temp, ncycles):
             pop = self.reg_evol_cycle(pop, float(temperature), curmaxsize, stats)
             for m in pop:
-                size = compute_complexity(m.tree, o)
+                size = m.get_complexity(o)
                 if 0 < size <= o.maxsize and (not best_seen.exists[size - 1]
                                               or m.score < best_seen.members[size - 1].score):
                     best_seen.exists[size - 1] = True
@@ -614,6 +630,7 @@ class Island:
         if search_option(o, "should_simplify"):
             for m in pop:
                 m.tree = combine_operators(simplify_tree(m.tree, o, self.dtype), o, self.dtype)
+                m.complexity = -1
         if search_option(o, "should_optimize_constants"):
             chosen = [m for m, d in zip(pop, do_opt) if d and count_constants(m.tree) > 0]
             if chosen:
@@ -660,59 +677,82 @@ class SearchResult:
     populations: list
     num_evals: float
     coalescer_stats: dict
+    node_rows: float = 0.0  # tree-node x row evaluations scored on the device (all ranks)
 
     def pareto_frontier(self):
         return self.hall_of_fame.pareto_frontier()
 
 
 def equation_search(X, y, options, niterations: int = 10, weights=None, seed=None, scorer=None,
-                    verbosity: int = 0) -> SearchResult:
+                    verbosity: int = 0, distributed=None, group=None) -> SearchResult:
     """equation_search (src/SymbolicRegression.jl:357-1000) for one output, populations as
     concurrent island threads, every score through the device.  ``scorer`` (testing hook):
     any object with ``score(tree, complexity=None) -> (score, loss)``; default: the device
-    coalescer."""
+    coalescer.
+
+    Multi-GPU: under torch.distributed with world size > 1 (or
+    ``distributed=True``), rank r owns the populations k with k % world == r on its own GPU
+    (device = LOCAL_RANK) with a full dataset replica; no collective touches evaluation.  After
+    every iteration the ranks exchange their best_sub_pops and hall-of-fame frontiers as node
+    tables (:func:`srhip.parallel.exchange_members`, an all-gather over RCCL / xGMI), fold the
+    remote members into their hall of fame, all-reduce the adaptive-parsimony size counts, and
+    migrate from the global candidate set (src/Migration.jl:16-38).  Islands run in lock step
+    across ranks; every rank returns the same global hall of fame."""
+    from . import parallel
+
     dataset = X if isinstance(X, Dataset) else Dataset(X, y, weights)
     dtype = dataset.X.dtype
     npops = search_option(options, "populations")
     psize = search_option(options, "population_size")
-    det = bool(options.deterministic)
+    rank, ws = parallel.world()
+    if distributed is False:
+        rank, ws = 0, 1
+    dist_mode = ws > 1
+    det = bool(options.deterministic) or dist_mode
     base_seed = options.seed if seed is None else seed
     ss = np.random.SeedSequence(base_seed)
     rngs = [np.random.default_rng(s) for s in ss.spawn(npops + 1)]
-    head_rng = rngs[-1]
+    head_rng = rngs[-1] if not dist_mode else np.random.default_rng([int(base_seed or 0), rank, 7919])
+    local = [k for k in range(npops) if k % ws == rank]
     own_scorer = scorer is None
     if own_scorer:
+        if dist_mode:
+            import os
+
+            options.device = int(os.environ.get("LOCAL_RANK", options.device))
         update_baseline_loss(dataset, options)
-        scorer = DeviceScorer(dataset, options, nclients=npops)
+        scorer = DeviceScorer(dataset, options, nclients=len(local))
     try:
-        islands = [Island(k, dataset, options, scorer, rngs[k], dtype) for k in range(npops)]
+        islands = {k: Island(k, dataset, options, scorer, rngs[k], dtype) for k in local}
         # initial populations: gen_random_tree(3, ...) scored (src/Population.jl:40-63)
-        pops = []
-        for isl in islands:
+        pops = {}
+        for k in local:
+            isl = islands[k]
             trees = [gen_random_tree(3, options, dataset.nfeatures, dtype, isl.rng) for _ in range(psize)]
             members = []
             for t in trees:
                 sc, lo = scorer.score(t)
                 members.append(PopMember(t, sc, lo))
-            pops.append(members)
+            pops[k] = members
         stats = RunningSearchStatistics(options)
         hof = HallOfFame(options)
-        best_sub_pops = [[] for _ in range(npops)]
+        best_sub_pops = {k: [] for k in local}
         total_cycles = npops * niterations
         cycles_remaining = total_cycles
         curmaxsize = get_cur_maxsize(options, total_cycles, cycles_remaining)
-        num_evals = float(npops * psize)
+        num_evals = float(len(local) * psize)
+        topn = search_option(options, "topn")
 
         def process(k, pop, best_seen):
             nonlocal cycles_remaining, curmaxsize, num_evals
-            best_sub_pops[k] = [m for m in sorted(pop, key=lambda m: m.score)][:search_option(options, "topn")]
+            best_sub_pops[k] = [m for m in sorted(pop, key=lambda m: m.score)][:topn]
             for m in pop:
-                stats.update_frequencies(compute_complexity(m.tree, options))
+                stats.update_frequencies(m.get_complexity(options))
             hof.update(pop, options)
             hof.update([m for m, e in zip(best_seen.members, best_seen.exists) if e], options)
             dominating = hof.pareto_frontier()
             if search_option(options, "migration"):
-                cands = [m for sp in best_sub_pops for m in sp]
+                cands = [m for sp in best_sub_pops.values() for m in sp]
                 migrate(cands, pop, options, search_option(options, "fraction_replaced"), head_rng)
             if search_option(options, "hof_migration") and dominating:
                 migrate(dominating, pop, options, search_option(options, "fraction_replaced_hof"), head_rng)
@@ -721,20 +761,65 @@ def equation_search(X, y, options, niterations: int = 10, weights=None, seed=Non
             stats.move_window()
             pops[k] = pop
 
-        with ThreadPoolExecutor(max_workers=npops) as ex:
+        def process_distributed(results, it):
+            """One lock-step iteration's bookkeeping across ranks (see the docstring)."""
+            nonlocal cycles_remaining, curmaxsize
+            nbin = len(stats.frequencies)
+            counts = np.zeros(nbin)
+            for k in local:
+                pop, best_seen = results[k]
+                best_sub_pops[k] = [m for m in sorted(pop, key=lambda m: m.score)][:topn]
+                for m in pop:
+                    size = m.get_complexity(options)
+                    if 0 < size <= nbin:
+                        counts[size - 1] += 1
+                hof.update(pop, options)
+                hof.update([m for m, e in zip(best_seen.members, best_seen.exists) if e], options)
+                pops[k] = pop
+            stats.frequencies += parallel.allreduce_np(counts, "sum", group)
+            stats.move_window()
+            mine = [m for k in local for m in best_sub_pops[k]]
+            front = hof.pareto_frontier()
+            nsub = len(mine)
+            sent = mine + front
+            got = parallel.exchange_members([m.tree for m in sent], [m.score for m in sent],
+                                            [m.loss for m in sent], options, dtype, group)
+            # every rank's contribution = its best_sub_pops, then its frontier; the counts travel too
+            nsubs = parallel.allgather_f64(np.array([nsub, len(sent)], dtype=np.float64), group)
+            cands, remote_front, pos = [], [], 0
+            for v in nsubs:
+                ns, nt = int(v[0]), int(v[1])
+                chunk = [PopMember(t, sc, lo) for t, sc, lo in got[pos: pos + nt]]
+                cands.extend(chunk[:ns])
+                remote_front.extend(chunk[ns:])
+                pos += nt
+            hof.update(cands + remote_front, options)
+            dominating = hof.pareto_frontier()
+            for k in local:
+                if search_option(options, "migration"):
+                    migrate(cands, pops[k], options, search_option(options, "fraction_replaced"), head_rng)
+                if search_option(options, "hof_migration") and dominating:
+                    migrate(dominating, pops[k], options, search_option(options, "fraction_replaced_hof"), head_rng)
+            cycles_remaining = total_cycles - (it + 1) * npops
+            curmaxsize = get_cur_maxsize(options, total_cycles, cycles_remaining)
+
+        with ThreadPoolExecutor(max_workers=max(1, len(local))) as ex:
             if det:
                 for it in range(niterations):
-                    futs = [ex.submit(islands[k].run_iteration, pops[k], curmaxsize, stats) for k in range(npops)]
-                    for k, f in enumerate(futs):
-                        pop, best_seen = f.result()
-                        process(k, pop, best_seen)
-                    if verbosity:
+                    futs = {k: ex.submit(islands[k].run_iteration, pops[k], curmaxsize, stats) for k in local}
+                    if dist_mode:
+                        process_distributed({k: f.result() for k, f in futs.items()}, it)
+                    else:
+                        for k in local:
+                            pop, best_seen = futs[k].result()
+                            process(k, pop, best_seen)
+                    if verbosity and rank == 0:
                         print(f"iteration {it + 1}/{niterations}: best loss "
                               f"{min(m.loss for m in hof.pareto_frontier()):.4g}", flush=True)
             else:
                 # asynchronous like the reference: a finished population is processed and re-dispatched
-                remaining = [niterations] * npops
-                running = {ex.submit(islands[k].run_iteration, pops[k], curmaxsize, stats): k for k in range(npops)}
+                remaining = {k: niterations for k in local}
+                running = {ex.submit(islands[k].run_iteration, pops[k], curmaxsize, stats): k for k in local}
                 from concurrent.futures import FIRST_COMPLETED, wait
 
                 while running:
@@ -748,10 +833,15 @@ def equation_search(X, y, options, niterations: int = 10, weights=None, seed=Non
                             running[ex.submit(islands[k].run_iteration, pops[k], curmaxsize, stats)] = k
                         elif own_scorer:
                             # one client fewer: the coalescer stops waiting for this island
-                            scorer.coalescer.set_clients(sum(1 for r in remaining if r > 0))
-        num_evals += sum(isl.num_evals for isl in islands)
+                            scorer.coalescer.set_clients(sum(1 for r in remaining.values() if r > 0))
+        num_evals += sum(isl.num_evals for isl in islands.values())
+        if dist_mode:
+            num_evals = float(parallel.allreduce_np(np.array([num_evals]), "sum", group)[0])
         cstats = scorer.coalescer.stats() if own_scorer else {}
-        return SearchResult(hof, pops, num_evals, cstats)
+        node_rows = float(getattr(scorer, "node_rows", 0))
+        if dist_mode:
+            node_rows = float(parallel.allreduce_np(np.array([node_rows]), "sum", group)[0])
+        return SearchResult(hof, [pops[k] for k in local], num_evals, cstats, node_rows)
     finally:
         if own_scorer:
             scorer.close()

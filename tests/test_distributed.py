@@ -123,3 +123,64 @@ def test_row_sharded_and_migration_gloo_world2(oracle, dtype):
         for _, _, _, got in res:
             assert got[rank][0] == mn.tobytes()
             assert np.array_equal(got[rank][1], mo)
+
+
+def _search_rank_main(rank, world, port, q):
+    """One rank of the island search (C3 protocol) with the oracle scorer standing in for the GPU."""
+    try:
+        sys.path[:0] = [os.path.join(ROOT, "symbolicregression.jl_amd"), os.path.join(ROOT, "oracle"),
+                        os.path.join(ROOT, "tests")]
+        import torch.distributed as dist
+
+        import oracle
+        import srhip
+        from srhip import search as S
+        from test_search import OracleScorer, _data
+
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        X, y = _data(100, seed=3)
+        o = srhip.Options(binary_operators=("+", "*", "/", "-"), unary_operators=("cos", "exp"),
+                          populations=4, population_size=20, ncycles_per_iteration=30, maxsize=15, seed=9,
+                          should_optimize_constants=False)
+        d = srhip.Dataset(X, y)
+        d.baseline_loss, d.use_baseline = np.float64(np.mean((y - y.mean()) ** 2)), True
+        sc = OracleScorer(d, o, oracle)
+        res = S.equation_search(d, None, o, niterations=3, scorer=sc)
+        front = [(srhip.string_tree(m.tree, o), m.loss) for m in res.pareto_frontier()]
+        q.put((rank, front, len(res.populations), res.num_evals, sc.calls))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # surface the failure to the parent
+        import traceback
+
+        q.put((rank, traceback.format_exc() + repr(e), None, None, None))
+
+
+def test_island_search_gloo_world2():
+    """C3's protocol at world size 2: each rank evolves its half of the populations; after every
+    iteration the ranks exchange best_sub_pops + hall-of-fame frontiers (all-gather) and migrate
+    from the global set, so both ranks end with the same hall of fame, which beats the constant
+    baseline."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_search_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    res.sort(key=lambda r: r[0])
+    for r in res:
+        assert r[2] is not None, r[1]
+    (_, f0, np0, ne0, c0), (_, f1, np1, ne1, c1) = res
+    assert np0 == 2 and np1 == 2          # populations 0,2 on rank 0; 1,3 on rank 1
+    assert ne0 == ne1 and ne0 >= c0 + c1 - 1  # global evaluation count on every rank
+    assert [l for _, l in f0] == [l for _, l in f1]  # one global hall of fame
+    import srhip  # noqa: F401
+    from test_search import _data
+
+    X, y = _data(100, seed=3)
+    assert min(l for _, l in f0) < 0.5 * np.mean((y - y.mean()) ** 2)
