@@ -103,15 +103,70 @@ template <typename T> __device__ __attribute__((always_inline)) inline T imm_as(
 template <typename T, int R> struct RowVec { typedef T type __attribute__((ext_vector_type(R))); };
 template <typename T, int R> using RV = typename RowVec<T, R>::type;
 
+// v_cvt_i32_f64 as an opaque instruction: saturating for out-of-range input and 0 for NaN (the C++
+// conversion of such values is undefined, and the compiler may exploit that).
+__device__ __attribute__((always_inline)) inline int cvt_i32_sat(double k) {
+  int m;
+  asm("v_cvt_i32_f64 %0, %1" : "=v"(m) : "v"(k));
+  return m;
+}
+
+// srm_sincosf_fast (include/srhip_math.h) for the device rows, bit-identical for every finite x:
+// the sign (-1)^(m+1) of cos is a free negation modifier on the product plus the bit of m, and
+// Inf / NaN need no select: they reach here unreduced and come out of the reduction as NaN.
+template <int KIND>
+__device__ __attribute__((always_inline)) inline float sincosf_dev(double x) {
+  const double invpi = 0.3183098861837907, pi_hi = 3.141592653589793, pi_lo = 1.2246467991473532e-16;
+  double k = __builtin_rint(__builtin_fma(x, invpi, KIND == 0 ? -0.5 : 0.0));
+  const int m = cvt_i32_sat(k);
+  if (KIND == 0) k += 0.5;
+  const double y = __builtin_fma(-k, pi_lo, __builtin_fma(-k, pi_hi, x));
+  const double p = srm_psin(y * y);
+  const float r = KIND == 0 ? (float)(-y * p) : (float)(y * p);
+  return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, r) ^ ((uint32_t)m << 31));
+}
+
+// srm_expf for the device rows, bit-identical for every x: the clamp is one v_med3_f32 (exact:
+// the bounds are floats) and NaN is restored by the final select as before.
+__device__ __attribute__((always_inline)) inline float expf_dev(float xf) {
+  const double invln2 = 1.4426950408889634, ln2_hi = 0.6931471805599453, ln2_lo = 2.3190468138462996e-17;
+  const double x = (double)__builtin_amdgcn_fmed3f(xf, -104.0f, 89.0f);
+  const double k = __builtin_rint(x * invln2);
+  double r = __builtin_fma(-k, ln2_hi, x);
+  r = __builtin_fma(-k, ln2_lo, r);
+  double p = 2.4736025668457734e-05;
+  p = __builtin_fma(p, r, 0.00019914637854529652);
+  p = __builtin_fma(p, r, 0.0013889148047310426);
+  p = __builtin_fma(p, r, 0.008333268860258102);
+  p = __builtin_fma(p, r, 0.04166666458462912);
+  p = __builtin_fma(p, r, 0.16666666872538483);
+  p = __builtin_fma(p, r, 0.5000000000448828);
+  p = __builtin_fma(p, r, 0.9999999999832456);
+  p = __builtin_fma(p, r, 1.0);
+  const float res = (float)__builtin_ldexp(p, cvt_i32_sat(k));
+  return (xf == xf) ? res : xf;
+}
+
 // Float32 cos/sin/tan over a lane's R rows.  Every row takes the fast path (|x| < 2^28 pi/2 after
 // mapping Inf/NaN and large |x| to 0); rows that are finite and large are redone by the scalar
 // srm_trigf out of line, once per call and only if some row needs it.  The same pieces as the
 // scalar srm_trigf (include/srhip_math.h), so the values are bit-identical.
 // (A call inside the batched body would pin its live rows to callee-saved, high-numbered VGPRs.)
-template <int R, int KIND>
-__device__ __attribute__((noinline)) RV<float, R> trigf_fix(RV<float, R> v, RV<float, R> res) {
+// cos / sin: rows still holding their (finite, large) argument are redone; every other row holds a
+// result in [-1, 1], so the argument itself marks the row (the inputs need not stay live).
+// tan (KIND 2): a tan result can be large, so the inputs are passed (trigf_fix_tan).
+template <int R>
+__device__ __attribute__((noinline)) RV<float, R> trigf_fix_tan(RV<float, R> v, RV<float, R> res) {
   UNR for (int r = 0; r < R; ++r) {
     const float x = v[r];
+    if (x - x == 0.0f && srm_pio2f_is_big((double)x)) res[r] = srm_trigf(2, x);
+  }
+  return res;
+}
+template <int R, int KIND>
+__device__ __attribute__((noinline)) RV<float, R> trigf_fix(RV<float, R> res) {
+  UNR for (int r = 0; r < R; ++r) {
+    const float x = res[r];
     if (x - x == 0.0f && srm_pio2f_is_big((double)x)) res[r] = srm_trigf(KIND, x);
   }
   return res;
@@ -122,22 +177,27 @@ __device__ __attribute__((always_inline)) inline RV<float, R> trigf_rows(RV<floa
   bool big = false;
   UNR for (int r = 0; r < R; ++r) {
     const float x = v[r];
-    const bool fin = x - x == 0.0f;
+    const bool fin = __builtin_isfinite(x);
     const double xd = (double)x;
     const bool b = srm_pio2f_is_big(xd);  // also true for Inf / NaN
-    big |= b && fin;
-    const double xs = b ? 0.0 : xd;
-    float f;
+    const bool bf = b && fin;  // finite and large: keeps x, redone out of line below
+    big |= bf;
     if constexpr (KIND == 2) {
       double y;
-      const int n = srm_rem_pio2f_fast(xs, &y);
-      f = srm_trigf_finish(KIND, n, y);
+      const int n = srm_rem_pio2f_fast(b ? 0.0 : xd, &y);
+      const float f = srm_trigf_finish(KIND, n, y);
+      res[r] = fin ? f : x - x;
     } else {
-      f = srm_sincosf_fast(KIND, xs);
+      const float f = sincosf_dev<KIND>(bf ? 0.0 : xd);  // Inf / NaN -> NaN through the reduction
+      res[r] = bf ? x : f;
     }
-    res[r] = fin ? f : x - x;
+    if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
   }
-  if (big) res = trigf_fix<R, KIND>(v, res);
+  if constexpr (KIND == 2) {
+    if (big) res = trigf_fix_tan<R>(v, res);
+  } else {
+    if (big) res = trigf_fix<R, KIND>(res);
+  }
   return res;
 }
 
@@ -146,6 +206,13 @@ __device__ __attribute__((noinline)) RV<T, R> heavy_un(RV<T, R> v) {
   using O = OpsT<T>;
   if constexpr (SRHIP_TRIG_ROWS && std::is_same<T, float>::value && (U == UN_COS || U == UN_SIN || U == UN_TAN))
     return trigf_rows<R, U == UN_COS ? 0 : (U == UN_SIN ? 1 : 2)>(v);
+  if constexpr (std::is_same<T, float>::value && U == UN_EXP) {
+    UNR for (int r = 0; r < R; ++r) {
+      v[r] = expf_dev(v[r]);
+      if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
+    }
+    return v;
+  }
   UNR for (int r = 0; r < R; ++r) {
     T x = v[r];
     switch (U) {
@@ -209,6 +276,43 @@ __device__ __attribute__((always_inline)) inline void apply_heavy(T (&A)[R], con
   UNR for (int r = 0; r < R; ++r) { a[r] = X[r]; b[r] = Y[r]; }
   a = heavy_bin<T, R, HB>(a, b);
   UNR for (int r = 0; r < R; ++r) A[r] = a[r];
+}
+
+// Specialised binary operator over a lane's rows: A = A op B (SWAP: A = B op A).  Float32 + - *
+// run as packed FP32 (v_pk_add_f32 / v_pk_mul_f32: two rows per instruction, each rounded exactly
+// as the scalar instruction would); the rest row by row.
+typedef float PkF32 __attribute__((ext_vector_type(2)));
+template <typename T, int SB> __device__ __attribute__((always_inline)) inline T sb_apply(T a, T b) {
+  using O = OpsT<T>;
+  switch (SB) {
+#define X_(NAME, FN) case SB_##NAME: if constexpr (sb_ok<T>(SB_##NAME)) return O::FN(a, b); break;
+    SRHIP_SPEC_BINOPS(X_)
+#undef X_
+    default: break;
+  }
+  return a;
+}
+template <typename T, int R, int SB, bool SWAP>
+__device__ __attribute__((always_inline)) inline void bin_rows(T (&A)[R], const T (&B)[R]) {
+  if constexpr (std::is_same<T, float>::value && R % 2 == 0 && (SB == SB_ADD || SB == SB_SUB || SB == SB_MUL)) {
+    UNR for (int r = 0; r < R; r += 2) {
+      const PkF32 a = {A[r], A[r + 1]}, b = {B[r], B[r + 1]};
+      PkF32 c;
+      if constexpr (SB == SB_ADD) c = SWAP ? b + a : a + b;
+      else if constexpr (SB == SB_SUB) c = SWAP ? b - a : a - b;
+      else c = SWAP ? b * a : a * b;
+      A[r] = c.x;
+      A[r + 1] = c.y;
+    }
+  } else {
+    UNR for (int r = 0; r < R; ++r) A[r] = SWAP ? sb_apply<T, SB>(B[r], A[r]) : sb_apply<T, SB>(A[r], B[r]);
+  }
+}
+template <typename T, int R, int SB, bool SWAP>
+__device__ __attribute__((always_inline)) inline void bin_rows_c(T (&A)[R], T c) {
+  T B[R];
+  UNR for (int r = 0; r < R; ++r) B[r] = c;
+  bin_rows<T, R, SB, SWAP>(A, B);
 }
 
 // Check accumulator: max |v| over every operator output (NaN-propagating, v_maximum3_f32) for
@@ -295,7 +399,11 @@ __device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& 
     const T p0 = (T)p.loss_p0;
     T lv[R];
     if (p.loss_kind == SRHIP_LOSS_L2) {
-      UNR for (int r = 0; r < R; ++r) { const T d = A[r] - yv[r]; lv[r] = d * d; }
+      UNR for (int r = 0; r < R; ++r) lv[r] = A[r];
+      bin_rows<T, R, SB_SUB, false>(lv, yv);
+      T dv[R];
+      UNR for (int r = 0; r < R; ++r) dv[r] = lv[r];
+      bin_rows<T, R, SB_MUL, false>(lv, dv);
     } else if (p.loss_kind == SRHIP_LOSS_L1) {
       UNR for (int r = 0; r < R; ++r) lv[r] = m_abs(A[r] - yv[r]);
     } else {
@@ -522,7 +630,7 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       T xv[R];                                                                                     \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
-      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(A[r], xv[r]);                                   \
+      bin_rows<T, R, SB_##NAME, false>(A, xv);                                                     \
       chk_update<R>(M, A);                                                                         \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     }                                                                                              \
@@ -531,34 +639,32 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       T xv[R];                                                                                     \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
-      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(xv[r], A[r]);                                   \
+      bin_rows<T, R, SB_##NAME, true>(A, xv);                                                      \
       chk_update<R>(M, A);                                                                         \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
   case h_spec(SB_##NAME, SPEC_AC):                                                                 \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
-      const T c = imm_as<T>(ins.imm);                                                              \
-      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(A[r], c);                                       \
+      bin_rows_c<T, R, SB_##NAME, false>(A, imm_as<T>(ins.imm));                                   \
       chk_update<R>(M, A);                                                                         \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
   case h_spec(SB_##NAME, SPEC_CA):                                                                 \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
-      const T c = imm_as<T>(ins.imm);                                                              \
-      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(c, A[r]);                                       \
+      bin_rows_c<T, R, SB_##NAME, true>(A, imm_as<T>(ins.imm));                                    \
       chk_update<R>(M, A);                                                                         \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
     SRHIP_K_CASES(h_spec(SB_##NAME, SPEC_SA0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
-      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(S[k][r], A[r]);                                 \
+      bin_rows<T, R, SB_##NAME, true>(A, S[k]);                                                    \
       chk_update<R>(M, A);                                                                         \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     })                                                                                             \
     SRHIP_K_CASES(h_spec(SB_##NAME, SPEC_AS0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
-      UNR for (int r = 0; r < R; ++r) A[r] = O::FN(A[r], S[k][r]);                                 \
+      bin_rows<T, R, SB_##NAME, false>(A, S[k]);                                                   \
       chk_update<R>(M, A);                                                                         \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     })

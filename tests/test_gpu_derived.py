@@ -97,3 +97,38 @@ def test_derived_with_idx_batching_and_weights(ctx, oracle):
     assert np.array_equal(aok, ook)
     for t in np.nonzero(ook)[0]:
         assert _rel(a[t], ol[t]) < F32_REL, (t, a[t], ol[t])
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_transcendentals_bitwise_at_special_values(ctx, oracle, dtype):
+    """cos / sin / tan / exp on the device equal the oracle's scalar functions bit for bit at
+    Inf, NaN, the fast / Payne-Hanek reduction boundary (2^28 pi/2), overflow / underflow edges and
+    random arguments — through a derived column, through a plain U(x) instruction and through U of
+    an operator output (x * 1), with large and small rows mixed inside a lane."""
+    import srhip as sr
+
+    special = [np.inf, -np.inf, np.nan, 4.2e8, 4.3e8, -4.3e8, 1e9, 3e38, -1e30, 88.72, 89.5, 100.0,
+               -103.0, -105.0, -87.3, 1e-45, -1e-40, 0.0, -0.0, 1.5707964, 3.1415927, 1e6, 1e7 + 1]
+    rng = np.random.default_rng(7)
+    vals = np.concatenate([special, rng.uniform(-1e3, 1e3, 2000), rng.standard_normal(1000) * 1e7,
+                           np.pi / 2 * rng.integers(-10**6, 10**6, 500)])
+    X = vals.astype(dtype)[None, :]
+    una = ("cos", "sin", "tan", "exp")
+    opts = sr.Options(binary_operators=("*",), unary_operators=una)
+    trees = [sr.Node(u, sr.Node("x1")) for u in una]                         # derived (each used twice)
+    trees += [sr.Node(u, sr.Node("x1")) * 1.0 for u in una]
+    trees += [sr.Node(u, sr.Node("x1") * 1.0) for u in una]                   # U of an operator output
+    nodes, offs = sr.flatten(trees, opts, dtype)
+    prog = sr.Program(ctx, nodes, offs, opts, dtype)
+    assert len(prog.derived_columns()) == 4
+    pred, _ = prog.eval_predict(sr.DeviceDataset(ctx, X))
+    bits = np.uint32 if dtype == np.float32 else np.uint64
+    for i, u in enumerate(una):
+        code = opts.unaop_codes[opts.unary_index(u) - 1]
+        ref = np.array([oracle.scalar_un(code, v, dtype) for v in X[0]], dtype=dtype)
+        for t in (i, i + 4, i + 8):
+            got = pred[t].astype(dtype)
+            nan = np.isnan(ref)
+            assert np.array_equal(np.isnan(got), nan), (u, t, X[0][np.isnan(got) != nan])
+            bad = got[~nan].view(bits) != ref[~nan].view(bits)
+            assert not bad.any(), (u, t, X[0][~nan][bad][:5], got[~nan][bad][:5], ref[~nan][bad][:5])
