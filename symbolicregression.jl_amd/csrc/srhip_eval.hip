@@ -845,7 +845,9 @@ static hipError_t launch_eval_m(const EvalArgs& a, int K, int mode, bool xlds, d
 int rows_per_lane(int dtype) { return dtype == SRHIP_F64 ? R_F64 : R_F32; }
 
 int pick_rows_per_lane(int dtype, int K, int mode, int64_t m) {
-  if (dtype == SRHIP_F32 && K <= 2 && mode != MODE_PRECISE && m >= WIDE_MIN_ROWS && R_F32_WIDE != R_F32)
+  // SRHIP_NO_WIDE=1 (tuning runs): never the R = 16 variant
+  static const bool no_wide = [] { const char* e = getenv("SRHIP_NO_WIDE"); return e && *e && *e != '0'; }();
+  if (!no_wide && dtype == SRHIP_F32 && K <= 2 && mode != MODE_PRECISE && m >= WIDE_MIN_ROWS && R_F32_WIDE != R_F32)
     return R_F32_WIDE;
   return rows_per_lane(dtype);
 }

@@ -867,7 +867,8 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   if (nd > 0 && mode != MODE_PRECISE) {
     K = kvariant(P->dkmax);
     R = pick_rows_per_lane(dtype, K, mode, v.m);
-    const size_t budget = (dtype == SRHIP_F32 && R == R_F32_WIDE) ? 80 * 1024 - 512 : 64 * 1024 - 512;
+    // two workgroups per CU: the R = 16 variant's registers (or >= 12-wave workgroups) allow no more
+    const size_t budget = ((dtype == SRHIP_F32 && R == R_F32_WIDE) || EVAL_WAVES >= 12) ? 80 * 1024 - 512 : 64 * 1024 - 512;
     L = plan_launch(ctx, dtype, P->maxfeat + nd, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R, budget);
     use_d = L.xlds;
   }
