@@ -31,6 +31,7 @@ a search is reproducible run to run (islands iterate in lock step, fixed process
 """
 from __future__ import annotations
 
+import functools
 import itertools
 import math
 import threading
@@ -86,10 +87,25 @@ def search_option(options, name):
     return options.unused.get(name, SEARCH_DEFAULTS[name])
 
 
+@functools.lru_cache(maxsize=64)
+def _tournament_cdf(n: int, p: float) -> tuple:
+    w = tournament_selection_weights(n, p)
+    return tuple(np.cumsum(w))
+
+
 def tournament_selection_weights(n: int, p: float) -> np.ndarray:
     """src/Options.jl: weights p (1-p)^(k-1), k = 1..n, normalised."""
     w = np.array([p * (1 - p) ** k for k in range(n)])
     return w / w.sum()
+
+
+def _draw(cdf, u: float) -> int:
+    """Index k with cdf[k-1] <= u * cdf[-1] < cdf[k] (inverse-CDF draw on a short list)."""
+    t = u * cdf[-1]
+    for k, c in enumerate(cdf):
+        if t < c:
+            return k
+    return len(cdf) - 1
 
 
 # ---- members, populations, statistics ------------------------------------------------------------
@@ -464,8 +480,8 @@ def condition_mutation_weights(w: MutationWeights, member: PopMember, options, c
 
 
 def sample_mutation(w: MutationWeights, rng) -> str:
-    p = np.array([getattr(w, k) for k in MUTATIONS])
-    return MUTATIONS[int(rng.choice(len(p), p=p / p.sum()))]
+    cdf = list(itertools.accumulate(getattr(w, k) for k in MUTATIONS))
+    return MUTATIONS[_draw(cdf, rng.random())]
 
 
 class Island:
@@ -565,7 +581,8 @@ class Island:
     def best_of_sample(self, pop, stats):
         o, rng = self.options, self.rng
         n = search_option(o, "tournament_selection_n")
-        sample = [pop[i] for i in rng.choice(len(pop), size=min(n, len(pop)), replace=False)]
+        # n distinct members uniformly at random (argsort of uniform keys: one RNG call)
+        sample = [pop[i] for i in np.argsort(rng.random(len(pop)))[:min(n, len(pop))]]
         if search_option(o, "use_frequency_in_tournament"):
             a = search_option(o, "adaptive_parsimony_scaling")
             scores = []
@@ -578,10 +595,9 @@ class Island:
         p = search_option(o, "tournament_selection_p")
         if p == 1.0:
             return sample[int(np.argmin(scores))]
-        w = tournament_selection_weights(len(sample), p)
-        k = int(rng.choice(len(w), p=w)) + 1
-        order = np.argsort(np.asarray(scores, dtype=np.float64), kind="stable")
-        return sample[int(order[k - 1])]
+        k = _draw(_tournament_cdf(len(sample), float(p)), rng.random())
+        order = sorted(range(len(scores)), key=scores.__getitem__)  # stable
+        return sample[order[k]]
 
     # src/RegularizedEvolution.jl:13-111
     def reg_evol_cycle(self, pop, temperature, curmaxsize, stats):
