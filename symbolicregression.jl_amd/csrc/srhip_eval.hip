@@ -334,18 +334,43 @@ template <int R> __device__ __attribute__((always_inline)) inline void chk_updat
 template <typename T> using LAccT = typename std::conditional<kIsInt<T>, long long, double>::type;
 
 
-__device__ __attribute__((always_inline)) inline double wave_sum(double v) {
-  UNR for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+// Wave reductions on DPP lane moves (no LDS round trip per step): quad butterflies, half-row and
+// row mirrors, then row_bcast15 / row_bcast31 fold the four rows into lane WAVE_LAST.  Only that
+// lane's result is meaningful; the order is fixed, so results are deterministic.
+constexpr int WAVE_LAST = 63;
+template <int CTRL, int ROWS = 0xf>
+__device__ __attribute__((always_inline)) inline uint32_t dpp32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS = 0xf, typename U>
+__device__ __attribute__((always_inline)) inline U dpp(U v) {
+  if constexpr (sizeof(U) == 8) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint64_t r = (uint64_t)dpp32<CTRL, ROWS>((uint32_t)b) | ((uint64_t)dpp32<CTRL, ROWS>((uint32_t)(b >> 32)) << 32);
+    return __builtin_bit_cast(U, r);
+  } else {
+    return __builtin_bit_cast(U, dpp32<CTRL, ROWS>(__builtin_bit_cast(uint32_t, v)));
+  }
+}
+template <typename U, typename F>
+__device__ __attribute__((always_inline)) inline U wave_fold(U v, F op) {
+  v = op(v, dpp<0xB1>(v));       // quad_perm [1,0,3,2]
+  v = op(v, dpp<0x4E>(v));       // quad_perm [2,3,0,1]
+  v = op(v, dpp<0x141>(v));      // row_half_mirror
+  v = op(v, dpp<0x140>(v));      // row_mirror: every lane of a row holds the row's fold
+  v = op(v, dpp<0x142, 0xa>(v)); // row_bcast15 -> rows 1, 3
+  v = op(v, dpp<0x143, 0xc>(v)); // row_bcast31 -> rows 2, 3: lane 63 holds the wave's fold
   return v;
+}
+__device__ __attribute__((always_inline)) inline double wave_sum(double v) {
+  return wave_fold(v, [](double a, double b) { return a + b; });
 }
 __device__ __attribute__((always_inline)) inline double wave_sum_d(double v) { return wave_sum(v); }
 __device__ __attribute__((always_inline)) inline long long wave_sum(long long v) {
-  UNR for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  return wave_fold(v, [](long long a, long long b) { return a + b; });
 }
 __device__ __attribute__((always_inline)) inline float wave_chk(float v) {
-  UNR for (int o = 32; o > 0; o >>= 1) v = __builtin_elementwise_maximum(v, __shfl_xor(v, o));
-  return v;
+  return wave_fold(v, [](float a, float b) { return __builtin_elementwise_maximum(a, b); });
 }
 __device__ __attribute__((always_inline)) inline double wave_chk(double v) { return wave_sum(v); }
 __device__ __attribute__((always_inline)) inline int32_t wave_chk(int32_t v) { return v; }
@@ -367,7 +392,7 @@ __device__ __attribute__((always_inline)) inline void precise_hook(const EvalArg
       s += row < p.nvalid ? v : 0.0;
     }
     s = wave_sum_d(s);
-    if (lane == 0) {
+    if (lane == WAVE_LAST) {
       double* slot = reinterpret_cast<double*>(p.slab_prec) + ((int64_t)ti * p.prec_stride + (opidx - 1)) * p.nrb + rb;
       *slot += s;
     }
@@ -485,7 +510,7 @@ __device__ __attribute__((always_inline)) inline void derive_columns(const EvalA
       }
     }
     m = wave_chk(m);
-    if (lane == 0) part[wave] = m;
+    if (lane == WAVE_LAST) part[wave] = m;
     __syncthreads();
     if (threadIdx.x == 0) {
       CT t = part[0];
@@ -588,7 +613,7 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
           const int d = __builtin_ctzll(msk);
           msk &= msk - 1;
           if constexpr (sizeof(T) == 4) M = __builtin_elementwise_maximum(M, dchk[d]);
-          else if (lane == 0) M += dchk[d];  // a wave sum follows: count the column once
+          else if (lane == WAVE_LAST) M += dchk[d];  // a wave sum follows: count the column once
         }
       }
     }
@@ -707,7 +732,7 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
         static_assert(CH % TILE == 0, "a loss chunk is whole tiles");
         if ((tile + 1) % (CH / TILE) == 0 || row0 + TILE >= p.nvalid) {  // chunk done (or last valid tile)
           const LAccT<T> s = wave_sum(lacc);
-          if (lane == 0) reinterpret_cast<LAccT<T>*>(p.slab_loss)[(int64_t)tree * p.nch + row0 / CH] = s;
+          if (lane == WAVE_LAST) reinterpret_cast<LAccT<T>*>(p.slab_loss)[(int64_t)tree * p.nch + row0 / CH] = s;
           lacc = 0;
         }
       } else if constexpr (MODE == MODE_PRED) {
@@ -720,7 +745,7 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
     // ---- wave reduction, one partial per (tree, row block) ----
     if constexpr (!kIsInt<T> && MODE != MODE_PRECISE) {
       M = wave_chk(M);
-      if (lane == 0) reinterpret_cast<CT*>(p.slab_chk)[(int64_t)tree * p.nrb + rb] = M;
+      if (lane == WAVE_LAST) reinterpret_cast<CT*>(p.slab_chk)[(int64_t)tree * p.nrb + rb] = M;
     }
     KMARK(8 + wave, 13);
   }
