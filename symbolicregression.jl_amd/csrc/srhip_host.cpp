@@ -606,6 +606,10 @@ int srhip::compile_grad_program(srhip_program& P) {
 
 int srhip::compile_program(srhip_program& P) {
   P.grad_ready = false;
+  {
+    std::lock_guard<std::mutex> g(P.ord_mu);  // costs and live trees change: new schedule
+    P.ord_key[0] = P.ord_key[1] = P.ord_key[2] = -1;
+  }
   switch (P.dtype) {
     case SRHIP_F32: return compile_program_t<float>(P);
     case SRHIP_F64: return compile_program_t<double>(P);
@@ -817,9 +821,8 @@ int srhip::check_eval_args(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_
   if (!P->ctx) return fail(SRHIP_ERR_INVALID, "host-only program (created without a context) cannot be evaluated");
   if (ds->dtype != P->dtype) return fail(SRHIP_ERR_INVALID, "dataset dtype %d != program dtype %d", ds->dtype, P->dtype);
   if (ds->ctx != ctx || P->ctx != ctx) return fail(SRHIP_ERR_INVALID, "handles belong to a different context");
-  for (const srhip_node& n : P->nodes)
-    if (n.degree == 0 && !n.constant && n.feature > ds->nfeat)
-      return fail(SRHIP_ERR_INVALID, "tree uses feature %d but dataset has %lld features", (int)n.feature, (long long)ds->nfeat);
+  if (P->maxfeat > ds->nfeat)
+    return fail(SRHIP_ERR_INVALID, "tree uses feature %d but dataset has %lld features", (int)P->maxfeat, (long long)ds->nfeat);
   if (mode == MODE_LOSS) {
     if (!loss) return fail(SRHIP_ERR_INVALID, "null loss");
     if (P->dtype == SRHIP_I32 && loss->kind != SRHIP_LOSS_L2 && loss->kind != SRHIP_LOSS_L1)
@@ -878,10 +881,21 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     L = plan_launch(ctx, dtype, P->maxfeat, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R);
   }
   const int nl = (int)live.size();
-  std::vector<int32_t> order = make_order(*P, live, L.groups, L.tpg, use_d);
-  HIP_TRY(ctx->order_prec.ensure(order.size() * sizeof(int32_t)));
-  HIP_TRY(hipMemcpyAsync(ctx->order_prec.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                         ctx->stream));
+  const void* d_order;
+  {
+    std::lock_guard<std::mutex> g(P->ord_mu);
+    if (P->ord_key[0] != L.groups || P->ord_key[1] != L.tpg || P->ord_key[2] != (int)use_d) {
+      std::vector<int32_t> order = make_order(*P, live, L.groups, L.tpg, use_d);
+      HIP_TRY(P->d_order.ensure(order.size() * sizeof(int32_t)));
+      HIP_TRY(hipMemcpyAsync(P->d_order.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                             ctx->stream));
+      HIP_TRY(hipStreamSynchronize(ctx->stream));  // the host vector dies here
+      P->ord_key[0] = L.groups;
+      P->ord_key[1] = L.tpg;
+      P->ord_key[2] = (int)use_d;
+    }
+    d_order = P->d_order.p;
+  }
   const int nch = (int)((v.m + loss_chunk(dtype) - 1) / loss_chunk(dtype));
   HIP_TRY(ctx->slab_loss.ensure((size_t)nt * nch * 8));
   HIP_TRY(ctx->slab_chk.ensure((size_t)nt * L.nrb * 8));
@@ -892,7 +906,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   EvalArgs a{};
   a.code = (const Ins*)(use_d ? P->d_dcode.p : P->d_code.p);
   a.prog_off = (const int32_t*)(use_d ? P->d_doff.p : P->d_off.p);
-  a.order = (const int32_t*)ctx->order_prec.p;
+  a.order = (const int32_t*)d_order;
   a.nd = use_d ? nd : 0;
   a.dspec = use_d ? (const uint32_t*)P->d_dspec.p : nullptr;
   a.dmask = use_d ? (const uint64_t*)P->d_dmask.p : nullptr;

@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -153,6 +154,11 @@ struct srhip_program {
   std::vector<double> dcost;
   int32_t dkmax = 0, dmax_len = 0;
   srhip::DevBuf d_dcode, d_doff, d_dspec, d_dmask;
+  // launch schedule cache: the cost-sorted tree order of the last plan (groups, tpg, derived),
+  // resident on the device; a program evaluated again with the same plan skips the sort and upload
+  mutable std::mutex ord_mu;
+  mutable int ord_key[3] = {-1, -1, -1};
+  mutable srhip::DevBuf d_order;
   // gradient program (constants not folded, constant leaves carry their get_constants index);
   // compiled on first use by the constant-gradient path
   bool grad_ready = false;
