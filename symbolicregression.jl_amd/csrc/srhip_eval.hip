@@ -123,14 +123,19 @@ __device__ __attribute__((always_inline)) inline float sincosf_dev(double x) {
   const double y = __builtin_fma(-k, pi_lo, __builtin_fma(-k, pi_hi, x));
   const double p = srm_psin(y * y);
   const float r = KIND == 0 ? (float)(-y * p) : (float)(y * p);
-  return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, r) ^ ((uint32_t)m << 31));
+  // sign flip by m's low bit: adding m << 31 is the xor on the sign bit (the carry leaves the word),
+  // one v_lshl_add_u32 instead of a shift and an xor
+  uint32_t o;
+  asm("v_lshl_add_u32 %0, %1, 31, %2" : "=v"(o) : "v"(m), "v"(__builtin_bit_cast(uint32_t, r)));
+  return __builtin_bit_cast(float, o);
 }
 
-// srm_expf for the device rows, bit-identical for every x: the clamp is one v_med3_f32 (exact:
-// the bounds are floats) and NaN is restored by the final select as before.
+// srm_expf for the device rows, bit-identical for every non-NaN x: the clamp is a NaN-propagating
+// minimum / maximum pair (exact: the bounds are floats), so a NaN argument flows through the
+// reduction and comes out NaN without a final select (the oracle returns the argument's NaN).
 __device__ __attribute__((always_inline)) inline float expf_dev(float xf) {
   const double invln2 = 1.4426950408889634, ln2_hi = 0.6931471805599453, ln2_lo = 2.3190468138462996e-17;
-  const double x = (double)__builtin_amdgcn_fmed3f(xf, -104.0f, 89.0f);
+  const double x = (double)__builtin_elementwise_maximum(__builtin_elementwise_minimum(xf, 89.0f), -104.0f);
   const double k = __builtin_rint(x * invln2);
   double r = __builtin_fma(-k, ln2_hi, x);
   r = __builtin_fma(-k, ln2_lo, r);
@@ -143,8 +148,7 @@ __device__ __attribute__((always_inline)) inline float expf_dev(float xf) {
   p = __builtin_fma(p, r, 0.5000000000448828);
   p = __builtin_fma(p, r, 0.9999999999832456);
   p = __builtin_fma(p, r, 1.0);
-  const float res = (float)__builtin_ldexp(p, cvt_i32_sat(k));
-  return (xf == xf) ? res : xf;
+  return (float)__builtin_ldexp(p, cvt_i32_sat(k));
 }
 
 // Float32 cos/sin/tan over a lane's R rows.  Every row takes the fast path (|x| < 2^28 pi/2 after
@@ -188,7 +192,8 @@ __device__ __attribute__((always_inline)) inline RV<float, R> trigf_rows(RV<floa
       const float f = srm_trigf_finish(KIND, n, y);
       res[r] = fin ? f : x - x;
     } else {
-      const float f = sincosf_dev<KIND>(bf ? 0.0 : xd);  // Inf / NaN -> NaN through the reduction
+      // large finite rows reduce to garbage here and keep x below; Inf / NaN -> NaN through the reduction
+      const float f = sincosf_dev<KIND>(xd);
       res[r] = bf ? x : f;
     }
     if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
