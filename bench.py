@@ -133,7 +133,7 @@ def main():
     kst = 2 if st["max_stack"] <= 2 else (4 if st["max_stack"] <= 4 else 8)
     rpl = 16 if (kst == 2 and n >= 4096) else 8
     kname = f"srhip::eval_kernel<float, {rpl}, {kst}, 0, true>"
-    traffic, traffic_src = pmc_traffic(kname)
+    traffic, valu_issue, traffic_src = pmc_summary(kname)
 
     if rank == 0:
         out = {
@@ -168,6 +168,10 @@ def main():
                 "kernel": kname,
                 "kernel_ms": kern_ms,
                 "flops_per_launch": int(flops),
+                # SQ_ACTIVE_INST_VALU x 4 / (GRBM_GUI_ACTIVE x 1024 SIMDs) from the same PMC summary:
+                # the issue-slot bound the kernel actually runs against
+                "valu_issue_util": valu_issue,
+                "op_mix": op_mix(nodes, opts),
             },
             "cpu_baseline": cpu,
             "extra": {"compile_ms_1024_trees": compile_ms, "end_to_end_ms_per_population": e2e_ms},
@@ -178,24 +182,39 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(kname):
-    """HBM bytes per launch of the eval kernel from the committed rocprofv3 --pmc summary of this
-    same command (scripts/pmc.sh + scripts/pmc_summary.py --json; separate counter passes, FETCH_SIZE
-    doubled per MI355X_MICROARCH.md).  None if no summary for this kernel variant is committed."""
+def pmc_summary(kname):
+    """The committed rocprofv3 --pmc summary of this same command for the eval kernel
+    (scripts/pmc.sh + scripts/pmc_summary.py --json; separate counter passes, FETCH_SIZE doubled per
+    MI355X_MICROARCH.md): (HBM bytes per launch, VALU issue utilisation, source file).  Nones if no
+    summary for this kernel variant is committed."""
     import glob
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_c2*.json")))
     if not files:
-        return None, None
+        return None, None, None
     try:
         summ = json.load(open(files[-1]))
     except (OSError, ValueError):
-        return None, None
+        return None, None, None
     want = kname.replace("srhip::", "").replace(" ", "")
     for k, d in summ.items():
         if want in k.replace(" ", "") and "hbm_bytes" in d:
-            return d["hbm_bytes"], os.path.relpath(files[-1], ROOT)
-    return None, None
+            return d["hbm_bytes"], d.get("valu_issue_util"), os.path.relpath(files[-1], ROOT)
+    return None, None, None
+
+
+def op_mix(nodes, opts):
+    """Operator-node counts of the population by operator name (report the op mix
+    beside the flop fraction — a transcendental is one algorithmic flop but ~20 VALU issues)."""
+    import collections
+
+    c = collections.Counter()
+    for nd in nodes:
+        if nd["degree"] == 1:
+            c[opts.unary_operators[nd["op"] - 1]] += 1
+        elif nd["degree"] == 2:
+            c[opts.binary_operators[nd["op"] - 1]] += 1
+    return dict(c)
 
 
 def cpu_baseline(nodes, offs, opts, X, y, target_s):

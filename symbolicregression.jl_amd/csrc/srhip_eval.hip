@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "srhip_isa.h"
@@ -804,15 +805,18 @@ __global__ void gather_kernel(const T* __restrict__ X, const T* __restrict__ y, 
 
 // Per-feature statistics over the first m rows, for DynamicExpressions' feature-array checks
 // (isfinite(sum(X[f, :]))): count of non-finite entries and the f64 sum (Float64 data: sum of
-// x * 2^-64 so that it cannot overflow).  One block per feature.
+// x * 2^-64 so that it cannot overflow).  grid = (nb row chunks, nfeat): block (b, f) folds chunk b
+// of column f into part[f * nb + b]; feature_stats_final folds the nb partials of a feature in
+// chunk order (a fixed order: the result does not depend on scheduling).
 template <typename T>
 __global__ __launch_bounds__(256) void feature_stats_kernel(const T* __restrict__ X, int64_t ld, int64_t m,
-                                                            FeatStat* __restrict__ out) {
-  const int f = blockIdx.x;
+                                                            int64_t chunk, FeatStat* __restrict__ part) {
+  const int f = blockIdx.y, b = blockIdx.x, nb = gridDim.x;
   const T* col = X + (int64_t)f * ld;
+  const int64_t lo = (int64_t)b * chunk, hi = min(m, lo + chunk);
   double s = 0.0;
   unsigned long long bad = 0;
-  for (int64_t i = threadIdx.x; i < m; i += blockDim.x) {
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     const T v = col[i];
     if (!m_isfinite(v)) bad++;
     else s += sizeof(T) == 8 ? (double)v * 0x1p-64 : (double)v;
@@ -830,9 +834,21 @@ __global__ __launch_bounds__(256) void feature_stats_kernel(const T* __restrict_
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    out[f].sum = ss[0];
-    out[f].nonfinite = (long long)sb[0];
+    part[(int64_t)f * nb + b].sum = ss[0];
+    part[(int64_t)f * nb + b].nonfinite = (long long)sb[0];
   }
+}
+__global__ void feature_stats_final(const FeatStat* __restrict__ part, int nb, int nfeat, FeatStat* __restrict__ out) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= nfeat) return;
+  double s = 0.0;
+  long long bad = 0;
+  for (int b = 0; b < nb; ++b) {
+    s += part[(int64_t)f * nb + b].sum;
+    bad += part[(int64_t)f * nb + b].nonfinite;
+  }
+  out[f].sum = s;
+  out[f].nonfinite = bad;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -945,15 +961,21 @@ hipError_t launch_gather(int dtype, const void* X, const void* y, const void* w,
 hipError_t launch_feature_stats(int dtype, const void* X, int64_t ld, int64_t m, int nfeat, FeatStat* out,
                                 hipStream_t s) {
   if (nfeat <= 0) return hipSuccess;
+  // out holds nfeat results followed by nfeat * FEAT_STAT_BLOCKS partials (feature_stats_scratch)
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(FEAT_STAT_BLOCKS, m / 65536));
+  const int64_t chunk = (m + nb - 1) / nb;
+  FeatStat* part = out + nfeat;
+  const dim3 grid(nb, nfeat), block(256);
   switch (dtype) {
     case SRHIP_F32:
-      hipLaunchKernelGGL(feature_stats_kernel<float>, dim3(nfeat), dim3(256), 0, s, (const float*)X, ld, m, out);
+      hipLaunchKernelGGL(feature_stats_kernel<float>, grid, block, 0, s, (const float*)X, ld, m, chunk, part);
       break;
     case SRHIP_F64:
-      hipLaunchKernelGGL(feature_stats_kernel<double>, dim3(nfeat), dim3(256), 0, s, (const double*)X, ld, m, out);
+      hipLaunchKernelGGL(feature_stats_kernel<double>, grid, block, 0, s, (const double*)X, ld, m, chunk, part);
       break;
     default: return hipSuccess;
   }
+  hipLaunchKernelGGL(feature_stats_final, dim3((nfeat + 63) / 64), dim3(64), 0, s, (const FeatStat*)part, nb, nfeat, out);
   return hipGetLastError();
 }
 

@@ -672,7 +672,7 @@ int srhip::make_view(srhip_ctx* ctx, const srhip_dataset* ds, const int64_t* idx
   HIP_TRY(ctx->vy.ensure((size_t)ld * es));
   HIP_TRY(ctx->vw.ensure((size_t)ld * es));
   HIP_TRY(ctx->vidx.ensure((size_t)nidx * sizeof(int64_t)));
-  HIP_TRY(ctx->vstats.ensure((size_t)std::max<int64_t>(1, ds->nfeat) * sizeof(FeatStat)));
+  HIP_TRY(ctx->vstats.ensure(feature_stats_scratch(ds->nfeat) * sizeof(FeatStat)));
   HIP_TRY(ctx->h_stats.ensure((size_t)std::max<int64_t>(1, ds->nfeat) * sizeof(FeatStat)));
   HIP_TRY(hipMemcpyAsync(ctx->vidx.p, idx, (size_t)nidx * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(launch_gather(ds->dtype, ds->X.p, ds->has_y ? ds->y.p : nullptr, ds->weighted ? ds->w.p : nullptr, ds->ld,
@@ -1198,7 +1198,7 @@ int srhip_dataset_create(srhip_ctx* ctx, int dtype, const void* X, int64_t nfeat
   }
   d->hstats.assign(std::max<int64_t>(1, nfeat), FeatStat{0.0, 0});
   if (dtype != SRHIP_I32 && nfeat > 0) {
-    HIP_TRY(d->stats.ensure((size_t)nfeat * sizeof(FeatStat)));
+    HIP_TRY(d->stats.ensure(feature_stats_scratch(nfeat) * sizeof(FeatStat)));
     HIP_TRY(launch_feature_stats(dtype, d->X.p, d->ld, n, (int)nfeat, (FeatStat*)d->stats.p, ctx->stream));
     HIP_TRY(hipMemcpyAsync(d->hstats.data(), d->stats.p, (size_t)nfeat * sizeof(FeatStat), hipMemcpyDeviceToHost,
                            ctx->stream));

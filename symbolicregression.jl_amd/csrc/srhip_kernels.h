@@ -34,6 +34,10 @@ struct FeatStat {
   double sum;           // f64 sum (Float64 data: sum of x * 2^-64)
   long long nonfinite;  // count of Inf/NaN entries
 };
+// launch_feature_stats splits each column into at most FEAT_STAT_BLOCKS row chunks; its output
+// buffer holds the nfeat results followed by the partials.
+constexpr int FEAT_STAT_BLOCKS = 64;
+inline size_t feature_stats_scratch(int64_t nfeat) { return (size_t)(nfeat < 1 ? 1 : nfeat) * (1 + FEAT_STAT_BLOCKS); }
 
 struct EvalArgs {
   const Ins* code;          // all trees' bytecode
