@@ -580,11 +580,84 @@ int compile_grad_t(srhip_program& P) {
   return SRHIP_OK;
 }
 
+void grad_snapshot(const srhip_program& P, std::vector<double>& out) {
+  out.clear();
+  for (const srhip_node& n : P.nodes)
+    if (n.degree == 0 && n.constant) out.push_back(n.val);
+}
+
+// Recompile in place only the trees whose constant values differ (bitwise) from the snapshot the
+// gradient program was compiled with.  A tree's code depends on its own nodes only and is
+// position-independent, so an unchanged length means the new code drops into the old slot; any
+// other outcome (length change, no snapshot) returns patched = false and the caller recompiles all.
+template <typename T>
+int patch_grad_t(srhip_program& P, bool& patched, int64_t& lo, int64_t& hi) {
+  patched = false;
+  lo = INT64_MAX;
+  hi = -1;
+  if (P.gsnap.empty() || P.gprog_off.size() != (size_t)P.ntrees || P.ginfo.size() != (size_t)P.ntrees) return SRHIP_OK;
+  std::vector<Ins> scratch;
+  size_t k = 0;
+  for (int32_t t = 0; t < P.ntrees; ++t) {
+    const int64_t b = P.offsets[t], e = P.offsets[t + 1];
+    bool dirty = false;
+    for (int64_t i = b; i < e; ++i) {
+      const srhip_node& n = P.nodes[(size_t)i];
+      if (n.degree != 0 || !n.constant) continue;
+      if (k >= P.gsnap.size()) return SRHIP_OK;
+      dirty |= memcmp(&n.val, &P.gsnap[k++], sizeof(double)) != 0;
+    }
+    if (!dirty) continue;
+    scratch.clear();
+    TreeCompiler<T> tc(P.nodes.data() + b, e - b, P, 0, true);
+    TreeInfo gi;
+    int rc = tc.compile(gi, scratch);
+    if (rc) return fail(rc, "tree %d (gradient program): %s", (int)t, g_err.c_str());
+    TreeInfo& old = P.ginfo[t];
+    if (gi.code_len != old.code_len) return SRHIP_OK;
+    std::copy(scratch.begin(), scratch.end(), P.gcode.begin() + old.code_begin);
+    lo = std::min<int64_t>(lo, old.code_begin);
+    hi = std::max<int64_t>(hi, (int64_t)old.code_begin + old.code_len);
+    gi.code_begin = old.code_begin;
+    old = std::move(gi);
+  }
+  if (k != P.gsnap.size()) return SRHIP_OK;
+  P.gkmax = 0;
+  P.gmax_len = 0;
+  for (const TreeInfo& gi : P.ginfo) {
+    P.gkmax = std::max(P.gkmax, gi.need);
+    P.gmax_len = std::max(P.gmax_len, gi.code_len);
+  }
+  patched = true;
+  return SRHIP_OK;
+}
+
 }  // namespace
 
 int srhip::compile_grad_program(srhip_program& P) {
   if (P.grad_ready) return SRHIP_OK;
+  static const bool no_patch = [] { const char* e = getenv("SRHIP_NO_GRAD_PATCH"); return e && *e && *e != '0'; }();
   int rc;
+  bool patched = false;
+  int64_t lo = 0, hi = -1;  // patched instruction range
+  if (!no_patch && P.ctx && P.d_gcode.p) {  // a previous full compile is on the device
+    switch (P.dtype) {
+      case SRHIP_F32: rc = patch_grad_t<float>(P, patched, lo, hi); break;
+      case SRHIP_F64: rc = patch_grad_t<double>(P, patched, lo, hi); break;
+      default: rc = SRHIP_OK; break;
+    }
+    if (rc) return rc;
+  }
+  if (patched) {  // the device copy differs only in [lo, hi)
+    grad_snapshot(P, P.gsnap);
+    HIP_TRY(hipSetDevice(P.ctx->device));
+    if (hi > lo)
+      HIP_TRY(hipMemcpyAsync((Ins*)P.d_gcode.p + lo, P.gcode.data() + lo, (size_t)(hi - lo) * sizeof(Ins),
+                             hipMemcpyHostToDevice, P.ctx->stream));
+    HIP_TRY(hipStreamSynchronize(P.ctx->stream));
+    P.grad_ready = true;
+    return SRHIP_OK;
+  }
   switch (P.dtype) {
     case SRHIP_F32: rc = compile_grad_t<float>(P); break;
     case SRHIP_F64: rc = compile_grad_t<double>(P); break;
@@ -592,6 +665,7 @@ int srhip::compile_grad_program(srhip_program& P) {
   }
   if (rc) return rc;
   if (!P.ctx) return fail(SRHIP_ERR_INVALID, "host-only program");
+  grad_snapshot(P, P.gsnap);
   HIP_TRY(hipSetDevice(P.ctx->device));
   HIP_TRY(P.d_gcode.ensure(P.gcode.size() * sizeof(Ins)));
   HIP_TRY(P.d_goff.ensure(std::max<size_t>(1, P.gprog_off.size()) * sizeof(int32_t)));

@@ -167,6 +167,9 @@ struct srhip_program {
   std::vector<srhip::TreeInfo> ginfo;  // did_succeed metadata for the gradient program's constants
   int32_t gkmax = 0, gmax_len = 0;
   srhip::DevBuf d_gcode, d_goff;
+  // constant-leaf values (node storage order) the gradient program was last compiled with: when only
+  // constants change (the optimiser's line search), just the trees whose constants moved recompile
+  std::vector<double> gsnap;
 };
 
 namespace srhip {

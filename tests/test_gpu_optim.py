@@ -157,3 +157,37 @@ def test_optimizer_outcome_vs_oracle(ctx, oracle):
         wins += dl[t] <= ol * (1 + 1e-6) + 1e-12
     assert total >= 10
     assert wins >= 0.85 * total, (wins, total)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_grad_program_patch_equals_full_compile(ctx, dtype):
+    """After set_constants, the gradient program recompiles only the trees whose constants moved
+    (in place, srhip_host.cpp patch_grad_t); its losses, gradients and masks equal, bit for bit, a
+    fresh program compiled in full with the same constants — including a tree whose new constant
+    is NaN (a static did_succeed failure) and a second patch on top of the first."""
+    sr = _sr()
+    opts, _, nodes, offs, X, y = _problem(sr, dtype, ntrees=48)
+    ds = sr.DeviceDataset(ctx, X, y)
+    loss = sr.L2DistLoss()
+    prog = sr.Program(ctx, nodes, offs, opts, dtype)
+    prog.eval_loss_grad(ds, loss)  # full compile of the gradient program
+    c = prog.get_constants()
+    rng = np.random.default_rng(3)
+    with_c = [t for t in range(len(c)) if len(c[t]) > 0]
+    assert len(with_c) >= 6
+    for step in range(2):
+        for t in with_c[step::3]:
+            c[t] = c[t] * (1.0 + 0.25 * rng.standard_normal(len(c[t])))
+        if step == 0:
+            c[with_c[1]][0] = np.nan
+        flat = np.concatenate(c)
+        prog.set_constants(flat)
+        pl, pg, pok = prog.eval_loss_grad(ds, loss)
+        fresh = sr.Program(ctx, nodes, offs, opts, dtype)
+        fresh.set_constants(flat)
+        fl, fg, fok = fresh.eval_loss_grad(ds, loss)
+        fresh.close()
+        assert np.array_equal(pok, fok)
+        assert not pok[with_c[1]]
+        assert np.array_equal(pl.view(np.uint64), fl.view(np.uint64))
+        assert np.array_equal(np.concatenate(pg).view(np.uint64), np.concatenate(fg).view(np.uint64))
