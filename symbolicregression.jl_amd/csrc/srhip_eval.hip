@@ -591,8 +591,11 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
   KMARK(0, 2);
   if (p.debug_stop == 2) return;
 
-  const int group_base = blockIdx.y * p.trees_per_group;
-  const int group_n = min(p.trees_per_group, p.ntrees - group_base);
+  // tree group of this workgroup: uniform, or the host's tail-shaped sizes (group_off)
+  const int group_base = p.group_off ? __builtin_amdgcn_readfirstlane(p.group_off[blockIdx.y])
+                                     : (int)blockIdx.y * p.trees_per_group;
+  const int group_n = p.group_off ? __builtin_amdgcn_readfirstlane(p.group_off[blockIdx.y + 1]) - group_base
+                                  : min(p.trees_per_group, p.ntrees - group_base);
 
   // static assignment: the host deals cost-sorted trees round-robin, wave w takes w, w+WAVES, ...
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

@@ -683,6 +683,7 @@ int srhip::compile_program(srhip_program& P) {
   {
     std::lock_guard<std::mutex> g(P.ord_mu);  // costs and live trees change: new schedule
     P.ord_key[0] = P.ord_key[1] = P.ord_key[2] = -1;
+    P.ord_goff.clear();
   }
   switch (P.dtype) {
     case SRHIP_F32: return compile_program_t<float>(P);
@@ -803,21 +804,65 @@ LaunchPlan srhip::plan_launch(const srhip_ctx* ctx, int dtype, int64_t nxcols, b
 
 namespace {
 
-// trees sorted by estimated cost (desc), dealt round-robin to groups; returns order [ntrees]
-std::vector<int32_t> make_order(const srhip_program& P, const std::vector<int32_t>& trees, int groups, int tpg,
-                                bool derived) {
+// Tree groups of a launch (grid.y), as offsets into the order: the plan's uniform groups, or —
+// when the launch spans several waves of workgroups over the chip's 2-per-CU slots — the bulk in
+// g equal groups plus ~1/32 of the trees in halving tail groups (..., 32, 16, <=16).  Workgroups
+// dispatch group by group, so the small ones come last and fill the slots the bulk leaves idle:
+// identical workgroups over 977 row tiles x 2 groups use <= 95 % of 512 slots.  Measured on C2
+// (scripts/tail_sweep.sh): uniform 2.13 ms, tail 1/32 2.04-2.06 ms, 1/16 2.10, 1/8 2.18 (every
+// extra workgroup restages its rows and derived columns, so bigger tails or more bulk groups lose).
+// SRHIP_NO_TAIL=1: uniform groups.
+std::vector<int32_t> shape_groups(const LaunchPlan& L, int32_t ntrees, int num_cu) {
+  static const bool no_tail = [] { const char* e = getenv("SRHIP_NO_TAIL"); return e && *e && *e != '0'; }();
+  std::vector<int32_t> off(1, 0);
+  const bool tail = !no_tail && ntrees >= 128 && (int64_t)L.groups * L.nrb > 2 * (int64_t)num_cu;
+  if (!tail) {
+    for (int g = 0; g < L.groups; ++g) off.push_back(std::min(ntrees, off.back() + L.tpg));
+    return off;
+  }
+  // tuning hooks: SRHIP_TAIL_DIV (tail = trees / DIV, default 32), SRHIP_BULK_GROUPS (default: the
+  // plan's), SRHIP_TAIL_MIN (smallest tail group, default 16)
+  static const int tail_div = [] { const char* e = getenv("SRHIP_TAIL_DIV"); return e && atoi(e) >= 2 ? atoi(e) : 32; }();
+  static const int bulk_g = [] { const char* e = getenv("SRHIP_BULK_GROUPS"); return e ? atoi(e) : 0; }();
+  const int32_t tl = std::max<int32_t>(16, ntrees / tail_div), bulk = ntrees - tl;
+  const int groups = bulk_g > 0 ? std::min<int>(bulk_g, std::max(1, bulk / 16)) : L.groups;
+  const int32_t tpg = (bulk + groups - 1) / groups;
+  while (off.back() < bulk) off.push_back(std::min(bulk, off.back() + tpg));
+  static const int tail_min = [] { const char* e = getenv("SRHIP_TAIL_MIN"); return e && atoi(e) > 0 ? atoi(e) : 16; }();
+  int32_t t = tl;
+  while (t > tail_min) {
+    const int32_t h = t / 2;
+    off.push_back(off.back() + h);
+    t -= h;
+  }
+  if (t > 0) off.push_back(off.back() + t);
+  return off;
+}
+
+// trees sorted by estimated cost (desc), dealt to the groups in proportion to their sizes (each
+// tree to the group with the largest free fraction), so every group gets the same cost mix;
+// returns order [ntrees], group g's trees at [goff[g], goff[g+1])
+std::vector<int32_t> make_order(const srhip_program& P, const std::vector<int32_t>& trees,
+                                const std::vector<int32_t>& goff, bool derived) {
   std::vector<int32_t> s(trees);
   auto cost = [&](int32_t t) { return derived ? P.dcost[t] : P.info[t].cost; };
   std::stable_sort(s.begin(), s.end(), [&](int32_t a, int32_t b) { return cost(a) > cost(b); });
-  const int n = (int)s.size();
+  const int groups = (int)goff.size() - 1;
   std::vector<int32_t> order(s.size());
-  std::vector<int> fill(groups, 0), cap(groups, 0);
-  for (int g = 0; g < groups; ++g) cap[g] = std::max(0, std::min(tpg, n - g * tpg));
-  int g = 0;
-  for (int i = 0; i < n; ++i) {
-    while (fill[g] >= cap[g]) g = (g + 1) % groups;  // the last group may be shorter
-    order[(size_t)g * tpg + fill[g]++] = s[i];
-    g = (g + 1) % groups;
+  std::vector<int> fill(groups, 0);
+  for (int32_t t : s) {
+    int best = -1;
+    double bf = -1.0;
+    for (int g = 0; g < groups; ++g) {
+      const int cap = goff[g + 1] - goff[g];
+      if (fill[g] >= cap) continue;
+      const double f = (double)(cap - fill[g]) / cap;
+      if (f > bf) {
+        bf = f;
+        best = g;
+      }
+    }
+    order[(size_t)goff[best] + fill[best]++] = t;
   }
   return order;
 }
@@ -956,10 +1001,12 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   }
   const int nl = (int)live.size();
   const void* d_order;
+  const std::vector<int32_t> goff = shape_groups(L, nl, ctx->num_cu);
   {
     std::lock_guard<std::mutex> g(P->ord_mu);
-    if (P->ord_key[0] != L.groups || P->ord_key[1] != L.tpg || P->ord_key[2] != (int)use_d) {
-      std::vector<int32_t> order = make_order(*P, live, L.groups, L.tpg, use_d);
+    if (P->ord_key[0] != L.groups || P->ord_key[1] != L.tpg || P->ord_key[2] != (int)use_d || P->ord_goff != goff) {
+      std::vector<int32_t> order = make_order(*P, live, goff, use_d);
+      order.insert(order.end(), goff.begin(), goff.end());  // the group offsets follow the order
       HIP_TRY(P->d_order.ensure(order.size() * sizeof(int32_t)));
       HIP_TRY(hipMemcpyAsync(P->d_order.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                              ctx->stream));
@@ -967,6 +1014,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       P->ord_key[0] = L.groups;
       P->ord_key[1] = L.tpg;
       P->ord_key[2] = (int)use_d;
+      P->ord_goff = goff;
     }
     d_order = P->d_order.p;
   }
@@ -997,6 +1045,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   a.nrb = L.nrb;
   a.nch = nch;
   a.trees_per_group = L.tpg;
+  a.group_off = (const int32_t*)d_order + nl;
   a.loss_kind = loss ? loss->kind : 0;
   a.loss_p0 = loss ? loss->p0 : 0.0;
   a.weighted = weighted ? 1 : 0;
@@ -1013,7 +1062,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     HIP_TRY(pred.ensure((size_t)nt * v.m * es));
     a.out_pred = pred.p;
   }
-  dim3 grid(L.nrb, L.groups);
+  dim3 grid(L.nrb, (unsigned)goff.size() - 1);
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
   HIP_TRY(launch_eval(dtype, a, R, K, mode, L.xlds, grid, L.lds, ctx->stream));
   HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));

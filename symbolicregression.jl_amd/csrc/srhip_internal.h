@@ -158,6 +158,7 @@ struct srhip_program {
   // resident on the device; a program evaluated again with the same plan skips the sort and upload
   mutable std::mutex ord_mu;
   mutable int ord_key[3] = {-1, -1, -1};
+  mutable std::vector<int32_t> ord_goff;  // group offsets of that plan (appended to d_order)
   mutable srhip::DevBuf d_order;
   // gradient program (constants not folded, constant leaves carry their get_constants index);
   // compiled on first use by the constant-gradient path

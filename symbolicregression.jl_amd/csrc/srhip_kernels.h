@@ -57,7 +57,8 @@ struct EvalArgs {
   int32_t rb_rows;          // rows per workgroup (multiple of 64*R)
   int32_t nrb;              // row blocks
   int32_t nch;              // loss chunks: ceil(nvalid / loss_chunk)
-  int32_t trees_per_group;  // trees per grid.y group
+  int32_t trees_per_group;  // trees per grid.y group (group_off == nullptr)
+  const int32_t* group_off; // [grid.y + 1] first order slot of each group, or nullptr (uniform groups)
   int32_t loss_kind;
   double loss_p0;
   int32_t weighted;
