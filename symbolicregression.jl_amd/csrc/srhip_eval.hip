@@ -582,6 +582,8 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
     xstride = p.ld;
   }
   KDBG("[k] staged, ntiles=%d rb_rows=%d nvalid=%ld max_steps=%d\n", ntiles, p.rb_rows, (long)p.nvalid, p.max_steps);
+  __shared__ int next_tree;  // the group's next unclaimed tree (waves claim trees dynamically)
+  if (threadIdx.x == 0) next_tree = EVAL_WAVES;
   __syncthreads();
   constexpr bool DERIVED = XLDS && !kIsInt<T> && MODE != MODE_PRECISE;
   __shared__ CT dchk[DERIVED ? DERIVE_MAX : 1];
@@ -597,11 +599,15 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
   const int group_n = p.group_off ? __builtin_amdgcn_readfirstlane(p.group_off[blockIdx.y + 1]) - group_base
                                   : min(p.trees_per_group, p.ntrees - group_base);
 
-  // static assignment: the host deals cost-sorted trees round-robin, wave w takes w, w+WAVES, ...
+  // the group's trees are in descending estimated cost (host make_order): wave w starts with tree w,
+  // then each wave claims the next unclaimed tree from an LDS counter as it finishes one — longest
+  // first, so the waves of a workgroup end within about one cheap tree of each other (a static
+  // round-robin left up to the cost spread idle at every workgroup's end).  The counter only grows:
+  // every wave leaves the loop once it passes group_n.
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const CIns* code = (const CIns*)(uintptr_t)p.code;
   KMARK(8 + wave, 10);
-  for (int ti = wave; ti < group_n; ti += EVAL_WAVES) {
+  for (int ti = wave; ti < group_n;) {
     KMARK(8 + wave, 11);
     const int tree = __builtin_amdgcn_readfirstlane(p.order[group_base + ti]);
     const int pc0 = __builtin_amdgcn_readfirstlane(p.prog_off[tree]);
@@ -609,7 +615,7 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
     KDBG("[k] ti=%d tree=%d pc0=%d group_n=%d\n", ti, tree, pc0, group_n);
     KMARK(0, 3);
     KMARK(1, tree);
-    if (p.debug_stop == 3) continue;
+    if (p.debug_stop == 3) break;  // (diagnostic) skip the trees; a continue would not claim the next one
 
     LAccT<T> lacc = 0;
     CT M = 0;
@@ -757,6 +763,9 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
       if (lane == WAVE_LAST) reinterpret_cast<CT*>(p.slab_chk)[(int64_t)tree * p.nrb + rb] = M;
     }
     KMARK(8 + wave, 13);
+    int claim = 0;
+    if (lane == 0) claim = atomicAdd(&next_tree, 1);
+    ti = __builtin_amdgcn_readfirstlane(claim);
   }
   KMARK(8 + wave, 14);
 }
