@@ -2,9 +2,6 @@
 set -u
 run() { tag=$1; shift; env "$@" timeout -k 10 120 python3 bench.py --no-cpu --steps 20 > gpurun_out/sw_$tag.log 2>&1 || exit 1; }
 run d32 SRHIP_TAIL_DIV=32
-run notail SRHIP_NO_TAIL=1
-run d16 SRHIP_TAIL_DIV=16
-run d64 SRHIP_TAIL_DIV=64
 run g1 SRHIP_BULK_GROUPS=1
 run g4 SRHIP_BULK_GROUPS=4
 run d32b SRHIP_TAIL_DIV=32

@@ -493,12 +493,15 @@ __device__ __attribute__((noinline)) RV<T, R> derive_un(int u, RV<T, R> v) {
   return v;
 }
 
+// Every thread takes DV = 2 rows of a column per call (512 threads cover a 1024-row block in one
+// pass); each wave folds its column statistic with DPP and parks it in LDS, and one barrier after
+// all columns lets the first nd threads fold the wave partials in wave order (fixed: deterministic).
 template <typename T>
 __device__ __attribute__((always_inline)) inline void derive_columns(const EvalArgs& p, T* lx, int rbb,
                                                                      typename Chk<T>::type* dchk) {
   using CT = typename Chk<T>::type;
-  constexpr int VEC = 16 / sizeof(T);
-  __shared__ CT part[EVAL_WAVES];
+  constexpr int DV = 2;
+  __shared__ CT part[EVAL_WAVES][DERIVE_MAX];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int d = 0; d < p.nd; ++d) {
     const uint32_t spec = __builtin_amdgcn_readfirstlane(p.dspec[d]);
@@ -506,28 +509,29 @@ __device__ __attribute__((always_inline)) inline void derive_columns(const EvalA
     const T* src = lx + (int64_t)f * rbb;
     T* dst = lx + (int64_t)(p.nfeat + d) * rbb;
     CT m = 0;
-    for (int c = threadIdx.x; c < rbb / VEC; c += blockDim.x) {
-      RV<T, VEC> v = reinterpret_cast<const RV<T, VEC>*>(src)[c];
-      v = derive_un<T, VEC>(u, v);
-      reinterpret_cast<RV<T, VEC>*>(dst)[c] = v;
-      UNR for (int e = 0; e < VEC; ++e) {
+    for (int c = threadIdx.x; c < rbb / DV; c += blockDim.x) {
+      RV<T, DV> v = reinterpret_cast<const RV<T, DV>*>(src)[c];
+      v = derive_un<T, DV>(u, v);
+      reinterpret_cast<RV<T, DV>*>(dst)[c] = v;
+      UNR for (int e = 0; e < DV; ++e) {
         if constexpr (sizeof(T) == 4) m = __builtin_elementwise_maximum(m, __builtin_fabsf(v[e]));
         else m = __builtin_fma(__builtin_fabs(v[e]), 0x1p-512, m);
       }
     }
     m = wave_chk(m);
-    if (lane == WAVE_LAST) part[wave] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      CT t = part[0];
-      for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
-        if constexpr (sizeof(T) == 4) t = __builtin_elementwise_maximum(t, part[w]);
-        else t += part[w];
-      }
-      dchk[d] = t;
-    }
-    __syncthreads();
+    if (lane == WAVE_LAST) part[wave][d] = m;
   }
+  __syncthreads();
+  if ((int)threadIdx.x < p.nd) {
+    const int d = threadIdx.x;
+    CT t = part[0][d];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+      if constexpr (sizeof(T) == 4) t = __builtin_elementwise_maximum(t, part[w][d]);
+      else t += part[w][d];
+    }
+    dchk[d] = t;
+  }
+  __syncthreads();
 }
 
 // ------------------------------------------------------------------------------------------------
