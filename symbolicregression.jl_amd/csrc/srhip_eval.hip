@@ -493,14 +493,15 @@ __device__ __attribute__((noinline)) RV<T, R> derive_un(int u, RV<T, R> v) {
   return v;
 }
 
-// Every thread takes DV = 2 rows of a column per call (512 threads cover a 1024-row block in one
-// pass); each wave folds its column statistic with DPP and parks it in LDS, and one barrier after
-// all columns lets the first nd threads fold the wave partials in wave order (fixed: deterministic).
+// A thread takes one 16-byte vector (DV rows) of a column per call; each wave folds its column
+// statistic with DPP and parks it in LDS, and one barrier after all columns lets the first nd
+// threads fold the wave partials in wave order (fixed: deterministic).  (DV = 2 for Float32 kept all
+// 512 threads busy but cost more VALU in call overhead; the kernel is VALU-issue bound.)
 template <typename T>
 __device__ __attribute__((always_inline)) inline void derive_columns(const EvalArgs& p, T* lx, int rbb,
                                                                      typename Chk<T>::type* dchk) {
   using CT = typename Chk<T>::type;
-  constexpr int DV = 2;
+  constexpr int DV = 16 / sizeof(T);
   __shared__ CT part[EVAL_WAVES][DERIVE_MAX];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int d = 0; d < p.nd; ++d) {
