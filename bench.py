@@ -308,6 +308,8 @@ def bench_c4(args):
         "objective_evals_per_s": float(np.sum(fcalls)) / dt,
         "improved_trees": int(improved.sum()),
         "mean_loss_before": float(np.mean(base[fin])), "mean_loss_after": float(np.mean(out[fin])),
+        # the mean is dominated by a few overflow-scale losses; the median shows the typical tree
+        "median_loss_before": float(np.median(base[fin])), "median_loss_after": float(np.median(out[fin])),
         "grad_launch_ms": gdt * 1e3,
         "grad_node_row_evals_per_s": st["total_nodes"] * rows / gdt,
     }))
