@@ -654,7 +654,8 @@ int srhip::compile_grad_program(srhip_program& P) {
     if (hi > lo)
       HIP_TRY(hipMemcpyAsync((Ins*)P.d_gcode.p + lo, P.gcode.data() + lo, (size_t)(hi - lo) * sizeof(Ins),
                              hipMemcpyHostToDevice, P.ctx->stream));
-    HIP_TRY(hipStreamSynchronize(P.ctx->stream));
+    // no synchronisation here: the gradient launch follows on the same stream, and eval_grad
+    // synchronises before it returns, so gcode is not touched while this copy is in flight
     P.grad_ready = true;
     return SRHIP_OK;
   }

@@ -80,7 +80,10 @@ static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, 
     }
   }
   const int nch = (int)chunks.size() / 2;
-  if (nch == 0) return SRHIP_OK;
+  if (nch == 0) {  // a patched gradient program may still be uploading from P->gcode
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return SRHIP_OK;
+  }
   LaunchPlan L = plan_launch(ctx, dtype, ds->nfeat, weighted, true, v.m, nch, 64);
   const int K = P->gkmax <= 4 ? 4 : 8;
   HIP_TRY(ctx->g_chunks.ensure(chunks.size() * sizeof(int32_t)));
@@ -302,6 +305,176 @@ static int bfgs(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const
   return SRHIP_OK;
 }
 
+// All restarts of all trees as one pipelined batch.  Every tree runs its own state machine
+// (initial point -> BFGS iterations -> next restart); each launch evaluates the one point every
+// active tree needs next, so a tree never waits for a slower tree's line search or restart.  A
+// tree's loss and gradient do not depend on which other trees share the launch (fixed row chunks,
+// fixed reduction order), so each tree's trajectory -- and the outcome -- is the one bfgs() above
+// computes per restart in lock-step; only the number of launches drops (≈ the longest tree's
+// evaluation count instead of the sum over iterations of the slowest line search).
+static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
+                          const View& v, const std::vector<int32_t>& trees, const std::vector<int64_t>& coff,
+                          int iterations, double g_tol, const std::vector<std::vector<double>>& starts,
+                          std::vector<double>& best_x, std::vector<double>& best_f, std::vector<int64_t>& fcalls) {
+  enum { INIT = 0, TRIAL = 1, DONE = 2 };
+  const int nstarts = (int)starts.size();
+  const size_t nall = best_x.size();
+  std::vector<double> x(nall), g(nall), s(nall), xe(nall), fe(P->ntrees), ge(nall), f(P->ntrees, INFINITY);
+  std::vector<int64_t> hoff(P->ntrees + 1, 0);
+  for (int32_t t = 0; t < P->ntrees; ++t) {
+    const int64_t n = coff[t + 1] - coff[t];
+    hoff[t + 1] = hoff[t] + n * n;
+  }
+  std::vector<double> H(hoff.back(), 0.0);
+  std::vector<int> phase(P->ntrees, DONE), start(P->ntrees, 0), iter(P->ntrees, 0), nround(P->ntrees, 0);
+  std::vector<uint8_t> first(P->ntrees, 1);
+  std::vector<LineSearch> ls(P->ntrees);
+  for (size_t k = 0; k < nall; ++k) xe[k] = best_x[k];
+  auto gnorm = [&](int32_t t, const std::vector<double>& gg) {
+    double m = 0.0;
+    for (int64_t k = coff[t]; k < coff[t + 1]; ++k) m = std::max(m, fabs(gg[k]));
+    return m;
+  };
+  auto begin_start = [&](int32_t t) {
+    const int64_t n = coff[t + 1] - coff[t], o = coff[t];
+    for (int64_t k = o; k < o + n; ++k) x[k] = starts[start[t]][k];
+    for (int64_t i = 0; i < n; ++i)
+      for (int64_t j = 0; j < n; ++j) H[hoff[t] + i * n + j] = i == j ? 1.0 : 0.0;
+    phase[t] = INIT;
+  };
+  auto finish_start = [&](int32_t t) {
+    if (f[t] < best_f[t]) {  // src/ConstantOptimization.jl:62-64
+      best_f[t] = f[t];
+      for (int64_t k = coff[t]; k < coff[t + 1]; ++k) best_x[k] = x[k];
+    }
+    if (++start[t] < nstarts) begin_start(t);
+    else phase[t] = DONE;
+  };
+  // next BFGS iteration of t from (x, f, g): search direction and a fresh line search
+  auto begin_iter = [&](int32_t t) {
+    if (iter[t] >= iterations) {
+      finish_start(t);
+      return;
+    }
+    const int64_t n = coff[t + 1] - coff[t], o = coff[t];
+    double dphi = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+      double acc = 0.0;
+      for (int64_t j = 0; j < n; ++j) acc += H[hoff[t] + i * n + j] * g[o + j];
+      s[o + i] = -acc;
+      dphi += g[o + i] * s[o + i];
+    }
+    if (!(dphi < 0.0)) {
+      dphi = 0.0;
+      for (int64_t i = 0; i < n; ++i) {
+        for (int64_t j = 0; j < n; ++j) H[hoff[t] + i * n + j] = i == j ? 1.0 : 0.0;
+        s[o + i] = -g[o + i];
+        dphi -= g[o + i] * g[o + i];
+      }
+    }
+    LineSearch& L = ls[t];
+    L = LineSearch();
+    L.phi0 = f[t];
+    L.dphi0 = dphi;
+    L.a1 = L.a2 = 1.0;
+    L.phix0 = L.phix1 = f[t];
+    first[t] = 1;
+    nround[t] = 0;
+    phase[t] = TRIAL;
+  };
+  for (int32_t t : trees) begin_start(t);
+  std::vector<int32_t> act;
+  for (;;) {
+    act.clear();
+    for (int32_t t : trees) {
+      if (phase[t] == DONE) continue;
+      act.push_back(t);
+      if (phase[t] == INIT)
+        for (int64_t k = coff[t]; k < coff[t + 1]; ++k) xe[k] = x[k];
+      else
+        for (int64_t k = coff[t]; k < coff[t + 1]; ++k) xe[k] = x[k] + ls[t].a2 * s[k];
+    }
+    if (act.empty()) break;
+    set_all_consts(*P, xe.data());
+    int rc = eval_grad(ctx, ds, P, loss, v, act, coff, fe.data(), ge.data());
+    if (rc) return rc;
+    for (int32_t t : act) {
+      fcalls[t] += 1;
+      if (phase[t] == INIT) {
+        f[t] = fe[t];
+        for (int64_t k = coff[t]; k < coff[t + 1]; ++k) g[k] = ge[k];
+        iter[t] = 0;
+        if (std::isfinite(f[t]) && !(gnorm(t, g) <= g_tol)) begin_iter(t);
+        else finish_start(t);
+        continue;
+      }
+      LineSearch& L = ls[t];
+      const double phi = fe[t];
+      if (first[t]) {
+        first[t] = 0;
+        L.phix0 = L.phi0;
+      }
+      L.phix1 = phi;
+      nround[t] += 1;
+      bool accept = false;
+      if (!std::isfinite(phi)) {  // hard-coded halving until finite (iterfinitemax = 52)
+        if (++L.iterfinite >= 52) L.stop = true;
+        else {
+          L.a1 = L.a2;
+          L.a2 = L.a1 / 2.0;
+        }
+      } else if (phi > L.phi0 + 1e-4 * L.a2 * L.dphi0) {
+        if (++L.iter > 40) L.stop = true;
+        else {
+          const double a2 = backtrack_step(L);
+          L.phix0 = L.phix1;
+          L.a2 = a2;
+        }
+      } else {
+        accept = true;
+      }
+      if (!accept) {
+        if (L.stop || nround[t] >= 60) finish_start(t);  // line search failed: this start ends here
+        continue;
+      }
+      const int64_t n = coff[t + 1] - coff[t], o = coff[t];
+      std::vector<double> dx(n), dg(n), u(n);
+      double dxdg = 0.0;
+      for (int64_t i = 0; i < n; ++i) {
+        dx[i] = L.a2 * s[o + i];
+        dg[i] = ge[o + i] - g[o + i];
+        dxdg += dx[i] * dg[i];
+      }
+      if (dxdg > 0.0) {
+        double dgu = 0.0;
+        for (int64_t i = 0; i < n; ++i) {
+          double acc = 0.0;
+          for (int64_t j = 0; j < n; ++j) acc += H[hoff[t] + i * n + j] * dg[j];
+          u[i] = acc;
+          dgu += dg[i] * acc;
+        }
+        const double c1 = (dxdg + dgu) / (dxdg * dxdg), c2 = 1.0 / dxdg;
+        for (int64_t i = 0; i < n; ++i)
+          for (int64_t j = 0; j < n; ++j)
+            H[hoff[t] + i * n + j] += c1 * dx[i] * dx[j] - c2 * (u[i] * dx[j] + dx[i] * u[j]);
+      }
+      const double fold = f[t];
+      for (int64_t k = o; k < o + n; ++k) {
+        x[k] = xe[k];
+        g[k] = ge[k];
+      }
+      f[t] = phi;
+      if (phi == fold || gnorm(t, g) <= g_tol) {
+        finish_start(t);  // converged
+      } else {
+        iter[t] += 1;
+        begin_iter(t);
+      }
+    }
+  }
+  return SRHIP_OK;
+}
+
 extern "C" {
 
 int srhip_eval_loss_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
@@ -359,7 +532,24 @@ int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_prog
   std::mt19937_64 rng(opt->seed);
   std::normal_distribution<double> randn(0.0, 1.0);
   const double g_tol = opt->g_tol > 0 ? opt->g_tol : 1e-8;
-  for (int start = 0; start <= opt->nrestarts && !trees.empty(); ++start) {
+  // SRHIP_OPTIM_LOCKSTEP=1: one lock-step BFGS per restart (bfgs above) instead of the pipelined batch
+  const char* lse = getenv("SRHIP_OPTIM_LOCKSTEP");  // read per call (tests switch it)
+  const bool lockstep = lse && *lse && *lse != '0';
+  if (!lockstep && !trees.empty()) {
+    // the starting points in the lock-step loop's draw order (start-major, then tree, then constant)
+    std::vector<std::vector<double>> starts(opt->nrestarts + 1, x0);
+    for (int start = 1; start <= opt->nrestarts; ++start)
+      for (int32_t t : trees)
+        for (int64_t k = coff[t]; k < coff[t + 1]; ++k) starts[start][k] = x0[k] * (1.0 + 0.5 * randn(rng));
+    rc = bfgs_pipelined(ctx, ds, P, loss, v, trees, coff, opt->iterations, g_tol, starts, best_x, best_f, fcalls);
+    if (rc) {
+      set_all_consts(*P, x0.data());
+      compile_program(*P);
+      upload_program(*P);
+      return rc;
+    }
+  }
+  for (int start = 0; lockstep && start <= opt->nrestarts && !trees.empty(); ++start) {
     x = x0;
     if (start > 0)  // src/ConstantOptimization.jl:53-60: c * (1 + randn/2)
       for (int32_t t : trees)

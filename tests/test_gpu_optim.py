@@ -191,3 +191,30 @@ def test_grad_program_patch_equals_full_compile(ctx, dtype):
         assert not pok[with_c[1]]
         assert np.array_equal(pl.view(np.uint64), fl.view(np.uint64))
         assert np.array_equal(np.concatenate(pg).view(np.uint64), np.concatenate(fg).view(np.uint64))
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_pipelined_optimizer_equals_lockstep(ctx, dtype, monkeypatch):
+    """The pipelined optimiser (srhip_optim.cpp bfgs_pipelined: every tree runs its own
+    restart / iteration / line-search state machine, one launch per round over the trees that are
+    still active) returns, bit for bit, the losses, improvement flags, evaluation counts and
+    constants of the lock-step one (one BFGS per restart over the whole population,
+    SRHIP_OPTIM_LOCKSTEP=1) — a tree's loss and gradient do not depend on which trees share a
+    launch."""
+    sr = _sr()
+    opts, _, nodes, offs, X, y = _problem(sr, dtype, ntrees=48)
+    ds = sr.DeviceDataset(ctx, X, y)
+    loss = sr.L2DistLoss()
+    res = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SRHIP_OPTIM_LOCKSTEP", mode)
+        prog = sr.Program(ctx, nodes, offs, opts, dtype)
+        out, improved, fcalls = prog.optimize_constants(ds, loss, iterations=8, nrestarts=2, seed=11)
+        res.append((out, improved, fcalls, np.concatenate(prog.get_constants())))
+        prog.close()
+    (l0, i0, f0, c0), (l1, i1, f1, c1) = res
+    assert i0.any()
+    assert np.array_equal(i0, i1)
+    assert np.array_equal(f0, f1)
+    assert np.array_equal(np.asarray(l0, dtype=np.float64).view(np.uint64), np.asarray(l1, dtype=np.float64).view(np.uint64))
+    assert np.array_equal(np.asarray(c0, dtype=np.float64).view(np.uint64), np.asarray(c1, dtype=np.float64).view(np.uint64))
