@@ -12,6 +12,8 @@
 //   (dual-number) gradients instead of Optim's finite differences, and BFGS also for one-constant
 //   trees (the reference uses Newton there) — parity is on the optimised loss, SURVEY.md 8(a) A13.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <random>
 #include <vector>
 
@@ -61,9 +63,18 @@ void set_all_consts(srhip_program& P, const double* c) {
 
 // Loss and gradient for `trees` (f[t] = +Inf where did_succeed fails or is undecided); gradients
 // land at g[coff[t] ..].  The gradient program must match the program's current constants.
+// SRHIP_OPTIM_TIMING=1: host-side time split of the optimiser (compile/patch vs the rest), stderr
+static double g_t_compile = 0.0, g_t_eval = 0.0, g_t_host = 0.0;
+static int64_t g_n_launch = 0;
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss, const View& v,
                      const std::vector<int32_t>& trees, const std::vector<int64_t>& coff, double* f, double* g) {
+  const double t0 = now_s();
   int rc = compile_grad_program(*P);
+  g_t_compile += now_s() - t0;
+  g_n_launch += 1;
   if (rc) return rc;
   const int dtype = P->dtype;
   const bool weighted = ds->weighted;
@@ -395,9 +406,14 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
         for (int64_t k = coff[t]; k < coff[t + 1]; ++k) xe[k] = x[k] + ls[t].a2 * s[k];
     }
     if (act.empty()) break;
+    const double t0 = now_s();
     set_all_consts(*P, xe.data());
+    const double t1 = now_s();
     int rc = eval_grad(ctx, ds, P, loss, v, act, coff, fe.data(), ge.data());
     if (rc) return rc;
+    const double t2 = now_s();
+    g_t_host += t1 - t0;
+    g_t_eval += t2 - t1;
     for (int32_t t : act) {
       fcalls[t] += 1;
       if (phase[t] == INIT) {
@@ -541,7 +557,14 @@ int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_prog
     for (int start = 1; start <= opt->nrestarts; ++start)
       for (int32_t t : trees)
         for (int64_t k = coff[t]; k < coff[t + 1]; ++k) starts[start][k] = x0[k] * (1.0 + 0.5 * randn(rng));
+    const double tb = now_s();
+    g_t_compile = g_t_eval = g_t_host = 0.0;
+    g_n_launch = 0;
     rc = bfgs_pipelined(ctx, ds, P, loss, v, trees, coff, opt->iterations, g_tol, starts, best_x, best_f, fcalls);
+    const char* te = getenv("SRHIP_OPTIM_TIMING");
+    if (te && *te == '1')
+      fprintf(stderr, "srhip optim: %.1f ms total, %lld launches, eval_grad %.1f ms (compile/patch %.1f ms), set_consts %.1f ms\n",
+              1e3 * (now_s() - tb), (long long)g_n_launch, 1e3 * g_t_eval, 1e3 * g_t_compile, 1e3 * g_t_host);
     if (rc) {
       set_all_consts(*P, x0.data());
       compile_program(*P);
