@@ -21,6 +21,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <memory>
 #include <numeric>
 #include <string>
@@ -614,6 +615,15 @@ int patch_grad_t(srhip_program& P, bool& patched, int64_t& lo, int64_t& hi) {
     int rc = tc.compile(gi, scratch);
     if (rc) return fail(rc, "tree %d (gradient program): %s", (int)t, g_err.c_str());
     TreeInfo& old = P.ginfo[t];
+    if (gi.static_fail) {
+      // a non-finite constant: eval_grad skips the tree, so its slot keeps the last code (and
+      // length) and a later finite point patches into the same slot instead of forcing a full
+      // recompile of the whole population (trial points of the line search do overflow)
+      gi.code_begin = old.code_begin;
+      gi.code_len = old.code_len;
+      old = std::move(gi);
+      continue;
+    }
     if (gi.code_len != old.code_len) return SRHIP_OK;
     std::copy(scratch.begin(), scratch.end(), P.gcode.begin() + old.code_begin);
     lo = std::min<int64_t>(lo, old.code_begin);
@@ -634,21 +644,28 @@ int patch_grad_t(srhip_program& P, bool& patched, int64_t& lo, int64_t& hi) {
 
 }  // namespace
 
+double srhip::g_patch_scan_s = 0.0, srhip::g_patch_copy_s = 0.0;
+static double host_now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 int srhip::compile_grad_program(srhip_program& P) {
   if (P.grad_ready) return SRHIP_OK;
   static const bool no_patch = [] { const char* e = getenv("SRHIP_NO_GRAD_PATCH"); return e && *e && *e != '0'; }();
   int rc;
   bool patched = false;
   int64_t lo = 0, hi = -1;  // patched instruction range
+  const double t_patch0 = host_now_s();
   if (!no_patch && P.ctx && P.d_gcode.p) {  // a previous full compile is on the device
     switch (P.dtype) {
       case SRHIP_F32: rc = patch_grad_t<float>(P, patched, lo, hi); break;
       case SRHIP_F64: rc = patch_grad_t<double>(P, patched, lo, hi); break;
       default: rc = SRHIP_OK; break;
     }
+    g_patch_scan_s += host_now_s() - t_patch0;
     if (rc) return rc;
   }
   if (patched) {  // the device copy differs only in [lo, hi)
+    const double t_copy0 = host_now_s();
     grad_snapshot(P, P.gsnap);
     HIP_TRY(hipSetDevice(P.ctx->device));
     if (hi > lo)
@@ -656,6 +673,7 @@ int srhip::compile_grad_program(srhip_program& P) {
                              hipMemcpyHostToDevice, P.ctx->stream));
     // no synchronisation here: the gradient launch follows on the same stream, and eval_grad
     // synchronises before it returns, so gcode is not touched while this copy is in flight
+    g_patch_copy_s += host_now_s() - t_copy0;
     P.grad_ready = true;
     return SRHIP_OK;
   }

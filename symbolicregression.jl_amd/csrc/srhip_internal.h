@@ -190,6 +190,7 @@ struct LaunchPlan {
   size_t lds;
 };
 int compile_program(srhip_program& P);       // eval program (+ invalidates the gradient program)
+extern double g_patch_scan_s, g_patch_copy_s;  // optimiser timing split (SRHIP_OPTIM_TIMING)
 int compile_grad_program(srhip_program& P);  // gradient program, uploaded
 int upload_program(srhip_program& P);
 int make_view(srhip_ctx* ctx, const srhip_dataset* ds, const int64_t* idx, int64_t nidx, bool need_y, View& v);

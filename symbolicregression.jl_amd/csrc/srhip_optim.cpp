@@ -559,12 +559,16 @@ int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_prog
         for (int64_t k = coff[t]; k < coff[t + 1]; ++k) starts[start][k] = x0[k] * (1.0 + 0.5 * randn(rng));
     const double tb = now_s();
     g_t_compile = g_t_eval = g_t_host = 0.0;
+    g_patch_scan_s = g_patch_copy_s = 0.0;
     g_n_launch = 0;
     rc = bfgs_pipelined(ctx, ds, P, loss, v, trees, coff, opt->iterations, g_tol, starts, best_x, best_f, fcalls);
     const char* te = getenv("SRHIP_OPTIM_TIMING");
     if (te && *te == '1')
-      fprintf(stderr, "srhip optim: %.1f ms total, %lld launches, eval_grad %.1f ms (compile/patch %.1f ms), set_consts %.1f ms\n",
-              1e3 * (now_s() - tb), (long long)g_n_launch, 1e3 * g_t_eval, 1e3 * g_t_compile, 1e3 * g_t_host);
+      fprintf(stderr,
+              "srhip optim: %.1f ms total, %lld launches, eval_grad %.1f ms (compile/patch %.1f ms: scan+recompile %.1f, "
+              "snapshot+upload %.1f), set_consts %.1f ms\n",
+              1e3 * (now_s() - tb), (long long)g_n_launch, 1e3 * g_t_eval, 1e3 * g_t_compile, 1e3 * g_patch_scan_s,
+              1e3 * g_patch_copy_s, 1e3 * g_t_host);
     if (rc) {
       set_all_consts(*P, x0.data());
       compile_program(*P);
