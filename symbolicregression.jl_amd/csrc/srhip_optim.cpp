@@ -407,7 +407,11 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
     }
     if (act.empty()) break;
     const double t0 = now_s();
-    set_all_consts(*P, xe.data());
+    for (int32_t t : act) {  // only the active trees' constants change (get_constants order per tree)
+      const double* c = xe.data() + coff[t];
+      set_consts_rec(P->nodes.data() + P->offsets[t], 0, c);
+    }
+    P->grad_ready = false;
     const double t1 = now_s();
     int rc = eval_grad(ctx, ds, P, loss, v, act, coff, fe.data(), ge.data());
     if (rc) return rc;
