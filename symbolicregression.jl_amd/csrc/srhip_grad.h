@@ -31,7 +31,8 @@ struct GradArgs {
   int32_t max_steps;
 };
 
-hipError_t launch_grad(int dtype, int K, const GradArgs& a, dim3 grid, hipStream_t s);
-hipError_t launch_grad_reduce(int dtype, const double* slab, int nrb, int nchunks, double* out, hipStream_t s);
+// kt = tangent components per chunk: 4 or GRAD_KT (the slab / reduced layout stride is kt + 2)
+hipError_t launch_grad(int dtype, int K, int kt, const GradArgs& a, dim3 grid, hipStream_t s);
+hipError_t launch_grad_reduce(int dtype, int kt, const double* slab, int nrb, int nchunks, double* out, hipStream_t s);
 
 }  // namespace srhip

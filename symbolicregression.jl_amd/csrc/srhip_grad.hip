@@ -353,22 +353,29 @@ static hipError_t launch_grad_t(const GradArgs& a, dim3 grid, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_grad(int dtype, int K, const GradArgs& a, dim3 grid, hipStream_t s) {
+hipError_t launch_grad(int dtype, int K, int kt, const GradArgs& a, dim3 grid, hipStream_t s) {
+  if (kt != 4 && kt != GRAD_KT) return hipErrorInvalidValue;
   switch (dtype) {
     case SRHIP_F32:
+      if (kt == 4) return K <= 4 ? launch_grad_t<float, 4, 4>(a, grid, s) : launch_grad_t<float, 4, 8>(a, grid, s);
       return K <= 4 ? launch_grad_t<float, GRAD_KT, 4>(a, grid, s) : launch_grad_t<float, GRAD_KT, 8>(a, grid, s);
     case SRHIP_F64:
+      if (kt == 4) return K <= 4 ? launch_grad_t<double, 4, 4>(a, grid, s) : launch_grad_t<double, 4, 8>(a, grid, s);
       return K <= 4 ? launch_grad_t<double, GRAD_KT, 4>(a, grid, s) : launch_grad_t<double, GRAD_KT, 8>(a, grid, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-hipError_t launch_grad_reduce(int dtype, const double* slab, int nrb, int nchunks, double* out, hipStream_t s) {
+hipError_t launch_grad_reduce(int dtype, int kt, const double* slab, int nrb, int nchunks, double* out, hipStream_t s) {
+  if (kt != 4 && kt != GRAD_KT) return hipErrorInvalidValue;
   dim3 grid((nchunks + 3) / 4), block(256);
-  if (dtype == SRHIP_F32)
-    hipLaunchKernelGGL((grad_reduce_kernel<GRAD_KT, true>), grid, block, 0, s, slab, nrb, nchunks, out);
-  else
-    hipLaunchKernelGGL((grad_reduce_kernel<GRAD_KT, false>), grid, block, 0, s, slab, nrb, nchunks, out);
+  if (dtype == SRHIP_F32) {
+    if (kt == 4) hipLaunchKernelGGL((grad_reduce_kernel<4, true>), grid, block, 0, s, slab, nrb, nchunks, out);
+    else hipLaunchKernelGGL((grad_reduce_kernel<GRAD_KT, true>), grid, block, 0, s, slab, nrb, nchunks, out);
+  } else {
+    if (kt == 4) hipLaunchKernelGGL((grad_reduce_kernel<4, false>), grid, block, 0, s, slab, nrb, nchunks, out);
+    else hipLaunchKernelGGL((grad_reduce_kernel<GRAD_KT, false>), grid, block, 0, s, slab, nrb, nchunks, out);
+  }
   return hipGetLastError();
 }
 

@@ -79,13 +79,27 @@ static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, 
   const int dtype = P->dtype;
   const bool weighted = ds->weighted;
   const double wsum = weighted ? v.sum_w : (double)v.m;
+  // tangent width of this launch: a chunk carries the primal plus kt tangents, so trees with few
+  // constants waste most of an 8-wide chunk; estimated cost per chunk ~ (3 + kt) (the primal's
+  // transcendentals and derivative factors cost about three tangent updates).  Values and the
+  // tangents of each constant do not depend on kt (independent components, same primal code).
+  int64_t cost4 = 0, cost8 = 0;
+  for (int32_t t : trees) {
+    if (P->ginfo[t].static_fail) continue;
+    const int nc = std::max(P->info[t].nconst, 1);
+    cost4 += (int64_t)((nc + 3) / 4) * (3 + 4);
+    cost8 += (int64_t)((nc + GRAD_KT - 1) / GRAD_KT) * (3 + GRAD_KT);
+  }
+  const char* kte = getenv("SRHIP_GRAD_KT");  // tuning / tests: force 4 or 8
+  int kt = cost4 < cost8 ? 4 : GRAD_KT;
+  if (kte && (atoi(kte) == 4 || atoi(kte) == GRAD_KT)) kt = atoi(kte);
   std::vector<int32_t> chunks;
   for (int32_t t : trees) {
     f[t] = INFINITY;
     for (int64_t k = coff[t]; k < coff[t + 1]; ++k) g[k] = 0.0;
     if (P->ginfo[t].static_fail) continue;
     const int nc = P->info[t].nconst;
-    for (int c0 = 0; c0 < std::max(nc, 1); c0 += GRAD_KT) {
+    for (int c0 = 0; c0 < std::max(nc, 1); c0 += kt) {
       chunks.push_back(t);
       chunks.push_back(c0);
     }
@@ -100,9 +114,9 @@ static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, 
   HIP_TRY(ctx->g_chunks.ensure(chunks.size() * sizeof(int32_t)));
   HIP_TRY(hipMemcpyAsync(ctx->g_chunks.p, chunks.data(), chunks.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                          ctx->stream));
-  const size_t slab_n = (size_t)nch * L.nrb * (GRAD_KT + 2);
+  const size_t slab_n = (size_t)nch * L.nrb * (kt + 2);
   HIP_TRY(ctx->g_slab.ensure(slab_n * sizeof(double)));
-  HIP_TRY(ctx->g_red.ensure((size_t)nch * (GRAD_KT + 2) * sizeof(double)));
+  HIP_TRY(ctx->g_red.ensure((size_t)nch * (kt + 2) * sizeof(double)));
   GradArgs a{};
   a.code = (const Ins*)P->d_gcode.p;
   a.prog_off = (const int32_t*)P->d_goff.p;
@@ -122,9 +136,9 @@ static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, 
   a.loss_p0 = loss->p0;
   a.weighted = weighted ? 1 : 0;
   a.max_steps = P->gmax_len;
-  HIP_TRY(launch_grad(dtype, K, a, dim3(L.nrb, L.groups), ctx->stream));
-  HIP_TRY(launch_grad_reduce(dtype, (const double*)ctx->g_slab.p, L.nrb, nch, (double*)ctx->g_red.p, ctx->stream));
-  std::vector<double> red((size_t)nch * (GRAD_KT + 2));
+  HIP_TRY(launch_grad(dtype, K, kt, a, dim3(L.nrb, L.groups), ctx->stream));
+  HIP_TRY(launch_grad_reduce(dtype, kt, (const double*)ctx->g_slab.p, L.nrb, nch, (double*)ctx->g_red.p, ctx->stream));
+  std::vector<double> red((size_t)nch * (kt + 2));
   HIP_TRY(hipMemcpyAsync(red.data(), ctx->g_red.p, red.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   // decision inputs in the partials layout: only the feature statistics and the row count are read
@@ -136,11 +150,11 @@ static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, 
   sums.back() = (double)v.m;
   for (int c = 0; c < nch; ++c) {
     const int32_t t = chunks[2 * c], c0 = chunks[2 * c + 1];
-    const double* r = red.data() + (size_t)c * (GRAD_KT + 2);
+    const double* r = red.data() + (size_t)c * (kt + 2);
     const int nc = P->info[t].nconst;
-    for (int j = 0; j < GRAD_KT && c0 + j < nc; ++j) g[coff[t] + c0 + j] = r[1 + j] / wsum;
+    for (int j = 0; j < kt && c0 + j < nc; ++j) g[coff[t] + c0 + j] = r[1 + j] / wsum;
     if (c0 == 0) {
-      const int st = decide_tree(P->ginfo[t], *P, ds->nfeat, sums.data(), r[GRAD_KT + 1]);
+      const int st = decide_tree(P->ginfo[t], *P, ds->nfeat, sums.data(), r[kt + 1]);
       f[t] = st == 0 ? r[0] / wsum : INFINITY;  // undecided counts as failed for the optimiser
     }
   }

@@ -218,3 +218,23 @@ def test_pipelined_optimizer_equals_lockstep(ctx, dtype, monkeypatch):
     assert np.array_equal(f0, f1)
     assert np.array_equal(np.asarray(l0, dtype=np.float64).view(np.uint64), np.asarray(l1, dtype=np.float64).view(np.uint64))
     assert np.array_equal(np.asarray(c0, dtype=np.float64).view(np.uint64), np.asarray(c1, dtype=np.float64).view(np.uint64))
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_grad_tangent_width_4_equals_8(ctx, dtype, monkeypatch):
+    """Gradient launches carry 4 or 8 tangents per chunk (chosen per launch from the population's
+    constant counts, srhip_optim.cpp eval_grad); losses, gradients and masks are bit-identical
+    either way (independent tangent components over the same primal code)."""
+    sr = _sr()
+    opts, _, nodes, offs, X, y = _problem(sr, dtype, ntrees=48)
+    ds = sr.DeviceDataset(ctx, X, y)
+    prog = sr.Program(ctx, nodes, offs, opts, dtype)
+    res = []
+    for kt in ("4", "8"):
+        monkeypatch.setenv("SRHIP_GRAD_KT", kt)
+        res.append(prog.eval_loss_grad(ds, sr.L2DistLoss()))
+    (l4, g4, o4), (l8, g8, o8) = res
+    assert max(len(c) for c in prog.get_constants()) > 4  # some trees span several 4-wide chunks
+    assert np.array_equal(o4, o8)
+    assert np.array_equal(l4.view(np.uint64), l8.view(np.uint64))
+    assert np.array_equal(np.concatenate(g4).view(np.uint64), np.concatenate(g8).view(np.uint64))
