@@ -67,16 +67,12 @@ def main():
 
     import srhip
 
-    opts = srhip.Options(binary_operators=tuple(o for o in args.binops.split(",") if o),
-                         unary_operators=tuple(o for o in args.unaops.split(",") if o))
-    nfeat, n = 5, args.rows
-    rng = np.random.default_rng(0 + 1000 * rank)
-    X = rng.standard_normal((nfeat, n)).astype(np.float32)
-    rng_y = np.random.default_rng(1 + 1000 * rank)
-    y = (2 * np.cos(X[3].astype(np.float64)) + X[0].astype(np.float64) ** 2 - 2
-         + 0.1 * rng_y.standard_normal(n)).astype(np.float32)
-    trees = srhip.random_population(args.ntrees, opts, nfeat, np.float32, seed=2 + 1000 * rank, max_size=30)
-    nodes, offs = srhip.flatten(trees, opts, np.float32)
+    from srhip import workloads
+
+    opts, X, y, trees, nodes, offs = workloads.c2(rank, args.ntrees, args.rows,
+                                                  tuple(o for o in args.binops.split(",") if o),
+                                                  tuple(o for o in args.unaops.split(",") if o))
+    nfeat, n = X.shape
 
     ctx = srhip.get_context(local_rank)
     ds = srhip.DeviceDataset(ctx, X, y)
@@ -258,18 +254,11 @@ def bench_c4(args):
 
     import srhip
 
+    from srhip import workloads
+
     rows = 100_000 if args.rows == 1_000_000 else args.rows
     ntrees = 512 if args.ntrees == 1024 else args.ntrees
-    opts = srhip.Options(binary_operators=("+", "-", "*", "/"), unary_operators=("cos", "exp"))
-    rng = np.random.default_rng(4)
-    trees = []
-    while len(trees) < ntrees:
-        t = srhip.gen_random_tree_fixed_size(20, opts, 5, np.float64, rng)
-        if srhip.count_constants(t) >= 2:
-            trees.append(t)
-    nodes, offs = srhip.flatten(trees, opts, np.float64)
-    X = rng.standard_normal((5, rows))
-    y = 2 * np.cos(X[3]) + X[0] ** 2 - 2 + 0.1 * rng.standard_normal(rows)
+    opts, X, y, trees, nodes, offs = workloads.c4(ntrees, rows)
     ctx = srhip.get_context(0)
     ds = srhip.DeviceDataset(ctx, X, y)
     prog = srhip.Program(ctx, nodes, offs, opts, np.float64)
@@ -348,12 +337,10 @@ def bench_search(args):
         y = 2 * np.cos(X[1]) + X[0] ** 2 - 2
         npops, iters = 20, args.iterations or 2
     else:
+        from srhip import workloads
+
         n = 10_000_000 if args.rows == 1_000_000 else args.rows
-        rng = np.random.default_rng(0)  # same dataset on every rank (replicas)
-        X = rng.standard_normal((10, n)).astype(np.float32)
-        Xd = X.astype(np.float64)
-        y = (2 * np.cos(Xd[3]) + Xd[0] ** 2 - 2 + 0.5 * Xd[6] * Xd[2] - np.exp(Xd[9] / 4)).astype(np.float32)
-        del Xd
+        X, y = workloads.c3_data(n)  # same dataset on every rank (replicas)
         npops, iters = 15 * world, args.iterations or 1
     kw = dict(populations=npops, deterministic=True, seed=1, device=local_rank, **ops)
     if args.ncycles:
@@ -432,9 +419,9 @@ def cpu_search_baseline(args, c1, X, y, opts, iters, gpu_dt):
         return {"value": sc.node_rows / dt, "unit": "node-row evals/s", "cores": 1, "kind": "port",
                 "sample": f"1 iteration of the same search (20 populations, Python islands) with the "
                           f"oracle (oracle/sr_oracle.c) as scorer, {dt:.1f} s"}
-    rng = np.random.default_rng(5)
-    trees = srhip.random_population(64, opts, 10, np.float32, seed=6, max_size=20)
-    nodes, offs = srhip.flatten(trees, opts, np.float32)
+    from srhip import workloads
+
+    _, trees, nodes, offs = workloads.c3_population(opts)
     threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1), os.cpu_count() or 1)
     m = 100_000
     t0 = time.perf_counter()

@@ -199,8 +199,9 @@ int32_t srhip_program_max_ops(const srhip_program* prog);
 
 /* ---- constant optimisation (src/ConstantOptimization.jl) ------------------------------------ */
 /* Loss and its exact gradient with respect to every tree's constants (forward-mode dual numbers
- * on the device), for every tree of prog: out_loss[T] (+Inf where did_succeed fails),
- * out_grad[sum nconst] in get_constants order per tree (srhip_program_num_constants), out_ok[T].
+ * on the device), for every tree of prog: out_loss[T] (+Inf where did_succeed fails; as eval_loss,
+ * also +Inf for a succeeding tree whose loss overflows), out_grad[sum nconst] in get_constants order
+ * per tree (srhip_program_num_constants), out_ok[T] = did_succeed (srhip_eval_loss's decision).
  * Replaces the finite-difference gradient Optim derives from f(t) = eval_loss(t, dataset,
  * options; regularization=false) (src/ConstantOptimization.jl:48-50); the counterpart of
  * eval_grad_tree_array(tree, X, options; variable=false) (src/InterfaceDynamicExpressions.jl:118-124)
@@ -209,6 +210,19 @@ int srhip_eval_loss_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program*
                          const srhip_loss* loss, const int64_t* idx, int64_t nidx,
                          double* out_loss, double* out_grad, uint8_t* out_ok);
 
+/* Per-row derivatives: eval_grad_tree_array(tree, X, options; variable) and eval_diff_tree_array(tree, X,
+ * options, direction) (src/InterfaceDynamicExpressions.jl:90-95,118-124; DynamicExpressions v0.16,
+ * external) for every tree of prog, forward-mode dual numbers on the device.
+ *   wrt = SRHIP_WRT_CONSTANTS: d out / d c for each constant (get_constants order), nconst_t rows per tree
+ *   wrt = SRHIP_WRT_FEATURES, direction = 0: d out / d x_f for every feature, nfeatures rows per tree
+ *   wrt = SRHIP_WRT_FEATURES, direction = d >= 1: d out / d x_d only, 1 row per tree
+ * out_pred: T[ntrees][m] (the evaluator's predictions, as srhip_eval_predict); out_grad: T[sum of rows][m],
+ * tree-major, m = n or nidx; out_ok[t] = did_succeed of the evaluation && every derivative finite. */
+enum { SRHIP_WRT_CONSTANTS = 0, SRHIP_WRT_FEATURES = 1 };
+int srhip_eval_grad_predict(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* prog, int32_t wrt,
+                            int32_t direction, const int64_t* idx, int64_t nidx, void* out_pred, void* out_grad,
+                            uint8_t* out_ok);
+
 typedef struct srhip_optim_options {
   int32_t iterations;  /* BFGS iterations per start (Optim.Options(iterations=8), src/Options.jl:693) */
   int32_t nrestarts;   /* perturbed restarts c * (1 + randn/2) (optimizer_nrestarts=2, src/Options.jl:432) */
@@ -216,12 +230,13 @@ typedef struct srhip_optim_options {
   double g_tol;        /* gradient infinity-norm tolerance (Optim default 1e-8; <= 0 -> 1e-8) */
 } srhip_optim_options;
 
-/* optimize_constants for every tree of prog at once (src/ConstantOptimization.jl:11-81): BFGS +
- * BackTracking line search from the current constants and nrestarts perturbed starts; a tree's
- * constants are replaced (in prog) only where the best minimum beats its baseline loss.
- * out_loss[T]: the loss of the returned trees (eval_loss, regularization=false); out_improved[T];
- * out_fcalls[T] (nullable): objective evaluations per tree (num_evals bookkeeping).  Trees whose
- * constants need no optimisation (none, or a static did_succeed failure) are left unchanged. */
+/* optimize_constants for every tree of prog at once (src/ConstantOptimization.jl:11-81): per tree
+ * Newton (one constant) or BFGS (several), each with the BackTracking line search, from the current
+ * constants and nrestarts perturbed starts; a tree's constants are replaced (in prog) only where the
+ * best minimum beats its baseline loss.  out_loss[T]: the loss of the returned trees (eval_loss,
+ * regularization=false); out_improved[T]; out_fcalls[T] (nullable): the reference's num_evals per
+ * tree -- objective calls of all starts (result.f_calls) + 1 if improved (the re-score), 0 for a tree
+ * without constants or with a static did_succeed failure (left unchanged). */
 int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* prog,
                              const srhip_loss* loss, const int64_t* idx, int64_t nidx,
                              const srhip_optim_options* opt, double* out_loss,

@@ -318,7 +318,8 @@ SRM_FN double srm_qsin(double z) {
 SRM_FN int srm_rem_pio2f_fast(double x, double* y) {
   const double invpio2 = 6.36619772367581382433e-01, pio2_hi = 1.5707963267948966,
                pio2_lo = 6.123233995736766e-17;
-  const double fn = srm_rint(x * invpio2);
+  /* + 0.0: a -0 quotient becomes +0, so y = x - 0 (pi/2) keeps the sign of a zero x (tan(-0) = -0) */
+  const double fn = srm_rint(x * invpio2) + 0.0;
   *y = srm_fma(-fn, pio2_lo, srm_fma(-fn, pio2_hi, x));
   return (int)fn;
 }

@@ -9,11 +9,19 @@ namespace srhip {
 
 constexpr int GRAD_WAVES = 8;  // wavefronts per workgroup
 constexpr int GRAD_KT = 8;     // tangent components per pass (constants per chunk)
+// What a launch computes:
+//   GMODE_LOSS  loss + d loss / d constants per (chunk, row block) -> slab (the optimiser's objective)
+//   GMODE_ROWC  per-row d out / d constants -> out_der (eval_grad_tree_array, variable = false)
+//   GMODE_ROWF  per-row d out / d features -> out_der (variable = true, and eval_diff_tree_array)
+constexpr int GMODE_LOSS = 0, GMODE_ROWC = 1, GMODE_ROWF = 2;
+constexpr int GRAD_ROW_KT = 4;  // tangent components per chunk of the per-row modes
 
 struct GradArgs {
   const Ins* code;          // gradient programs of all trees
   const int32_t* prog_off;  // [ntrees]
-  const int32_t* chunks;    // [nchunks][2]: (tree, first constant)
+  const int32_t* chunks;    // GMODE_LOSS: [nchunks][2] (tree, first constant); per-row modes:
+                            // [nchunks][4] (tree, first component c0, end component, output row of
+                            // component c0)
   const void* X;            // [nfeat][ld]
   const void* y;            // [ld]
   const void* w;            // [ld] or nullptr
@@ -29,10 +37,15 @@ struct GradArgs {
   double loss_p0;
   int32_t weighted;
   int32_t max_steps;
+  // per-row modes: out_der[row + j][nvalid] for the components c0 + j < end (the values come from the
+  // evaluator, which also decides did_succeed)
+  void* out_der;
 };
 
 // kt = tangent components per chunk: 4 or GRAD_KT (the slab / reduced layout stride is kt + 2)
 hipError_t launch_grad(int dtype, int K, int kt, const GradArgs& a, dim3 grid, hipStream_t s);
+// per-row modes (GMODE_ROWC / GMODE_ROWF), GRAD_ROW_KT tangents per chunk
+hipError_t launch_grad_rows(int dtype, int K, int gmode, const GradArgs& a, dim3 grid, hipStream_t s);
 hipError_t launch_grad_reduce(int dtype, int kt, const double* slab, int nrb, int nchunks, double* out, hipStream_t s);
 
 }  // namespace srhip

@@ -175,13 +175,15 @@ template <typename T, int KT> struct Dual {
   T d[KT];
 };
 
-template <typename T, int KT> DI void set_const(Dual<T, KT>& a, T c, int rel) {  // rel = cidx - c0
+// leaves: tangents are seeded on the constants (GMODE_LOSS / GMODE_ROWC: rel = constant index - c0)
+// or on the features (GMODE_ROWF: rel = feature index - c0)
+template <int GM, typename T, int KT> DI void set_const(Dual<T, KT>& a, T c, int rel) {
   a.v = c;
-  UNR for (int j = 0; j < KT; ++j) a.d[j] = (rel == j) ? T(1) : T(0);
+  UNR for (int j = 0; j < KT; ++j) a.d[j] = (GM != GMODE_ROWF && rel == j) ? T(1) : T(0);
 }
-template <typename T, int KT> DI void set_feat(Dual<T, KT>& a, T x) {
+template <int GM, typename T, int KT> DI void set_feat(Dual<T, KT>& a, T x, int rel) {
   a.v = x;
-  UNR for (int j = 0; j < KT; ++j) a.d[j] = T(0);
+  UNR for (int j = 0; j < KT; ++j) a.d[j] = (GM == GMODE_ROWF && rel == j) ? T(1) : T(0);
 }
 // out = f(l, r) with partials: out.d = fl * l.d + fr * r.d (out may alias l or r)
 template <typename T, int KT>
@@ -196,8 +198,9 @@ DI void combine(Dual<T, KT>& out, const Dual<T, KT>& l, const Dual<T, KT>& r, T 
 DI void chk_fold(float& M, float v) { M = __builtin_elementwise_maximum(M, __builtin_fabsf(v)); }
 DI void chk_fold(double& M, double v) { M = __builtin_fma(__builtin_fabs(v), 0x1p-512, M); }
 
-template <typename T, int KT, int K>
+template <typename T, int KT, int K, int GM>
 __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
+  constexpr int CW = GM == GMODE_LOSS ? 2 : 4;  // ints per chunk record
   const int lane = threadIdx.x & 63;
   const int rb = blockIdx.x;
   const int64_t row_base = (int64_t)rb * p.rb_rows;
@@ -213,8 +216,8 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   const int max_steps = __builtin_amdgcn_readfirstlane(p.max_steps);
   for (int ci = wave; ci < group_n; ci += GRAD_WAVES) {
     const int chunk = group_base + ci;
-    const int tree = __builtin_amdgcn_readfirstlane(p.chunks[2 * chunk]);
-    const int c0 = __builtin_amdgcn_readfirstlane(p.chunks[2 * chunk + 1]);
+    const int tree = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk]);
+    const int c0 = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk + 1]);
     const int pc0 = __builtin_amdgcn_readfirstlane(p.prog_off[tree]);
     double lacc = 0.0;
     double gacc[KT];
@@ -225,8 +228,8 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
       if (row0 >= p.nvalid) break;
       const int64_t row = row0 + lane;  // rows up to ld are finite replicas; masked at the loss
       Dual<T, KT> A, S[K];
-      set_feat(A, T(0));
-      UNR for (int k = 0; k < K; ++k) set_feat(S[k], T(0));
+      set_feat<GMODE_LOSS>(A, T(0), -1);
+      UNR for (int k = 0; k < K; ++k) set_feat<GMODE_LOSS>(S[k], T(0), -1);
       GIns* prog = code + pc0;
       Ins nxt = prog[0];
       for (int step = 0; step < max_steps; ++step) {
@@ -236,8 +239,8 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
         const int opnd = (int)(ins.a & 0xffff);
         const T imm = imm_bits<T>(ins.imm);
         switch (ins.h) {
-          case H_LOADF: set_feat(A, X[(int64_t)opnd * p.ld + row]); break;
-          case H_LOADC: set_const(A, imm, opnd - c0); break;
+          case H_LOADF: set_feat<GM>(A, X[(int64_t)opnd * p.ld + row], opnd - c0); break;
+          case H_LOADC: set_const<GM>(A, imm, opnd - c0); break;
 #define GK_CASES(BASE, ...)                                                                        \
   case BASE + 0: if constexpr (0 < K) { constexpr int k = 0; __VA_ARGS__ } break;                \
   case BASE + 1: if constexpr (1 < K) { constexpr int k = 1; __VA_ARGS__ } break;                \
@@ -248,23 +251,23 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   case BASE + 6: if constexpr (6 < K) { constexpr int k = 6; __VA_ARGS__ } break;                \
   case BASE + 7: if constexpr (7 < K) { constexpr int k = 7; __VA_ARGS__ } break;
           GK_CASES(H_PUSH0, { S[k] = A; })
-          GK_CASES(H_SLOADF0, { set_feat(S[k], X[(int64_t)opnd * p.ld + row]); })
-          GK_CASES(H_SLOADC0, { set_const(S[k], imm, opnd - c0); })
+          GK_CASES(H_SLOADF0, { set_feat<GM>(S[k], X[(int64_t)opnd * p.ld + row], opnd - c0); })
+          GK_CASES(H_SLOADC0, { set_const<GM>(S[k], imm, opnd - c0); })
 #define GK_SPEC(NAME, FN)                                                                          \
   case h_spec(SB_##NAME, SPEC_AF): {                                                               \
-    Dual<T, KT> o; set_feat(o, X[(int64_t)opnd * p.ld + row]);                                     \
+    Dual<T, KT> o; set_feat<GM>(o, X[(int64_t)opnd * p.ld + row], opnd - c0);                      \
     T f, fl, fr; dual_spec<T, SB_##NAME>(A.v, o.v, f, fl, fr); combine(A, A, o, f, fl, fr);        \
     chk_fold(M, A.v); break; }                                                                     \
   case h_spec(SB_##NAME, SPEC_FA): {                                                               \
-    Dual<T, KT> o; set_feat(o, X[(int64_t)opnd * p.ld + row]);                                     \
+    Dual<T, KT> o; set_feat<GM>(o, X[(int64_t)opnd * p.ld + row], opnd - c0);                      \
     T f, fl, fr; dual_spec<T, SB_##NAME>(o.v, A.v, f, fl, fr); combine(A, o, A, f, fl, fr);        \
     chk_fold(M, A.v); break; }                                                                     \
   case h_spec(SB_##NAME, SPEC_AC): {                                                               \
-    Dual<T, KT> o; set_const(o, imm, opnd - c0);                                                   \
+    Dual<T, KT> o; set_const<GM>(o, imm, opnd - c0);                                               \
     T f, fl, fr; dual_spec<T, SB_##NAME>(A.v, o.v, f, fl, fr); combine(A, A, o, f, fl, fr);        \
     chk_fold(M, A.v); break; }                                                                     \
   case h_spec(SB_##NAME, SPEC_CA): {                                                               \
-    Dual<T, KT> o; set_const(o, imm, opnd - c0);                                                   \
+    Dual<T, KT> o; set_const<GM>(o, imm, opnd - c0);                                               \
     T f, fl, fr; dual_spec<T, SB_##NAME>(o.v, A.v, f, fl, fr); combine(A, o, A, f, fl, fr);        \
     chk_fold(M, A.v); break; }                                                                     \
   GK_CASES(h_spec(SB_##NAME, SPEC_SA0), {                                                          \
@@ -296,6 +299,17 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
           default: break;
         }
       }
+      if constexpr (GM != GMODE_LOSS) {
+        if (row < p.nvalid) {
+          // record: (tree, c0, end component, output row of component c0)
+          const int cend = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk + 2]);
+          const int orow = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk + 3]);
+          T* der = reinterpret_cast<T*>(p.out_der) + (int64_t)orow * p.nvalid + row;
+          UNR for (int j = 0; j < KT; ++j)
+            if (c0 + j < cend) der[(int64_t)j * p.nvalid] = A.d[j];
+        }
+        continue;
+      }
       if (row < p.nvalid) {
         const T d = A.v - Y[row];
         T l = loss_elem<T>(p.loss_kind, d, p0);
@@ -309,6 +323,7 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
         UNR for (int j = 0; j < KT; ++j) gacc[j] += (double)(dl * A.d[j]);
       }
     }
+    if constexpr (GM != GMODE_LOSS) continue;
     // wave reductions, one slab entry per (chunk, row block)
     UNR for (int o = 32; o > 0; o >>= 1) {
       lacc += __shfl_xor(lacc, o);
@@ -347,10 +362,28 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(const double* __restri
   }
 }
 
-template <typename T, int KT, int K>
+template <typename T, int KT, int K, int GM = GMODE_LOSS>
 static hipError_t launch_grad_t(const GradArgs& a, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((grad_kernel<T, KT, K>), grid, dim3(64 * GRAD_WAVES), 0, s, a);
+  hipLaunchKernelGGL((grad_kernel<T, KT, K, GM>), grid, dim3(64 * GRAD_WAVES), 0, s, a);
   return hipGetLastError();
+}
+
+template <typename T, int GM>
+static hipError_t launch_grad_rows_t(int K, const GradArgs& a, dim3 grid, hipStream_t s) {
+  return K <= 4 ? launch_grad_t<T, GRAD_ROW_KT, 4, GM>(a, grid, s) : launch_grad_t<T, GRAD_ROW_KT, 8, GM>(a, grid, s);
+}
+
+hipError_t launch_grad_rows(int dtype, int K, int gmode, const GradArgs& a, dim3 grid, hipStream_t s) {
+  if (gmode != GMODE_ROWC && gmode != GMODE_ROWF) return hipErrorInvalidValue;
+  switch (dtype) {
+    case SRHIP_F32:
+      return gmode == GMODE_ROWC ? launch_grad_rows_t<float, GMODE_ROWC>(K, a, grid, s)
+                                 : launch_grad_rows_t<float, GMODE_ROWF>(K, a, grid, s);
+    case SRHIP_F64:
+      return gmode == GMODE_ROWC ? launch_grad_rows_t<double, GMODE_ROWC>(K, a, grid, s)
+                                 : launch_grad_rows_t<double, GMODE_ROWF>(K, a, grid, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_grad(int dtype, int K, int kt, const GradArgs& a, dim3 grid, hipStream_t s) {

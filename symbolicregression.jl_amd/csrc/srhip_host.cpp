@@ -388,7 +388,10 @@ template <typename T> class TreeCompiler {
   void push_ins(uint32_t h, uint32_t a, uint64_t imm) { code_->push_back(Ins{h, a, imm}); }
   // operator instruction: a = (op ordinal + 1) << 16 | operand
   void push_op(uint32_t h, uint32_t operand, uint64_t imm, int64_t node, int64_t parent) {
-    info_->op_sumcheck.push_back((parent < 0 || !fused_inner(node, parent)) ? 1 : 0);
+    // the gradient program evaluates constant subtrees per row (their constants need tangents); the
+    // reference evaluates them as scalars (_eval_constant_tree): finiteness only, no isfinite(sum)
+    const bool scalar = grad_ && is_const(node);
+    info_->op_sumcheck.push_back((!scalar && (parent < 0 || !fused_inner(node, parent))) ? 1 : 0);
     const uint32_t ord = (uint32_t)info_->op_sumcheck.size();
     push_ins(h, (ord << 16) | (operand & 0xffff), imm);
   }
@@ -568,6 +571,7 @@ int compile_grad_t(srhip_program& P) {
   P.ginfo.assign(P.ntrees, TreeInfo());
   P.gkmax = 0;
   P.gmax_len = 0;
+  P.gmax_ops = 0;
   for (int32_t t = 0; t < P.ntrees; ++t) {
     const int64_t b = P.offsets[t], e = P.offsets[t + 1];
     TreeCompiler<T> tc(P.nodes.data() + b, e - b, P, 0, true);
@@ -577,6 +581,7 @@ int compile_grad_t(srhip_program& P) {
     P.gprog_off[t] = gi.code_begin;
     P.gkmax = std::max(P.gkmax, gi.need);
     P.gmax_len = std::max(P.gmax_len, gi.code_len);
+    P.gmax_ops = std::max(P.gmax_ops, (int32_t)gi.op_sumcheck.size());
   }
   return SRHIP_OK;
 }
@@ -634,9 +639,11 @@ int patch_grad_t(srhip_program& P, bool& patched, int64_t& lo, int64_t& hi) {
   if (k != P.gsnap.size()) return SRHIP_OK;
   P.gkmax = 0;
   P.gmax_len = 0;
+  P.gmax_ops = 0;
   for (const TreeInfo& gi : P.ginfo) {
     P.gkmax = std::max(P.gkmax, gi.need);
     P.gmax_len = std::max(P.gmax_len, gi.code_len);
+    P.gmax_ops = std::max(P.gmax_ops, (int32_t)gi.op_sumcheck.size());
   }
   patched = true;
   return SRHIP_OK;
@@ -644,7 +651,7 @@ int patch_grad_t(srhip_program& P, bool& patched, int64_t& lo, int64_t& hi) {
 
 }  // namespace
 
-double srhip::g_patch_scan_s = 0.0, srhip::g_patch_copy_s = 0.0;
+thread_local double srhip::g_patch_scan_s = 0.0, srhip::g_patch_copy_s = 0.0;
 static double host_now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -929,11 +936,11 @@ static void finalize(const srhip_program& P, int64_t nfeat, const double* sums, 
 
 // opsums[u][k]: exact-ish (f64) sum over all rows of operator output k of tree trees[u]
 static void finalize_precise(const srhip_program& P, const int32_t* trees, int32_t nsel, const double* opsums,
-                             uint8_t* out_ok) {
-  const int stride = std::max(1, P.max_ops);
+                             uint8_t* out_ok, bool grad = false) {
+  const int stride = std::max(1, grad ? P.gmax_ops : P.max_ops);
   const long double ovf = ovf_threshold(P.dtype);
   for (int u = 0; u < nsel; ++u) {
-    const TreeInfo& I = P.info[trees[u]];
+    const TreeInfo& I = grad ? P.ginfo[trees[u]] : P.info[trees[u]];
     int st = I.static_fail ? 1 : 0;
     for (size_t k = 0; k < I.op_sumcheck.size() && !st; ++k) {
       const double s = opsums[(size_t)u * stride + k];
@@ -1132,9 +1139,9 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
 // Precise stage: per-(tree, operator node) f64 sums over the view's rows for the selected trees;
 // opsums[u * max(1, max_ops) + k].
 static int eval_precise(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const View& v,
-                        const int32_t* trees, int32_t nu, double* opsums) {
+                        const int32_t* trees, int32_t nu, double* opsums, bool grad = false) {
   const int dtype = P->dtype;
-  const int stride = std::max(1, P->max_ops);
+  const int stride = std::max(1, grad ? P->gmax_ops : P->max_ops);
   for (size_t i = 0; i < (size_t)nu * stride; ++i) opsums[i] = 0.0;
   if (nu == 0 || dtype == SRHIP_I32) return SRHIP_OK;
   const int R = pick_rows_per_lane(dtype, K_MAX, MODE_PRECISE, v.m);
@@ -1147,8 +1154,8 @@ static int eval_precise(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pro
   HIP_TRY(ctx->order_prec.ensure((size_t)nu * sizeof(int32_t)));
   HIP_TRY(hipMemcpyAsync(ctx->order_prec.p, trees, (size_t)nu * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
   EvalArgs a{};
-  a.code = (const Ins*)P->d_code.p;
-  a.prog_off = (const int32_t*)P->d_off.p;
+  a.code = (const Ins*)(grad ? P->d_gcode.p : P->d_code.p);
+  a.prog_off = (const int32_t*)(grad ? P->d_goff.p : P->d_off.p);
   a.order = (const int32_t*)ctx->order_prec.p;
   a.X = v.X;
   a.ld = v.ld;
@@ -1160,7 +1167,7 @@ static int eval_precise(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pro
   a.trees_per_group = nu;
   a.slab_prec = ctx->slab_prec.p;
   a.prec_stride = stride;
-  a.max_steps = P->max_len;
+  a.max_steps = grad ? P->gmax_len : P->max_len;
   HIP_TRY(launch_eval(dtype, a, R, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, 1), 16, ctx->stream));
   HIP_TRY(ctx->h_prec.ensure(slab_bytes));
   HIP_TRY(hipMemcpyAsync(ctx->h_prec.p, ctx->slab_prec.p, slab_bytes, hipMemcpyDeviceToHost, ctx->stream));
@@ -1172,6 +1179,17 @@ static int eval_precise(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pro
       for (int b = 0; b < Lp.nrb; ++b) s += hp[((size_t)u * stride + k) * Lp.nrb + b];
       opsums[(size_t)u * stride + k] = (double)s;
     }
+  return SRHIP_OK;
+}
+
+int srhip::precise_decide(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const View& v,
+                          const int32_t* trees, int32_t nu, bool grad, uint8_t* out_ok) {
+  if (nu <= 0) return SRHIP_OK;
+  const int stride = std::max(1, grad ? P->gmax_ops : P->max_ops);
+  std::vector<double> opsums((size_t)nu * stride);
+  const int rc = eval_precise(ctx, ds, P, v, trees, nu, opsums.data(), grad);
+  if (rc) return rc;
+  finalize_precise(*P, trees, nu, opsums.data(), out_ok, grad);
   return SRHIP_OK;
 }
 

@@ -166,7 +166,7 @@ struct srhip_program {
   std::vector<srhip::Ins> gcode;
   std::vector<int32_t> gprog_off;
   std::vector<srhip::TreeInfo> ginfo;  // did_succeed metadata for the gradient program's constants
-  int32_t gkmax = 0, gmax_len = 0;
+  int32_t gkmax = 0, gmax_len = 0, gmax_ops = 0;
   srhip::DevBuf d_gcode, d_goff;
   // constant-leaf values (node storage order) the gradient program was last compiled with: when only
   // constants change (the optimiser's line search), just the trees whose constants moved recompile
@@ -190,7 +190,7 @@ struct LaunchPlan {
   size_t lds;
 };
 int compile_program(srhip_program& P);       // eval program (+ invalidates the gradient program)
-extern double g_patch_scan_s, g_patch_copy_s;  // optimiser timing split (SRHIP_OPTIM_TIMING)
+extern thread_local double g_patch_scan_s, g_patch_copy_s;  // optimiser timing split (SRHIP_OPTIM_TIMING), per thread
 int compile_grad_program(srhip_program& P);  // gradient program, uploaded
 int upload_program(srhip_program& P);
 int make_view(srhip_ctx* ctx, const srhip_dataset* ds, const int64_t* idx, int64_t nidx, bool need_y, View& v);
@@ -204,5 +204,9 @@ int decide_tree(const TreeInfo& I, const srhip_program& P, int64_t nfeat, const 
 int check_eval_args(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss);
 int run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
              const int64_t* idx, int64_t nidx, double* out_loss, void* out_pred, uint8_t* out_ok);
+// The precise did_succeed pass for undecided trees (exact per-operator-node sums over the view), on the
+// evaluation program or (grad = true) on the gradient program: out_ok[u] for trees[u].
+int precise_decide(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const View& v,
+                   const int32_t* trees, int32_t nu, bool grad, uint8_t* out_ok);
 
 }  // namespace srhip

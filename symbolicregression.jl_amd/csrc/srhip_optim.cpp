@@ -3,14 +3,17 @@
 // srhip_eval_loss_grad: loss + exact d loss / d constants for every tree of a program (one launch of
 //   the dual-number kernel, srhip_grad.hip, over (tree, constant-chunk) pairs).
 // srhip_optimize_constants: optimize_constants / _optimize_constants (src/ConstantOptimization.jl:
-//   11-81) for a whole population at once: BFGS with LineSearches' BackTracking (order 3,
-//   c1 = 1e-4, rho in [0.1, 0.5]) from the current constants and from `nrestarts` perturbed starts
-//   x0 .* (1 + randn/2), `iterations` iterations each (Optim.Options(iterations = 8),
-//   src/Options.jl:691-705); a tree's constants are replaced only if the best minimum beats its
-//   baseline loss (:70-78).  All trees advance in lockstep, so every objective/gradient evaluation
-//   of the population is one kernel launch.  Differences from the reference, by design: exact
-//   (dual-number) gradients instead of Optim's finite differences, and BFGS also for one-constant
-//   trees (the reference uses Newton there) — parity is on the optimised loss, SURVEY.md 8(a) A13.
+//   11-81) for a whole population at once.  dispatch_optimize_constants (:22-41) picks the method
+//   per tree: no constants -> untouched; one constant -> Optim.Newton(linesearch=BackTracking());
+//   otherwise options.optimizer_algorithm = BFGS(linesearch=BackTracking()) (src/Options.jl:429-431).
+//   LineSearches' BackTracking: order 3, c1 = 1e-4, rho in [0.1, 0.5]; `iterations` iterations per
+//   start (Optim.Options(iterations = 8), src/Options.jl:691-705) from the current constants and from
+//   `nrestarts` perturbed starts x0 .* (1 + randn/2); a tree's constants are replaced only if the best
+//   minimum beats its baseline loss (:70-78).  Every tree runs its own state machine and each kernel
+//   launch evaluates the one point every still-active tree needs next (bfgs_pipelined).
+//   Differences from the reference, by design: exact (dual-number) gradients instead of Optim's
+//   finite differences, and Newton's Hessian as a central difference of those exact gradients instead
+//   of a second difference of losses -- parity is on the optimised loss, SURVEY.md 8(a) A13.
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -64,18 +67,32 @@ void set_all_consts(srhip_program& P, const double* c) {
 // Loss and gradient for `trees` (f[t] = +Inf where did_succeed fails or is undecided); gradients
 // land at g[coff[t] ..].  The gradient program must match the program's current constants.
 // SRHIP_OPTIM_TIMING=1: host-side time split of the optimiser (compile/patch vs the rest), stderr
-static double g_t_compile = 0.0, g_t_eval = 0.0, g_t_host = 0.0;
-static int64_t g_n_launch = 0;
+static thread_local double g_t_compile = 0.0, g_t_eval = 0.0, g_t_host = 0.0;
+static thread_local int64_t g_n_launch = 0;
 static double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
+static int eval_grad_body(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
+                          const View& v, const std::vector<int32_t>& trees, const std::vector<int64_t>& coff, double* f,
+                          double* g, uint8_t* ok);
+// ok (nullable): did_succeed per tree (a tree can succeed with an overflowing loss: f = Inf, ok = 1)
 static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss, const View& v,
-                     const std::vector<int32_t>& trees, const std::vector<int64_t>& coff, double* f, double* g) {
+                     const std::vector<int32_t>& trees, const std::vector<int64_t>& coff, double* f, double* g,
+                     uint8_t* ok = nullptr) {
   const double t0 = now_s();
   int rc = compile_grad_program(*P);
   g_t_compile += now_s() - t0;
   g_n_launch += 1;
   if (rc) return rc;
+  rc = eval_grad_body(ctx, ds, P, loss, v, trees, coff, f, g, ok);
+  // a patched gradient program's upload (compile_grad_program) may still be in flight from P->gcode:
+  // on an error return, drain the stream before the caller can destroy or recompile the program
+  if (rc) (void)hipStreamSynchronize(ctx->stream);
+  return rc;
+}
+static int eval_grad_body(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
+                          const View& v, const std::vector<int32_t>& trees, const std::vector<int64_t>& coff, double* f,
+                          double* g, uint8_t* ok) {
   const int dtype = P->dtype;
   const bool weighted = ds->weighted;
   const double wsum = weighted ? v.sum_w : (double)v.m;
@@ -96,6 +113,7 @@ static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, 
   std::vector<int32_t> chunks;
   for (int32_t t : trees) {
     f[t] = INFINITY;
+    if (ok) ok[t] = 0;
     for (int64_t k = coff[t]; k < coff[t + 1]; ++k) g[k] = 0.0;
     if (P->ginfo[t].static_fail) continue;
     const int nc = P->info[t].nconst;
@@ -148,6 +166,7 @@ static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, 
     sums[2 * (size_t)P->ntrees + 2 * fi + 1] = (double)v.stats[fi].nonfinite;
   }
   sums.back() = (double)v.m;
+  std::vector<int32_t> undecided;
   for (int c = 0; c < nch; ++c) {
     const int32_t t = chunks[2 * c], c0 = chunks[2 * c + 1];
     const double* r = red.data() + (size_t)c * (kt + 2);
@@ -155,20 +174,38 @@ static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, 
     for (int j = 0; j < kt && c0 + j < nc; ++j) g[coff[t] + c0 + j] = r[1 + j] / wsum;
     if (c0 == 0) {
       const int st = decide_tree(P->ginfo[t], *P, ds->nfeat, sums.data(), r[kt + 1]);
-      f[t] = st == 0 ? r[0] / wsum : INFINITY;  // undecided counts as failed for the optimiser
+      f[t] = st == 1 ? INFINITY : r[0] / wsum;
+      if (ok) ok[t] = st != 1;
+      if (st == 2) undecided.push_back(t);
     }
+  }
+  // near-overflow sums: the exact per-operator-node pass on the gradient program decides, so the
+  // objective is eval_loss's (L(Inf) exactly where did_succeed fails)
+  if (!undecided.empty()) {
+    std::vector<uint8_t> uok(undecided.size());
+    const int rc = precise_decide(ctx, ds, P, v, undecided.data(), (int32_t)undecided.size(), true, uok.data());
+    if (rc) return rc;
+    for (size_t u = 0; u < undecided.size(); ++u)
+      if (!uok[u]) {
+        f[undecided[u]] = INFINITY;
+        if (ok) ok[undecided[u]] = 0;
+      }
   }
   return SRHIP_OK;
 }
 
 namespace {
 
-// LineSearches.jl BackTracking (order 3) state of one tree
+// LineSearches.jl BackTracking (order 3) state of one tree: a finite-value phase (halve alpha while
+// phi(alpha) is not finite, at most iterfinitemax = 52 times), then the sufficient-decrease phase
+// (cubic / quadratic interpolation, alpha shrunk into [0.1, 0.5] of its last value, at most
+// iterations = 1000 times; a non-finite phi there simply fails the test and is interpolated on).
 struct LineSearch {
   double phi0, dphi0, a1, a2, phix0, phix1;
   int iter = 0, iterfinite = 0;
-  bool accepted = false, stop = false;  // stop: line search failed or the tree converged
+  bool armijo = false;  // the finite-value phase is over
 };
+constexpr int LS_ITERFINITEMAX = 52, LS_ITERATIONS = 1000;
 
 // next trial step after phi(a2) = phix1 failed the sufficient-decrease test
 double backtrack_step(LineSearch& s) {
@@ -191,170 +228,41 @@ double backtrack_step(LineSearch& s) {
 
 }  // namespace
 
-// One BFGS run (lockstep over `trees`) from x (all constants; only `trees`' entries move).
-// On return x holds each tree's final point and f its objective value there.
-static int bfgs(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss, const View& v,
-                const std::vector<int32_t>& trees, const std::vector<int64_t>& coff, int iterations, double g_tol,
-                std::vector<double>& x, std::vector<double>& f, std::vector<int64_t>& fcalls) {
-  const size_t nall = x.size();
-  std::vector<double> g(nall), xt(nall), gt(nall), ft(P->ntrees), s(nall);
-  // per-tree inverse Hessian approximations (identity start, Optim's default)
-  std::vector<int64_t> hoff(P->ntrees + 1, 0);
-  for (int32_t t = 0; t < P->ntrees; ++t) {
-    const int64_t n = coff[t + 1] - coff[t];
-    hoff[t + 1] = hoff[t] + n * n;
-  }
-  std::vector<double> H(hoff.back(), 0.0);
-  for (int32_t t : trees)
-    for (int64_t i = 0; i < coff[t + 1] - coff[t]; ++i) H[hoff[t] + i * (coff[t + 1] - coff[t]) + i] = 1.0;
-  auto gnorm = [&](int32_t t, const std::vector<double>& gg) {
-    double m = 0.0;
-    for (int64_t k = coff[t]; k < coff[t + 1]; ++k) m = std::max(m, fabs(gg[k]));
-    return m;
-  };
-  set_all_consts(*P, x.data());
-  int rc = eval_grad(ctx, ds, P, loss, v, trees, coff, f.data(), g.data());
-  if (rc) return rc;
-  std::vector<int32_t> live;
-  for (int32_t t : trees) {
-    fcalls[t] += 1;
-    if (std::isfinite(f[t]) && !(gnorm(t, g) <= g_tol)) live.push_back(t);
-  }
-  std::vector<LineSearch> ls(P->ntrees);
-  for (int it = 0; it < iterations && !live.empty(); ++it) {
-    // search directions s = -H g (reset to steepest descent if not a descent direction)
-    for (int32_t t : live) {
-      const int64_t n = coff[t + 1] - coff[t], o = coff[t];
-      double dphi = 0.0;
-      for (int64_t i = 0; i < n; ++i) {
-        double acc = 0.0;
-        for (int64_t j = 0; j < n; ++j) acc += H[hoff[t] + i * n + j] * g[o + j];
-        s[o + i] = -acc;
-        dphi += g[o + i] * s[o + i];
-      }
-      if (!(dphi < 0.0)) {
-        dphi = 0.0;
-        for (int64_t i = 0; i < n; ++i) {
-          for (int64_t j = 0; j < n; ++j) H[hoff[t] + i * n + j] = i == j ? 1.0 : 0.0;
-          s[o + i] = -g[o + i];
-          dphi -= g[o + i] * g[o + i];
-        }
-      }
-      LineSearch& L = ls[t];
-      L = LineSearch();
-      L.phi0 = f[t];
-      L.dphi0 = dphi;
-      L.a1 = L.a2 = 1.0;
-      L.phix0 = L.phix1 = f[t];
-    }
-    // batched backtracking: every round evaluates all trees still searching in one launch
-    std::vector<int32_t> pending = live;
-    std::vector<uint8_t> first(P->ntrees, 1);
-    for (int round = 0; round < 60 && !pending.empty(); ++round) {
-      xt = x;
-      for (int32_t t : pending)
-        for (int64_t k = coff[t]; k < coff[t + 1]; ++k) xt[k] = x[k] + ls[t].a2 * s[k];
-      set_all_consts(*P, xt.data());
-      rc = eval_grad(ctx, ds, P, loss, v, pending, coff, ft.data(), gt.data());
-      if (rc) return rc;
-      std::vector<int32_t> next;
-      for (int32_t t : pending) {
-        fcalls[t] += 1;
-        LineSearch& L = ls[t];
-        const double phi = ft[t];
-        if (first[t]) {
-          first[t] = 0;
-          L.phix0 = L.phi0;
-        }
-        L.phix1 = phi;
-        bool accept = false;
-        if (!std::isfinite(phi)) {  // hard-coded halving until finite (iterfinitemax = 52)
-          if (++L.iterfinite >= 52) L.stop = true;
-          else {
-            L.a1 = L.a2;
-            L.a2 = L.a1 / 2.0;
-          }
-        } else if (phi > L.phi0 + 1e-4 * L.a2 * L.dphi0) {
-          if (++L.iter > 40) L.stop = true;
-          else {
-            const double a2 = backtrack_step(L);
-            L.phix0 = L.phix1;
-            L.a2 = a2;
-          }
-        } else {
-          accept = true;
-        }
-        if (accept) {
-          // BFGS update with dx = a s, dg = g_new - g (skipped unless dx'dg > 0, as Optim)
-          const int64_t n = coff[t + 1] - coff[t], o = coff[t];
-          std::vector<double> dx(n), dg(n), u(n);
-          double dxdg = 0.0;
-          for (int64_t i = 0; i < n; ++i) {
-            dx[i] = L.a2 * s[o + i];
-            dg[i] = gt[o + i] - g[o + i];
-            dxdg += dx[i] * dg[i];
-          }
-          if (dxdg > 0.0) {
-            double dgu = 0.0;
-            for (int64_t i = 0; i < n; ++i) {
-              double acc = 0.0;
-              for (int64_t j = 0; j < n; ++j) acc += H[hoff[t] + i * n + j] * dg[j];
-              u[i] = acc;
-              dgu += dg[i] * acc;
-            }
-            const double c1 = (dxdg + dgu) / (dxdg * dxdg), c2 = 1.0 / dxdg;
-            for (int64_t i = 0; i < n; ++i)
-              for (int64_t j = 0; j < n; ++j)
-                H[hoff[t] + i * n + j] += c1 * dx[i] * dx[j] - c2 * (u[i] * dx[j] + dx[i] * u[j]);
-          }
-          const double fold = f[t];
-          for (int64_t k = coff[t]; k < coff[t + 1]; ++k) {
-            x[k] = xt[k];
-            g[k] = gt[k];
-          }
-          f[t] = phi;
-          L.accepted = true;
-          // Optim's stopping rules with f_reltol = x_abstol = 0: no change, or |g| <= g_tol
-          if (phi == fold || gnorm(t, g) <= g_tol) L.stop = true;  // converged: leave the live set
-        } else if (!L.stop) {
-          next.push_back(t);
-        }
-      }
-      pending.swap(next);
-    }
-    std::vector<int32_t> still;
-    for (int32_t t : live)
-      if (ls[t].accepted && !ls[t].stop) still.push_back(t);
-    live.swap(still);
-  }
-  return SRHIP_OK;
-}
-
 // All restarts of all trees as one pipelined batch.  Every tree runs its own state machine
-// (initial point -> BFGS iterations -> next restart); each launch evaluates the one point every
-// active tree needs next, so a tree never waits for a slower tree's line search or restart.  A
-// tree's loss and gradient do not depend on which other trees share the launch (fixed row chunks,
-// fixed reduction order), so each tree's trajectory -- and the outcome -- is the one bfgs() above
-// computes per restart in lock-step; only the number of launches drops (≈ the longest tree's
-// evaluation count instead of the sum over iterations of the slowest line search).
+// (initial point -> [Hessian probes] -> line-search trials -> ... -> next restart); each launch
+// evaluates the one point every active tree needs next, so a tree never waits for a slower tree's
+// line search or restart.  A tree's loss and gradient do not depend on which other trees share the
+// launch (fixed row chunks, fixed reduction order), so each tree's trajectory -- and the outcome --
+// is the one it would follow optimised alone (tests/test_gpu_optim.py checks this bit for bit).
+//
+// BFGS (nconst >= 2): Optim's BFGS -- inverse-Hessian approximation from the identity, direction
+//   s = -H g (steepest descent if that is not a descent direction), update skipped unless
+//   dx'dg > 0.
+// Newton (nconst == 1, src/ConstantOptimization.jl:27-31): direction s = -g / |h| (Optim's
+//   cholesky!(Positive, H) of a 1x1 Hessian flips a negative curvature and replaces a zero one by
+//   1), h = (g(c + e) - g(c - e)) / 2e with e = cbrt(eps) max(1, |c|): two extra gradient launches
+//   per iteration ("Hessian probes", not counted as objective calls, as Optim counts h_calls apart).
+// Both: BackTracking line search from alpha = 1 (InitialStatic), stop on |g|_inf <= g_tol, on an
+//   unchanged objective (f_reltol = x_abstol = 0) or after `iterations` iterations.
 static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
                           const View& v, const std::vector<int32_t>& trees, const std::vector<int64_t>& coff,
                           int iterations, double g_tol, const std::vector<std::vector<double>>& starts,
                           std::vector<double>& best_x, std::vector<double>& best_f, std::vector<int64_t>& fcalls) {
-  enum { INIT = 0, TRIAL = 1, DONE = 2 };
+  enum { INIT = 0, TRIAL = 1, DONE = 2, HESS_P = 3, HESS_M = 4 };
   const int nstarts = (int)starts.size();
   const size_t nall = best_x.size();
   std::vector<double> x(nall), g(nall), s(nall), xe(nall), fe(P->ntrees), ge(nall), f(P->ntrees, INFINITY);
+  std::vector<double> hstep(P->ntrees, 0.0), gplus(P->ntrees, 0.0), hcurv(P->ntrees, 1.0);
   std::vector<int64_t> hoff(P->ntrees + 1, 0);
   for (int32_t t = 0; t < P->ntrees; ++t) {
     const int64_t n = coff[t + 1] - coff[t];
     hoff[t + 1] = hoff[t] + n * n;
   }
   std::vector<double> H(hoff.back(), 0.0);
-  std::vector<int> phase(P->ntrees, DONE), start(P->ntrees, 0), iter(P->ntrees, 0), nround(P->ntrees, 0);
-  std::vector<uint8_t> first(P->ntrees, 1);
+  std::vector<int> phase(P->ntrees, DONE), start(P->ntrees, 0), iter(P->ntrees, 0);
   std::vector<LineSearch> ls(P->ntrees);
   for (size_t k = 0; k < nall; ++k) xe[k] = best_x[k];
+  auto newton = [&](int32_t t) { return coff[t + 1] - coff[t] == 1; };
   auto gnorm = [&](int32_t t, const std::vector<double>& gg) {
     double m = 0.0;
     for (int64_t k = coff[t]; k < coff[t + 1]; ++k) m = std::max(m, fabs(gg[k]));
@@ -375,7 +283,12 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
     if (++start[t] < nstarts) begin_start(t);
     else phase[t] = DONE;
   };
-  // next BFGS iteration of t from (x, f, g): search direction and a fresh line search
+  // Newton: probe the gradient at c + e and c - e for the curvature at the current point
+  auto begin_hess = [&](int32_t t) {
+    hstep[t] = 6.055454452393343e-06 * std::max(1.0, fabs(x[coff[t]]));  // cbrt(eps(Float64))
+    phase[t] = HESS_P;
+  };
+  // next iteration of t from (x, f, g): search direction and a fresh line search
   auto begin_iter = [&](int32_t t) {
     if (iter[t] >= iterations) {
       finish_start(t);
@@ -383,41 +296,55 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
     }
     const int64_t n = coff[t + 1] - coff[t], o = coff[t];
     double dphi = 0.0;
-    for (int64_t i = 0; i < n; ++i) {
-      double acc = 0.0;
-      for (int64_t j = 0; j < n; ++j) acc += H[hoff[t] + i * n + j] * g[o + j];
-      s[o + i] = -acc;
-      dphi += g[o + i] * s[o + i];
-    }
-    if (!(dphi < 0.0)) {
-      dphi = 0.0;
+    if (newton(t)) {
+      s[o] = -g[o] / hcurv[t];
+      dphi = g[o] * s[o];
+    } else {
       for (int64_t i = 0; i < n; ++i) {
-        for (int64_t j = 0; j < n; ++j) H[hoff[t] + i * n + j] = i == j ? 1.0 : 0.0;
-        s[o + i] = -g[o + i];
-        dphi -= g[o + i] * g[o + i];
+        double acc = 0.0;
+        for (int64_t j = 0; j < n; ++j) acc += H[hoff[t] + i * n + j] * g[o + j];
+        s[o + i] = -acc;
+        dphi += g[o + i] * s[o + i];
+      }
+      if (!(dphi < 0.0)) {
+        dphi = 0.0;
+        for (int64_t i = 0; i < n; ++i) {
+          for (int64_t j = 0; j < n; ++j) H[hoff[t] + i * n + j] = i == j ? 1.0 : 0.0;
+          s[o + i] = -g[o + i];
+          dphi -= g[o + i] * g[o + i];
+        }
       }
     }
     LineSearch& L = ls[t];
     L = LineSearch();
     L.phi0 = f[t];
     L.dphi0 = dphi;
-    L.a1 = L.a2 = 1.0;
+    L.a1 = L.a2 = 1.0;  // InitialStatic: alpha = 1
     L.phix0 = L.phix1 = f[t];
-    first[t] = 1;
-    nround[t] = 0;
     phase[t] = TRIAL;
   };
+  auto next_iter = [&](int32_t t) {  // after an accepted step
+    iter[t] += 1;
+    if (newton(t) && iter[t] < iterations) begin_hess(t);
+    else begin_iter(t);
+  };
   for (int32_t t : trees) begin_start(t);
+  const char* tre = getenv("SRHIP_OPTIM_TRACE");
+  const int trace_tree = tre && *tre ? atoi(tre) : -1;
   std::vector<int32_t> act;
   for (;;) {
     act.clear();
     for (int32_t t : trees) {
       if (phase[t] == DONE) continue;
       act.push_back(t);
-      if (phase[t] == INIT)
-        for (int64_t k = coff[t]; k < coff[t + 1]; ++k) xe[k] = x[k];
-      else
-        for (int64_t k = coff[t]; k < coff[t + 1]; ++k) xe[k] = x[k] + ls[t].a2 * s[k];
+      const int64_t o = coff[t], e = coff[t + 1];
+      switch (phase[t]) {
+        case INIT: for (int64_t k = o; k < e; ++k) xe[k] = x[k]; break;
+        case TRIAL: for (int64_t k = o; k < e; ++k) xe[k] = x[k] + ls[t].a2 * s[k]; break;
+        case HESS_P: xe[o] = x[o] + hstep[t]; break;
+        case HESS_M: xe[o] = x[o] - hstep[t]; break;
+        default: break;
+      }
     }
     if (act.empty()) break;
     const double t0 = now_s();
@@ -433,64 +360,80 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
     g_t_host += t1 - t0;
     g_t_eval += t2 - t1;
     for (int32_t t : act) {
+      const int64_t o = coff[t];
+      if (t == trace_tree) {  // SRHIP_OPTIM_TRACE=<tree>: every evaluation of one tree, stderr
+        fprintf(stderr, "[srhip optim] tree %d start %d iter %d phase %d a %.17g f %.17g x", t, start[t], iter[t],
+                phase[t], phase[t] == TRIAL ? ls[t].a2 : 0.0, fe[t]);
+        for (int64_t k = o; k < coff[t + 1]; ++k) fprintf(stderr, " %.17g", xe[k]);
+        fprintf(stderr, " g");
+        for (int64_t k = o; k < coff[t + 1]; ++k) fprintf(stderr, " %.17g", ge[k]);
+        fprintf(stderr, "\n");
+      }
+      if (phase[t] == HESS_P) {
+        gplus[t] = std::isfinite(fe[t]) ? ge[o] : NAN;
+        phase[t] = HESS_M;
+        continue;
+      }
+      if (phase[t] == HESS_M) {
+        const double h = std::isfinite(fe[t]) ? (gplus[t] - ge[o]) / (2.0 * hstep[t]) : NAN;
+        hcurv[t] = (std::isfinite(h) && h != 0.0) ? fabs(h) : 1.0;  // cholesky!(Positive, [h])
+        begin_iter(t);
+        continue;
+      }
       fcalls[t] += 1;
       if (phase[t] == INIT) {
         f[t] = fe[t];
         for (int64_t k = coff[t]; k < coff[t + 1]; ++k) g[k] = ge[k];
         iter[t] = 0;
-        if (std::isfinite(f[t]) && !(gnorm(t, g) <= g_tol)) begin_iter(t);
-        else finish_start(t);
+        if (!std::isfinite(f[t]) || gnorm(t, g) <= g_tol) finish_start(t);
+        else if (newton(t) && iterations > 0) begin_hess(t);
+        else begin_iter(t);
         continue;
       }
       LineSearch& L = ls[t];
       const double phi = fe[t];
-      if (first[t]) {
-        first[t] = 0;
-        L.phix0 = L.phi0;
-      }
       L.phix1 = phi;
-      nround[t] += 1;
-      bool accept = false;
-      if (!std::isfinite(phi)) {  // hard-coded halving until finite (iterfinitemax = 52)
-        if (++L.iterfinite >= 52) L.stop = true;
-        else {
+      if (!L.armijo) {
+        if (!std::isfinite(phi) && L.iterfinite < LS_ITERFINITEMAX) {  // hard-coded halving until finite
+          L.iterfinite += 1;
           L.a1 = L.a2;
           L.a2 = L.a1 / 2.0;
+          continue;
         }
-      } else if (phi > L.phi0 + 1e-4 * L.a2 * L.dphi0) {
-        if (++L.iter > 40) L.stop = true;
-        else {
-          const double a2 = backtrack_step(L);
-          L.phix0 = L.phix1;
-          L.a2 = a2;
-        }
-      } else {
-        accept = true;
+        L.armijo = true;
       }
-      if (!accept) {
-        if (L.stop || nround[t] >= 60) finish_start(t);  // line search failed: this start ends here
+      if (phi > L.phi0 + 1e-4 * L.a2 * L.dphi0) {  // sufficient decrease not met (or phi = Inf)
+        if (++L.iter > LS_ITERATIONS) {
+          finish_start(t);  // LineSearchException: this start ends at its last accepted point
+          continue;
+        }
+        const double a2 = backtrack_step(L);
+        L.phix0 = L.phix1;
+        L.a2 = a2;
         continue;
       }
-      const int64_t n = coff[t + 1] - coff[t], o = coff[t];
-      std::vector<double> dx(n), dg(n), u(n);
-      double dxdg = 0.0;
-      for (int64_t i = 0; i < n; ++i) {
-        dx[i] = L.a2 * s[o + i];
-        dg[i] = ge[o + i] - g[o + i];
-        dxdg += dx[i] * dg[i];
-      }
-      if (dxdg > 0.0) {
-        double dgu = 0.0;
+      const int64_t n = coff[t + 1] - coff[t];
+      if (!newton(t)) {
+        std::vector<double> dx(n), dg(n), u(n);
+        double dxdg = 0.0;
         for (int64_t i = 0; i < n; ++i) {
-          double acc = 0.0;
-          for (int64_t j = 0; j < n; ++j) acc += H[hoff[t] + i * n + j] * dg[j];
-          u[i] = acc;
-          dgu += dg[i] * acc;
+          dx[i] = L.a2 * s[o + i];
+          dg[i] = ge[o + i] - g[o + i];
+          dxdg += dx[i] * dg[i];
         }
-        const double c1 = (dxdg + dgu) / (dxdg * dxdg), c2 = 1.0 / dxdg;
-        for (int64_t i = 0; i < n; ++i)
-          for (int64_t j = 0; j < n; ++j)
-            H[hoff[t] + i * n + j] += c1 * dx[i] * dx[j] - c2 * (u[i] * dx[j] + dx[i] * u[j]);
+        if (dxdg > 0.0) {
+          double dgu = 0.0;
+          for (int64_t i = 0; i < n; ++i) {
+            double acc = 0.0;
+            for (int64_t j = 0; j < n; ++j) acc += H[hoff[t] + i * n + j] * dg[j];
+            u[i] = acc;
+            dgu += dg[i] * acc;
+          }
+          const double c1 = (dxdg + dgu) / (dxdg * dxdg), c2 = 1.0 / dxdg;
+          for (int64_t i = 0; i < n; ++i)
+            for (int64_t j = 0; j < n; ++j)
+              H[hoff[t] + i * n + j] += c1 * dx[i] * dx[j] - c2 * (u[i] * dx[j] + dx[i] * u[j]);
+        }
       }
       const double fold = f[t];
       for (int64_t k = o; k < o + n; ++k) {
@@ -498,12 +441,8 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
         g[k] = ge[k];
       }
       f[t] = phi;
-      if (phi == fold || gnorm(t, g) <= g_tol) {
-        finish_start(t);  // converged
-      } else {
-        iter[t] += 1;
-        begin_iter(t);
-      }
+      if (phi == fold || gnorm(t, g) <= g_tol) finish_start(t);  // converged
+      else next_iter(t);
     }
   }
   return SRHIP_OK;
@@ -528,9 +467,105 @@ int srhip_eval_loss_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program*
   const std::vector<int64_t> coff = const_offsets(*P);
   std::vector<int32_t> all(P->ntrees);
   for (int32_t t = 0; t < P->ntrees; ++t) all[t] = t;
-  rc = eval_grad(ctx, ds, P, loss, v, all, coff, out_loss, out_grad);
+  rc = eval_grad(ctx, ds, P, loss, v, all, coff, out_loss, out_grad, out_ok);
   if (rc) return rc;
-  for (int32_t t = 0; t < P->ntrees; ++t) out_ok[t] = std::isfinite(out_loss[t]) ? 1 : 0;
+  return SRHIP_OK;
+}
+
+int srhip_eval_grad_predict(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, int32_t wrt, int32_t direction,
+                            const int64_t* idx, int64_t nidx, void* out_pred, void* out_grad, uint8_t* out_ok) {
+  if (!out_pred || !out_grad || !out_ok) return fail(SRHIP_ERR_INVALID, "null output");
+  if (wrt != SRHIP_WRT_CONSTANTS && wrt != SRHIP_WRT_FEATURES) return fail(SRHIP_ERR_INVALID, "wrt %d", wrt);
+  int rc = check_eval_args(ctx, ds, P, MODE_PRED, nullptr);
+  if (rc) return rc;
+  if (P->dtype == SRHIP_I32) return fail(SRHIP_ERR_UNSUPPORTED, "derivatives need Float32 / Float64");
+  if (direction < 0 || (direction > 0 && (wrt != SRHIP_WRT_FEATURES || direction > ds->nfeat)))
+    return fail(SRHIP_ERR_INVALID, "direction %d (wrt %d, %lld features)", direction, wrt, (long long)ds->nfeat);
+  // values and did_succeed: the evaluator itself (eval_tree_array semantics, bit-identical predictions)
+  rc = run_eval(ctx, ds, P, MODE_PRED, nullptr, idx, nidx, nullptr, out_pred, out_ok);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(ctx->device));
+  View v;
+  rc = make_view(ctx, ds, idx, nidx, false, v);
+  if (rc) return rc;
+  rc = compile_grad_program(*P);
+  if (rc) return rc;
+  const int32_t nt = P->ntrees;
+  const int64_t m = v.m;
+  const size_t es = dtype_size(P->dtype);
+  // derivative rows of each tree: nconst (constants), nfeatures, or 1 (one direction)
+  std::vector<int64_t> row0(nt + 1, 0);
+  for (int32_t t = 0; t < nt; ++t)
+    row0[t + 1] = row0[t] + (wrt == SRHIP_WRT_CONSTANTS ? P->info[t].nconst : (direction > 0 ? 1 : ds->nfeat));
+  const int64_t nrows_out = row0[nt];
+  if (nrows_out == 0) {
+    HIP_TRY(hipStreamSynchronize(ctx->stream));  // a patched gradient program may still be uploading
+    return SRHIP_OK;
+  }
+  std::vector<int32_t> chunks;
+  for (int32_t t = 0; t < nt; ++t) {
+    if (P->ginfo[t].static_fail) continue;
+    const int64_t nc = row0[t + 1] - row0[t];
+    const int32_t first = direction > 0 ? direction - 1 : 0, end = direction > 0 ? direction : (int32_t)nc;
+    for (int32_t c0 = first; c0 < end; c0 += GRAD_ROW_KT) {
+      chunks.push_back(t);
+      chunks.push_back(c0);
+      chunks.push_back(end);
+      chunks.push_back((int32_t)(row0[t] + c0 - first));
+    }
+  }
+  auto body = [&]() -> int {
+    const int nch = (int)chunks.size() / 4;
+    DevBuf der;
+    HIP_TRY(der.ensure((size_t)nrows_out * m * es));
+    if (nch > 0) {
+      LaunchPlan L = plan_launch(ctx, P->dtype, ds->nfeat, false, false, m, nch, 64);
+      HIP_TRY(ctx->g_chunks.ensure(chunks.size() * sizeof(int32_t)));
+      HIP_TRY(hipMemcpyAsync(ctx->g_chunks.p, chunks.data(), chunks.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                             ctx->stream));
+      GradArgs a{};
+      a.code = (const Ins*)P->d_gcode.p;
+      a.prog_off = (const int32_t*)P->d_goff.p;
+      a.chunks = (const int32_t*)ctx->g_chunks.p;
+      a.X = v.X;
+      a.ld = v.ld;
+      a.nvalid = m;
+      a.nchunks = nch;
+      a.nfeat = (int32_t)ds->nfeat;
+      a.rb_rows = L.rb_rows;
+      a.nrb = L.nrb;
+      a.chunks_per_group = L.tpg;
+      a.max_steps = P->gmax_len;
+      a.out_der = der.p;
+      HIP_TRY(launch_grad_rows(P->dtype, P->gkmax <= 4 ? 4 : 8, wrt == SRHIP_WRT_CONSTANTS ? GMODE_ROWC : GMODE_ROWF, a,
+                               dim3(L.nrb, L.groups), ctx->stream));
+    }
+    HIP_TRY(hipMemcpyAsync(out_grad, der.p, (size_t)nrows_out * m * es, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return SRHIP_OK;
+  };
+  rc = body();
+  if (rc) {
+    (void)hipStreamSynchronize(ctx->stream);
+    return rc;
+  }
+  // complete = did_succeed of the evaluation and every derivative finite; a static failure's rows NaN
+  for (int32_t t = 0; t < nt; ++t) {
+    const int64_t n = (row0[t + 1] - row0[t]) * m;
+    if (P->ginfo[t].static_fail || P->info[t].static_fail) {
+      for (int64_t i = 0; i < n; ++i) {
+        if (es == 8) ((double*)out_grad)[row0[t] * m + i] = NAN;
+        else ((float*)out_grad)[row0[t] * m + i] = NAN;
+      }
+      out_ok[t] = 0;
+      continue;
+    }
+    bool fin = true;
+    for (int64_t i = 0; i < n && fin; ++i)
+      fin = es == 8 ? std::isfinite(((const double*)out_grad)[row0[t] * m + i])
+                    : std::isfinite(((const float*)out_grad)[row0[t] * m + i]);
+    if (!fin) out_ok[t] = 0;
+  }
   return SRHIP_OK;
 }
 
@@ -561,16 +596,14 @@ int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_prog
   std::vector<int32_t> trees;  // trees with constants (nconst == 0: nothing to optimise, :35)
   for (int32_t t = 0; t < nt; ++t)
     if (P->info[t].nconst > 0 && !P->info[t].static_fail) trees.push_back(t);
-  std::vector<double> best_x = x0, best_f(nt, INFINITY), x(x0.size()), f(nt);
+  std::vector<double> best_x = x0, best_f(nt, INFINITY);
   std::vector<int64_t> fcalls(nt, 0);
   std::mt19937_64 rng(opt->seed);
   std::normal_distribution<double> randn(0.0, 1.0);
   const double g_tol = opt->g_tol > 0 ? opt->g_tol : 1e-8;
-  // SRHIP_OPTIM_LOCKSTEP=1: one lock-step BFGS per restart (bfgs above) instead of the pipelined batch
-  const char* lse = getenv("SRHIP_OPTIM_LOCKSTEP");  // read per call (tests switch it)
-  const bool lockstep = lse && *lse && *lse != '0';
-  if (!lockstep && !trees.empty()) {
-    // the starting points in the lock-step loop's draw order (start-major, then tree, then constant)
+  if (!trees.empty()) {
+    // the starting points: x0, then nrestarts perturbed copies drawn start-major, then tree, then
+    // constant (src/ConstantOptimization.jl:53-60: c * (1 + randn/2))
     std::vector<std::vector<double>> starts(opt->nrestarts + 1, x0);
     for (int start = 1; start <= opt->nrestarts; ++start)
       for (int32_t t : trees)
@@ -594,24 +627,6 @@ int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_prog
       return rc;
     }
   }
-  for (int start = 0; lockstep && start <= opt->nrestarts && !trees.empty(); ++start) {
-    x = x0;
-    if (start > 0)  // src/ConstantOptimization.jl:53-60: c * (1 + randn/2)
-      for (int32_t t : trees)
-        for (int64_t k = coff[t]; k < coff[t + 1]; ++k) x[k] = x0[k] * (1.0 + 0.5 * randn(rng));
-    rc = bfgs(ctx, ds, P, loss, v, trees, coff, opt->iterations, g_tol, x, f, fcalls);
-    if (rc) {
-      set_all_consts(*P, x0.data());
-      compile_program(*P);
-      upload_program(*P);
-      return rc;
-    }
-    for (int32_t t : trees)
-      if (f[t] < best_f[t]) {  // :62-64
-        best_f[t] = f[t];
-        for (int64_t k = coff[t]; k < coff[t + 1]; ++k) best_x[k] = x[k];
-      }
-  }
   // accept where the best minimum beats the baseline (:70-78)
   std::vector<double> final_x = x0;
   for (int32_t t = 0; t < nt; ++t) {
@@ -629,8 +644,10 @@ int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_prog
   std::vector<uint8_t> ok(nt);
   rc = run_eval(ctx, ds, P, MODE_LOSS, loss, idx, nidx, out_loss, nullptr, ok.data());
   if (rc) return rc;
+  // num_evals bookkeeping (src/ConstantOptimization.jl:51,65,79): the objective calls of every start
+  // (result.f_calls), plus one for the re-score of an accepted tree; 0 for a tree left alone
   if (out_fcalls)
-    for (int32_t t = 0; t < nt; ++t) out_fcalls[t] = fcalls[t] + 1;
+    for (int32_t t = 0; t < nt; ++t) out_fcalls[t] = fcalls[t] + out_improved[t];
   return SRHIP_OK;
 }
 

@@ -8,11 +8,14 @@ from .api import (
     batch_sample,
     compile_trees,
     compute_complexity,
+    dimensional_regularization,
     eval_loss,
     eval_loss_batch,
     eval_loss_batched,
-    eval_tree_array,
+    eval_diff_tree_array,
     eval_grad_loss_batch,
+    eval_grad_tree_array,
+    eval_tree_array,
     eval_tree_array_batch,
     optimize_constants,
     loss_to_score,

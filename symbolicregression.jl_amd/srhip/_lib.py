@@ -94,6 +94,7 @@ SIGNATURES = {
     "srhip_chk_reduce_op": (ctypes.c_int, [ctypes.c_int]),
     "srhip_program_max_ops": (_i32, [_vp]),
     "srhip_eval_loss_grad": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(Loss), _vp, _i64, _vp, _vp, _vp]),
+    "srhip_eval_grad_predict": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _vp]),
     "srhip_optimize_constants": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(Loss), _vp, _i64,
                                                 ctypes.POINTER(OptimOptions), _vp, _vp, _vp]),
     "srhip_batcher_create": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(Operators), ctypes.POINTER(Loss), _i32, _i32,

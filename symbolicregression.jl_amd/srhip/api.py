@@ -1,6 +1,7 @@
 """The reference's hot-path API, backed by libsrhip:
 
   eval_tree_array(tree, X, options)        src/InterfaceDynamicExpressions.jl:56-63
+  eval_diff_tree_array / eval_grad_tree_array   src/InterfaceDynamicExpressions.jl:90-95,118-124
   eval_loss(tree, dataset, options; ...)   src/LossFunctions.jl:97-112 (-> _eval_loss :45-75)
   eval_loss_batched / batch_sample         src/LossFunctions.jl:114-127
   loss_to_score                            src/LossFunctions.jl:138-158
@@ -60,6 +61,33 @@ def eval_tree_array(tree, X, options, **kws):
     return out[0], bool(ok[0])
 
 
+def eval_grad_tree_array(tree, X, options, variable: bool = False, **kws):
+    """(output, gradient, complete) -- src/InterfaceDynamicExpressions.jl:118-124.  gradient is
+    [nfeatures, n] (variable=True: d output / d x_f) or [nconst, n] (variable=False: d output / d c in
+    get_constants order); forward-mode dual numbers on the device."""
+    ds = X if isinstance(X, Dataset) else Dataset(np.asarray(X))
+    prog = compile_trees([tree], options, ds.X.dtype)
+    try:
+        out, grads, ok = prog.eval_grad_predict(ds.device(_ctx(options)), variable=variable)
+    finally:
+        prog.close()
+    return out[0], grads[0], bool(ok[0])
+
+
+def eval_diff_tree_array(tree, X, options, direction: int):
+    """(output, d output / d x_direction, complete) -- src/InterfaceDynamicExpressions.jl:90-95
+    (direction is 1-based, as in Julia)."""
+    ds = X if isinstance(X, Dataset) else Dataset(np.asarray(X))
+    if not 1 <= int(direction) <= ds.nfeatures:
+        raise ValueError(f"direction {direction} out of range 1..{ds.nfeatures}")
+    prog = compile_trees([tree], options, ds.X.dtype)
+    try:
+        out, grads, ok = prog.eval_grad_predict(ds.device(_ctx(options)), variable=True, direction=int(direction))
+    finally:
+        prog.close()
+    return out[0], grads[0][0], bool(ok[0])
+
+
 # ---- losses ------------------------------------------------------------------------------------
 def _host_elementwise_loss(pred, y, w, loss):
     """User-defined elementwise loss (a Julia function in the reference): evaluated on the host
@@ -72,15 +100,38 @@ def _host_elementwise_loss(pred, y, w, loss):
     return float(np.sum(vals.astype(np.float64)) / np.sum(w.astype(np.float64)))
 
 
+def dimensional_regularization(tree, dataset: Dataset, options):
+    """src/LossFunctions.jl:217-227: 0 unless the tree violates the dataset's units (checked on row 1,
+    srhip.units), then options.dimensional_constraint_penalty (default 1000)."""
+    L = dataset.loss_type.type
+    if not dataset.has_units():
+        return L(0)
+    from .units import violates_dimensional_constraints
+
+    if not violates_dimensional_constraints(tree, dataset, options):
+        return L(0)
+    pen = options.dimensional_constraint_penalty
+    return L(1000) if pen is None else L(pen)
+
+
 def eval_loss_batch(trees, dataset: Dataset, options, regularization: bool = True, idx=None):
     """_eval_loss for every tree in one device launch: returns (loss[ntrees] float64, ok[ntrees]).
 
-    Loss is +Inf where did_succeed is false (L(Inf), src/LossFunctions.jl:55-57)."""
+    Loss is +Inf where did_succeed is false (L(Inf), src/LossFunctions.jl:55-57); with units and
+    regularization, dimensional_regularization is added to the finite losses (:70-72)."""
     trees = _as_trees(trees)
     if options.loss_function is not None:
         out = np.array([eval_loss(t, dataset, options, regularization=regularization, idx=idx) for t in trees],
                        dtype=np.float64)
         return out, np.isfinite(out)
+    out, ok = _eval_loss_batch_device(trees, dataset, options, idx)
+    if regularization and dataset.has_units():
+        for t in np.nonzero(ok)[0]:
+            out[t] = out[t] + float(dimensional_regularization(trees[t], dataset, options))
+    return out, ok
+
+
+def _eval_loss_batch_device(trees, dataset: Dataset, options, idx):
     ctx = _ctx(options)
     loss = options.elementwise_loss
     prog = compile_trees(trees, options, dataset.X.dtype)
@@ -121,7 +172,6 @@ def eval_loss(tree, dataset: Dataset, options, regularization: bool = True, idx=
     if options.loss_function is not None:
         return L(_evaluator(options.loss_function, tree, dataset, options, idx))
     loss, _ = eval_loss_batch([tree], dataset, options, regularization=regularization, idx=idx)
-    # dimensional_regularization (units) is out of scope for the device path: no units -> 0
     return L(loss[0])
 
 
@@ -223,35 +273,81 @@ def eval_grad_loss_batch(trees, dataset: Dataset, options, idx=None):
 def optimize_constants(dataset: Dataset, members, options, rng=None, idx=None):
     """optimize_constants (src/ConstantOptimization.jl:11-81) for one member or a whole list at once.
 
-    Members are PopMember-like objects (``.tree``, ``.loss``, ``.score``) or bare Nodes.  Where the
-    optimised constants beat the member's baseline loss, its tree constants are replaced and loss and
-    score re-computed (:70-78).  Returns (members, num_evals) like the reference (num_evals summed)."""
+    Members are PopMember-like objects (``.tree``, ``.loss``, ``.score``, ``.birth``) or bare Nodes.
+    Where the optimised constants beat the member's baseline loss, its tree constants are replaced,
+    loss and score re-computed on the same rows (:70-78) and its birth renewed (:76).  Returns
+    (members, num_evals) like the reference (num_evals summed over the members).
+
+    Built-in distance losses: one batched device call (srhip_optimize_constants: dual-number
+    gradients, Newton / BFGS per tree).  With ``options.batching`` every member draws its own
+    minibatch (src/ConstantOptimization.jl:14-16), so members are optimised one device call each.
+    A user ``loss_function`` (or a Python elementwise loss): host Newton / BFGS with finite
+    differences over ``eval_loss`` (srhip.host_optim), whose evaluations run on the device."""
     from .node import get_constants, set_constants
+    from .utils import get_birth_order
 
     single = not isinstance(members, (list, tuple))
     mlist = [members] if single else list(members)
     trees = [m.tree if hasattr(m, "tree") else m for m in mlist]
-    if options.loss_function is not None or not is_device_loss(options.elementwise_loss):
-        raise NotImplementedError("device constant optimisation needs a built-in elementwise loss")
-    if idx is None and options.batching:
-        idx = batch_sample(dataset, options, rng)
-    seed = int((rng or np.random.default_rng()).integers(0, 2**63 - 1))
-    prog = compile_trees(trees, options, dataset.X.dtype)
-    try:
-        losses, improved, fcalls = prog.optimize_constants(
-            dataset.device(_ctx(options)), options.elementwise_loss, iterations=options.optimizer_iterations,
-            nrestarts=options.optimizer_nrestarts, seed=seed, idx=idx)
-        consts = prog.get_constants()
-    finally:
-        prog.close()
+    rng = np.random.default_rng() if rng is None else rng
     eval_fraction = (options.batch_size / dataset.n) if options.batching else 1.0
     L = dataset.loss_type.type
-    for m, t, ok, c, lo in zip(mlist, trees, improved, consts, losses):
-        if not ok:
-            continue
-        set_constants(t, c)
-        if hasattr(m, "tree"):
-            m.loss = L(lo)
-            m.score = loss_to_score(m.loss, dataset.use_baseline, dataset.baseline_loss, m, options)
-    num_evals = float(np.sum(fcalls)) * eval_fraction
+    if idx is not None or not options.batching:
+        groups = [(list(range(len(mlist))), idx)]
+    else:
+        groups = [([i], batch_sample(dataset, options, rng)) for i in range(len(mlist))]
+    num_evals = 0.0
+    for members_idx, gidx in groups:
+        if options.loss_function is not None or not is_device_loss(options.elementwise_loss):
+            results = _optimize_constants_host(dataset, [trees[i] for i in members_idx], options, rng, gidx)
+        else:
+            seed = int(rng.integers(0, 2**63 - 1))
+            prog = compile_trees([trees[i] for i in members_idx], options, dataset.X.dtype)
+            try:
+                losses, improved, fcalls = prog.optimize_constants(
+                    dataset.device(_ctx(options)), options.elementwise_loss, iterations=options.optimizer_iterations,
+                    nrestarts=options.optimizer_nrestarts, seed=seed, idx=gidx)
+                consts = prog.get_constants()
+            finally:
+                prog.close()
+            results = list(zip(improved, consts, losses, fcalls))
+        for i, (ok, c, lo, fc) in zip(members_idx, results):
+            num_evals += float(fc) * eval_fraction
+            if not ok:
+                continue
+            set_constants(trees[i], c)
+            m = mlist[i]
+            if hasattr(m, "tree"):
+                if options.loss_function is not None or not is_device_loss(options.elementwise_loss):
+                    lo = eval_loss(trees[i], dataset, options, regularization=True, idx=gidx)
+                elif dataset.has_units():
+                    lo = lo + dimensional_regularization(trees[i], dataset, options)
+                m.loss = L(lo)
+                m.score = loss_to_score(m.loss, dataset.use_baseline, dataset.baseline_loss, m, options)
+                if hasattr(m, "birth"):
+                    m.birth = get_birth_order()
     return (mlist[0] if single else mlist), num_evals
+
+
+def _optimize_constants_host(dataset, trees, options, rng, idx):
+    """Host Newton / BFGS with finite differences over eval_loss(regularization=false), per tree:
+    [(improved, constants, loss, f_calls)] (src/ConstantOptimization.jl:43-81)."""
+    from . import host_optim
+    from .node import get_constants, set_constants
+
+    out = []
+    for tree in trees:
+        x0 = np.asarray(get_constants(tree), dtype=np.float64)
+        if len(x0) == 0:
+            out.append((False, x0, np.inf, 0))
+            continue
+        work = tree.copy()
+
+        def objective(c, work=work):
+            set_constants(work, c)
+            return eval_loss(work, dataset, options, regularization=False, idx=idx)
+
+        x, fx, improved, calls, _ = host_optim.optimize(objective, x0, iterations=options.optimizer_iterations,
+                                                        nrestarts=options.optimizer_nrestarts, rng=rng)
+        out.append((improved, x, fx, calls + (1 if improved else 0)))
+    return out

@@ -10,7 +10,8 @@ import numpy as np
 
 
 class Dataset:
-    def __init__(self, X, y=None, weights=None, loss_type=None, variable_names=None, extra=None):
+    def __init__(self, X, y=None, weights=None, loss_type=None, variable_names=None, extra=None, X_units=None,
+                 y_units=None):
         X = np.asarray(X)
         if X.ndim == 1:
             X = X.reshape(1, -1)
@@ -42,7 +43,17 @@ class Dataset:
         self.extra = extra or {}
         self.use_baseline = True
         self.baseline_loss = self.loss_type.type(1)
+        # units (src/Dataset.jl:170-193): y_units without X_units makes every feature dimensionless
+        from .units import get_units
+
+        self.y_units = get_units(y_units)
+        self.X_units = get_units(X_units, self.nfeatures)
+        if self.X_units is None and self.y_units is not None:
+            self.X_units = get_units(["1"] * self.nfeatures)
         self._dev = {}
+
+    def has_units(self) -> bool:
+        return self.X_units is not None
 
     def device(self, ctx):
         """The DeviceDataset for `ctx` (uploaded on first use)."""

@@ -182,6 +182,24 @@ class Program:
         splits = np.cumsum(nconst)[:-1]
         return out, np.split(grad, splits), ok.astype(bool)
 
+    def eval_grad_predict(self, ds: DeviceDataset, variable: bool = False, direction: int = 0, idx=None):
+        """Per-row derivatives (srhip_eval_grad_predict): (pred[T, m], grads: list of per-tree arrays
+        [rows, m], ok[T]); rows = the tree's constants (variable=False, get_constants order), every
+        feature (variable=True), or feature `direction` alone (direction >= 1)."""
+        idxa = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        m = ds.n if idxa is None else len(idxa)
+        if variable:
+            rows = np.full(self.ntrees, 1 if direction else ds.nfeatures, dtype=np.int64)
+        else:
+            rows = self.num_constants().astype(np.int64)
+        pred = np.empty((self.ntrees, m), dtype=self.dtype)
+        grad = np.empty((int(rows.sum()), m), dtype=self.dtype)
+        ok = np.empty(self.ntrees, dtype=np.uint8)
+        check(_lib.load().srhip_eval_grad_predict(self.ctx.handle, ds.handle, self.handle, 1 if variable else 0,
+                                                  int(direction), ptr(idxa), 0 if idxa is None else len(idxa),
+                                                  ptr(pred), ptr(grad), ptr(ok)))
+        return pred, np.split(grad, np.cumsum(rows)[:-1]), ok.astype(bool)
+
     def optimize_constants(self, ds: DeviceDataset, loss, iterations=8, nrestarts=2, seed=0, g_tol=1e-8, idx=None):
         """Batched optimize_constants; updates this program's constants in place.
 

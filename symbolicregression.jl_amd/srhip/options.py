@@ -49,6 +49,8 @@ class Options:
         deterministic: bool = False,
         seed=None,
         device: int = 0,
+        dimensional_constraint_penalty=None,
+        dimensionless_constants_only: bool = False,
         **unused,
     ):
         # operator aliasing: binopmap / unaopmap (src/Options.jl:92-150)
@@ -78,6 +80,10 @@ class Options:
         self.deterministic = deterministic
         self.seed = seed
         self.device = device
+        # dimensional_regularization (src/LossFunctions.jl:217-227, src/OptionsStruct.jl)
+        self.dimensional_constraint_penalty = (None if dimensional_constraint_penalty is None
+                                               else np.float32(dimensional_constraint_penalty))
+        self.dimensionless_constants_only = bool(dimensionless_constants_only)
         self.unused = unused
         use_cm = any(x is not None for x in (complexity_of_operators, complexity_of_constants, complexity_of_variables))
         cop = dict(complexity_of_operators or {})

@@ -109,14 +109,7 @@ def _draw(cdf, u: float) -> int:
 
 
 # ---- members, populations, statistics ------------------------------------------------------------
-_birth = itertools.count()
-_birth_lock = threading.Lock()
-
-
-def get_birth_order() -> int:
-    """src/Utils.jl get_birth_order (deterministic counter form)."""
-    with _birth_lock:
-        return next(_birth)
+from .utils import get_birth_order  # noqa: E402  (shared with api.optimize_constants)
 
 
 @dataclass

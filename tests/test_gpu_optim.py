@@ -135,9 +135,11 @@ def test_optimizer_recovers_reference_constants(ctx):
 
 
 def test_optimizer_outcome_vs_oracle(ctx, oracle):
-    """Batched device BFGS (exact gradients) vs the reference procedure restated with finite
+    """Batched device BFGS / Newton (exact gradients) vs the reference procedure restated with finite
     differences (oracle/optim.py), single start: never worse than the baseline, and at least as
-    good as the oracle's optimum (to 1e-6 relative) on nearly every tree."""
+    good as the oracle's optimum (1e-6 relative) on every tree whose reference optimum is resolved
+    (optim.reference_outcome: reproduced with 4x the difference step); the unresolved ones are listed
+    and must stay a minority."""
     import optim
 
     sr = _sr()
@@ -147,16 +149,20 @@ def test_optimizer_outcome_vs_oracle(ctx, oracle):
     base, base_ok = prog.eval_loss(ds, sr.L2DistLoss())
     dl, improved, _ = prog.optimize_constants(ds, sr.L2DistLoss(), nrestarts=0, seed=3)
     assert np.all(dl[base_ok] <= base[base_ok] * (1 + 1e-12))
-    wins = total = 0
+    total, lost, unresolved = 0, [], []
     for t in range(len(trees)):
         tn = nodes[offs[t]:offs[t + 1]].copy()
         if not base_ok[t] or not _order(tn):
             continue
-        _, ol, _ = optim.optimize_constants(tn, opts.binop_codes, opts.unaop_codes, X, y, nrestarts=0)
+        ol, stable = optim.reference_outcome(tn, opts.binop_codes, opts.unaop_codes, X, y)
         total += 1
-        wins += dl[t] <= ol * (1 + 1e-6) + 1e-12
-    assert total >= 10
-    assert wins >= 0.85 * total, (wins, total)
+        if not stable:
+            unresolved.append((t, sr.string_tree(trees[t], opts)))
+        elif not dl[t] <= ol * (1 + 1e-6) + 1e-12:
+            lost.append((t, len(_order(tn)), dl[t], ol, base[t]))
+    assert total >= 10 and total - len(unresolved) >= 8
+    assert len(unresolved) <= total // 3, unresolved
+    assert not lost, (lost, unresolved)
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
@@ -164,22 +170,30 @@ def test_grad_program_patch_equals_full_compile(ctx, dtype):
     """After set_constants, the gradient program recompiles only the trees whose constants moved
     (in place, srhip_host.cpp patch_grad_t); its losses, gradients and masks equal, bit for bit, a
     fresh program compiled in full with the same constants — including a tree whose new constant
-    is NaN (a static did_succeed failure) and a second patch on top of the first."""
+    is NaN (a static did_succeed failure), a second patch on top of the first, and that tree patched
+    back into its kept slot once its constants are finite again."""
     sr = _sr()
     opts, _, nodes, offs, X, y = _problem(sr, dtype, ntrees=48)
     ds = sr.DeviceDataset(ctx, X, y)
     loss = sr.L2DistLoss()
     prog = sr.Program(ctx, nodes, offs, opts, dtype)
-    prog.eval_loss_grad(ds, loss)  # full compile of the gradient program
+    ok0 = prog.eval_loss_grad(ds, loss)[2]  # full compile of the gradient program
     c = prog.get_constants()
     rng = np.random.default_rng(3)
     with_c = [t for t in range(len(c)) if len(c[t]) > 0]
     assert len(with_c) >= 6
-    for step in range(2):
+    victim = next(t for t in with_c[1:] if ok0[t])
+    with_c.remove(victim)
+    with_c.insert(1, victim)
+    keep = c[with_c[1]].copy()
+    for step in range(3):
         for t in with_c[step::3]:
-            c[t] = c[t] * (1.0 + 0.25 * rng.standard_normal(len(c[t])))
+            if t != with_c[1]:
+                c[t] = c[t] * (1.0 + 0.25 * rng.standard_normal(len(c[t])))
         if step == 0:
-            c[with_c[1]][0] = np.nan
+            c[with_c[1]][0] = np.nan  # a static failure: the tree keeps its slot
+        if step == 2:
+            c[with_c[1]] = keep.copy()  # finite again, same code length: patched back into its slot
         flat = np.concatenate(c)
         prog.set_constants(flat)
         pl, pg, pok = prog.eval_loss_grad(ds, loss)
@@ -188,36 +202,94 @@ def test_grad_program_patch_equals_full_compile(ctx, dtype):
         fl, fg, fok = fresh.eval_loss_grad(ds, loss)
         fresh.close()
         assert np.array_equal(pok, fok)
-        assert not pok[with_c[1]]
+        assert pok[with_c[1]] == (step == 2)
         assert np.array_equal(pl.view(np.uint64), fl.view(np.uint64))
         assert np.array_equal(np.concatenate(pg).view(np.uint64), np.concatenate(fg).view(np.uint64))
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_pipelined_optimizer_equals_lockstep(ctx, dtype, monkeypatch):
+def test_batched_optimizer_equals_per_tree(ctx, dtype):
     """The pipelined optimiser (srhip_optim.cpp bfgs_pipelined: every tree runs its own
-    restart / iteration / line-search state machine, one launch per round over the trees that are
-    still active) returns, bit for bit, the losses, improvement flags, evaluation counts and
-    constants of the lock-step one (one BFGS per restart over the whole population,
-    SRHIP_OPTIM_LOCKSTEP=1) — a tree's loss and gradient do not depend on which trees share a
-    launch."""
+    start / Hessian-probe / line-search state machine, one launch per round over the trees still
+    active) returns, bit for bit, the losses, improvement flags, evaluation counts and constants that
+    optimising each tree alone returns -- a tree's loss and gradient do not depend on which trees
+    share a launch.  The population mixes Newton (one constant) and BFGS trees."""
     sr = _sr()
-    opts, _, nodes, offs, X, y = _problem(sr, dtype, ntrees=48)
+    opts, _, nodes, offs, X, y = _problem(sr, dtype, ntrees=40)
     ds = sr.DeviceDataset(ctx, X, y)
     loss = sr.L2DistLoss()
-    res = []
-    for mode in ("1", "0"):
-        monkeypatch.setenv("SRHIP_OPTIM_LOCKSTEP", mode)
-        prog = sr.Program(ctx, nodes, offs, opts, dtype)
-        out, improved, fcalls = prog.optimize_constants(ds, loss, iterations=8, nrestarts=2, seed=11)
-        res.append((out, improved, fcalls, np.concatenate(prog.get_constants())))
-        prog.close()
-    (l0, i0, f0, c0), (l1, i1, f1, c1) = res
-    assert i0.any()
-    assert np.array_equal(i0, i1)
-    assert np.array_equal(f0, f1)
-    assert np.array_equal(np.asarray(l0, dtype=np.float64).view(np.uint64), np.asarray(l1, dtype=np.float64).view(np.uint64))
-    assert np.array_equal(np.asarray(c0, dtype=np.float64).view(np.uint64), np.asarray(c1, dtype=np.float64).view(np.uint64))
+    prog = sr.Program(ctx, nodes, offs, opts, dtype)
+    nconst = prog.num_constants()
+    assert (nconst == 1).sum() >= 3 and (nconst >= 2).sum() >= 10
+    out, improved, fcalls = prog.optimize_constants(ds, loss, iterations=8, nrestarts=0, seed=11)
+    consts = prog.get_constants()
+    assert improved[nconst == 1].any() and improved[nconst >= 2].any()
+    for t in range(len(offs) - 1):
+        one = sr.Program(ctx, nodes[offs[t]:offs[t + 1]], np.array([0, offs[t + 1] - offs[t]]), opts, dtype)
+        o1, i1, f1 = one.optimize_constants(ds, loss, iterations=8, nrestarts=0, seed=11)
+        assert i1[0] == improved[t] and f1[0] == fcalls[t], t
+        assert np.asarray(o1[0], np.float64).view(np.uint64) == np.asarray(out[t], np.float64).view(np.uint64), t
+        assert np.array_equal(one.get_constants()[0].view(np.uint64), consts[t].view(np.uint64)), t
+        one.close()
+
+
+def test_optimizer_fcalls_accounting(ctx):
+    """num_evals bookkeeping (src/ConstantOptimization.jl:51,65,79; ADVICE r1): no constants -> 0;
+    otherwise the objective calls of every start, + 1 when the tree was improved (its re-score)."""
+    sr = _sr()
+    opts = sr.Options(binary_operators=("+", "*"), unary_operators=("cos",))
+    x1 = sr.Node("x1")
+    X = np.random.default_rng(1).standard_normal((1, 500))
+    y = 2.5 * X[0] + 0.5
+    trees = [sr.cos(x1) + x1,                              # no constants
+             sr.Node(val=1.0) * x1 + sr.Node(val=0.1),     # BFGS, improves
+             sr.Node(val=2.5) * x1 + sr.Node(val=0.5)]     # already optimal: gradient 0 at start
+    nodes, offs = sr.flatten(trees, opts, np.float64)
+    ds = sr.DeviceDataset(ctx, X, y)
+    prog = sr.Program(ctx, nodes, offs, opts, np.float64)
+    _, improved, fcalls = prog.optimize_constants(ds, sr.L2DistLoss(), nrestarts=2, seed=5)
+    assert fcalls[0] == 0 and not improved[0]
+    assert improved[1] and fcalls[1] >= 3 * 2 + 1  # >= initial + one trial per start, + the re-score
+    prog = sr.Program(ctx, nodes, offs, opts, np.float64)
+    _, improved, fcalls = prog.optimize_constants(ds, sr.L2DistLoss(), nrestarts=0, seed=5)
+    assert fcalls[0] == 0 and not improved[0]
+    assert not improved[2] and fcalls[2] == 1  # zero gradient at the start: one call, nothing accepted
+
+
+def test_newton_outcome_vs_oracle(ctx, oracle):
+    """One-constant trees take Newton (src/ConstantOptimization.jl:27-31) on the device and in the
+    oracle: the device optimum matches or beats the oracle's (1e-6 relative) on every tree whose
+    reference optimum is resolved (optim.reference_outcome)."""
+    import optim
+
+    sr = _sr()
+    opts = sr.Options(binary_operators=("+", "-", "*", "/"), unary_operators=("cos", "exp", "sin"))
+    rng = np.random.default_rng(21)
+    trees = []
+    while len(trees) < 24:
+        t = sr.gen_random_tree_fixed_size(int(rng.integers(3, 12)), opts, 3, np.float64, rng)
+        if sr.count_constants(t) == 1:
+            trees.append(t)
+    nodes, offs = sr.flatten(trees, opts, np.float64)
+    X = rng.standard_normal((3, 2000))
+    y = np.cos(1.3 * X[0]) * 2.0 + X[1] * 0.7 - 0.3
+    prog = sr.Program(ctx, nodes, offs, opts, np.float64)
+    ds = sr.DeviceDataset(ctx, X, y)
+    base, base_ok = prog.eval_loss(ds, sr.L2DistLoss())
+    dl, improved, _ = prog.optimize_constants(ds, sr.L2DistLoss(), nrestarts=0, seed=3)
+    checked, unresolved = 0, []
+    for t in range(len(trees)):
+        if not base_ok[t]:
+            continue
+        tn = nodes[offs[t]:offs[t + 1]].copy()
+        assert dl[t] <= base[t] * (1 + 1e-12)
+        ol, stable = optim.reference_outcome(tn, opts.binop_codes, opts.unaop_codes, X, y)
+        if not stable:  # e.g. sin(exp(c - (x2 - exp(x1)))): the loss oscillates below the difference step
+            unresolved.append((t, sr.string_tree(trees[t], opts)))
+            continue
+        assert dl[t] <= ol * (1 + 1e-6) + 1e-12, (t, dl[t], ol, base[t])
+        checked += 1
+    assert checked >= 12 and improved.sum() >= 8, (checked, unresolved)
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])

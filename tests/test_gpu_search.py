@@ -80,10 +80,10 @@ def test_device_search_finds_readme_equation():
     device: the best hall-of-fame loss falls far below the constant baseline, and the HoF losses
     equal fresh device evaluations of their trees."""
     X, y = _data()
-    o = srhip.Options(populations=6, population_size=33, ncycles_per_iteration=60, maxsize=20,
+    o = srhip.Options(populations=8, population_size=33, ncycles_per_iteration=100, maxsize=20,
                       deterministic=True, seed=1, **OPS)
     print("search start", flush=True)
-    res = S.equation_search(X, y, o, niterations=6)
+    res = S.equation_search(X, y, o, niterations=10)
     front = res.pareto_frontier()
     best = min(m.loss for m in front)
     base = np.mean((y - y.mean()) ** 2)
