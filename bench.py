@@ -23,6 +23,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "symbolicregression.jl_amd"))
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector (= FP32 MFMA) peak, MI355X_MICROARCH.md
+PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 vector peak
 
 
 def parse():
@@ -114,6 +115,31 @@ def main():
     kern_ms = float(np.mean(kms))
     achieved = flops / (kern_ms * 1e-3) / 1e12
 
+    # the same population without derived columns: every node of every tree evaluated by its own
+    # instruction (the headline counts the U(X[f]) reads served from shared LDS columns as evaluated
+    # nodes) -- reported beside it
+    os.environ["SRHIP_NO_DERIVE"] = "1"
+    p_plain = srhip.Program(ctx, nodes, offs, opts, np.float32)
+    del os.environ["SRHIP_NO_DERIVE"]
+    for _ in range(args.warmup):
+        p_plain.eval_loss(ds, loss)
+    barrier()
+    t0 = time.perf_counter()
+    kms_plain = []
+    for _ in range(args.steps):
+        p_plain.eval_loss(ds, loss)
+        kms_plain.append(ctx.last_kernel_ms())
+    barrier()
+    dt_plain = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        tt = torch.tensor([dt_plain], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt_plain = float(tt.item())
+    kern_plain = float(np.mean(kms_plain))
+    p_plain.close()
+
     # end-to-end per population (host compile of 1024 fresh trees + upload + eval)
     t0 = time.perf_counter()
     p2 = srhip.Program(ctx, nodes, offs, opts, np.float32)
@@ -170,7 +196,12 @@ def main():
                 "op_mix": op_mix(nodes, opts),
             },
             "cpu_baseline": cpu,
-            "extra": {"compile_ms_1024_trees": compile_ms, "end_to_end_ms_per_population": e2e_ms},
+            "extra": {
+                "compile_ms_1024_trees": compile_ms, "end_to_end_ms_per_population": e2e_ms,
+                "no_derive": {"value": work * world * args.steps / dt_plain, "kernel_ms": kern_plain,
+                              "frac": flops / (kern_plain * 1e-3) / 1e12 / PEAK_FP32_TFLOPS,
+                              "note": "SRHIP_NO_DERIVE=1: no derived columns, every node evaluated per tree"},
+            },
         }
         print(json.dumps(out))
     if dist is not None:
@@ -278,15 +309,25 @@ def bench_c4(args):
         out, improved, fcalls = step()
     ctx.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
-    # gradient launch alone
+    # gradient launch alone (all 512 trees' loss + d loss / d c), HIP events around the dual-number
+    # kernel on the library's stream
     st = prog.stats()
     for _ in range(3):
         prog.eval_loss_grad(ds, loss)
     ctx.synchronize()
     t0 = time.perf_counter()
+    gkms = []
     for _ in range(10):
         prog.eval_loss_grad(ds, loss)
+        gkms.append(ctx.last_kernel_ms())
     gdt = (time.perf_counter() - t0) / 10
+    gk_ms = float(np.mean(gkms))
+    # algorithmic flops of one gradient launch: per row, every operator node costs its
+    # value plus one chain-rule product per constant of the tree; the fused loss 3 + 2 per constant
+    nconst = prog.num_constants().astype(np.int64)
+    opn = np.array([int(np.sum(nodes[offs[t]:offs[t + 1]]["degree"] > 0)) for t in range(len(offs) - 1)])
+    gflops = float(rows * np.sum(opn * (1 + nconst) + 3 + 2 * nconst))
+    cpu = None if args.no_cpu else cpu_c4_baseline(nodes, offs, opts, X, y, args.cpu_seconds)
     fin = np.isfinite(base)
     print(json.dumps({
         "metric": "C4 batched constant optimisation: wall time per optimize_constants over the population",
@@ -301,7 +342,37 @@ def bench_c4(args):
         "median_loss_before": float(np.median(base[fin])), "median_loss_after": float(np.median(out[fin])),
         "grad_launch_ms": gdt * 1e3,
         "grad_node_row_evals_per_s": st["total_nodes"] * rows / gdt,
+        "roofline": {"bound": "valu", "kernel": "srhip::grad_kernel<double, KT, K, 0>", "kernel_ms": gk_ms,
+                     "flops_per_launch": gflops, "achieved": gflops / (gk_ms * 1e-3) / 1e12,
+                     "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                     "frac": gflops / (gk_ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS, "traffic": None},
+        "cpu_baseline": cpu,
     }))
+
+
+def cpu_c4_baseline(nodes, offs, opts, X, y, target_s):
+    """The reference procedure (oracle/optim.py: finite-difference BFGS / Newton + BackTracking,
+    iterations 8, 2 restarts) on one core over a sample of the population's trees, extrapolated to all
+    of them: ms per optimize_constants of the whole population on one core."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import optim
+
+    order = np.random.default_rng(3).permutation(len(offs) - 1)
+    t0 = time.perf_counter()
+    done = 0
+    for t in order:
+        tn = nodes[offs[t]:offs[t + 1]].copy()
+        optim.optimize_constants(tn, opts.binop_codes, opts.unaop_codes, X, y, iterations=8, nrestarts=2,
+                                 rng=np.random.default_rng(int(t)))
+        done += 1
+        if time.perf_counter() - t0 > target_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": dt / done * (len(offs) - 1) * 1e3, "unit": "ms", "cores": 1, "kind": "port",
+            "sample": f"{done} of the {len(offs) - 1} trees ({dt:.1f} s), oracle/optim.py finite-difference "
+                      f"BFGS/Newton(8) + 2 restarts over the C oracle's eval_loss, one core, extrapolated"}
 
 
 def bench_search(args):

@@ -243,8 +243,9 @@ int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_prog
                              uint8_t* out_improved, int64_t* out_fcalls);
 
 /* ---- measurement hooks (bench / profiling) --------------------------------------------- */
-/* Device time (ms) of the last srhip_eval_loss/predict's main evaluation kernel, measured with
- * HIP events recorded on the context's stream; < 0 if unavailable. */
+/* Device time (ms) of the last main kernel on this context -- the interpreter of srhip_eval_loss /
+ * srhip_eval_predict, or the dual-number kernel of srhip_eval_loss_grad / the optimiser's last
+ * gradient launch -- measured with HIP events recorded on the context's stream; < 0 if unavailable. */
 double srhip_last_kernel_ms(const srhip_ctx* ctx);
 /* Per-program work counters: sum over trees of count_nodes / operator nodes. */
 int srhip_program_stats(const srhip_program* prog, int64_t* total_nodes, int64_t* total_opnodes,

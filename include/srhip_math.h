@@ -14,8 +14,9 @@
  * which also pins every function against glibc: <= 1 ULP in Float64, and Float32 values that are
  * the correctly rounded results in all but double-rounding cases).
  *
- * Float32 evaluation widens to Float64 and rounds once (srm_*f below), as Julia does for Float32
- * trigonometry (DoubleFloat32 kernels) and for Float32 `^`.
+ * Float32 sin / cos / tan / log widen to Float64 and round once (srm_*f below), as Julia does for
+ * Float32 trigonometry (DoubleFloat32 kernels) and for Float32 `^`; Float32 exp is Julia's own
+ * Float32 algorithm (srm_expf).
  *
  * Usable from C99 (oracle, gcc) and HIP C++ (host and device).  Compile WITHOUT fp contraction
  * (-ffp-contract=off): the explicit fma() calls are the only fused operations.
@@ -378,27 +379,37 @@ SRM_FN float srm_trigf(int kind, float x) {
 SRM_FN float srm_cosf(float x) { return srm_trigf(0, x); }
 SRM_FN float srm_sinf(float x) { return srm_trigf(1, x); }
 SRM_FN float srm_tanf(float x) { return srm_trigf(2, x); }
-SRM_FN float srm_expf(float xf) {
-  const double invln2 = 1.4426950408889634, ln2_hi = 0.6931471805599453, ln2_lo = 2.3190468138462996e-17;
-  double x = (double)xf;
-  /* clamp to where the float result is already 0 or Inf (also maps NaN to a finite value) */
-  x = __builtin_fmin(__builtin_fmax(x, -104.0), 89.0);
-  const double k = srm_rint(x * invln2);
-  double r = srm_fma(-k, ln2_hi, x);
-  r = srm_fma(-k, ln2_lo, r);
-  /* exp r = 1 + r Q(r) on |r| <= ln2/2 (+1e-4): minimax on relative error, < 2^-40 */
-  double p = 2.4736025668457734e-05;
-  p = srm_fma(p, r, 0.00019914637854529652);
-  p = srm_fma(p, r, 0.0013889148047310426);
-  p = srm_fma(p, r, 0.008333268860258102);
-  p = srm_fma(p, r, 0.04166666458462912);
-  p = srm_fma(p, r, 0.16666666872538483);
-  p = srm_fma(p, r, 0.5000000000448828);
-  p = srm_fma(p, r, 0.9999999999832456);
-  p = srm_fma(p, r, 1.0);
-  /* |k| <= 151: p 2^k is exact in Float64 (no rounding before the one to Float32) */
-  const float res = (float)__builtin_ldexp(p, (int)k);
-  return (xf == xf) ? res : xf;
+/* Float32 exp: Julia Base.Math exp_impl(x::Float32, Val(:e)) (base/special/exp.jl, Julia >= 1.7), a
+ * Float32 algorithm (unlike Float32 sin / cos, which Julia evaluates in Float64): N = round(x log2 e)
+ * in Float32, r = x - N ln2 with -ln2 split into two Float32 parts (two fmas: Julia's muladd on FMA
+ * hardware), e^r by Julia's degree-6 Float32 minimax polynomial (evalpoly = Horner with muladd), and
+ * p 2^N with one rounding (Julia's subnormal / N = 128 rescalings are that same single rounding);
+ * x > 88.72284 -> Inf, x < -103.97208 -> 0.  Max error 1 ULP (tests/test_math_accuracy.py; every
+ * Float32 input is checked by tools/check_expf.c).  The device runs the same operations two rows per
+ * packed instruction (srhip_eval.hip expf_rows), proven bit-identical by the same exhaustive check. */
+#define SRM_EXPF_LOG2E 1.442695f
+#define SRM_EXPF_NLN2_HI (-0.6931472f)
+#define SRM_EXPF_NLN2_LO 1.9046542e-9f
+#define SRM_EXPF_C6 0.0013956056f
+#define SRM_EXPF_C5 0.008375129f
+#define SRM_EXPF_C4 0.041666083f
+#define SRM_EXPF_C3 0.16666415f
+SRM_FN float srm_fmaf(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+SRM_FN float srm_expf(float x) {
+  if (!(x == x)) return x + x;
+  if (x > 88.72284f) return __builtin_inff();
+  if (x < -103.97208f) return 0.0f;
+  const float n = __builtin_rintf(x * SRM_EXPF_LOG2E);
+  float r = srm_fmaf(n, SRM_EXPF_NLN2_HI, x);
+  r = srm_fmaf(n, SRM_EXPF_NLN2_LO, r);
+  float p = SRM_EXPF_C6;
+  p = srm_fmaf(r, p, SRM_EXPF_C5);
+  p = srm_fmaf(r, p, SRM_EXPF_C4);
+  p = srm_fmaf(r, p, SRM_EXPF_C3);
+  p = srm_fmaf(r, p, 0.5f);
+  p = srm_fmaf(r, p, 1.0f);
+  p = srm_fmaf(r, p, 1.0f);
+  return __builtin_ldexpf(p, (int)n);
 }
 SRM_FN float srm_logf(float x) { return (float)srm_log((double)x); }
 

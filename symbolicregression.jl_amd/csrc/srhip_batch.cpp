@@ -60,12 +60,30 @@ struct srhip_batcher {
   int64_t n_requests = 0, max_seen = 0;
   std::atomic<int64_t> n_launches{0};
   std::thread worker;
+  srhip_program* slot = nullptr;  // the long-lived program every flush recompiles (worker thread only)
 
   void run();
   void flush(std::vector<Request>& batch);
 };
 
 namespace {
+
+// The batcher's one long-lived program: every flush recompiles it in place (host) and re-uploads
+// into its device buffers, which only grow -- no allocation, free or program object per flush (a
+// hipFree synchronises the whole device), and the upload is not synchronised separately: the
+// evaluation that follows on the same stream synchronises once, at its end.
+int run_slot_program(srhip_batcher* b, std::vector<srhip_node>&& nodes, std::vector<int64_t>&& offs,
+                     const std::vector<int64_t>& idx, double* loss, uint8_t* ok) {
+  srhip_program& P = *b->slot;
+  P.ntrees = (int32_t)offs.size() - 1;
+  P.nodes = std::move(nodes);
+  P.offsets = std::move(offs);
+  int rc = compile_program(P);
+  if (rc) return rc;
+  rc = upload_program(P, false);
+  if (rc) return rc;
+  return srhip_eval_loss(b->ctx, b->ds, &P, &b->loss, idx.empty() ? nullptr : idx.data(), (int64_t)idx.size(), loss, ok);
+}
 
 // One launch over the trees of `reqs` (same row subset); results keyed by ticket.
 void launch_group(srhip_batcher* b, const std::vector<Request*>& reqs, std::vector<std::pair<uint64_t, Result>>& out) {
@@ -76,12 +94,10 @@ void launch_group(srhip_batcher* b, const std::vector<Request*>& reqs, std::vect
     nodes.insert(nodes.end(), r->nodes.begin(), r->nodes.end());
     offs.push_back((int64_t)nodes.size());
   }
-  srhip_operators ops{(int32_t)b->binops.size(), (int32_t)b->unaops.size(), b->binops.data(), b->unaops.data()};
   const std::vector<int64_t>& idx = reqs[0]->idx;
   std::vector<double> loss(n);
   std::vector<uint8_t> ok(n);
-  int rc = srhip_eval_loss_batch(b->ctx, b->ds, nodes.data(), offs.data(), n, &ops, &b->loss,
-                                 idx.empty() ? nullptr : idx.data(), (int64_t)idx.size(), loss.data(), ok.data());
+  int rc = run_slot_program(b, std::move(nodes), std::move(offs), idx, loss.data(), ok.data());
   b->n_launches++;
   if (rc != SRHIP_OK && n > 1 && rc != SRHIP_ERR_DEVICE) {
     // a malformed / unsupported tree fails the whole program: attribute errors per request
@@ -158,6 +174,13 @@ int srhip_batcher_create(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_op
   if (loss) b->loss = *loss;
   b->max_batch = max_batch;
   b->max_wait_us = max_wait_us;
+  // the slot program: an empty population for this operator table, on the batcher's context
+  const int64_t zero = 0;
+  int rc = srhip_program_create(ctx, ds->dtype, nullptr, &zero, 0, ops, &b->slot);
+  if (rc) {
+    delete b;
+    return rc;
+  }
   try {
     b->worker = std::thread([b] { b->run(); });
   } catch (...) {
@@ -239,6 +262,7 @@ void srhip_batcher_destroy(srhip_batcher* b) {
   }
   b->cv_work.notify_all();
   if (b->worker.joinable()) b->worker.join();
+  srhip_program_destroy(b->slot);
   delete b;
 }
 

@@ -131,25 +131,34 @@ __device__ __attribute__((always_inline)) inline float sincosf_dev(double x) {
   return __builtin_bit_cast(float, o);
 }
 
-// srm_expf for the device rows, bit-identical for every non-NaN x: the clamp is a NaN-propagating
-// minimum / maximum pair (exact: the bounds are floats), so a NaN argument flows through the
-// reduction and comes out NaN without a final select (the oracle returns the argument's NaN).
-__device__ __attribute__((always_inline)) inline float expf_dev(float xf) {
-  const double invln2 = 1.4426950408889634, ln2_hi = 0.6931471805599453, ln2_lo = 2.3190468138462996e-17;
-  const double x = (double)__builtin_elementwise_maximum(__builtin_elementwise_minimum(xf, 89.0f), -104.0f);
-  const double k = __builtin_rint(x * invln2);
-  double r = __builtin_fma(-k, ln2_hi, x);
-  r = __builtin_fma(-k, ln2_lo, r);
-  double p = 2.4736025668457734e-05;
-  p = __builtin_fma(p, r, 0.00019914637854529652);
-  p = __builtin_fma(p, r, 0.0013889148047310426);
-  p = __builtin_fma(p, r, 0.008333268860258102);
-  p = __builtin_fma(p, r, 0.04166666458462912);
-  p = __builtin_fma(p, r, 0.16666666872538483);
-  p = __builtin_fma(p, r, 0.5000000000448828);
-  p = __builtin_fma(p, r, 0.9999999999832456);
-  p = __builtin_fma(p, r, 1.0);
-  return (float)__builtin_ldexp(p, cvt_i32_sat(k));
+// Julia's Float32 exp (include/srhip_math.h srm_expf) on two rows per instruction: the clamp to
+// [-104, 89] (NaN-propagating minimum / maximum) replaces srm_expf's Inf / 0 branches and every other
+// step is the same Float32 operation, packed (v_pk_mul_f32, v_pk_fma_f32); v_cvt_i32_f32 saturates and
+// maps NaN to 0, v_ldexp_f32 rounds once.  tools/check_expf.c proves this formulation bit-identical
+// to srm_expf on all 2^32 inputs (NaN in, NaN out).
+typedef float F2 __attribute__((ext_vector_type(2)));
+__device__ __attribute__((always_inline)) inline int cvt_i32_f32(float x) {
+  int m;
+  asm("v_cvt_i32_f32 %0, %1" : "=v"(m) : "v"(x));
+  return m;
+}
+__device__ __attribute__((always_inline)) inline F2 expf2_dev(F2 x) {
+  x = __builtin_elementwise_minimum(__builtin_elementwise_maximum(x, (F2)(-104.0f)), (F2)(89.0f));
+  F2 n = x * (F2)(SRM_EXPF_LOG2E);
+  n.x = __builtin_rintf(n.x);
+  n.y = __builtin_rintf(n.y);
+  F2 r = __builtin_elementwise_fma(n, (F2)(SRM_EXPF_NLN2_HI), x);
+  r = __builtin_elementwise_fma(n, (F2)(SRM_EXPF_NLN2_LO), r);
+  F2 p = __builtin_elementwise_fma(r, (F2)(SRM_EXPF_C6), (F2)(SRM_EXPF_C5));
+  p = __builtin_elementwise_fma(r, p, (F2)(SRM_EXPF_C4));
+  p = __builtin_elementwise_fma(r, p, (F2)(SRM_EXPF_C3));
+  p = __builtin_elementwise_fma(r, p, (F2)(0.5f));
+  p = __builtin_elementwise_fma(r, p, (F2)(1.0f));
+  p = __builtin_elementwise_fma(r, p, (F2)(1.0f));
+  F2 out;
+  out.x = __builtin_ldexpf(p.x, cvt_i32_f32(n.x));
+  out.y = __builtin_ldexpf(p.y, cvt_i32_f32(n.y));
+  return out;
 }
 
 // Float32 cos/sin/tan over a lane's R rows.  Every row takes the fast path (|x| < 2^28 pi/2 after
@@ -212,10 +221,11 @@ __device__ __attribute__((noinline)) RV<T, R> heavy_un(RV<T, R> v) {
   using O = OpsT<T>;
   if constexpr (SRHIP_TRIG_ROWS && std::is_same<T, float>::value && (U == UN_COS || U == UN_SIN || U == UN_TAN))
     return trigf_rows<R, U == UN_COS ? 0 : (U == UN_SIN ? 1 : 2)>(v);
-  if constexpr (std::is_same<T, float>::value && U == UN_EXP) {
-    UNR for (int r = 0; r < R; ++r) {
-      v[r] = expf_dev(v[r]);
-      if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
+  if constexpr (std::is_same<T, float>::value && U == UN_EXP && R % 2 == 0) {
+    UNR for (int r = 0; r < R; r += 2) {
+      const F2 e = expf2_dev((F2){v[r], v[r + 1]});
+      v[r] = e.x;
+      v[r + 1] = e.y;
     }
     return v;
   }
@@ -284,10 +294,33 @@ __device__ __attribute__((always_inline)) inline void apply_heavy(T (&A)[R], con
   UNR for (int r = 0; r < R; ++r) A[r] = a[r];
 }
 
-// Specialised binary operator over a lane's rows: A = A op B (SWAP: A = B op A).  Float32 + - *
-// run as packed FP32 (v_pk_add_f32 / v_pk_mul_f32: two rows per instruction, each rounded exactly
-// as the scalar instruction would); the rest row by row.
-typedef float PkF32 __attribute__((ext_vector_type(2)));
+// IEEE Float32 division of two rows: the compiler's own a / b expansion (v_div_scale of the
+// denominator and of the numerator, v_rcp, Newton refinement, v_div_fmas with the numerator's scale
+// flag, v_div_fixup for the special cases), with its five fma / mul steps on packed row pairs
+// (v_pk_fma_f32, v_pk_mul_f32 round each lane exactly as the scalar instructions): the same bits as
+// n / d, 8 instead of 11 VALU instructions per row.
+__device__ __attribute__((always_inline)) inline F2 div2_dev(F2 n, F2 d) {
+  bool unused0, unused1, f0, f1;
+  const F2 ds = {__builtin_amdgcn_div_scalef(n.x, d.x, false, &unused0),
+                 __builtin_amdgcn_div_scalef(n.y, d.y, false, &unused1)};
+  F2 r = {__builtin_amdgcn_rcpf(ds.x), __builtin_amdgcn_rcpf(ds.y)};
+  const F2 e = __builtin_elementwise_fma(-ds, r, (F2)(1.0f));
+  r = __builtin_elementwise_fma(e, r, r);
+  const F2 ns = {__builtin_amdgcn_div_scalef(n.x, d.x, true, &f0), __builtin_amdgcn_div_scalef(n.y, d.y, true, &f1)};
+  F2 q = ns * r;
+  const F2 e2 = __builtin_elementwise_fma(-ds, q, ns);
+  q = __builtin_elementwise_fma(e2, r, q);
+  const F2 e3 = __builtin_elementwise_fma(-ds, q, ns);
+  F2 out;
+  out.x = __builtin_amdgcn_div_fixupf(__builtin_amdgcn_div_fmasf(e3.x, r.x, q.x, f0), d.x, n.x);
+  out.y = __builtin_amdgcn_div_fixupf(__builtin_amdgcn_div_fmasf(e3.y, r.y, q.y, f1), d.y, n.y);
+  return out;
+}
+
+// Specialised binary operator over a lane's rows: A = A op B (SWAP: A = B op A).  Float32 + - * /
+// run on packed row pairs (v_pk_add_f32 / v_pk_mul_f32, div2_dev: each lane rounded exactly as
+// the scalar instruction would); the rest row by row.
+typedef F2 PkF32;
 template <typename T, int SB> __device__ __attribute__((always_inline)) inline T sb_apply(T a, T b) {
   using O = OpsT<T>;
   switch (SB) {
@@ -300,13 +333,15 @@ template <typename T, int SB> __device__ __attribute__((always_inline)) inline T
 }
 template <typename T, int R, int SB, bool SWAP>
 __device__ __attribute__((always_inline)) inline void bin_rows(T (&A)[R], const T (&B)[R]) {
-  if constexpr (std::is_same<T, float>::value && R % 2 == 0 && (SB == SB_ADD || SB == SB_SUB || SB == SB_MUL)) {
+  if constexpr (std::is_same<T, float>::value && R % 2 == 0 &&
+                (SB == SB_ADD || SB == SB_SUB || SB == SB_MUL || SB == SB_DIV)) {
     UNR for (int r = 0; r < R; r += 2) {
       const PkF32 a = {A[r], A[r + 1]}, b = {B[r], B[r + 1]};
       PkF32 c;
       if constexpr (SB == SB_ADD) c = SWAP ? b + a : a + b;
       else if constexpr (SB == SB_SUB) c = SWAP ? b - a : a - b;
-      else c = SWAP ? b * a : a * b;
+      else if constexpr (SB == SB_MUL) c = SWAP ? b * a : a * b;
+      else c = SWAP ? div2_dev(b, a) : div2_dev(a, b);
       A[r] = c.x;
       A[r + 1] = c.y;
     }

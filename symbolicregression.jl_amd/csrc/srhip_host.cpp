@@ -719,7 +719,7 @@ int srhip::compile_program(srhip_program& P) {
   }
 }
 
-int srhip::upload_program(srhip_program& P) {
+int srhip::upload_program(srhip_program& P, bool sync) {
   HIP_TRY(hipSetDevice(P.ctx->device));
   HIP_TRY(P.d_code.ensure(P.code.size() * sizeof(Ins)));
   HIP_TRY(P.d_off.ensure(std::max<size_t>(1, P.prog_off.size()) * sizeof(int32_t)));
@@ -740,7 +740,7 @@ int srhip::upload_program(srhip_program& P) {
     HIP_TRY(hipMemcpyAsync(P.d_dmask.p, P.dmask.data(), P.dmask.size() * sizeof(uint64_t), hipMemcpyHostToDevice,
                            P.ctx->stream));
   }
-  HIP_TRY(hipStreamSynchronize(P.ctx->stream));
+  if (sync) HIP_TRY(hipStreamSynchronize(P.ctx->stream));
   return SRHIP_OK;
 }
 
@@ -1031,12 +1031,12 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   {
     std::lock_guard<std::mutex> g(P->ord_mu);
     if (P->ord_key[0] != L.groups || P->ord_key[1] != L.tpg || P->ord_key[2] != (int)use_d || P->ord_goff != goff) {
-      std::vector<int32_t> order = make_order(*P, live, goff, use_d);
+      std::vector<int32_t>& order = P->ord_host;  // lives in the program: the copy below is asynchronous
+      order = make_order(*P, live, goff, use_d);
       order.insert(order.end(), goff.begin(), goff.end());  // the group offsets follow the order
       HIP_TRY(P->d_order.ensure(order.size() * sizeof(int32_t)));
       HIP_TRY(hipMemcpyAsync(P->d_order.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                              ctx->stream));
-      HIP_TRY(hipStreamSynchronize(ctx->stream));  // the host vector dies here
       P->ord_key[0] = L.groups;
       P->ord_key[1] = L.tpg;
       P->ord_key[2] = (int)use_d;

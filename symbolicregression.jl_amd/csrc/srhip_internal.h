@@ -159,6 +159,7 @@ struct srhip_program {
   mutable std::mutex ord_mu;
   mutable int ord_key[3] = {-1, -1, -1};
   mutable std::vector<int32_t> ord_goff;  // group offsets of that plan (appended to d_order)
+  mutable std::vector<int32_t> ord_host;  // the uploaded order (kept alive: its copy is asynchronous)
   mutable srhip::DevBuf d_order;
   // gradient program (constants not folded, constant leaves carry their get_constants index);
   // compiled on first use by the constant-gradient path
@@ -192,7 +193,9 @@ struct LaunchPlan {
 int compile_program(srhip_program& P);       // eval program (+ invalidates the gradient program)
 extern thread_local double g_patch_scan_s, g_patch_copy_s;  // optimiser timing split (SRHIP_OPTIM_TIMING), per thread
 int compile_grad_program(srhip_program& P);  // gradient program, uploaded
-int upload_program(srhip_program& P);
+// sync = false: the copies stay queued on the context's stream (the caller's next evaluation, which
+// synchronises before returning, must follow before P's host code changes again)
+int upload_program(srhip_program& P, bool sync = true);
 int make_view(srhip_ctx* ctx, const srhip_dataset* ds, const int64_t* idx, int64_t nidx, bool need_y, View& v);
 int gathered_weight_sum(srhip_ctx* ctx, const srhip_dataset* ds, int64_t nidx, View& v);
 // ncols: feature (+ derived) columns staged; lds_budget: bytes of LDS a workgroup may use

@@ -154,7 +154,10 @@ static int eval_grad_body(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
   a.loss_p0 = loss->p0;
   a.weighted = weighted ? 1 : 0;
   a.max_steps = P->gmax_len;
+  HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));  // srhip_last_kernel_ms: this gradient kernel
   HIP_TRY(launch_grad(dtype, K, kt, a, dim3(L.nrb, L.groups), ctx->stream));
+  HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+  ctx->timed = true;
   HIP_TRY(launch_grad_reduce(dtype, kt, (const double*)ctx->g_slab.p, L.nrb, nch, (double*)ctx->g_red.p, ctx->stream));
   std::vector<double> red((size_t)nch * (kt + 2));
   HIP_TRY(hipMemcpyAsync(red.data(), ctx->g_red.p, red.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));

@@ -5,7 +5,9 @@ device build has).  Single-operator trees exp / log / sin / cos / tan run throug
 srhip_eval_predict (the interpreter and, for U(x1), the derived-column path) on >= 1e6 inputs per
 (operator, type) -- ordinary, huge and special arguments -- and are compared with glibc through
 numpy (Float64: <= 1 ULP, tan <= 2) and with mpmath's correctly rounded value (Float32: <= 1 ULP,
-< 1 % of inputs differing), the bounds tests/test_math_accuracy.py asserts for the CPU build.
+< 1 % of inputs differing; exp, Julia's 1-ULP Float32 algorithm: < 15 %), the bounds
+tests/test_math_accuracy.py asserts for the CPU build.  test_device_float32_exp_bits_equal_oracle
+compares the device's packed exp with the oracle's scalar one bit for bit.
 """
 import numpy as np
 import pytest
@@ -79,11 +81,13 @@ def test_device_float64_within_ulp_of_glibc(ctx, name):
 def test_device_float32_vs_correctly_rounded(ctx, name):
     x = _inputs32(name)
     got = _device(ctx, name, x)
-    # every input against glibc in Float64 rounded once (itself within 1/2 ULP + 2^-52 relative)
+    # every input against glibc in Float64 rounded once (itself within 1/2 ULP + 2^-52 relative);
+    # exp is Julia's 1-ULP Float32 algorithm (~8 % of these arguments round the other way)
+    differ = 0.15 if name == "exp" else 0.01
     ref = getattr(np, name)(x.astype(np.float64)).astype(np.float32)
     u = _ulps32(got, ref)
     assert u.max() <= 1, (name, x[np.argmax(u)])
-    assert np.mean(u > 0) < 0.01, np.mean(u > 0)
+    assert np.mean(u > 0) < differ, np.mean(u > 0)
     # a sample against the correctly rounded value (mpmath, 200 bits)
     mpmath.mp.prec = 200
     idx = RNG.choice(len(x), 4000, replace=False)
@@ -91,7 +95,7 @@ def test_device_float32_vs_correctly_rounded(ctx, name):
     cr = np.array([float(fn(mpmath.mpf(float(v)))) for v in x[idx]]).astype(np.float32)
     u = _ulps32(got[idx], cr)
     assert u.max() <= 1, (name, x[idx][np.argmax(u)])
-    assert np.mean(u > 0) < 0.01
+    assert np.mean(u > 0) < differ
 
 
 def test_device_special_values(ctx):
@@ -111,3 +115,14 @@ def test_device_special_values(ctx):
         tiny = np.array([np.finfo(dt).tiny, np.finfo(dt).tiny / 4, -np.finfo(dt).tiny / 4], dtype=dt)
         for name in ("sin", "tan"):
             assert np.array_equal(_device(ctx, name, tiny), tiny)  # sin x = x for subnormal / tiny x
+
+
+def test_device_float32_exp_bits_equal_oracle(ctx, oracle):
+    """The packed device exp (srhip_eval.hip expf2_dev) returns the oracle's srm_expf bits on 16.7M
+    inputs: every 256th bit pattern of the whole float range (all exponents, both signs, NaN / Inf)."""
+    x = (np.arange(0, 2**32, 256, dtype=np.uint64).astype(np.uint32)).view(np.float32)
+    got = _device(ctx, "exp", x)
+    ref = oracle.srm("exp", x)
+    nan = np.isnan(x)
+    assert np.array_equal(np.isnan(got), nan)
+    assert np.array_equal(got[~nan].view(np.uint32), ref[~nan].view(np.uint32))

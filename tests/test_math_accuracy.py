@@ -1,5 +1,6 @@
 """Pins the shared scalar libm (include/srhip_math.h) that the device kernels and the oracle both
-use for exp / log / sin / cos / tan (see DESIGN.md "transcendentals").
+use for exp / log / sin / cos / tan (see DESIGN.md "transcendentals").  Float32 exp is Julia's own
+Float32 algorithm (1 ULP); the others widen to Float64.
 
 The reference evaluates these with Julia Base.Math (fdlibm / FreeBSD msun lineage; not available
 here), so the pin is accuracy, not bits: against glibc (Float64, <= 1 ULP; tan <= 2) and against
@@ -122,6 +123,13 @@ F32_CASES = {
 }
 
 
+# share of inputs allowed to differ from the correctly rounded value: sin / cos / tan / log evaluate in
+# Float64 and round once (~correctly rounded); exp is Julia's Float32 algorithm (exp_impl(::Float32)),
+# a 1-ULP algorithm: ~8 % of arguments in [-104, 89] round the other way (0.36 % of all 2^32 inputs,
+# tools/check_expf.c)
+F32_DIFFER = {"exp": 0.15}
+
+
 @pytest.mark.parametrize("name", list(F32_CASES))
 def test_float32_vs_correctly_rounded(oracle, name):
     mpmath.mp.prec = 200
@@ -131,7 +139,26 @@ def test_float32_vs_correctly_rounded(oracle, name):
     cr = np.array([float(fn(mpmath.mpf(float(v)))) for v in x]).astype(np.float32)
     u = _ulps32(got, cr)
     assert u.max() <= 1, (name, x[np.argmax(u)])
-    assert np.mean(u > 0) < 0.01, np.mean(u > 0)
+    assert np.mean(u > 0) < F32_DIFFER.get(name, 0.01), np.mean(u > 0)
+
+
+def test_float32_exp_is_julias_algorithm(oracle):
+    """srm_expf restates Julia's exp_impl(x::Float32): exact at 0, the Inf / 0 thresholds at
+    MAX_EXP = 88.72284f0 / MIN_EXP = -103.97208f0, subnormal results rounded once, and the
+    exhaustive 2^32-input property (max 1 ULP) re-checked on a dense sample here."""
+    f = lambda v: oracle.srm("exp", np.array(v, dtype=np.float32))  # noqa: E731
+    assert f([0.0, -0.0])[0] == 1.0 and f([0.0, -0.0])[1] == 1.0
+    lo = np.float32(88.72284)
+    # exp(88.72284f0) already rounds past floatmax: the float just below is the last finite one
+    assert np.isinf(f([np.nextafter(lo, np.float32(np.inf))])[0]) and np.isinf(f([lo])[0])
+    assert np.isfinite(f([np.nextafter(lo, np.float32(-np.inf))])[0])
+    mn = np.float32(-103.97208)
+    assert f([np.nextafter(mn, np.float32(-np.inf))])[0] == 0.0
+    sub = f(np.linspace(-103.9, -87.4, 20001, dtype=np.float32))
+    ref = np.exp(np.linspace(-103.9, -87.4, 20001, dtype=np.float32).astype(np.float64)).astype(np.float32)
+    assert _ulps32(sub, ref).max() <= 1
+    x = np.random.default_rng(5).uniform(-104, 89, 2_000_000).astype(np.float32)
+    assert _ulps32(oracle.srm("exp", x), np.exp(x.astype(np.float64)).astype(np.float32)).max() <= 1
 
 
 @pytest.mark.parametrize("name", list(F32_CASES))
@@ -141,4 +168,4 @@ def test_float32_vs_glibc_widened_large_sample(oracle, name):
     ref = getattr(np, name)(x.astype(np.float64)).astype(np.float32)
     u = _ulps32(got, ref)
     assert u.max() <= 1
-    assert np.mean(u > 0) < 0.01
+    assert np.mean(u > 0) < F32_DIFFER.get(name, 0.01)
