@@ -80,16 +80,19 @@ def _backtracking(phi, phi0, dphi0, c1=1e-4, rho_hi=0.5, rho_lo=0.1, iterations=
         if it > iterations:
             return None, None
         if it == 1:
-            a_tmp = -(dphi0 * a2 ** 2) / (2 * (phix1 - phi0 - dphi0 * a2))
+            with np.errstate(all="ignore"):
+                a_tmp = -(dphi0 * a2 ** 2) / np.float64(2 * (phix1 - phi0 - dphi0 * a2))
         else:
-            div = 1.0 / (a1 ** 2 * a2 ** 2 * (a2 - a1))
+            with np.errstate(all="ignore"):  # IEEE like Julia: a1 == a2 (alpha underflowed) gives Inf / NaN
+                div = np.float64(1.0) / np.float64(a1 ** 2 * a2 ** 2 * (a2 - a1))
             e1, e0 = phix1 - phi0 - dphi0 * a2, phix0 - phi0 - dphi0 * a1
             a = (a1 ** 2 * e1 - a2 ** 2 * e0) * div
             b = (-a1 ** 3 * e1 + a2 ** 3 * e0) * div
-            if abs(a) <= np.finfo(float).eps:
-                a_tmp = dphi0 / (2 * b)
-            else:
-                a_tmp = (-b + np.sqrt(max(b * b - 3 * a * dphi0, 0.0))) / (3 * a)
+            with np.errstate(all="ignore"):
+                if abs(a) <= np.finfo(float).eps:
+                    a_tmp = np.float64(dphi0) / np.float64(2 * b)
+                else:
+                    a_tmp = (-b + np.sqrt(max(b * b - 3 * a * dphi0, 0.0))) / np.float64(3 * a)
         a1 = a2
         a_tmp = a2 * rho_hi if np.isnan(a_tmp) else min(a_tmp, a2 * rho_hi)
         a2 = max(a_tmp, a2 * rho_lo)

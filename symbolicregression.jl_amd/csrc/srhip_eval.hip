@@ -672,6 +672,11 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
         }
       }
     }
+    // loss slab layout [row block][order slot][chunk of the block] (p.cpb chunks per block): a
+    // workgroup's partials are one contiguous range (its group's slots), so L2 lines fill before
+    // write-back
+    LAccT<T>* lslab = reinterpret_cast<LAccT<T>*>(p.slab_loss) +
+                      ((int64_t)rb * p.ntrees + group_base + ti) * __builtin_amdgcn_readfirstlane(p.cpb);
     for (int tile = 0; tile < ntiles; ++tile) {
       const int64_t row0 = row_base + (int64_t)tile * TILE;
       if (row0 >= p.nvalid) break;  // whole tile is padding
@@ -787,7 +792,7 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
         static_assert(CH % TILE == 0, "a loss chunk is whole tiles");
         if ((tile + 1) % (CH / TILE) == 0 || row0 + TILE >= p.nvalid) {  // chunk done (or last valid tile)
           const LAccT<T> s = wave_sum(lacc);
-          if (lane == WAVE_LAST) reinterpret_cast<LAccT<T>*>(p.slab_loss)[(int64_t)tree * p.nch + row0 / CH] = s;
+          if (lane == WAVE_LAST) lslab[tile / (CH / TILE)] = s;
           lacc = 0;
         }
       } else if constexpr (MODE == MODE_PRED) {
@@ -800,7 +805,7 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
     // ---- wave reduction, one partial per (tree, row block) ----
     if constexpr (!kIsInt<T> && MODE != MODE_PRECISE) {
       M = wave_chk(M);
-      if (lane == WAVE_LAST) reinterpret_cast<CT*>(p.slab_chk)[(int64_t)tree * p.nrb + rb] = M;
+      if (lane == WAVE_LAST) reinterpret_cast<CT*>(p.slab_chk)[(int64_t)rb * p.ntrees + group_base + ti] = M;
     }
     KMARK(8 + wave, 13);
     int claim = 0;
@@ -810,22 +815,25 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
   KMARK(8 + wave, 14);
 }
 
-// Per-tree reduction of the (tree, row block) partials, fixed order (deterministic).
-// One wavefront per tree.
+// Per-tree reduction of the partials, fixed order (deterministic): one wavefront per order slot
+// (slab layout of eval_kernel: loss [row block][slot][chunk of the block], check [row block][slot]);
+// the loss chunks are summed in chunk order c = 0.. nch-1 (lane-strided, then a fixed shuffle tree),
+// whatever the launch's row-block size; results land at the slot's tree index order[slot].
 template <typename LT, typename CT, bool CHK_MAX>
-__global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab_loss, int nch,
-                                                     const CT* __restrict__ slab_chk, int nrb, int ntrees,
-                                                     LT* __restrict__ out_loss, CT* __restrict__ out_chk) {
+__global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab_loss, int nch, int cpb,
+                                                     const CT* __restrict__ slab_chk, int nrb, int nslots,
+                                                     const int32_t* __restrict__ order, LT* __restrict__ out_loss,
+                                                     CT* __restrict__ out_chk) {
   const int lane = threadIdx.x & 63;
-  const int tree = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-  if (tree >= ntrees) return;
+  const int slot = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (slot >= nslots) return;
   LT s = 0;
   CT m = 0;
   if (slab_loss)
-    for (int i = lane; i < nch; i += 64) s += slab_loss[(int64_t)tree * nch + i];
+    for (int c = lane; c < nch; c += 64) s += slab_loss[((int64_t)(c / cpb) * nslots + slot) * cpb + c % cpb];
   for (int i = lane; i < nrb; i += 64) {
     if (slab_chk) {
-      const CT v = slab_chk[(int64_t)tree * nrb + i];
+      const CT v = slab_chk[(int64_t)i * nslots + slot];
       if constexpr (CHK_MAX) m = __builtin_elementwise_maximum(m, v); else m += v;
     }
   }
@@ -835,6 +843,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab
     else m += __shfl_xor(m, o);
   }
   if (lane == 0) {
+    const int tree = order[slot];
     if (out_loss) out_loss[tree] = s;
     if (out_chk) out_chk[tree] = m;
   }
@@ -968,21 +977,21 @@ hipError_t launch_eval(int dtype, const EvalArgs& a, int R, int K, int mode, boo
   }
 }
 
-hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, const void* slab_chk, int nrb, int ntrees, void* out_loss,
-                         void* out_chk, hipStream_t s) {
-  dim3 grid((ntrees + 3) / 4), block(256);
+hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, int cpb, const void* slab_chk, int nrb, int nslots,
+                         const int32_t* order, void* out_loss, void* out_chk, hipStream_t s) {
+  dim3 grid((nslots + 3) / 4), block(256);
   switch (dtype) {
     case SRHIP_F32:
-      hipLaunchKernelGGL((reduce_kernel<double, float, true>), grid, block, 0, s, (const double*)slab_loss, nch,
-                         (const float*)slab_chk, nrb, ntrees, (double*)out_loss, (float*)out_chk);
+      hipLaunchKernelGGL((reduce_kernel<double, float, true>), grid, block, 0, s, (const double*)slab_loss, nch, cpb,
+                         (const float*)slab_chk, nrb, nslots, order, (double*)out_loss, (float*)out_chk);
       break;
     case SRHIP_F64:
-      hipLaunchKernelGGL((reduce_kernel<double, double, false>), grid, block, 0, s, (const double*)slab_loss, nch,
-                         (const double*)slab_chk, nrb, ntrees, (double*)out_loss, (double*)out_chk);
+      hipLaunchKernelGGL((reduce_kernel<double, double, false>), grid, block, 0, s, (const double*)slab_loss, nch, cpb,
+                         (const double*)slab_chk, nrb, nslots, order, (double*)out_loss, (double*)out_chk);
       break;
     case SRHIP_I32:
       hipLaunchKernelGGL((reduce_kernel<long long, float, true>), grid, block, 0, s, (const long long*)slab_loss, nch,
-                         (const float*)nullptr, nrb, ntrees, (long long*)out_loss, (float*)nullptr);
+                         cpb, (const float*)nullptr, nrb, nslots, order, (long long*)out_loss, (float*)nullptr);
       break;
     default: return hipErrorInvalidValue;
   }

@@ -583,13 +583,119 @@ int compile_grad_t(srhip_program& P) {
     P.gmax_len = std::max(P.gmax_len, gi.code_len);
     P.gmax_ops = std::max(P.gmax_ops, (int32_t)gi.op_sumcheck.size());
   }
+  // speculative slots: the constant-carrying instructions of every tree, and the region itself
+  P.gci_off.assign(P.ntrees + 1, 0);
+  P.gci.clear();
+  P.gspec_ok.assign(P.ntrees, 0);
+  P.gbase.assign(P.ntrees, TreeInfo());
+  for (int32_t t = 0; t < P.ntrees; ++t) {
+    const TreeInfo& gi = P.ginfo[t];
+    if (!gi.static_fail && gi.fill_consts.empty()) {
+      int32_t nc = 0;
+      for (int32_t i = 0; i < gi.code_len; ++i) {
+        const Ins& ins = P.gcode[(size_t)gi.code_begin + i];
+        bool carries = ins.h == H_LOADC || (ins.h >= H_SLOADC0 && ins.h < H_SLOADC0 + K_MAX);
+        if (ins.h >= H_BIN0 && ins.h < H_HEAVY0) {
+          const uint32_t form = (ins.h - H_BIN0) % SPEC_STRIDE;
+          carries = form == SPEC_AC || form == SPEC_CA;
+        }
+        if (!carries) continue;
+        P.gci.push_back(i);
+        P.gci.push_back((int32_t)(ins.a & 0xffff));
+        ++nc;
+      }
+      // every constant leaf is consumed by exactly one such instruction
+      P.gspec_ok[t] = nc == gi.nconst;
+      if (P.gspec_ok[t]) P.gbase[t] = gi;
+      else P.gci.resize(P.gci_off[t]);
+    }
+    P.gci_off[t + 1] = (int32_t)P.gci.size();
+  }
+  P.gspec_alloc = P.gspec_cap;
+  P.gspec_stride = std::max<int32_t>(1, P.gmax_len);
+  P.gspec_base = (int64_t)P.gcode.size();
+  P.gcode.resize(P.gcode.size() + (size_t)P.gspec_alloc * P.gspec_stride, Ins{H_END, 0, 0});
+  for (int32_t sl = 0; sl < P.gspec_alloc; ++sl) {
+    P.gprog_off.push_back((int32_t)(P.gspec_base + (int64_t)sl * P.gspec_stride));
+    TreeInfo si;
+    si.static_fail = true;
+    si.code_begin = P.gprog_off.back();
+    si.code_len = 1;
+    P.ginfo.push_back(si);
+  }
   return SRHIP_OK;
 }
 
-void grad_snapshot(const srhip_program& P, std::vector<double>& out) {
-  out.clear();
-  for (const srhip_node& n : P.nodes)
-    if (n.degree == 0 && n.constant) out.push_back(n.val);
+template <typename T>
+bool spec_instantiate_t(srhip_program& P, int32_t slot, int32_t t, const double* c, bool* static_fail, int64_t& lo,
+                        int64_t& hi) {
+  if (slot < 0 || slot >= P.gspec_alloc || t < 0 || t >= P.ntrees || P.gspec_ok.size() != (size_t)P.ntrees)
+    return false;
+  TreeInfo& si = P.ginfo[(size_t)P.ntrees + slot];
+  const int64_t dst = P.gspec_base + (int64_t)slot * P.gspec_stride;
+  if (!P.gspec_ok[t]) {
+    // constant subtrees fold and fail by value: compile the tree at these constants
+    const int64_t b = P.offsets[t], e = P.offsets[t + 1];
+    std::vector<srhip_node> nd(P.nodes.begin() + b, P.nodes.begin() + e);
+    const double* cp = c;
+    struct Rec {
+      static void set(std::vector<srhip_node>& v, int64_t i, const double*& c) {
+        srhip_node& n = v[(size_t)i];
+        if (n.degree == 0) {
+          if (n.constant) n.val = *c++;
+          return;
+        }
+        set(v, n.l, c);
+        if (n.degree == 2) set(v, n.r, c);
+      }
+    };
+    Rec::set(nd, 0, cp);
+    std::vector<Ins> scratch;
+    TreeCompiler<T> tc(nd.data(), e - b, P, 0, true);
+    TreeInfo gi;
+    if (tc.compile(gi, scratch)) return false;
+    *static_fail = gi.static_fail;
+    if (!gi.static_fail) {
+      if (gi.code_len > P.gspec_stride || (size_t)gi.code_len != scratch.size()) return false;
+      std::copy(scratch.begin(), scratch.end(), P.gcode.begin() + dst);
+      lo = std::min<int64_t>(lo, dst);
+      hi = std::max<int64_t>(hi, dst + gi.code_len);
+    }
+    si = std::move(gi);
+    si.code_begin = (int32_t)dst;
+    if (si.static_fail) si.code_len = 1;
+    return true;
+  }
+  const TreeInfo& base = P.gbase[t];
+  if (base.code_len > P.gspec_stride) return false;
+  bool fin = true;
+  for (int32_t k = 0; k < base.nconst; ++k) fin &= m_isfinite(HostVal<T>::from(c[k]));
+  *static_fail = !fin;
+  if (!fin) {  // @return_on_check: did_succeed = false, nothing to evaluate
+    si = TreeInfo();
+    si.static_fail = true;
+    si.code_begin = (int32_t)dst;
+    si.code_len = 1;
+    return true;
+  }
+  std::copy(P.gcode.begin() + base.code_begin, P.gcode.begin() + base.code_begin + base.code_len, P.gcode.begin() + dst);
+  for (int32_t j = P.gci_off[t]; j < P.gci_off[t + 1]; j += 2)
+    P.gcode[(size_t)dst + P.gci[j]].imm = HostVal<T>::bits(HostVal<T>::from(c[P.gci[j + 1]]));
+  si = base;
+  si.code_begin = (int32_t)dst;
+  lo = std::min<int64_t>(lo, dst);
+  hi = std::max<int64_t>(hi, dst + base.code_len);
+  return true;
+}
+
+void grad_snapshot(srhip_program& P) {
+  P.gsnap.clear();
+  P.gsnap_off.assign(P.ntrees + 1, 0);
+  for (int32_t t = 0; t < P.ntrees; ++t) {
+    for (int64_t i = P.offsets[t]; i < P.offsets[t + 1]; ++i)
+      if (P.nodes[(size_t)i].degree == 0 && P.nodes[(size_t)i].constant) P.gsnap.push_back(P.nodes[(size_t)i].val);
+    P.gsnap_off[t + 1] = (int64_t)P.gsnap.size();
+  }
 }
 
 // Recompile in place only the trees whose constant values differ (bitwise) from the snapshot the
@@ -601,17 +707,30 @@ int patch_grad_t(srhip_program& P, bool& patched, int64_t& lo, int64_t& hi) {
   patched = false;
   lo = INT64_MAX;
   hi = -1;
-  if (P.gsnap.empty() || P.gprog_off.size() != (size_t)P.ntrees || P.ginfo.size() != (size_t)P.ntrees) return SRHIP_OK;
+  const size_t nslots = (size_t)P.ntrees + P.gspec_alloc;
+  if (P.gsnap.empty() || P.gprog_off.size() != nslots || P.ginfo.size() != nslots ||
+      P.gsnap_off.size() != (size_t)P.ntrees + 1 || (size_t)P.gsnap_off[P.ntrees] != P.gsnap.size() ||
+      P.gspec_cap != P.gspec_alloc)
+    return SRHIP_OK;
   std::vector<Ins> scratch;
-  size_t k = 0;
-  for (int32_t t = 0; t < P.ntrees; ++t) {
+  // the trees the optimiser wrote constants of (P.ghint), or all of them
+  std::vector<int32_t> all;
+  if (P.ghint.empty()) {
+    all.resize(P.ntrees);
+    for (int32_t t = 0; t < P.ntrees; ++t) all[t] = t;
+  }
+  const std::vector<int32_t>& scan = P.ghint.empty() ? all : P.ghint;
+  for (int32_t t : scan) {
+    if (t < 0 || t >= P.ntrees) return SRHIP_OK;
     const int64_t b = P.offsets[t], e = P.offsets[t + 1];
     bool dirty = false;
+    int64_t k = P.gsnap_off[t];
     for (int64_t i = b; i < e; ++i) {
       const srhip_node& n = P.nodes[(size_t)i];
       if (n.degree != 0 || !n.constant) continue;
-      if (k >= P.gsnap.size()) return SRHIP_OK;
-      dirty |= memcmp(&n.val, &P.gsnap[k++], sizeof(double)) != 0;
+      if (k >= P.gsnap_off[t + 1]) return SRHIP_OK;
+      dirty |= memcmp(&n.val, &P.gsnap[k], sizeof(double)) != 0;
+      P.gsnap[k++] = n.val;  // the snapshot follows the patch (this tree recompiles below if dirty)
     }
     if (!dirty) continue;
     scratch.clear();
@@ -636,7 +755,6 @@ int patch_grad_t(srhip_program& P, bool& patched, int64_t& lo, int64_t& hi) {
     gi.code_begin = old.code_begin;
     old = std::move(gi);
   }
-  if (k != P.gsnap.size()) return SRHIP_OK;
   P.gkmax = 0;
   P.gmax_len = 0;
   P.gmax_ops = 0;
@@ -655,6 +773,15 @@ thread_local double srhip::g_patch_scan_s = 0.0, srhip::g_patch_copy_s = 0.0;
 static double host_now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
+bool srhip::spec_instantiate(srhip_program& P, int32_t slot, int32_t t, const double* c, bool* static_fail,
+                             int64_t& lo, int64_t& hi) {
+  switch (P.dtype) {
+    case SRHIP_F32: return spec_instantiate_t<float>(P, slot, t, c, static_fail, lo, hi);
+    case SRHIP_F64: return spec_instantiate_t<double>(P, slot, t, c, static_fail, lo, hi);
+    default: return false;
+  }
+}
+
 int srhip::compile_grad_program(srhip_program& P) {
   if (P.grad_ready) return SRHIP_OK;
   static const bool no_patch = [] { const char* e = getenv("SRHIP_NO_GRAD_PATCH"); return e && *e && *e != '0'; }();
@@ -671,9 +798,9 @@ int srhip::compile_grad_program(srhip_program& P) {
     g_patch_scan_s += host_now_s() - t_patch0;
     if (rc) return rc;
   }
-  if (patched) {  // the device copy differs only in [lo, hi)
+  P.ghint.clear();
+  if (patched) {  // the device copy differs only in [lo, hi); the snapshot was updated by the patch
     const double t_copy0 = host_now_s();
-    grad_snapshot(P, P.gsnap);
     HIP_TRY(hipSetDevice(P.ctx->device));
     if (hi > lo)
       HIP_TRY(hipMemcpyAsync((Ins*)P.d_gcode.p + lo, P.gcode.data() + lo, (size_t)(hi - lo) * sizeof(Ins),
@@ -691,7 +818,7 @@ int srhip::compile_grad_program(srhip_program& P) {
   }
   if (rc) return rc;
   if (!P.ctx) return fail(SRHIP_ERR_INVALID, "host-only program");
-  grad_snapshot(P, P.gsnap);
+  grad_snapshot(P);
   HIP_TRY(hipSetDevice(P.ctx->device));
   HIP_TRY(P.d_gcode.ensure(P.gcode.size() * sizeof(Ins)));
   HIP_TRY(P.d_goff.ensure(std::max<size_t>(1, P.gprog_off.size()) * sizeof(int32_t)));
@@ -706,6 +833,7 @@ int srhip::compile_grad_program(srhip_program& P) {
 
 int srhip::compile_program(srhip_program& P) {
   P.grad_ready = false;
+  P.ghint.clear();
   {
     std::lock_guard<std::mutex> g(P.ord_mu);  // costs and live trees change: new schedule
     P.ord_key[0] = P.ord_key[1] = P.ord_key[2] = -1;
@@ -1045,8 +1173,9 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     d_order = P->d_order.p;
   }
   const int nch = (int)((v.m + loss_chunk(dtype) - 1) / loss_chunk(dtype));
-  HIP_TRY(ctx->slab_loss.ensure((size_t)nt * nch * 8));
-  HIP_TRY(ctx->slab_chk.ensure((size_t)nt * L.nrb * 8));
+  const int cpb = L.rb_rows / loss_chunk(dtype);  // loss chunks per row block (row blocks are whole chunks)
+  HIP_TRY(ctx->slab_loss.ensure((size_t)nl * L.nrb * cpb * 8));
+  HIP_TRY(ctx->slab_chk.ensure((size_t)nl * L.nrb * 8));
   HIP_TRY(ctx->red_loss.ensure((size_t)nt * 8));
   HIP_TRY(ctx->red_chk.ensure((size_t)nt * 8));
   HIP_TRY(ctx->h_loss.ensure((size_t)nt * 8));
@@ -1070,6 +1199,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   a.rb_rows = L.rb_rows;
   a.nrb = L.nrb;
   a.nch = nch;
+  a.cpb = cpb;
   a.trees_per_group = L.tpg;
   a.group_off = (const int32_t*)d_order + nl;
   a.loss_kind = loss ? loss->kind : 0;
@@ -1117,9 +1247,10 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       }
     }
   }
-  HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, nch, dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p,
-                        L.nrb, nt, mode == MODE_LOSS ? ctx->red_loss.p : nullptr,
-                        dtype == SRHIP_I32 ? nullptr : ctx->red_chk.p, ctx->stream));
+  HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, nch, cpb,
+                        dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p, L.nrb, nl, (const int32_t*)d_order,
+                        mode == MODE_LOSS ? ctx->red_loss.p : nullptr, dtype == SRHIP_I32 ? nullptr : ctx->red_chk.p,
+                        ctx->stream));
   if (mode == MODE_LOSS)
     HIP_TRY(hipMemcpyAsync(ctx->h_loss.p, ctx->red_loss.p, (size_t)nt * 8, hipMemcpyDeviceToHost, ctx->stream));
   if (dtype != SRHIP_I32)

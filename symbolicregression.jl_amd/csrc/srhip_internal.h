@@ -172,6 +172,22 @@ struct srhip_program {
   // constant-leaf values (node storage order) the gradient program was last compiled with: when only
   // constants change (the optimiser's line search), just the trees whose constants moved recompile
   std::vector<double> gsnap;
+  std::vector<int64_t> gsnap_off;  // [ntrees] first snapshot entry of each tree
+  // trees whose constants were written since the last gradient compile/patch (set by the optimiser);
+  // empty = unknown, scan every tree.  Cleared by every full (re)compile.
+  std::vector<int32_t> ghint;
+  // Speculative slots of the gradient program (the optimiser's line searches): gspec_alloc copies of
+  // "a tree at other constants" after the trees' own code, gspec_stride instructions each, slot s at
+  // program index ntrees + s (gprog_off / ginfo).  A slot is instantiated from its tree's code by
+  // rewriting the constant immediates (gci: per tree, (instruction offset, constant index) pairs),
+  // for trees whose did_succeed metadata does not depend on the constants (gspec_ok: no operator
+  // over constants only) -- their TreeInfo is gbase's, failing statically iff a constant is
+  // non-finite.  gspec_cap is the optimiser's request; a full compile allocates it.
+  int32_t gspec_cap = 0, gspec_alloc = 0, gspec_stride = 0;
+  int64_t gspec_base = 0;
+  std::vector<int32_t> gci_off, gci;
+  std::vector<uint8_t> gspec_ok;
+  std::vector<srhip::TreeInfo> gbase;
 };
 
 namespace srhip {
@@ -193,6 +209,11 @@ struct LaunchPlan {
 int compile_program(srhip_program& P);       // eval program (+ invalidates the gradient program)
 extern thread_local double g_patch_scan_s, g_patch_copy_s;  // optimiser timing split (SRHIP_OPTIM_TIMING), per thread
 int compile_grad_program(srhip_program& P);  // gradient program, uploaded
+// Speculative slot `slot` := tree t at constants c[0 .. nconst) (get_constants order), host side;
+// false if the tree cannot be instantiated (gspec_ok).  *static_fail: a constant is non-finite in T
+// (no evaluation needed: did_succeed is false).  [lo, hi) grows by the instructions written.
+bool spec_instantiate(srhip_program& P, int32_t slot, int32_t t, const double* c, bool* static_fail, int64_t& lo,
+                      int64_t& hi);
 // sync = false: the copies stay queued on the context's stream (the caller's next evaluation, which
 // synchronises before returning, must follow before P's host code changes again)
 int upload_program(srhip_program& P, bool sync = true);

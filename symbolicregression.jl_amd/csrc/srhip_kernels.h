@@ -46,8 +46,9 @@ struct EvalArgs {
   const void* X;            // [>= nfeat][ld] SoA, padded (the first nfeat columns are staged)
   const void* y;            // [ld] (nullptr for prediction-only)
   const void* w;            // [ld] or nullptr
-  void* slab_loss;          // [ntrees][nch] loss partials per row chunk (double; int64 for Int32)
-  void* slab_chk;           // [ntrees][nrb] check partials (float max|v| / double sum|v|*2^-512)
+  void* slab_loss;          // [nrb][ntrees][rb_rows / loss chunk] loss partials per row chunk, by order slot
+                            // (double; int64 for Int32)
+  void* slab_chk;           // [nrb][ntrees] check partials by order slot (float max|v| / double sum|v|*2^-512)
   void* out_pred;           // [ntrees][nvalid] (MODE_PRED)
   void* slab_prec;          // [n][prec_stride][nrb] double (MODE_PRECISE)
   int64_t ld;               // padded rows of X / y / w
@@ -57,6 +58,7 @@ struct EvalArgs {
   int32_t rb_rows;          // rows per workgroup (multiple of 64*R)
   int32_t nrb;              // row blocks
   int32_t nch;              // loss chunks: ceil(nvalid / loss_chunk)
+  int32_t cpb;              // loss chunks per row block (rb_rows / loss_chunk)
   int32_t trees_per_group;  // trees per grid.y group (group_off == nullptr)
   const int32_t* group_off; // [grid.y + 1] first order slot of each group, or nullptr (uniform groups)
   int32_t loss_kind;
@@ -77,8 +79,10 @@ int rows_per_lane(int dtype);
 int pick_rows_per_lane(int dtype, int K, int mode, int64_t m);
 hipError_t launch_eval(int dtype, const EvalArgs& a, int R, int K, int mode, bool xlds, dim3 grid, size_t lds,
                        hipStream_t s);
-hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, const void* slab_chk, int nrb, int ntrees, void* out_loss,
-                         void* out_chk, hipStream_t s);
+// per-tree reduction of eval_kernel's slabs: nslots order slots, cpb loss chunks per row block, results
+// at out[order[slot]]
+hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, int cpb, const void* slab_chk, int nrb, int nslots,
+                         const int32_t* order, void* out_loss, void* out_chk, hipStream_t s);
 hipError_t launch_gather(int dtype, const void* X, const void* y, const void* w, int64_t ld_src, int nfeat,
                          const int64_t* idx, int64_t m, int64_t ld_dst, void* Xd, void* yd, void* wd, hipStream_t s);
 hipError_t launch_feature_stats(int dtype, const void* X, int64_t ld, int64_t m, int nfeat, FeatStat* out,

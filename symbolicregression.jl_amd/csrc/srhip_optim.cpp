@@ -27,6 +27,29 @@ using namespace srhip;
 
 namespace {
 
+// Launch geometry of the dual-number kernel: row blocks of a fixed size (SRHIP_GRAD_RB, default 256
+// rows = 4 tiles per wave, fewer for smaller datasets), independent of how many chunks a launch
+// carries -- a tree's per-block partial sums, and so its loss and gradient bits, depend on the dataset
+// alone -- and enough tree groups to fill the chip.  The optimiser's last rounds evaluate a handful
+// of trees: small blocks keep those launches short (many workgroups, each a few tiles deep).
+LaunchPlan grad_plan(const srhip_ctx* ctx, int64_t m, int32_t nchunks) {
+  static const int rb_env = [] { const char* e = getenv("SRHIP_GRAD_RB"); return e ? atoi(e) : 0; }();
+  int rb = (rb_env >= 64 && rb_env <= 4096 && (rb_env & (rb_env - 1)) == 0) ? rb_env : 256;
+  m = std::max<int64_t>(1, m);
+  while (rb > 64 && rb / 2 >= m) rb /= 2;
+  LaunchPlan L{};
+  L.rb_rows = rb;
+  L.nrb = (int)((m + rb - 1) / rb);
+  L.xlds = false;
+  L.lds = 0;
+  const int target_blocks = 4 * ctx->num_cu;
+  int g = (target_blocks + L.nrb - 1) / L.nrb;
+  g = std::max(1, std::min(g, std::max(1, nchunks / (2 * GRAD_WAVES))));
+  L.tpg = (std::max(1, nchunks) + g - 1) / g;
+  L.groups = (std::max(1, nchunks) + L.tpg - 1) / L.tpg;
+  return L;
+}
+
 // constant offsets (get_constants order) of every tree: coff[t] .. coff[t+1]
 std::vector<int64_t> const_offsets(const srhip_program& P) {
   std::vector<int64_t> c(P.ntrees + 1, 0);
@@ -60,6 +83,7 @@ std::vector<double> get_all_consts(const srhip_program& P) {
 void set_all_consts(srhip_program& P, const double* c) {
   for (int32_t t = 0; t < P.ntrees; ++t) set_consts_rec(P.nodes.data() + P.offsets[t], 0, c);
   P.grad_ready = false;
+  P.ghint.clear();  // every tree may have changed
 }
 
 }  // namespace
@@ -69,30 +93,53 @@ void set_all_consts(srhip_program& P, const double* c) {
 // SRHIP_OPTIM_TIMING=1: host-side time split of the optimiser (compile/patch vs the rest), stderr
 static thread_local double g_t_compile = 0.0, g_t_eval = 0.0, g_t_host = 0.0;
 static thread_local int64_t g_n_launch = 0;
+static thread_local bool g_stats_on = false;
+static thread_local int64_t g_hist[5] = {0, 0, 0, 0, 0}, g_nonfinite_trials = 0;
+static thread_local int64_t g_spec_launched = 0, g_spec_used = 0;  // speculative trial points
 static double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-static int eval_grad_body(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
-                          const View& v, const std::vector<int32_t>& trees, const std::vector<int64_t>& coff, double* f,
-                          double* g, uint8_t* ok);
-// ok (nullable): did_succeed per tree (a tree can succeed with an overflowing loss: f = Inf, ok = 1)
+// One gradient evaluation of the launch: program slot `slot` (a tree, or a speculative slot holding
+// tree `tree` at other constants) -> f (+Inf where did_succeed fails), g[0 .. nconst of tree), ok.
+struct GradItem {
+  int32_t slot, tree;
+  double* f;
+  double* g;
+  uint8_t* ok;  // nullable
+};
+static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
+                           const View& v, const std::vector<GradItem>& items);
+// Loss and gradient for `trees` at the program's current constants: f[t], g[coff[t] ..], ok[t]
+// (nullable; did_succeed -- a tree can succeed with an overflowing loss: f = Inf, ok = 1), plus the
+// items in `extra` (speculative slots, already instantiated; their instructions [spec_lo, spec_hi)
+// are uploaded with the launch).
 static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss, const View& v,
                      const std::vector<int32_t>& trees, const std::vector<int64_t>& coff, double* f, double* g,
-                     uint8_t* ok = nullptr) {
+                     uint8_t* ok = nullptr, const std::vector<GradItem>* extra = nullptr, int64_t spec_lo = 0,
+                     int64_t spec_hi = -1) {
   const double t0 = now_s();
   int rc = compile_grad_program(*P);
   g_t_compile += now_s() - t0;
   g_n_launch += 1;
   if (rc) return rc;
-  rc = eval_grad_body(ctx, ds, P, loss, v, trees, coff, f, g, ok);
+  std::vector<GradItem> items;
+  items.reserve(trees.size() + (extra ? extra->size() : 0));
+  for (int32_t t : trees) items.push_back(GradItem{t, t, f + t, g + coff[t], ok ? ok + t : nullptr});
+  if (extra) items.insert(items.end(), extra->begin(), extra->end());
+  auto body = [&]() -> int {
+    if (spec_hi > spec_lo)
+      HIP_TRY(hipMemcpyAsync((Ins*)P->d_gcode.p + spec_lo, P->gcode.data() + spec_lo,
+                             (size_t)(spec_hi - spec_lo) * sizeof(Ins), hipMemcpyHostToDevice, ctx->stream));
+    return eval_grad_items(ctx, ds, P, loss, v, items);
+  };
+  rc = body();
   // a patched gradient program's upload (compile_grad_program) may still be in flight from P->gcode:
   // on an error return, drain the stream before the caller can destroy or recompile the program
   if (rc) (void)hipStreamSynchronize(ctx->stream);
   return rc;
 }
-static int eval_grad_body(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
-                          const View& v, const std::vector<int32_t>& trees, const std::vector<int64_t>& coff, double* f,
-                          double* g, uint8_t* ok) {
+static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
+                           const View& v, const std::vector<GradItem>& items) {
   const int dtype = P->dtype;
   const bool weighted = ds->weighted;
   const double wsum = weighted ? v.sum_w : (double)v.m;
@@ -101,25 +148,27 @@ static int eval_grad_body(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
   // transcendentals and derivative factors cost about three tangent updates).  Values and the
   // tangents of each constant do not depend on kt (independent components, same primal code).
   int64_t cost4 = 0, cost8 = 0;
-  for (int32_t t : trees) {
-    if (P->ginfo[t].static_fail) continue;
-    const int nc = std::max(P->info[t].nconst, 1);
+  for (const GradItem& it : items) {
+    if (P->ginfo[it.slot].static_fail) continue;
+    const int nc = std::max(P->info[it.tree].nconst, 1);
     cost4 += (int64_t)((nc + 3) / 4) * (3 + 4);
     cost8 += (int64_t)((nc + GRAD_KT - 1) / GRAD_KT) * (3 + GRAD_KT);
   }
   const char* kte = getenv("SRHIP_GRAD_KT");  // tuning / tests: force 4 or 8
   int kt = cost4 < cost8 ? 4 : GRAD_KT;
   if (kte && (atoi(kte) == 4 || atoi(kte) == GRAD_KT)) kt = atoi(kte);
-  std::vector<int32_t> chunks;
-  for (int32_t t : trees) {
-    f[t] = INFINITY;
-    if (ok) ok[t] = 0;
-    for (int64_t k = coff[t]; k < coff[t + 1]; ++k) g[k] = 0.0;
-    if (P->ginfo[t].static_fail) continue;
-    const int nc = P->info[t].nconst;
+  std::vector<int32_t> chunks, chunk_item;
+  for (size_t i = 0; i < items.size(); ++i) {
+    const GradItem& it = items[i];
+    *it.f = INFINITY;
+    if (it.ok) *it.ok = 0;
+    const int nc = P->info[it.tree].nconst;
+    for (int k = 0; k < nc; ++k) it.g[k] = 0.0;
+    if (P->ginfo[it.slot].static_fail) continue;
     for (int c0 = 0; c0 < std::max(nc, 1); c0 += kt) {
-      chunks.push_back(t);
+      chunks.push_back(it.slot);
       chunks.push_back(c0);
+      chunk_item.push_back((int32_t)i);
     }
   }
   const int nch = (int)chunks.size() / 2;
@@ -127,7 +176,7 @@ static int eval_grad_body(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return SRHIP_OK;
   }
-  LaunchPlan L = plan_launch(ctx, dtype, ds->nfeat, weighted, true, v.m, nch, 64);
+  const LaunchPlan L = grad_plan(ctx, v.m, nch);
   const int K = P->gkmax <= 4 ? 4 : 8;
   HIP_TRY(ctx->g_chunks.ensure(chunks.size() * sizeof(int32_t)));
   HIP_TRY(hipMemcpyAsync(ctx->g_chunks.p, chunks.data(), chunks.size() * sizeof(int32_t), hipMemcpyHostToDevice,
@@ -169,17 +218,21 @@ static int eval_grad_body(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
     sums[2 * (size_t)P->ntrees + 2 * fi + 1] = (double)v.stats[fi].nonfinite;
   }
   sums.back() = (double)v.m;
-  std::vector<int32_t> undecided;
+  std::vector<int32_t> undecided, undecided_item;
   for (int c = 0; c < nch; ++c) {
-    const int32_t t = chunks[2 * c], c0 = chunks[2 * c + 1];
+    const GradItem& it = items[chunk_item[c]];
+    const int32_t c0 = chunks[2 * c + 1];
     const double* r = red.data() + (size_t)c * (kt + 2);
-    const int nc = P->info[t].nconst;
-    for (int j = 0; j < kt && c0 + j < nc; ++j) g[coff[t] + c0 + j] = r[1 + j] / wsum;
+    const int nc = P->info[it.tree].nconst;
+    for (int j = 0; j < kt && c0 + j < nc; ++j) it.g[c0 + j] = r[1 + j] / wsum;
     if (c0 == 0) {
-      const int st = decide_tree(P->ginfo[t], *P, ds->nfeat, sums.data(), r[kt + 1]);
-      f[t] = st == 1 ? INFINITY : r[0] / wsum;
-      if (ok) ok[t] = st != 1;
-      if (st == 2) undecided.push_back(t);
+      const int st = decide_tree(P->ginfo[it.slot], *P, ds->nfeat, sums.data(), r[kt + 1]);
+      *it.f = st == 1 ? INFINITY : r[0] / wsum;
+      if (it.ok) *it.ok = st != 1;
+      if (st == 2) {
+        undecided.push_back(it.slot);
+        undecided_item.push_back(chunk_item[c]);
+      }
     }
   }
   // near-overflow sums: the exact per-operator-node pass on the gradient program decides, so the
@@ -190,8 +243,9 @@ static int eval_grad_body(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
     if (rc) return rc;
     for (size_t u = 0; u < undecided.size(); ++u)
       if (!uok[u]) {
-        f[undecided[u]] = INFINITY;
-        if (ok) ok[undecided[u]] = 0;
+        const GradItem& it = items[undecided_item[u]];
+        *it.f = INFINITY;
+        if (it.ok) *it.ok = 0;
       }
   }
   return SRHIP_OK;
@@ -229,6 +283,33 @@ double backtrack_step(LineSearch& s) {
   return std::max(a_tmp, s.a2 * rho_lo);
 }
 
+// one BackTracking step on phi(a2): LS_CONTINUE (next trial at the new a2), LS_ACCEPT, or a failure
+// that ends the start: LS_FAIL (iterations exhausted, LineSearchException) or LS_FAIL_NEGINF (the
+// slope overflowed to -Inf: phi0 + c1 a dphi0 = -Inf for every alpha > 0 the remaining iterations can
+// reach, so every further trial fails and BackTracking throws after exactly LS_ITERATIONS of them)
+enum { LS_CONTINUE = 0, LS_ACCEPT = 1, LS_FAIL = 2, LS_FAIL_NEGINF = 3 };
+int ls_update(LineSearch& L, double phi) {
+  L.phix1 = phi;
+  if (!L.armijo) {
+    if (!std::isfinite(phi) && L.iterfinite < LS_ITERFINITEMAX) {  // hard-coded halving until finite
+      L.iterfinite += 1;
+      L.a1 = L.a2;
+      L.a2 = L.a1 / 2.0;
+      return LS_CONTINUE;
+    }
+    L.armijo = true;
+  }
+  if (phi > L.phi0 + 1e-4 * L.a2 * L.dphi0) {  // sufficient decrease not met (or phi = Inf)
+    if (L.dphi0 == -INFINITY) return LS_FAIL_NEGINF;
+    if (++L.iter > LS_ITERATIONS) return LS_FAIL;
+    const double a2 = backtrack_step(L);
+    L.phix0 = L.phix1;
+    L.a2 = a2;
+    return LS_CONTINUE;
+  }
+  return LS_ACCEPT;
+}
+
 }  // namespace
 
 // All restarts of all trees as one pipelined batch.  Every tree runs its own state machine
@@ -247,6 +328,16 @@ double backtrack_step(LineSearch& s) {
 //   per iteration ("Hessian probes", not counted as objective calls, as Optim counts h_calls apart).
 // Both: BackTracking line search from alpha = 1 (InitialStatic), stop on |g|_inf <= g_tol, on an
 //   unchanged objective (f_reltol = x_abstol = 0) or after `iterations` iterations.
+//
+// Speculative trial points (SRHIP_OPTIM_SPEC slots, default 256, 0 = off): a line search whose last
+// trial was non-finite usually keeps failing for many trials (an overflowing direction halves alpha
+// ~50 times, then shrinks it in the Armijo phase until x + a s rounds back to x -- hundreds of
+// launches for one tree at the pipeline's tail).  While few trees are active, the launch also
+// evaluates, in spare program slots (the tree's code with its constant immediates rewritten), the
+// next points the tree's BackTracking would try if every pending trial came back non-finite.  After
+// the launch they are consumed in order for as long as the line search really asks for exactly that
+// alpha (same line search, bitwise-equal alpha), so every consumed result is the one the sequential
+// pipeline would have launched for: trajectories, outcomes and objective-call counts are unchanged.
 static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
                           const View& v, const std::vector<int32_t>& trees, const std::vector<int64_t>& coff,
                           int iterations, double g_tol, const std::vector<std::vector<double>>& starts,
@@ -264,6 +355,19 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
   std::vector<double> H(hoff.back(), 0.0);
   std::vector<int> phase(P->ntrees, DONE), start(P->ntrees, 0), iter(P->ntrees, 0);
   std::vector<LineSearch> ls(P->ntrees);
+  // consecutive non-finite trials of the current line search, and a line-search generation counter
+  std::vector<int> nfstreak(P->ntrees, 0);
+  std::vector<int64_t> lsgen(P->ntrees, 0);
+  // the last two finite trial points (alpha, phi) of the current line search, newest first: the
+  // speculation's model of phi along the search direction
+  struct Hist {
+    int n = 0;
+    double a[2], f[2];
+  };
+  std::vector<Hist> hist(P->ntrees);
+  // per-tree speculation depth: doubled while every speculative point of a launch is consumed,
+  // cut back to what was consumed (+1) after a misprediction
+  std::vector<int> sdepth(P->ntrees, 4);
   for (size_t k = 0; k < nall; ++k) xe[k] = best_x[k];
   auto newton = [&](int32_t t) { return coff[t + 1] - coff[t] == 1; };
   auto gnorm = [&](int32_t t, const std::vector<double>& gg) {
@@ -325,15 +429,116 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
     L.a1 = L.a2 = 1.0;  // InitialStatic: alpha = 1
     L.phix0 = L.phix1 = f[t];
     phase[t] = TRIAL;
+    nfstreak[t] = 0;
+    lsgen[t] += 1;
+    hist[t] = Hist();
   };
   auto next_iter = [&](int32_t t) {  // after an accepted step
     iter[t] += 1;
     if (newton(t) && iter[t] < iterations) begin_hess(t);
     else begin_iter(t);
   };
-  for (int32_t t : trees) begin_start(t);
   const char* tre = getenv("SRHIP_OPTIM_TRACE");
   const int trace_tree = tre && *tre ? atoi(tre) : -1;
+  // one evaluation result of tree t at the point xv: loss phi, gradient gv
+  auto consume = [&](int32_t t, double phi, const double* gv, const double* xv) {
+    const int64_t o = coff[t], n = coff[t + 1] - coff[t];
+    if (t == trace_tree) {  // SRHIP_OPTIM_TRACE=<tree>: every evaluation of one tree, stderr
+      fprintf(stderr, "[srhip optim] tree %d start %d iter %d phase %d a %.17g f %.17g x", t, start[t], iter[t],
+              phase[t], phase[t] == TRIAL ? ls[t].a2 : 0.0, phi);
+      for (int64_t k = 0; k < n; ++k) fprintf(stderr, " %.17g", xv[k]);
+      fprintf(stderr, " g");
+      for (int64_t k = 0; k < n; ++k) fprintf(stderr, " %.17g", gv[k]);
+      fprintf(stderr, "\n");
+    }
+    if (phase[t] == HESS_P) {
+      gplus[t] = std::isfinite(phi) ? gv[0] : NAN;
+      phase[t] = HESS_M;
+      return;
+    }
+    if (phase[t] == HESS_M) {
+      const double h = std::isfinite(phi) ? (gplus[t] - gv[0]) / (2.0 * hstep[t]) : NAN;
+      hcurv[t] = (std::isfinite(h) && h != 0.0) ? fabs(h) : 1.0;  // cholesky!(Positive, [h])
+      begin_iter(t);
+      return;
+    }
+    fcalls[t] += 1;
+    if (phase[t] == INIT) {
+      f[t] = phi;
+      for (int64_t k = 0; k < n; ++k) g[o + k] = gv[k];
+      iter[t] = 0;
+      if (!std::isfinite(f[t]) || gnorm(t, g) <= g_tol) finish_start(t);
+      else if (newton(t) && iterations > 0) begin_hess(t);
+      else begin_iter(t);
+      return;
+    }
+    if (g_stats_on && !std::isfinite(phi)) g_nonfinite_trials += 1;
+    LineSearch& L = ls[t];
+    if (std::isfinite(phi)) {
+      Hist& h = hist[t];
+      h.a[1] = h.a[0];
+      h.f[1] = h.f[0];
+      h.a[0] = L.a2;
+      h.f[0] = phi;
+      h.n = std::min(h.n + 1, 2);
+    }
+    switch (ls_update(L, phi)) {
+      case LS_CONTINUE: nfstreak[t] = std::isfinite(phi) ? 0 : nfstreak[t] + 1; return;
+      case LS_FAIL_NEGINF: fcalls[t] += LS_ITERATIONS - L.iter; finish_start(t); return;  // counted, not launched
+      case LS_FAIL: finish_start(t); return;  // LineSearchException: the start ends at its last accepted point
+      default: break;
+    }
+    if (!newton(t)) {
+      std::vector<double> dx(n), dg(n), u(n);
+      double dxdg = 0.0;
+      for (int64_t i = 0; i < n; ++i) {
+        dx[i] = L.a2 * s[o + i];
+        dg[i] = gv[i] - g[o + i];
+        dxdg += dx[i] * dg[i];
+      }
+      if (dxdg > 0.0) {
+        double dgu = 0.0;
+        for (int64_t i = 0; i < n; ++i) {
+          double acc = 0.0;
+          for (int64_t j = 0; j < n; ++j) acc += H[hoff[t] + i * n + j] * dg[j];
+          u[i] = acc;
+          dgu += dg[i] * acc;
+        }
+        const double c1 = (dxdg + dgu) / (dxdg * dxdg), c2 = 1.0 / dxdg;
+        for (int64_t i = 0; i < n; ++i)
+          for (int64_t j = 0; j < n; ++j)
+            H[hoff[t] + i * n + j] += c1 * dx[i] * dx[j] - c2 * (u[i] * dx[j] + dx[i] * u[j]);
+      }
+    }
+    const double fold = f[t];
+    for (int64_t k = 0; k < n; ++k) {
+      x[o + k] = xv[k];
+      g[o + k] = gv[k];
+    }
+    f[t] = phi;
+    if (phi == fold || gnorm(t, g) <= g_tol) finish_start(t);  // converged
+    else next_iter(t);
+  };
+  for (int32_t t : trees) begin_start(t);
+  const char* spe = getenv("SRHIP_OPTIM_SPEC");
+  // default 32 slots: a launch of a few trees is latency-bound (one tree x 100k rows fills ~5 % of
+  // the wave slots), so a few dozen extra points cost little; more only adds mispredicted work
+  const int spec_cap = spe && *spe ? std::max(0, std::min(atoi(spe), 4096)) : 32;
+  constexpr size_t SPEC_MAX_ACTIVE = 64;  // speculate only in the pipeline's tail
+  constexpr int SPEC_MAX_DEPTH = 64;
+  if (P->gspec_cap != spec_cap) {
+    P->gspec_cap = spec_cap;  // the next gradient compile allocates the slots (a full compile)
+    P->grad_ready = false;
+  }
+  struct Spec {
+    int32_t t, slot;
+    int64_t gen;
+    double alpha;
+    int64_t off;  // into sx / sg
+  };
+  std::vector<Spec> spec;
+  std::vector<double> sx, sg, sf;
+  std::vector<GradItem> sitems;
   std::vector<int32_t> act;
   for (;;) {
     act.clear();
@@ -355,98 +560,112 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
       const double* c = xe.data() + coff[t];
       set_consts_rec(P->nodes.data() + P->offsets[t], 0, c);
     }
+    // the patch scans just the trees whose constants moved (a union if an earlier hint is pending;
+    // no hint at all -- an unknown change -- keeps the full scan)
+    if (P->grad_ready) P->ghint = act;
+    else if (!P->ghint.empty()) P->ghint.insert(P->ghint.end(), act.begin(), act.end());
     P->grad_ready = false;
+    // speculative points of trees in a non-finite streak (instantiated after the compile / patch:
+    // a full compile resets the slot region)
+    spec.clear();
+    sitems.clear();
+    int64_t spec_lo = INT64_MAX, spec_hi = -1;
+    if (spec_cap > 0 && act.size() <= SPEC_MAX_ACTIVE) {
+      // a line search that has already failed twice is likely to keep backtracking
+      auto candidate = [&](int32_t t) {
+        return phase[t] == TRIAL && ls[t].iter + ls[t].iterfinite >= 2;
+      };
+      int ncand = 0;
+      for (int32_t t : act) ncand += candidate(t);
+      if (ncand > 0) {
+        const double tc = now_s();
+        int rc = compile_grad_program(*P);
+        g_t_compile += now_s() - tc;
+        if (rc) return rc;
+        int slot = 0;
+        int64_t off = 0;
+        for (int32_t t : act) {
+          const int depth = std::min(std::min(sdepth[t], SPEC_MAX_DEPTH), P->gspec_alloc - slot);
+          if (depth < 1 || !candidate(t)) continue;
+          // the line search run ahead on predicted values: non-finite again after a non-finite
+          // trial; otherwise phi(a) = phi0 + d (a / a_k)^q through the last two finite points (q = 2
+          // from one).  Only the alphas matter, and BackTracking's steps are mostly its clamps
+          // (0.5 or 0.1 of the last alpha), which a rough model reproduces bit for bit.
+          const Hist& h = hist[t];
+          const double phi0 = ls[t].phi0;
+          double q = 2.0;
+          if (h.n == 2 && h.f[0] > phi0 && h.f[1] > phi0 && h.a[0] != h.a[1] && h.a[0] > 0.0 && h.a[1] > 0.0)
+            q = log((h.f[1] - phi0) / (h.f[0] - phi0)) / log(h.a[1] / h.a[0]);
+          const bool model = nfstreak[t] == 0 && h.n > 0 && h.f[0] > phi0 && h.a[0] > 0.0 && std::isfinite(q);
+          if (nfstreak[t] == 0 && !model) continue;
+          LineSearch Ls = ls[t];
+          for (int j = 0; j < depth; ++j) {
+            const double phi_pred = model ? phi0 + (h.f[0] - phi0) * pow(Ls.a2 / h.a[0], q) : INFINITY;
+            if (ls_update(Ls, phi_pred) != LS_CONTINUE) break;
+            spec.push_back(Spec{t, slot++, lsgen[t], Ls.a2, off});
+            off += coff[t + 1] - coff[t];
+          }
+        }
+        sx.resize(off);
+        sg.resize(off);
+        sf.resize(spec.size());
+        size_t keep = 0;
+        int32_t dead = -1;  // a tree whose chain broke (slot instantiation refused): drop its rest
+        for (size_t i = 0; i < spec.size(); ++i) {
+          const Spec& q = spec[i];
+          if (q.t == dead) continue;
+          const int64_t o = coff[q.t], n = coff[q.t + 1] - o;
+          for (int64_t k = 0; k < n; ++k) sx[q.off + k] = x[o + k] + q.alpha * s[o + k];
+          bool sfail = false;
+          if (!spec_instantiate(*P, q.slot, q.t, sx.data() + q.off, &sfail, spec_lo, spec_hi)) {
+            dead = q.t;
+            continue;
+          }
+          spec[keep++] = q;
+        }
+        spec.resize(keep);
+        for (size_t i = 0; i < spec.size(); ++i)
+          sitems.push_back(GradItem{P->ntrees + spec[i].slot, spec[i].t, &sf[i], sg.data() + spec[i].off, nullptr});
+        g_spec_launched += (int64_t)spec.size();
+      }
+    }
     const double t1 = now_s();
-    int rc = eval_grad(ctx, ds, P, loss, v, act, coff, fe.data(), ge.data());
+    int rc = eval_grad(ctx, ds, P, loss, v, act, coff, fe.data(), ge.data(), nullptr, &sitems, spec_lo, spec_hi);
     if (rc) return rc;
+    if (g_stats_on)  // SRHIP_OPTIM_TIMING=2: launch-size histogram
+      g_hist[act.size() <= 1 ? 0 : act.size() <= 4 ? 1 : act.size() <= 16 ? 2 : act.size() <= 64 ? 3 : 4] += 1;
     const double t2 = now_s();
     g_t_host += t1 - t0;
     g_t_eval += t2 - t1;
+    size_t si = 0;
     for (int32_t t : act) {
       const int64_t o = coff[t];
-      if (t == trace_tree) {  // SRHIP_OPTIM_TRACE=<tree>: every evaluation of one tree, stderr
-        fprintf(stderr, "[srhip optim] tree %d start %d iter %d phase %d a %.17g f %.17g x", t, start[t], iter[t],
-                phase[t], phase[t] == TRIAL ? ls[t].a2 : 0.0, fe[t]);
-        for (int64_t k = o; k < coff[t + 1]; ++k) fprintf(stderr, " %.17g", xe[k]);
-        fprintf(stderr, " g");
-        for (int64_t k = o; k < coff[t + 1]; ++k) fprintf(stderr, " %.17g", ge[k]);
-        fprintf(stderr, "\n");
+      consume(t, fe[t], ge.data() + o, xe.data() + o);
+      // then t's speculative points, in order, while its line search asks for exactly them
+      int launched = 0, used = 0;
+      bool hit = true;
+      for (; si < spec.size() && spec[si].t == t; ++si) {
+        const Spec& q = spec[si];
+        launched += 1;
+        hit = hit && phase[t] == TRIAL && lsgen[t] == q.gen && memcmp(&ls[t].a2, &q.alpha, sizeof(double)) == 0;
+        if (!hit) continue;
+        consume(t, sf[si], sg.data() + q.off, sx.data() + q.off);
+        used += 1;
       }
-      if (phase[t] == HESS_P) {
-        gplus[t] = std::isfinite(fe[t]) ? ge[o] : NAN;
-        phase[t] = HESS_M;
-        continue;
+      if (launched > 0) {
+        g_spec_used += used;
+        // all used and still searching: go deeper; else keep what would have been used (+1)
+        sdepth[t] = used == launched && phase[t] == TRIAL ? std::min(2 * sdepth[t], SPEC_MAX_DEPTH)
+                                                          : std::max(1, std::min(sdepth[t], used + 1));
       }
-      if (phase[t] == HESS_M) {
-        const double h = std::isfinite(fe[t]) ? (gplus[t] - ge[o]) / (2.0 * hstep[t]) : NAN;
-        hcurv[t] = (std::isfinite(h) && h != 0.0) ? fabs(h) : 1.0;  // cholesky!(Positive, [h])
-        begin_iter(t);
-        continue;
-      }
-      fcalls[t] += 1;
-      if (phase[t] == INIT) {
-        f[t] = fe[t];
-        for (int64_t k = coff[t]; k < coff[t + 1]; ++k) g[k] = ge[k];
-        iter[t] = 0;
-        if (!std::isfinite(f[t]) || gnorm(t, g) <= g_tol) finish_start(t);
-        else if (newton(t) && iterations > 0) begin_hess(t);
-        else begin_iter(t);
-        continue;
-      }
-      LineSearch& L = ls[t];
-      const double phi = fe[t];
-      L.phix1 = phi;
-      if (!L.armijo) {
-        if (!std::isfinite(phi) && L.iterfinite < LS_ITERFINITEMAX) {  // hard-coded halving until finite
-          L.iterfinite += 1;
-          L.a1 = L.a2;
-          L.a2 = L.a1 / 2.0;
-          continue;
-        }
-        L.armijo = true;
-      }
-      if (phi > L.phi0 + 1e-4 * L.a2 * L.dphi0) {  // sufficient decrease not met (or phi = Inf)
-        if (++L.iter > LS_ITERATIONS) {
-          finish_start(t);  // LineSearchException: this start ends at its last accepted point
-          continue;
-        }
-        const double a2 = backtrack_step(L);
-        L.phix0 = L.phix1;
-        L.a2 = a2;
-        continue;
-      }
-      const int64_t n = coff[t + 1] - coff[t];
-      if (!newton(t)) {
-        std::vector<double> dx(n), dg(n), u(n);
-        double dxdg = 0.0;
-        for (int64_t i = 0; i < n; ++i) {
-          dx[i] = L.a2 * s[o + i];
-          dg[i] = ge[o + i] - g[o + i];
-          dxdg += dx[i] * dg[i];
-        }
-        if (dxdg > 0.0) {
-          double dgu = 0.0;
-          for (int64_t i = 0; i < n; ++i) {
-            double acc = 0.0;
-            for (int64_t j = 0; j < n; ++j) acc += H[hoff[t] + i * n + j] * dg[j];
-            u[i] = acc;
-            dgu += dg[i] * acc;
-          }
-          const double c1 = (dxdg + dgu) / (dxdg * dxdg), c2 = 1.0 / dxdg;
-          for (int64_t i = 0; i < n; ++i)
-            for (int64_t j = 0; j < n; ++j)
-              H[hoff[t] + i * n + j] += c1 * dx[i] * dx[j] - c2 * (u[i] * dx[j] + dx[i] * u[j]);
-        }
-      }
-      const double fold = f[t];
-      for (int64_t k = o; k < o + n; ++k) {
-        x[k] = xe[k];
-        g[k] = ge[k];
-      }
-      f[t] = phi;
-      if (phi == fold || gnorm(t, g) <= g_tol) finish_start(t);  // converged
-      else next_iter(t);
     }
+  }
+  if (g_stats_on) {  // the trees with the most objective calls (the pipeline's tail)
+    std::vector<int32_t> by(trees);
+    std::sort(by.begin(), by.end(), [&](int32_t a, int32_t b) { return fcalls[a] > fcalls[b]; });
+    for (size_t i = 0; i < by.size() && i < 4; ++i)
+      fprintf(stderr, "srhip optim: tree %d: %lld objective calls, %d constants\n", by[i], (long long)fcalls[by[i]],
+              (int)(coff[by[i] + 1] - coff[by[i]]));
   }
   return SRHIP_OK;
 }
@@ -522,7 +741,7 @@ int srhip_eval_grad_predict(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progr
     DevBuf der;
     HIP_TRY(der.ensure((size_t)nrows_out * m * es));
     if (nch > 0) {
-      LaunchPlan L = plan_launch(ctx, P->dtype, ds->nfeat, false, false, m, nch, 64);
+      const LaunchPlan L = grad_plan(ctx, m, nch);
       HIP_TRY(ctx->g_chunks.ensure(chunks.size() * sizeof(int32_t)));
       HIP_TRY(hipMemcpyAsync(ctx->g_chunks.p, chunks.data(), chunks.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                              ctx->stream));
@@ -615,9 +834,18 @@ int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_prog
     g_t_compile = g_t_eval = g_t_host = 0.0;
     g_patch_scan_s = g_patch_copy_s = 0.0;
     g_n_launch = 0;
-    rc = bfgs_pipelined(ctx, ds, P, loss, v, trees, coff, opt->iterations, g_tol, starts, best_x, best_f, fcalls);
     const char* te = getenv("SRHIP_OPTIM_TIMING");
-    if (te && *te == '1')
+    g_stats_on = te && *te == '2';
+    for (int64_t& h : g_hist) h = 0;
+    g_nonfinite_trials = 0;
+    g_spec_launched = g_spec_used = 0;
+    rc = bfgs_pipelined(ctx, ds, P, loss, v, trees, coff, opt->iterations, g_tol, starts, best_x, best_f, fcalls);
+    if (g_stats_on)
+      fprintf(stderr, "srhip optim: launches by active trees: 1: %lld, 2-4: %lld, 5-16: %lld, 17-64: %lld, >64: %lld; "
+              "non-finite trial points %lld; speculative points %lld evaluated, %lld used\n", (long long)g_hist[0],
+              (long long)g_hist[1], (long long)g_hist[2], (long long)g_hist[3], (long long)g_hist[4],
+              (long long)g_nonfinite_trials, (long long)g_spec_launched, (long long)g_spec_used);
+    if (te && (*te == '1' || *te == '2'))
       fprintf(stderr,
               "srhip optim: %.1f ms total, %lld launches, eval_grad %.1f ms (compile/patch %.1f ms: scan+recompile %.1f, "
               "snapshot+upload %.1f), set_consts %.1f ms\n",

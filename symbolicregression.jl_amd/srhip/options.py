@@ -134,6 +134,12 @@ class Options:
         return all(n in INT_BINARY for n in self.binary_operators) and all(
             n in INT_UNARY for n in self.unary_operators)
 
+    def __getstate__(self):
+        # the cached C operator table holds raw pointers into this object's arrays: rebuilt on use
+        d = dict(self.__dict__)
+        d["_c_ops"] = None
+        return d
+
     def c_operators(self) -> Operators:
         if self._c_ops is None:
             ops = Operators()

@@ -310,3 +310,41 @@ def test_grad_tangent_width_4_equals_8(ctx, dtype, monkeypatch):
     assert np.array_equal(o4, o8)
     assert np.array_equal(l4.view(np.uint64), l8.view(np.uint64))
     assert np.array_equal(np.concatenate(g4).view(np.uint64), np.concatenate(g8).view(np.uint64))
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_speculative_trials_equal_sequential(ctx, dtype, monkeypatch, capfd):
+    """Speculative line-search points (SRHIP_OPTIM_SPEC slots: the next alphas a backtracking tree
+    would try, evaluated in spare program slots of the same launch and consumed only while the line
+    search asks for exactly that alpha) change nothing: losses, flags, objective-call counts and
+    constants equal the sequential pipeline's bit for bit, on C4-shaped trees whose overflowing
+    directions backtrack for hundreds of trials -- and the speculation is really used."""
+    import re
+
+    import srhip.workloads as wl
+
+    sr = _sr()
+    opts, X, y, trees, nodes, offs = wl.c4(ntrees=96, rows=2000)
+    if dtype == np.float32:
+        nodes, offs = sr.flatten(trees, opts, np.float32)
+        X, y = X.astype(np.float32), y.astype(np.float32)
+    ds = sr.DeviceDataset(ctx, X, y)
+    loss = sr.L2DistLoss()
+    res = {}
+    for spec in ("0", "256"):
+        monkeypatch.setenv("SRHIP_OPTIM_SPEC", spec)
+        monkeypatch.setenv("SRHIP_OPTIM_TIMING", "2")
+        prog = sr.Program(ctx, nodes, offs, opts, dtype)
+        out, improved, fcalls = prog.optimize_constants(ds, loss, iterations=8, nrestarts=2, seed=5)
+        res[spec] = (np.asarray(out, np.float64), improved.copy(), fcalls.copy(), prog.get_constants())
+        prog.close()
+        err = capfd.readouterr().err
+        m = re.findall(r"speculative points (\d+) evaluated, (\d+) used", err)
+        assert m, err[-2000:]
+        res[spec + "_used"] = int(m[-1][1])
+    assert res["0_used"] == 0 and res["256_used"] > 0
+    a, b = res["0"], res["256"]
+    assert np.array_equal(a[0].view(np.uint64), b[0].view(np.uint64))
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    for ca, cb in zip(a[3], b[3]):
+        assert np.array_equal(np.asarray(ca).view(np.uint64), np.asarray(cb).view(np.uint64))
