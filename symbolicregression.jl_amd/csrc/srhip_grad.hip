@@ -21,6 +21,9 @@
 #include "srhip_ops.h"
 
 #define UNR _Pragma("unroll")
+#ifndef GRAD_R
+#define GRAD_R 1  // 2 measured slower on C4 (2.60 -> 2.80 ms: 155 VGPRs, 3 waves per SIMD)
+#endif
 #define DI __device__ __attribute__((always_inline)) inline
 
 namespace srhip {
@@ -170,9 +173,11 @@ template <typename T> DI T imm_bits(uint64_t b) {
   else return __builtin_bit_cast(T, (uint32_t)b);
 }
 
+// KT = 0: values only (the line search's trial points): the primal code and its row-sum order are
+// the same as with tangents, so a value-only loss is bit-identical to the loss of a gradient launch
 template <typename T, int KT> struct Dual {
   T v;
-  T d[KT];
+  T d[KT > 0 ? KT : 1];
 };
 
 // leaves: tangents are seeded on the constants (GMODE_LOSS / GMODE_ROWC: rel = constant index - c0)
@@ -188,7 +193,7 @@ template <int GM, typename T, int KT> DI void set_feat(Dual<T, KT>& a, T x, int 
 // out = f(l, r) with partials: out.d = fl * l.d + fr * r.d (out may alias l or r)
 template <typename T, int KT>
 DI void combine(Dual<T, KT>& out, const Dual<T, KT>& l, const Dual<T, KT>& r, T f, T fl, T fr) {
-  T d[KT];
+  T d[KT > 0 ? KT : 1];
   UNR for (int j = 0; j < KT; ++j) d[j] = fl * l.d[j] + fr * r.d[j];
   out.v = f;
   UNR for (int j = 0; j < KT; ++j) out.d[j] = d[j];
@@ -198,19 +203,48 @@ DI void combine(Dual<T, KT>& out, const Dual<T, KT>& l, const Dual<T, KT>& r, T 
 DI void chk_fold(float& M, float v) { M = __builtin_elementwise_maximum(M, __builtin_fabsf(v)); }
 DI void chk_fold(double& M, double v) { M = __builtin_fma(__builtin_fabs(v), 0x1p-512, M); }
 
-template <typename T, int KT, int K, int GM>
+// XLDS: the workgroup stages its row block of X (and y) into LDS once -- feature leaves then read
+// LDS instead of issuing a dependent global load per leaf per tile (grad_lds_bytes: [nfeat + 1][rb_rows])
+// R rows per lane: a tile is 64 R rows (row tile_base + 64 r + lane), one bytecode dispatch per tile.
+// Every lane still folds its rows in ascending row order (tile-major, r inner), so losses and
+// gradients are bit-identical for any R.
+template <typename T, int KT, int K, int GM, bool XLDS, int R>
 __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   constexpr int CW = GM == GMODE_LOSS ? 2 : 4;  // ints per chunk record
   const int lane = threadIdx.x & 63;
   const int rb = blockIdx.x;
   const int64_t row_base = (int64_t)rb * p.rb_rows;
-  const int ntiles = p.rb_rows / 64;
+  const int ntiles = p.rb_rows / (64 * R);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int group_base = blockIdx.y * p.chunks_per_group;
   const int group_n = min(p.chunks_per_group, p.nchunks - group_base);
-  const T* X = reinterpret_cast<const T*>(p.X);
-  const T* Y = reinterpret_cast<const T*>(p.y);
+  const T* Xg = reinterpret_cast<const T*>(p.X);
+  const T* Yg = reinterpret_cast<const T*>(p.y);
   const T* W = reinterpret_cast<const T*>(p.w);
+  extern __shared__ __attribute__((aligned(16))) unsigned char grad_lds[];
+  T* xs = reinterpret_cast<T*>(grad_lds);
+  const int rbr = p.rb_rows;
+  if constexpr (XLDS) {
+    const int nf = p.nfeat;
+    const bool has_y = GM == GMODE_LOSS && Yg != nullptr;
+    for (int i = threadIdx.x; i < (nf + 1) * rbr; i += 64 * GRAD_WAVES) {
+      const int f = i / rbr, r = i - f * rbr;
+      const int64_t row = row_base + r;
+      T v = T(0);
+      if (row < p.ld) v = f < nf ? Xg[(int64_t)f * p.ld + row] : (has_y ? Yg[row] : T(0));
+      xs[i] = v;
+    }
+    __syncthreads();
+  }
+  // feature f / target at block-relative row rr of this row block
+  auto xat = [&](int f, int rr) -> T {
+    if constexpr (XLDS) return xs[f * rbr + rr];
+    else return Xg[(int64_t)f * p.ld + row_base + rr];
+  };
+  auto yat = [&](int rr) -> T {
+    if constexpr (XLDS) return xs[p.nfeat * rbr + rr];
+    else return Yg[row_base + rr];
+  };
   GIns* code = (GIns*)(uintptr_t)p.code;
   const T p0 = (T)p.loss_p0;
   const int max_steps = __builtin_amdgcn_readfirstlane(p.max_steps);
@@ -220,16 +254,18 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
     const int c0 = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk + 1]);
     const int pc0 = __builtin_amdgcn_readfirstlane(p.prog_off[tree]);
     double lacc = 0.0;
-    double gacc[KT];
+    double gacc[KT > 0 ? KT : 1];
     UNR for (int j = 0; j < KT; ++j) gacc[j] = 0.0;
     T M = T(0);
     for (int tile = 0; tile < ntiles; ++tile) {
-      const int64_t row0 = row_base + (int64_t)tile * 64;
-      if (row0 >= p.nvalid) break;
-      const int64_t row = row0 + lane;  // rows up to ld are finite replicas; masked at the loss
-      Dual<T, KT> A, S[K];
-      set_feat<GMODE_LOSS>(A, T(0), -1);
-      UNR for (int k = 0; k < K; ++k) set_feat<GMODE_LOSS>(S[k], T(0), -1);
+      const int tb = tile * 64 * R;  // block-relative first row of the tile
+      if (row_base + tb >= p.nvalid) break;
+      // rows up to ld are finite replicas; masked at the loss
+      Dual<T, KT> A[R], S[K][R];
+      UNR for (int r = 0; r < R; ++r) {
+        set_feat<GMODE_LOSS>(A[r], T(0), -1);
+        UNR for (int k = 0; k < K; ++k) set_feat<GMODE_LOSS>(S[k][r], T(0), -1);
+      }
       GIns* prog = code + pc0;
       Ins nxt = prog[0];
       for (int step = 0; step < max_steps; ++step) {
@@ -238,9 +274,10 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
         if (ins.h == H_END) break;
         const int opnd = (int)(ins.a & 0xffff);
         const T imm = imm_bits<T>(ins.imm);
+#define RR(...) UNR for (int r = 0; r < R; ++r) { const int rr = tb + 64 * r + lane; (void)rr; __VA_ARGS__ }
         switch (ins.h) {
-          case H_LOADF: set_feat<GM>(A, X[(int64_t)opnd * p.ld + row], opnd - c0); break;
-          case H_LOADC: set_const<GM>(A, imm, opnd - c0); break;
+          case H_LOADF: RR(set_feat<GM>(A[r], xat(opnd, rr), opnd - c0);) break;
+          case H_LOADC: RR(set_const<GM>(A[r], imm, opnd - c0);) break;
 #define GK_CASES(BASE, ...)                                                                        \
   case BASE + 0: if constexpr (0 < K) { constexpr int k = 0; __VA_ARGS__ } break;                \
   case BASE + 1: if constexpr (1 < K) { constexpr int k = 1; __VA_ARGS__ } break;                \
@@ -250,77 +287,84 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   case BASE + 5: if constexpr (5 < K) { constexpr int k = 5; __VA_ARGS__ } break;                \
   case BASE + 6: if constexpr (6 < K) { constexpr int k = 6; __VA_ARGS__ } break;                \
   case BASE + 7: if constexpr (7 < K) { constexpr int k = 7; __VA_ARGS__ } break;
-          GK_CASES(H_PUSH0, { S[k] = A; })
-          GK_CASES(H_SLOADF0, { set_feat<GM>(S[k], X[(int64_t)opnd * p.ld + row], opnd - c0); })
-          GK_CASES(H_SLOADC0, { set_const<GM>(S[k], imm, opnd - c0); })
+          GK_CASES(H_PUSH0, { RR(S[k][r] = A[r];) })
+          GK_CASES(H_SLOADF0, { RR(set_feat<GM>(S[k][r], xat(opnd, rr), opnd - c0);) })
+          GK_CASES(H_SLOADC0, { RR(set_const<GM>(S[k][r], imm, opnd - c0);) })
 #define GK_SPEC(NAME, FN)                                                                          \
   case h_spec(SB_##NAME, SPEC_AF): {                                                               \
-    Dual<T, KT> o; set_feat<GM>(o, X[(int64_t)opnd * p.ld + row], opnd - c0);                      \
-    T f, fl, fr; dual_spec<T, SB_##NAME>(A.v, o.v, f, fl, fr); combine(A, A, o, f, fl, fr);        \
-    chk_fold(M, A.v); break; }                                                                     \
+    RR(Dual<T, KT> o; set_feat<GM>(o, xat(opnd, rr), opnd - c0);                                   \
+       T f, fl, fr; dual_spec<T, SB_##NAME>(A[r].v, o.v, f, fl, fr); combine(A[r], A[r], o, f, fl, fr); \
+       chk_fold(M, A[r].v);) break; }                                                              \
   case h_spec(SB_##NAME, SPEC_FA): {                                                               \
-    Dual<T, KT> o; set_feat<GM>(o, X[(int64_t)opnd * p.ld + row], opnd - c0);                      \
-    T f, fl, fr; dual_spec<T, SB_##NAME>(o.v, A.v, f, fl, fr); combine(A, o, A, f, fl, fr);        \
-    chk_fold(M, A.v); break; }                                                                     \
+    RR(Dual<T, KT> o; set_feat<GM>(o, xat(opnd, rr), opnd - c0);                                   \
+       T f, fl, fr; dual_spec<T, SB_##NAME>(o.v, A[r].v, f, fl, fr); combine(A[r], o, A[r], f, fl, fr); \
+       chk_fold(M, A[r].v);) break; }                                                              \
   case h_spec(SB_##NAME, SPEC_AC): {                                                               \
-    Dual<T, KT> o; set_const<GM>(o, imm, opnd - c0);                                               \
-    T f, fl, fr; dual_spec<T, SB_##NAME>(A.v, o.v, f, fl, fr); combine(A, A, o, f, fl, fr);        \
-    chk_fold(M, A.v); break; }                                                                     \
+    RR(Dual<T, KT> o; set_const<GM>(o, imm, opnd - c0);                                            \
+       T f, fl, fr; dual_spec<T, SB_##NAME>(A[r].v, o.v, f, fl, fr); combine(A[r], A[r], o, f, fl, fr); \
+       chk_fold(M, A[r].v);) break; }                                                              \
   case h_spec(SB_##NAME, SPEC_CA): {                                                               \
-    Dual<T, KT> o; set_const<GM>(o, imm, opnd - c0);                                               \
-    T f, fl, fr; dual_spec<T, SB_##NAME>(o.v, A.v, f, fl, fr); combine(A, o, A, f, fl, fr);        \
-    chk_fold(M, A.v); break; }                                                                     \
+    RR(Dual<T, KT> o; set_const<GM>(o, imm, opnd - c0);                                            \
+       T f, fl, fr; dual_spec<T, SB_##NAME>(o.v, A[r].v, f, fl, fr); combine(A[r], o, A[r], f, fl, fr); \
+       chk_fold(M, A[r].v);) break; }                                                              \
   GK_CASES(h_spec(SB_##NAME, SPEC_SA0), {                                                          \
-    T f, fl, fr; dual_spec<T, SB_##NAME>(S[k].v, A.v, f, fl, fr); combine(A, S[k], A, f, fl, fr);  \
-    chk_fold(M, A.v); })                                                                           \
+    RR(T f, fl, fr; dual_spec<T, SB_##NAME>(S[k][r].v, A[r].v, f, fl, fr);                         \
+       combine(A[r], S[k][r], A[r], f, fl, fr); chk_fold(M, A[r].v);) })                           \
   GK_CASES(h_spec(SB_##NAME, SPEC_AS0), {                                                          \
-    T f, fl, fr; dual_spec<T, SB_##NAME>(A.v, S[k].v, f, fl, fr); combine(A, A, S[k], f, fl, fr);  \
-    chk_fold(M, A.v); })
+    RR(T f, fl, fr; dual_spec<T, SB_##NAME>(A[r].v, S[k][r].v, f, fl, fr);                         \
+       combine(A[r], A[r], S[k][r], f, fl, fr); chk_fold(M, A[r].v);) })
           SRHIP_SPEC_BINOPS(GK_SPEC)
 #undef GK_SPEC
 #define GK_HEAVY(NAME, FN)                                                                         \
   GK_CASES(h_heavy(HB_##NAME, HEAVY_SA0), {                                                        \
-    const typename V4<T>::type r = dual_heavy<T, HB_##NAME>(S[k].v, A.v);                          \
-    combine(A, S[k], A, r[0], r[1], r[2]); chk_fold(M, A.v); })                                    \
+    RR(const typename V4<T>::type q = dual_heavy<T, HB_##NAME>(S[k][r].v, A[r].v);                 \
+       combine(A[r], S[k][r], A[r], q[0], q[1], q[2]); chk_fold(M, A[r].v);) })                    \
   GK_CASES(h_heavy(HB_##NAME, HEAVY_AS0), {                                                        \
-    const typename V4<T>::type r = dual_heavy<T, HB_##NAME>(A.v, S[k].v);                          \
-    combine(A, A, S[k], r[0], r[1], r[2]); chk_fold(M, A.v); })
+    RR(const typename V4<T>::type q = dual_heavy<T, HB_##NAME>(A[r].v, S[k][r].v);                 \
+       combine(A[r], A[r], S[k][r], q[0], q[1], q[2]); chk_fold(M, A[r].v);) })
           SRHIP_HEAVY_BINOPS(GK_HEAVY)
 #undef GK_HEAVY
 #define GK_UN(NAME, FN)                                                                            \
   case h_un(UN_##NAME): {                                                                          \
-    T f, df; dual_un<T, UN_##NAME>(A.v, f, df);                                                    \
-    A.v = f;                                                                                       \
-    UNR for (int j = 0; j < KT; ++j) A.d[j] = df * A.d[j];                                         \
-    chk_fold(M, A.v); break; }
+    RR(T f, df; dual_un<T, UN_##NAME>(A[r].v, f, df);                                              \
+       A[r].v = f;                                                                                 \
+       UNR for (int j = 0; j < KT; ++j) A[r].d[j] = df * A[r].d[j];                                \
+       chk_fold(M, A[r].v);) break; }
           SRHIP_UNOPS(GK_UN)
 #undef GK_UN
 #undef GK_CASES
           default: break;
         }
+#undef RR
       }
       if constexpr (GM != GMODE_LOSS) {
-        if (row < p.nvalid) {
-          // record: (tree, c0, end component, output row of component c0)
-          const int cend = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk + 2]);
-          const int orow = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk + 3]);
-          T* der = reinterpret_cast<T*>(p.out_der) + (int64_t)orow * p.nvalid + row;
-          UNR for (int j = 0; j < KT; ++j)
-            if (c0 + j < cend) der[(int64_t)j * p.nvalid] = A.d[j];
+        // record: (tree, c0, end component, output row of component c0)
+        const int cend = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk + 2]);
+        const int orow = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk + 3]);
+        UNR for (int r = 0; r < R; ++r) {
+          const int64_t row = row_base + tb + 64 * r + lane;
+          if (row < p.nvalid) {
+            T* der = reinterpret_cast<T*>(p.out_der) + (int64_t)orow * p.nvalid + row;
+            UNR for (int j = 0; j < KT; ++j)
+              if (c0 + j < cend) der[(int64_t)j * p.nvalid] = A[r].d[j];
+          }
         }
         continue;
       }
-      if (row < p.nvalid) {
-        const T d = A.v - Y[row];
-        T l = loss_elem<T>(p.loss_kind, d, p0);
-        T dl = dloss_elem<T>(p.loss_kind, d, p0);
-        if (p.weighted) {
-          const T w = W[row];
-          l = w * l;
-          dl = w * dl;
+      UNR for (int r = 0; r < R; ++r) {
+        const int rr = tb + 64 * r + lane;
+        if (row_base + rr < p.nvalid) {
+          const T d = A[r].v - yat(rr);
+          T l = loss_elem<T>(p.loss_kind, d, p0);
+          T dl = dloss_elem<T>(p.loss_kind, d, p0);
+          if (p.weighted) {
+            const T w = W[row_base + rr];
+            l = w * l;
+            dl = w * dl;
+          }
+          lacc += (double)l;
+          UNR for (int j = 0; j < KT; ++j) gacc[j] += (double)(dl * A[r].d[j]);
         }
-        lacc += (double)l;
-        UNR for (int j = 0; j < KT; ++j) gacc[j] += (double)(dl * A.d[j]);
       }
     }
     if constexpr (GM != GMODE_LOSS) continue;
@@ -362,9 +406,24 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(const double* __restri
   }
 }
 
+// LDS staging of the row block when it fits (few features): [nfeat + 1][rb_rows] elements
+constexpr size_t GRAD_LDS_MAX = 48 * 1024;
+template <typename T> static size_t grad_lds_bytes(const GradArgs& a) {
+  return (size_t)(a.nfeat + 1) * (size_t)a.rb_rows * sizeof(T);
+}
+
+// rows per lane: 2 where the register budget allows (4 tangents, stack depth 4), else 1
+template <int KT, int K> constexpr int grad_rows() { return KT <= 4 && K <= 4 ? GRAD_R : 1; }
+
 template <typename T, int KT, int K, int GM = GMODE_LOSS>
 static hipError_t launch_grad_t(const GradArgs& a, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((grad_kernel<T, KT, K, GM>), grid, dim3(64 * GRAD_WAVES), 0, s, a);
+  constexpr int R = grad_rows<KT, K>();
+  if (a.rb_rows % (64 * R)) return hipErrorInvalidValue;
+  const size_t lds = grad_lds_bytes<T>(a);
+  if (lds <= GRAD_LDS_MAX)
+    hipLaunchKernelGGL((grad_kernel<T, KT, K, GM, true, R>), grid, dim3(64 * GRAD_WAVES), lds, s, a);
+  else
+    hipLaunchKernelGGL((grad_kernel<T, KT, K, GM, false, R>), grid, dim3(64 * GRAD_WAVES), 0, s, a);
   return hipGetLastError();
 }
 
@@ -387,12 +446,14 @@ hipError_t launch_grad_rows(int dtype, int K, int gmode, const GradArgs& a, dim3
 }
 
 hipError_t launch_grad(int dtype, int K, int kt, const GradArgs& a, dim3 grid, hipStream_t s) {
-  if (kt != 4 && kt != GRAD_KT) return hipErrorInvalidValue;
+  if (kt != 0 && kt != 4 && kt != GRAD_KT) return hipErrorInvalidValue;
   switch (dtype) {
     case SRHIP_F32:
+      if (kt == 0) return K <= 4 ? launch_grad_t<float, 0, 4>(a, grid, s) : launch_grad_t<float, 0, 8>(a, grid, s);
       if (kt == 4) return K <= 4 ? launch_grad_t<float, 4, 4>(a, grid, s) : launch_grad_t<float, 4, 8>(a, grid, s);
       return K <= 4 ? launch_grad_t<float, GRAD_KT, 4>(a, grid, s) : launch_grad_t<float, GRAD_KT, 8>(a, grid, s);
     case SRHIP_F64:
+      if (kt == 0) return K <= 4 ? launch_grad_t<double, 0, 4>(a, grid, s) : launch_grad_t<double, 0, 8>(a, grid, s);
       if (kt == 4) return K <= 4 ? launch_grad_t<double, 4, 4>(a, grid, s) : launch_grad_t<double, 4, 8>(a, grid, s);
       return K <= 4 ? launch_grad_t<double, GRAD_KT, 4>(a, grid, s) : launch_grad_t<double, GRAD_KT, 8>(a, grid, s);
     default: return hipErrorInvalidValue;
@@ -400,8 +461,13 @@ hipError_t launch_grad(int dtype, int K, int kt, const GradArgs& a, dim3 grid, h
 }
 
 hipError_t launch_grad_reduce(int dtype, int kt, const double* slab, int nrb, int nchunks, double* out, hipStream_t s) {
-  if (kt != 4 && kt != GRAD_KT) return hipErrorInvalidValue;
+  if (kt != 0 && kt != 4 && kt != GRAD_KT) return hipErrorInvalidValue;
   dim3 grid((nchunks + 3) / 4), block(256);
+  if (kt == 0) {
+    if (dtype == SRHIP_F32) hipLaunchKernelGGL((grad_reduce_kernel<0, true>), grid, block, 0, s, slab, nrb, nchunks, out);
+    else hipLaunchKernelGGL((grad_reduce_kernel<0, false>), grid, block, 0, s, slab, nrb, nchunks, out);
+    return hipGetLastError();
+  }
   if (dtype == SRHIP_F32) {
     if (kt == 4) hipLaunchKernelGGL((grad_reduce_kernel<4, true>), grid, block, 0, s, slab, nrb, nchunks, out);
     else hipLaunchKernelGGL((grad_reduce_kernel<GRAD_KT, true>), grid, block, 0, s, slab, nrb, nchunks, out);

@@ -36,7 +36,7 @@ LaunchPlan grad_plan(const srhip_ctx* ctx, int64_t m, int32_t nchunks) {
   static const int rb_env = [] { const char* e = getenv("SRHIP_GRAD_RB"); return e ? atoi(e) : 0; }();
   int rb = (rb_env >= 64 && rb_env <= 4096 && (rb_env & (rb_env - 1)) == 0) ? rb_env : 256;
   m = std::max<int64_t>(1, m);
-  while (rb > 64 && rb / 2 >= m) rb /= 2;
+  while (rb > 128 && rb / 2 >= m) rb /= 2;  // >= 128: two 64-row halves per lane (GRAD_R)
   LaunchPlan L{};
   L.rb_rows = rb;
   L.nrb = (int)((m + rb - 1) / rb);
@@ -104,8 +104,9 @@ static double now_s() {
 struct GradItem {
   int32_t slot, tree;
   double* f;
-  double* g;
-  uint8_t* ok;  // nullable
+  double* g;     // unused for value_only items
+  uint8_t* ok;   // nullable
+  bool value_only = false;  // loss only (a line-search trial point): the cheap KT = 0 kernel
 };
 static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
                            const View& v, const std::vector<GradItem>& items);
@@ -116,7 +117,7 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
 static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss, const View& v,
                      const std::vector<int32_t>& trees, const std::vector<int64_t>& coff, double* f, double* g,
                      uint8_t* ok = nullptr, const std::vector<GradItem>* extra = nullptr, int64_t spec_lo = 0,
-                     int64_t spec_hi = -1) {
+                     int64_t spec_hi = -1, const uint8_t* value_only = nullptr) {
   const double t0 = now_s();
   int rc = compile_grad_program(*P);
   g_t_compile += now_s() - t0;
@@ -124,7 +125,8 @@ static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, 
   if (rc) return rc;
   std::vector<GradItem> items;
   items.reserve(trees.size() + (extra ? extra->size() : 0));
-  for (int32_t t : trees) items.push_back(GradItem{t, t, f + t, g + coff[t], ok ? ok + t : nullptr});
+  for (int32_t t : trees)
+    items.push_back(GradItem{t, t, f + t, g + coff[t], ok ? ok + t : nullptr, value_only && value_only[t]});
   if (extra) items.insert(items.end(), extra->begin(), extra->end());
   auto body = [&]() -> int {
     if (spec_hi > spec_lo)
@@ -143,13 +145,14 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
   const int dtype = P->dtype;
   const bool weighted = ds->weighted;
   const double wsum = weighted ? v.sum_w : (double)v.m;
-  // tangent width of this launch: a chunk carries the primal plus kt tangents, so trees with few
-  // constants waste most of an 8-wide chunk; estimated cost per chunk ~ (3 + kt) (the primal's
+  // tangent width of the gradient pass: a chunk carries the primal plus kt tangents, so trees with
+  // few constants waste most of an 8-wide chunk; estimated cost per chunk ~ (3 + kt) (the primal's
   // transcendentals and derivative factors cost about three tangent updates).  Values and the
-  // tangents of each constant do not depend on kt (independent components, same primal code).
+  // tangents of each constant do not depend on kt (independent components, same primal code; kt = 0
+  // is the value-only pass).
   int64_t cost4 = 0, cost8 = 0;
   for (const GradItem& it : items) {
-    if (P->ginfo[it.slot].static_fail) continue;
+    if (P->ginfo[it.slot].static_fail || it.value_only) continue;
     const int nc = std::max(P->info[it.tree].nconst, 1);
     cost4 += (int64_t)((nc + 3) / 4) * (3 + 4);
     cost8 += (int64_t)((nc + GRAD_KT - 1) / GRAD_KT) * (3 + GRAD_KT);
@@ -157,59 +160,87 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
   const char* kte = getenv("SRHIP_GRAD_KT");  // tuning / tests: force 4 or 8
   int kt = cost4 < cost8 ? 4 : GRAD_KT;
   if (kte && (atoi(kte) == 4 || atoi(kte) == GRAD_KT)) kt = atoi(kte);
-  std::vector<int32_t> chunks, chunk_item;
+  // two passes on the stream (gradient chunks, then value-only chunks), one synchronisation
+  struct Pass {
+    int kt;
+    std::vector<int32_t> chunks, chunk_item;
+    std::vector<double> red;
+    LaunchPlan L;
+  } pass[2];
+  pass[0].kt = kt;
+  pass[1].kt = 0;
   for (size_t i = 0; i < items.size(); ++i) {
     const GradItem& it = items[i];
     *it.f = INFINITY;
     if (it.ok) *it.ok = 0;
     const int nc = P->info[it.tree].nconst;
-    for (int k = 0; k < nc; ++k) it.g[k] = 0.0;
+    if (!it.value_only)
+      for (int k = 0; k < nc; ++k) it.g[k] = 0.0;
     if (P->ginfo[it.slot].static_fail) continue;
-    for (int c0 = 0; c0 < std::max(nc, 1); c0 += kt) {
-      chunks.push_back(it.slot);
-      chunks.push_back(c0);
-      chunk_item.push_back((int32_t)i);
+    Pass& ps = pass[it.value_only ? 1 : 0];
+    const int span = it.value_only ? 1 : std::max(nc, 1);
+    for (int c0 = 0; c0 < span; c0 += std::max(ps.kt, 1)) {
+      ps.chunks.push_back(it.slot);
+      ps.chunks.push_back(c0);
+      ps.chunk_item.push_back((int32_t)i);
     }
   }
-  const int nch = (int)chunks.size() / 2;
-  if (nch == 0) {  // a patched gradient program may still be uploading from P->gcode
+  const int nch0 = (int)pass[0].chunks.size() / 2, nch1 = (int)pass[1].chunks.size() / 2;
+  if (nch0 + nch1 == 0) {  // a patched gradient program may still be uploading from P->gcode
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return SRHIP_OK;
   }
-  const LaunchPlan L = grad_plan(ctx, v.m, nch);
-  const int K = P->gkmax <= 4 ? 4 : 8;
-  HIP_TRY(ctx->g_chunks.ensure(chunks.size() * sizeof(int32_t)));
-  HIP_TRY(hipMemcpyAsync(ctx->g_chunks.p, chunks.data(), chunks.size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                         ctx->stream));
-  const size_t slab_n = (size_t)nch * L.nrb * (kt + 2);
+  // buffers sized for both passes before the first launch (no reallocation under a queued kernel)
+  size_t slab_n = 0, red_n = 0, chunk_n = 0;
+  for (Pass& ps : pass) {
+    const int nch = (int)ps.chunks.size() / 2;
+    if (nch == 0) continue;
+    ps.L = grad_plan(ctx, v.m, nch);
+    slab_n = std::max(slab_n, (size_t)nch * ps.L.nrb * (ps.kt + 2));
+    red_n = std::max(red_n, (size_t)nch * (ps.kt + 2));
+    chunk_n = std::max(chunk_n, ps.chunks.size());
+  }
+  HIP_TRY(ctx->g_chunks.ensure(chunk_n * sizeof(int32_t)));
   HIP_TRY(ctx->g_slab.ensure(slab_n * sizeof(double)));
-  HIP_TRY(ctx->g_red.ensure((size_t)nch * (kt + 2) * sizeof(double)));
-  GradArgs a{};
-  a.code = (const Ins*)P->d_gcode.p;
-  a.prog_off = (const int32_t*)P->d_goff.p;
-  a.chunks = (const int32_t*)ctx->g_chunks.p;
-  a.X = v.X;
-  a.y = v.y;
-  a.w = weighted ? v.w : nullptr;
-  a.slab = (double*)ctx->g_slab.p;
-  a.ld = v.ld;
-  a.nvalid = v.m;
-  a.nchunks = nch;
-  a.nfeat = (int32_t)ds->nfeat;
-  a.rb_rows = L.rb_rows;
-  a.nrb = L.nrb;
-  a.chunks_per_group = L.tpg;
-  a.loss_kind = loss->kind;
-  a.loss_p0 = loss->p0;
-  a.weighted = weighted ? 1 : 0;
-  a.max_steps = P->gmax_len;
-  HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));  // srhip_last_kernel_ms: this gradient kernel
-  HIP_TRY(launch_grad(dtype, K, kt, a, dim3(L.nrb, L.groups), ctx->stream));
+  HIP_TRY(ctx->g_red.ensure(red_n * sizeof(double)));
+  const int K = P->gkmax <= 4 ? 4 : 8;
+  bool first = true;
+  for (Pass& ps : pass) {
+    const int nch = (int)ps.chunks.size() / 2;
+    if (nch == 0) continue;
+    // stream order: this copy follows the previous pass's kernel, which has read its chunk list
+    HIP_TRY(hipMemcpyAsync(ctx->g_chunks.p, ps.chunks.data(), ps.chunks.size() * sizeof(int32_t),
+                           hipMemcpyHostToDevice, ctx->stream));
+    GradArgs a{};
+    a.code = (const Ins*)P->d_gcode.p;
+    a.prog_off = (const int32_t*)P->d_goff.p;
+    a.chunks = (const int32_t*)ctx->g_chunks.p;
+    a.X = v.X;
+    a.y = v.y;
+    a.w = weighted ? v.w : nullptr;
+    a.slab = (double*)ctx->g_slab.p;
+    a.ld = v.ld;
+    a.nvalid = v.m;
+    a.nchunks = nch;
+    a.nfeat = (int32_t)ds->nfeat;
+    a.rb_rows = ps.L.rb_rows;
+    a.nrb = ps.L.nrb;
+    a.chunks_per_group = ps.L.tpg;
+    a.loss_kind = loss->kind;
+    a.loss_p0 = loss->p0;
+    a.weighted = weighted ? 1 : 0;
+    a.max_steps = P->gmax_len;
+    if (first) HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));  // srhip_last_kernel_ms: the gradient kernels
+    first = false;
+    HIP_TRY(launch_grad(dtype, K, ps.kt, a, dim3(ps.L.nrb, ps.L.groups), ctx->stream));
+    HIP_TRY(launch_grad_reduce(dtype, ps.kt, (const double*)ctx->g_slab.p, ps.L.nrb, nch, (double*)ctx->g_red.p,
+                               ctx->stream));
+    ps.red.resize((size_t)nch * (ps.kt + 2));
+    HIP_TRY(hipMemcpyAsync(ps.red.data(), ctx->g_red.p, ps.red.size() * sizeof(double), hipMemcpyDeviceToHost,
+                           ctx->stream));
+  }
   HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
   ctx->timed = true;
-  HIP_TRY(launch_grad_reduce(dtype, kt, (const double*)ctx->g_slab.p, L.nrb, nch, (double*)ctx->g_red.p, ctx->stream));
-  std::vector<double> red((size_t)nch * (kt + 2));
-  HIP_TRY(hipMemcpyAsync(red.data(), ctx->g_red.p, red.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   // decision inputs in the partials layout: only the feature statistics and the row count are read
   std::vector<double> sums(2 * (size_t)P->ntrees + 2 * ds->nfeat + 1, 0.0);
@@ -219,19 +250,22 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
   }
   sums.back() = (double)v.m;
   std::vector<int32_t> undecided, undecided_item;
-  for (int c = 0; c < nch; ++c) {
-    const GradItem& it = items[chunk_item[c]];
-    const int32_t c0 = chunks[2 * c + 1];
-    const double* r = red.data() + (size_t)c * (kt + 2);
-    const int nc = P->info[it.tree].nconst;
-    for (int j = 0; j < kt && c0 + j < nc; ++j) it.g[c0 + j] = r[1 + j] / wsum;
-    if (c0 == 0) {
-      const int st = decide_tree(P->ginfo[it.slot], *P, ds->nfeat, sums.data(), r[kt + 1]);
-      *it.f = st == 1 ? INFINITY : r[0] / wsum;
-      if (it.ok) *it.ok = st != 1;
-      if (st == 2) {
-        undecided.push_back(it.slot);
-        undecided_item.push_back(chunk_item[c]);
+  for (const Pass& ps : pass) {
+    const int nch = (int)ps.chunks.size() / 2;
+    for (int c = 0; c < nch; ++c) {
+      const GradItem& it = items[ps.chunk_item[c]];
+      const int32_t c0 = ps.chunks[2 * c + 1];
+      const double* r = ps.red.data() + (size_t)c * (ps.kt + 2);
+      const int nc = P->info[it.tree].nconst;
+      for (int j = 0; j < ps.kt && c0 + j < nc; ++j) it.g[c0 + j] = r[1 + j] / wsum;
+      if (c0 == 0) {
+        const int st = decide_tree(P->ginfo[it.slot], *P, ds->nfeat, sums.data(), r[ps.kt + 1]);
+        *it.f = st == 1 ? INFINITY : r[0] / wsum;
+        if (it.ok) *it.ok = st != 1;
+        if (st == 2) {
+          undecided.push_back(it.slot);
+          undecided_item.push_back(ps.chunk_item[c]);
+        }
       }
     }
   }
@@ -342,7 +376,7 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
                           const View& v, const std::vector<int32_t>& trees, const std::vector<int64_t>& coff,
                           int iterations, double g_tol, const std::vector<std::vector<double>>& starts,
                           std::vector<double>& best_x, std::vector<double>& best_f, std::vector<int64_t>& fcalls) {
-  enum { INIT = 0, TRIAL = 1, DONE = 2, HESS_P = 3, HESS_M = 4 };
+  enum { INIT = 0, TRIAL = 1, DONE = 2, HESS_P = 3, HESS_M = 4, GRADAT = 5 };
   const int nstarts = (int)starts.size();
   const size_t nall = best_x.size();
   std::vector<double> x(nall), g(nall), s(nall), xe(nall), fe(P->ntrees), ge(nall), f(P->ntrees, INFINITY);
@@ -368,6 +402,13 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
   // per-tree speculation depth: doubled while every speculative point of a launch is consumed,
   // cut back to what was consumed (+1) after a misprediction
   std::vector<int> sdepth(P->ntrees, 4);
+  // value-only trial points (SRHIP_OPTIM_VALUE_TRIALS, default on): a line search's trials after its
+  // first are evaluated without tangents; an accepted one is re-evaluated with its gradient (phase
+  // GRADAT, same point, same loss bits, not an objective call)
+  const char* vte = getenv("SRHIP_OPTIM_VALUE_TRIALS");
+  const bool value_trials = !(vte && *vte == '0');
+  std::vector<uint8_t> vonly(P->ntrees, 0);
+  std::vector<double> xacc(nall), phiacc(P->ntrees, 0.0);
   for (size_t k = 0; k < nall; ++k) xe[k] = best_x[k];
   auto newton = [&](int32_t t) { return coff[t + 1] - coff[t] == 1; };
   auto gnorm = [&](int32_t t, const std::vector<double>& gg) {
@@ -441,6 +482,42 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
   const char* tre = getenv("SRHIP_OPTIM_TRACE");
   const int trace_tree = tre && *tre ? atoi(tre) : -1;
   // one evaluation result of tree t at the point xv: loss phi, gradient gv
+  // an accepted step to (xv, phi) with gradient gv there: BFGS update, then converge or iterate
+  auto accept = [&](int32_t t, double phi, const double* gv, const double* xv) {
+    const int64_t o = coff[t], n = coff[t + 1] - coff[t];
+    const LineSearch& L = ls[t];
+    if (!newton(t)) {
+      std::vector<double> dx(n), dg(n), u(n);
+      double dxdg = 0.0;
+      for (int64_t i = 0; i < n; ++i) {
+        dx[i] = L.a2 * s[o + i];
+        dg[i] = gv[i] - g[o + i];
+        dxdg += dx[i] * dg[i];
+      }
+      if (dxdg > 0.0) {
+        double dgu = 0.0;
+        for (int64_t i = 0; i < n; ++i) {
+          double acc = 0.0;
+          for (int64_t j = 0; j < n; ++j) acc += H[hoff[t] + i * n + j] * dg[j];
+          u[i] = acc;
+          dgu += dg[i] * acc;
+        }
+        const double c1 = (dxdg + dgu) / (dxdg * dxdg), c2 = 1.0 / dxdg;
+        for (int64_t i = 0; i < n; ++i)
+          for (int64_t j = 0; j < n; ++j)
+            H[hoff[t] + i * n + j] += c1 * dx[i] * dx[j] - c2 * (u[i] * dx[j] + dx[i] * u[j]);
+      }
+    }
+    const double fold = f[t];
+    for (int64_t k = 0; k < n; ++k) {
+      x[o + k] = xv[k];
+      g[o + k] = gv[k];
+    }
+    f[t] = phi;
+    if (phi == fold || gnorm(t, g) <= g_tol) finish_start(t);  // converged
+    else next_iter(t);
+  };
+  // one evaluation result of tree t at the point xv: loss phi, gradient gv (nullptr: value only)
   auto consume = [&](int32_t t, double phi, const double* gv, const double* xv) {
     const int64_t o = coff[t], n = coff[t + 1] - coff[t];
     if (t == trace_tree) {  // SRHIP_OPTIM_TRACE=<tree>: every evaluation of one tree, stderr
@@ -448,8 +525,12 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
               phase[t], phase[t] == TRIAL ? ls[t].a2 : 0.0, phi);
       for (int64_t k = 0; k < n; ++k) fprintf(stderr, " %.17g", xv[k]);
       fprintf(stderr, " g");
-      for (int64_t k = 0; k < n; ++k) fprintf(stderr, " %.17g", gv[k]);
+      for (int64_t k = 0; k < n; ++k) fprintf(stderr, gv ? " %.17g" : " -", gv ? gv[k] : 0.0);
       fprintf(stderr, "\n");
+    }
+    if (phase[t] == GRADAT) {  // the gradient at an accepted value-only trial point
+      accept(t, phiacc[t], gv, xacc.data() + o);
+      return;
     }
     if (phase[t] == HESS_P) {
       gplus[t] = std::isfinite(phi) ? gv[0] : NAN;
@@ -488,36 +569,13 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
       case LS_FAIL: finish_start(t); return;  // LineSearchException: the start ends at its last accepted point
       default: break;
     }
-    if (!newton(t)) {
-      std::vector<double> dx(n), dg(n), u(n);
-      double dxdg = 0.0;
-      for (int64_t i = 0; i < n; ++i) {
-        dx[i] = L.a2 * s[o + i];
-        dg[i] = gv[i] - g[o + i];
-        dxdg += dx[i] * dg[i];
-      }
-      if (dxdg > 0.0) {
-        double dgu = 0.0;
-        for (int64_t i = 0; i < n; ++i) {
-          double acc = 0.0;
-          for (int64_t j = 0; j < n; ++j) acc += H[hoff[t] + i * n + j] * dg[j];
-          u[i] = acc;
-          dgu += dg[i] * acc;
-        }
-        const double c1 = (dxdg + dgu) / (dxdg * dxdg), c2 = 1.0 / dxdg;
-        for (int64_t i = 0; i < n; ++i)
-          for (int64_t j = 0; j < n; ++j)
-            H[hoff[t] + i * n + j] += c1 * dx[i] * dx[j] - c2 * (u[i] * dx[j] + dx[i] * u[j]);
-      }
+    if (!gv) {  // accepted without a gradient: fetch it at this point next launch
+      for (int64_t k = 0; k < n; ++k) xacc[o + k] = xv[k];
+      phiacc[t] = phi;
+      phase[t] = GRADAT;
+      return;
     }
-    const double fold = f[t];
-    for (int64_t k = 0; k < n; ++k) {
-      x[o + k] = xv[k];
-      g[o + k] = gv[k];
-    }
-    f[t] = phi;
-    if (phi == fold || gnorm(t, g) <= g_tol) finish_start(t);  // converged
-    else next_iter(t);
+    accept(t, phi, gv, xv);
   };
   for (int32_t t : trees) begin_start(t);
   const char* spe = getenv("SRHIP_OPTIM_SPEC");
@@ -551,8 +609,11 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
         case TRIAL: for (int64_t k = o; k < e; ++k) xe[k] = x[k] + ls[t].a2 * s[k]; break;
         case HESS_P: xe[o] = x[o] + hstep[t]; break;
         case HESS_M: xe[o] = x[o] - hstep[t]; break;
+        case GRADAT: for (int64_t k = o; k < e; ++k) xe[k] = xacc[k]; break;
         default: break;
       }
+      // trials after a line search's first: loss only
+      vonly[t] = value_trials && phase[t] == TRIAL && ls[t].iter + ls[t].iterfinite >= 1;
     }
     if (act.empty()) break;
     const double t0 = now_s();
@@ -625,12 +686,14 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
         }
         spec.resize(keep);
         for (size_t i = 0; i < spec.size(); ++i)
-          sitems.push_back(GradItem{P->ntrees + spec[i].slot, spec[i].t, &sf[i], sg.data() + spec[i].off, nullptr});
+          sitems.push_back(GradItem{P->ntrees + spec[i].slot, spec[i].t, &sf[i], sg.data() + spec[i].off, nullptr,
+                                    value_trials});
         g_spec_launched += (int64_t)spec.size();
       }
     }
     const double t1 = now_s();
-    int rc = eval_grad(ctx, ds, P, loss, v, act, coff, fe.data(), ge.data(), nullptr, &sitems, spec_lo, spec_hi);
+    int rc = eval_grad(ctx, ds, P, loss, v, act, coff, fe.data(), ge.data(), nullptr, &sitems, spec_lo, spec_hi,
+                       vonly.data());
     if (rc) return rc;
     if (g_stats_on)  // SRHIP_OPTIM_TIMING=2: launch-size histogram
       g_hist[act.size() <= 1 ? 0 : act.size() <= 4 ? 1 : act.size() <= 16 ? 2 : act.size() <= 64 ? 3 : 4] += 1;
@@ -640,7 +703,7 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
     size_t si = 0;
     for (int32_t t : act) {
       const int64_t o = coff[t];
-      consume(t, fe[t], ge.data() + o, xe.data() + o);
+      consume(t, fe[t], vonly[t] ? nullptr : ge.data() + o, xe.data() + o);
       // then t's speculative points, in order, while its line search asks for exactly them
       int launched = 0, used = 0;
       bool hit = true;
@@ -649,7 +712,7 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
         launched += 1;
         hit = hit && phase[t] == TRIAL && lsgen[t] == q.gen && memcmp(&ls[t].a2, &q.alpha, sizeof(double)) == 0;
         if (!hit) continue;
-        consume(t, sf[si], sg.data() + q.off, sx.data() + q.off);
+        consume(t, sf[si], value_trials ? nullptr : sg.data() + q.off, sx.data() + q.off);
         used += 1;
       }
       if (launched > 0) {

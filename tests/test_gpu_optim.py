@@ -314,7 +314,8 @@ def test_grad_tangent_width_4_equals_8(ctx, dtype, monkeypatch):
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_speculative_trials_equal_sequential(ctx, dtype, monkeypatch, capfd):
-    """Speculative line-search points (SRHIP_OPTIM_SPEC slots: the next alphas a backtracking tree
+    """Value-only trial points (SRHIP_OPTIM_VALUE_TRIALS: a line search's later trials without
+    tangents, the gradient fetched at the accepted point) and speculative line-search points (SRHIP_OPTIM_SPEC slots: the next alphas a backtracking tree
     would try, evaluated in spare program slots of the same launch and consumed only while the line
     search asks for exactly that alpha) change nothing: losses, flags, objective-call counts and
     constants equal the sequential pipeline's bit for bit, on C4-shaped trees whose overflowing
@@ -331,20 +332,24 @@ def test_speculative_trials_equal_sequential(ctx, dtype, monkeypatch, capfd):
     ds = sr.DeviceDataset(ctx, X, y)
     loss = sr.L2DistLoss()
     res = {}
-    for spec in ("0", "256"):
+    # (speculative slots, value-only trials): the plain pipeline first
+    for spec, vt in (("0", "0"), ("0", "1"), ("256", "0"), ("256", "1")):
         monkeypatch.setenv("SRHIP_OPTIM_SPEC", spec)
+        monkeypatch.setenv("SRHIP_OPTIM_VALUE_TRIALS", vt)
         monkeypatch.setenv("SRHIP_OPTIM_TIMING", "2")
         prog = sr.Program(ctx, nodes, offs, opts, dtype)
         out, improved, fcalls = prog.optimize_constants(ds, loss, iterations=8, nrestarts=2, seed=5)
-        res[spec] = (np.asarray(out, np.float64), improved.copy(), fcalls.copy(), prog.get_constants())
+        res[spec, vt] = (np.asarray(out, np.float64), improved.copy(), fcalls.copy(), prog.get_constants())
         prog.close()
         err = capfd.readouterr().err
         m = re.findall(r"speculative points (\d+) evaluated, (\d+) used", err)
         assert m, err[-2000:]
-        res[spec + "_used"] = int(m[-1][1])
-    assert res["0_used"] == 0 and res["256_used"] > 0
-    a, b = res["0"], res["256"]
-    assert np.array_equal(a[0].view(np.uint64), b[0].view(np.uint64))
-    assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
-    for ca, cb in zip(a[3], b[3]):
-        assert np.array_equal(np.asarray(ca).view(np.uint64), np.asarray(cb).view(np.uint64))
+        res[spec, vt, "used"] = int(m[-1][1])
+    assert res["0", "0", "used"] == 0 and res["256", "1", "used"] > 0 and res["256", "0", "used"] > 0
+    a = res["0", "0"]
+    for key in (("0", "1"), ("256", "0"), ("256", "1")):
+        b = res[key]
+        assert np.array_equal(a[0].view(np.uint64), b[0].view(np.uint64)), key
+        assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]), key
+        for ca, cb in zip(a[3], b[3]):
+            assert np.array_equal(np.asarray(ca).view(np.uint64), np.asarray(cb).view(np.uint64)), key
