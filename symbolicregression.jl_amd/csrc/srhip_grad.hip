@@ -412,8 +412,9 @@ template <typename T> static size_t grad_lds_bytes(const GradArgs& a) {
   return (size_t)(a.nfeat + 1) * (size_t)a.rb_rows * sizeof(T);
 }
 
-// rows per lane: 2 where the register budget allows (4 tangents, stack depth 4), else 1
-template <int KT, int K> constexpr int grad_rows() { return KT <= 4 && K <= 4 ? GRAD_R : 1; }
+// rows per lane: value-only passes (no tangents) carry 4 rows per lane (one dispatch per 256-row
+// block); with tangents the register budget decides (GRAD_R)
+template <int KT, int K> constexpr int grad_rows() { return KT == 0 ? 4 : (KT <= 4 && K <= 4 ? GRAD_R : 1); }
 
 template <typename T, int KT, int K, int GM = GMODE_LOSS>
 static hipError_t launch_grad_t(const GradArgs& a, dim3 grid, hipStream_t s) {

@@ -34,9 +34,9 @@ namespace {
 // of trees: small blocks keep those launches short (many workgroups, each a few tiles deep).
 LaunchPlan grad_plan(const srhip_ctx* ctx, int64_t m, int32_t nchunks) {
   static const int rb_env = [] { const char* e = getenv("SRHIP_GRAD_RB"); return e ? atoi(e) : 0; }();
-  int rb = (rb_env >= 64 && rb_env <= 4096 && (rb_env & (rb_env - 1)) == 0) ? rb_env : 256;
+  int rb = (rb_env >= 256 && rb_env <= 4096 && (rb_env & (rb_env - 1)) == 0) ? rb_env : 256;
   m = std::max<int64_t>(1, m);
-  while (rb > 128 && rb / 2 >= m) rb /= 2;  // >= 128: two 64-row halves per lane (GRAD_R)
+  while (rb > 256 && rb / 2 >= m) rb /= 2;  // >= 256: the value-only pass runs 4 rows per lane
   LaunchPlan L{};
   L.rb_rows = rb;
   L.nrb = (int)((m + rb - 1) / rb);
