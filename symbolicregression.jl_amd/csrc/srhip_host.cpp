@@ -169,6 +169,13 @@ template <typename T> class TreeCompiler {
     dbase_ = dbase;
   }
   uint64_t dmask() const { return dmask_; }
+  // the value-dependent did_succeed metadata alone (static_fail, fill_consts, feat_checks) of a tree
+  // compiled before with other constant values: the gradient program's code does not depend on them
+  void static_info(TreeInfo& info) {
+    info = TreeInfo();
+    memo_const_.assign(nn_, -1);
+    static_checks(0, -1, info);
+  }
 
  private:
 
@@ -590,7 +597,7 @@ int compile_grad_t(srhip_program& P) {
   P.gbase.assign(P.ntrees, TreeInfo());
   for (int32_t t = 0; t < P.ntrees; ++t) {
     const TreeInfo& gi = P.ginfo[t];
-    if (!gi.static_fail && gi.fill_consts.empty()) {
+    if (!gi.static_fail) {
       int32_t nc = 0;
       for (int32_t i = 0; i < gi.code_len; ++i) {
         const Ins& ins = P.gcode[(size_t)gi.code_begin + i];
@@ -633,25 +640,25 @@ bool spec_instantiate_t(srhip_program& P, int32_t slot, int32_t t, const double*
     return false;
   TreeInfo& si = P.ginfo[(size_t)P.ntrees + slot];
   const int64_t dst = P.gspec_base + (int64_t)slot * P.gspec_stride;
-  if (!P.gspec_ok[t]) {
-    // constant subtrees fold and fail by value: compile the tree at these constants
-    const int64_t b = P.offsets[t], e = P.offsets[t + 1];
-    std::vector<srhip_node> nd(P.nodes.begin() + b, P.nodes.begin() + e);
-    const double* cp = c;
-    struct Rec {
-      static void set(std::vector<srhip_node>& v, int64_t i, const double*& c) {
-        srhip_node& n = v[(size_t)i];
-        if (n.degree == 0) {
-          if (n.constant) n.val = *c++;
-          return;
-        }
-        set(v, n.l, c);
-        if (n.degree == 2) set(v, n.r, c);
+  // the tree's nodes at the constants c (get_constants order = pre-order over constant leaves)
+  const int64_t b = P.offsets[t], e = P.offsets[t + 1];
+  std::vector<srhip_node> nd(P.nodes.begin() + b, P.nodes.begin() + e);
+  struct Rec {
+    static void set(std::vector<srhip_node>& v, int64_t i, const double*& c) {
+      srhip_node& n = v[(size_t)i];
+      if (n.degree == 0) {
+        if (n.constant) n.val = *c++;
+        return;
       }
-    };
-    Rec::set(nd, 0, cp);
+      set(v, n.l, c);
+      if (n.degree == 2) set(v, n.r, c);
+    }
+  };
+  const double* cp = c;
+  Rec::set(nd, 0, cp);
+  TreeCompiler<T> tc(nd.data(), e - b, P, 0, true);
+  if (!P.gspec_ok[t]) {  // the code's shape is not known to be value-independent: compile it
     std::vector<Ins> scratch;
-    TreeCompiler<T> tc(nd.data(), e - b, P, 0, true);
     TreeInfo gi;
     if (tc.compile(gi, scratch)) return false;
     *static_fail = gi.static_fail;
@@ -666,12 +673,13 @@ bool spec_instantiate_t(srhip_program& P, int32_t slot, int32_t t, const double*
     if (si.static_fail) si.code_len = 1;
     return true;
   }
+  // the base code with the constant immediates rewritten; metadata recomputed from the values
   const TreeInfo& base = P.gbase[t];
   if (base.code_len > P.gspec_stride) return false;
-  bool fin = true;
-  for (int32_t k = 0; k < base.nconst; ++k) fin &= m_isfinite(HostVal<T>::from(c[k]));
-  *static_fail = !fin;
-  if (!fin) {  // @return_on_check: did_succeed = false, nothing to evaluate
+  TreeInfo meta;
+  tc.static_info(meta);
+  *static_fail = meta.static_fail;
+  if (meta.static_fail) {  // @return_on_check: did_succeed = false, nothing to evaluate
     si = TreeInfo();
     si.static_fail = true;
     si.code_begin = (int32_t)dst;
@@ -682,6 +690,7 @@ bool spec_instantiate_t(srhip_program& P, int32_t slot, int32_t t, const double*
   for (int32_t j = P.gci_off[t]; j < P.gci_off[t + 1]; j += 2)
     P.gcode[(size_t)dst + P.gci[j]].imm = HostVal<T>::bits(HostVal<T>::from(c[P.gci[j + 1]]));
   si = base;
+  si.fill_consts = std::move(meta.fill_consts);
   si.code_begin = (int32_t)dst;
   lo = std::min<int64_t>(lo, dst);
   hi = std::max<int64_t>(hi, dst + base.code_len);
@@ -702,6 +711,17 @@ void grad_snapshot(srhip_program& P) {
 // gradient program was compiled with.  A tree's code depends on its own nodes only and is
 // position-independent, so an unchanged length means the new code drops into the old slot; any
 // other outcome (length change, no snapshot) returns patched = false and the caller recompiles all.
+// a tree's constant values in get_constants order (pre-order over constant leaves)
+void gather_consts_preorder(const srhip_node* nd, int64_t i, std::vector<double>& out) {
+  const srhip_node& n = nd[i];
+  if (n.degree == 0) {
+    if (n.constant) out.push_back(n.val);
+    return;
+  }
+  gather_consts_preorder(nd, n.l, out);
+  if (n.degree == 2) gather_consts_preorder(nd, n.r, out);
+}
+
 template <typename T>
 int patch_grad_t(srhip_program& P, bool& patched, int64_t& lo, int64_t& hi) {
   patched = false;
@@ -710,9 +730,10 @@ int patch_grad_t(srhip_program& P, bool& patched, int64_t& lo, int64_t& hi) {
   const size_t nslots = (size_t)P.ntrees + P.gspec_alloc;
   if (P.gsnap.empty() || P.gprog_off.size() != nslots || P.ginfo.size() != nslots ||
       P.gsnap_off.size() != (size_t)P.ntrees + 1 || (size_t)P.gsnap_off[P.ntrees] != P.gsnap.size() ||
-      P.gspec_cap != P.gspec_alloc)
+      P.gspec_cap != P.gspec_alloc || P.gspec_ok.size() != (size_t)P.ntrees || P.gci_off.size() != (size_t)P.ntrees + 1)
     return SRHIP_OK;
   std::vector<Ins> scratch;
+  std::vector<double> cvals;
   // the trees the optimiser wrote constants of (P.ghint), or all of them
   std::vector<int32_t> all;
   if (P.ghint.empty()) {
@@ -733,6 +754,25 @@ int patch_grad_t(srhip_program& P, bool& patched, int64_t& lo, int64_t& hi) {
       P.gsnap[k++] = n.val;  // the snapshot follows the patch (this tree recompiles below if dirty)
     }
     if (!dirty) continue;
+    if ((size_t)t < P.gspec_ok.size() && P.gspec_ok[t]) {
+      // the code is the full compile's with new constant immediates; the did_succeed metadata is
+      // recomputed from the new values (constant leaves' finiteness, constant subtrees folded)
+      cvals.clear();
+      gather_consts_preorder(P.nodes.data() + b, 0, cvals);
+      TreeInfo meta;
+      TreeCompiler<T>(P.nodes.data() + b, e - b, P, 0, true).static_info(meta);
+      TreeInfo& cur = P.ginfo[t];
+      const TreeInfo& base = P.gbase[t];
+      cur = base;
+      cur.static_fail = meta.static_fail;
+      cur.fill_consts = std::move(meta.fill_consts);
+      if (cur.static_fail) continue;  // skipped by the evaluation; the slot keeps its code
+      for (int32_t j = P.gci_off[t]; j < P.gci_off[t + 1]; j += 2)
+        P.gcode[(size_t)base.code_begin + P.gci[j]].imm = HostVal<T>::bits(HostVal<T>::from(cvals[P.gci[j + 1]]));
+      lo = std::min<int64_t>(lo, base.code_begin);
+      hi = std::max<int64_t>(hi, (int64_t)base.code_begin + base.code_len);
+      continue;
+    }
     scratch.clear();
     TreeCompiler<T> tc(P.nodes.data() + b, e - b, P, 0, true);
     TreeInfo gi;

@@ -178,11 +178,12 @@ struct srhip_program {
   std::vector<int32_t> ghint;
   // Speculative slots of the gradient program (the optimiser's line searches): gspec_alloc copies of
   // "a tree at other constants" after the trees' own code, gspec_stride instructions each, slot s at
-  // program index ntrees + s (gprog_off / ginfo).  A slot is instantiated from its tree's code by
-  // rewriting the constant immediates (gci: per tree, (instruction offset, constant index) pairs),
-  // for trees whose did_succeed metadata does not depend on the constants (gspec_ok: no operator
-  // over constants only) -- their TreeInfo is gbase's, failing statically iff a constant is
-  // non-finite.  gspec_cap is the optimiser's request; a full compile allocates it.
+  // program index ntrees + s (gprog_off / ginfo).  For trees whose code shape does not depend on the
+  // constant values (gspec_ok: every constant leaf is the immediate of exactly one instruction) a
+  // slot -- and the in-place patch of the tree's own code -- is the full compile's code (gbase) with
+  // the constant immediates rewritten (gci: per tree, (instruction offset, constant index) pairs) and
+  // the value-dependent did_succeed metadata recomputed (TreeCompiler::static_info); other trees are
+  // recompiled.  gspec_cap is the optimiser's request; a full compile allocates it.
   int32_t gspec_cap = 0, gspec_alloc = 0, gspec_stride = 0;
   int64_t gspec_base = 0;
   std::vector<int32_t> gci_off, gci;
@@ -210,8 +211,8 @@ int compile_program(srhip_program& P);       // eval program (+ invalidates the 
 extern thread_local double g_patch_scan_s, g_patch_copy_s;  // optimiser timing split (SRHIP_OPTIM_TIMING), per thread
 int compile_grad_program(srhip_program& P);  // gradient program, uploaded
 // Speculative slot `slot` := tree t at constants c[0 .. nconst) (get_constants order), host side;
-// false if the tree cannot be instantiated (gspec_ok).  *static_fail: a constant is non-finite in T
-// (no evaluation needed: did_succeed is false).  [lo, hi) grows by the instructions written.
+// false if the tree cannot be instantiated.  *static_fail: did_succeed is false before any row is
+// evaluated (a non-finite constant leaf or constant subtree; no evaluation needed).  [lo, hi) grows by the instructions written.
 bool spec_instantiate(srhip_program& P, int32_t slot, int32_t t, const double* c, bool* static_fail, int64_t& lo,
                       int64_t& hi);
 // sync = false: the copies stay queued on the context's stream (the caller's next evaluation, which
