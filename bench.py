@@ -340,6 +340,9 @@ def bench_c4(args):
         "mean_loss_before": float(np.mean(base[fin])), "mean_loss_after": float(np.mean(out[fin])),
         # the mean is dominated by a few overflow-scale losses; the median shows the typical tree
         "median_loss_before": float(np.median(base[fin])), "median_loss_after": float(np.median(out[fin])),
+        # a tree whose loss stays at ~1e250 fixes the arithmetic mean: the log-mean shows the whole population
+        "mean_log10_loss_before": float(np.mean(np.log10(np.maximum(base[fin], 1e-300)))),
+        "mean_log10_loss_after": float(np.mean(np.log10(np.maximum(out[fin], 1e-300)))),
         "grad_launch_ms": gdt * 1e3,
         "grad_node_row_evals_per_s": st["total_nodes"] * rows / gdt,
         "roofline": {"bound": "valu", "kernel": "srhip::grad_kernel<double, KT, K, 0>", "kernel_ms": gk_ms,
