@@ -209,14 +209,14 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_summary(kname):
-    """The committed rocprofv3 --pmc summary of this same command for the eval kernel
-    (scripts/pmc.sh + scripts/pmc_summary.py --json; separate counter passes, FETCH_SIZE doubled per
-    MI355X_MICROARCH.md): (HBM bytes per launch, VALU issue utilisation, source file).  Nones if no
-    summary for this kernel variant is committed."""
+def pmc_summary(kname, pattern="*pmc_c2*.json"):
+    """The committed rocprofv3 --pmc summary of this same command for the kernel `kname`
+    (scripts/pmc.sh / pmc_grad.sh + scripts/pmc_summary.py --json; separate counter passes,
+    FETCH_SIZE doubled per MI355X_MICROARCH.md): (HBM bytes per launch, VALU issue utilisation,
+    source file).  Nones if no summary for this kernel variant is committed."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_c2*.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
     if not files:
         return None, None, None
     try:
@@ -329,6 +329,10 @@ def bench_c4(args):
     gflops = float(rows * np.sum(opn * (1 + nconst) + 3 + 2 * nconst))
     cpu = None if args.no_cpu else cpu_c4_baseline(nodes, offs, opts, X, y, args.cpu_seconds)
     fin = np.isfinite(base)
+    # HBM bytes of the profiled gradient variant (scripts/pmc_grad.sh over scripts/grad_bench.py: the
+    # same 512 x 100k population, one full loss + gradient launch)
+    gname = "srhip::grad_kernel<double, 4, 4, 0, true, 1>"
+    gtraffic, gvalu, gsrc = pmc_summary(gname, "*pmc_grad_c4*.json")
     print(json.dumps({
         "metric": "C4 batched constant optimisation: wall time per optimize_constants over the population",
         "value": dt * 1e3, "unit": "ms", "higher_is_better": False, "n_gpus": 1, "steps": args.steps,
@@ -348,7 +352,9 @@ def bench_c4(args):
         "roofline": {"bound": "valu", "kernel": "srhip::grad_kernel<double, KT, K, 0>", "kernel_ms": gk_ms,
                      "flops_per_launch": gflops, "achieved": gflops / (gk_ms * 1e-3) / 1e12,
                      "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                     "frac": gflops / (gk_ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS, "traffic": None},
+                     "frac": gflops / (gk_ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS, "traffic": gtraffic,
+                     "traffic_kernel": gname if gtraffic is not None else None, "traffic_source": gsrc,
+                     "valu_issue_util": gvalu},
         "cpu_baseline": cpu,
     }))
 
