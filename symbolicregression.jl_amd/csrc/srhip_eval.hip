@@ -161,57 +161,54 @@ __device__ __attribute__((always_inline)) inline F2 expf2_dev(F2 x) {
   return out;
 }
 
-// Float32 cos/sin/tan over a lane's R rows.  Every row takes the fast path (|x| < 2^28 pi/2 after
-// mapping Inf/NaN and large |x| to 0); rows that are finite and large are redone by the scalar
-// srm_trigf out of line, once per call and only if some row needs it.  The same pieces as the
-// scalar srm_trigf (include/srhip_math.h), so the values are bit-identical.
+// Float32 cos/sin/tan over a lane's R rows.  Every row takes the fast path; rows outside it are
+// redone by the scalar srm_trigf out of line, once per call and only if some row needs it.  The
+// same pieces as the scalar srm_trigf (include/srhip_math.h), so the values are bit-identical.
 // (A call inside the batched body would pin its live rows to callee-saved, high-numbered VGPRs.)
-// cos / sin: rows still holding their (finite, large) argument are redone; every other row holds a
-// result in [-1, 1], so the argument itself marks the row (the inputs need not stay live).
-// tan (KIND 2): a tan result can be large, so the inputs are passed (trigf_fix_tan).
-template <int R>
-__device__ __attribute__((noinline)) RV<float, R> trigf_fix_tan(RV<float, R> v, RV<float, R> res) {
+// cos / sin: no per-row range test or select.  Large, Inf and NaN rows reduce to garbage; one
+// NaN-propagating max |x| over the lane's rows (v_maximum3_f32, half an instruction per row) tells
+// whether any row needs the scalar path, which redoes exactly the rows with !(|x| < 2^28 pi/2) from
+// the inputs (Inf / NaN -> NaN as srm_trigf).  tan (KIND 2): Inf / NaN handled inline, finite large
+// rows redone the same way.
+// Smallest float above SRM_PIO2F_BIG (not itself a float): for every float a,
+// (double)|a| < SRM_PIO2F_BIG  <=>  |a| < SRM_PIO2F_BIG_F.
+#define SRM_PIO2F_BIG_F 421657440.0f
+template <int R, int KIND>
+__device__ __attribute__((noinline)) RV<float, R> trigf_fix(RV<float, R> v, RV<float, R> res) {
   UNR for (int r = 0; r < R; ++r) {
     const float x = v[r];
-    if (x - x == 0.0f && srm_pio2f_is_big((double)x)) res[r] = srm_trigf(2, x);
-  }
-  return res;
-}
-template <int R, int KIND>
-__device__ __attribute__((noinline)) RV<float, R> trigf_fix(RV<float, R> res) {
-  UNR for (int r = 0; r < R; ++r) {
-    const float x = res[r];
-    if (x - x == 0.0f && srm_pio2f_is_big((double)x)) res[r] = srm_trigf(KIND, x);
+    if (srm_pio2f_is_big((double)x)) res[r] = srm_trigf(KIND, x);  // Inf / NaN: x - x
   }
   return res;
 }
 template <int R, int KIND>
 __device__ __attribute__((always_inline)) inline RV<float, R> trigf_rows(RV<float, R> v) {
   RV<float, R> res;
-  bool big = false;
-  UNR for (int r = 0; r < R; ++r) {
-    const float x = v[r];
-    const bool fin = __builtin_isfinite(x);
-    const double xd = (double)x;
-    const bool b = srm_pio2f_is_big(xd);  // also true for Inf / NaN
-    const bool bf = b && fin;  // finite and large: keeps x, redone out of line below
-    big |= bf;
-    if constexpr (KIND == 2) {
+  if constexpr (KIND == 2) {
+    bool big = false;
+    UNR for (int r = 0; r < R; ++r) {
+      const float x = v[r];
+      const bool fin = __builtin_isfinite(x);
+      const double xd = (double)x;
+      const bool b = srm_pio2f_is_big(xd);  // also true for Inf / NaN
+      big |= b && fin;
       double y;
       const int n = srm_rem_pio2f_fast(b ? 0.0 : xd, &y);
       const float f = srm_trigf_finish(KIND, n, y);
       res[r] = fin ? f : x - x;
-    } else {
-      // large finite rows reduce to garbage here and keep x below; Inf / NaN -> NaN through the reduction
-      const float f = sincosf_dev<KIND>(xd);
-      res[r] = bf ? x : f;
+      if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
     }
-    if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
-  }
-  if constexpr (KIND == 2) {
-    if (big) res = trigf_fix_tan<R>(v, res);
+    if (big) res = trigf_fix<R, KIND>(v, res);
   } else {
-    if (big) res = trigf_fix<R, KIND>(res);
+    float mx = 0.0f;
+    static_assert(R % 2 == 0, "row pairs");
+    UNR for (int r = 0; r < R; r += 2)
+      asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(v[r]), "v"(v[r + 1]));
+    UNR for (int r = 0; r < R; ++r) {
+      res[r] = sincosf_dev<KIND>((double)v[r]);
+      if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
+    }
+    if (!(mx < SRM_PIO2F_BIG_F)) res = trigf_fix<R, KIND>(v, res);
   }
   return res;
 }
@@ -317,8 +314,53 @@ __device__ __attribute__((always_inline)) inline F2 div2_dev(F2 n, F2 d) {
   return out;
 }
 
+// The same division without its range machinery, for operands with |n|, |d| in [2^-40, 2^40]:
+// there v_div_scale returns its operand unchanged with no scale flag (exponent difference < 96, no
+// denormal divisor, reciprocal or quotient, numerator exponent > 23), so v_div_fmas is a plain fma,
+// and v_div_fixup passes a finite normal quotient through -- the identical operation sequence on the
+// same values, 4 instead of 8 VALU instructions per row.
+__device__ __attribute__((always_inline)) inline F2 div2_inrange(F2 n, F2 d) {
+  F2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  const F2 e = __builtin_elementwise_fma(-d, r, (F2)(1.0f));
+  r = __builtin_elementwise_fma(e, r, r);
+  F2 q = n * r;
+  const F2 e2 = __builtin_elementwise_fma(-d, q, n);
+  q = __builtin_elementwise_fma(e2, r, q);
+  const F2 e3 = __builtin_elementwise_fma(-d, q, n);
+  return __builtin_elementwise_fma(e3, r, q);
+}
+constexpr float DIV_FAST_LO = 0x1p-40f, DIV_FAST_HI = 0x1p40f;
+
+// A = A / B (SWAP: B / A) over a lane's rows: the whole wave takes div2_inrange when every operand
+// of every lane is in its range (one NaN-propagating v_maximum3 and v_minimum3 of |a|, |b| per row,
+// a ballot), else the full div2_dev.  C2's population: ~5 % of (division node, tile) pairs fall back.
+template <int R, bool SWAP>
+__device__ __attribute__((always_inline)) inline void div_rows(float (&A)[R], const float (&B)[R]) {
+  float mx = 0.0f, mn = __builtin_inff();
+  UNR for (int r = 0; r < R; ++r) {
+    asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(A[r]), "v"(B[r]));
+    asm("v_minimum3_f32 %0, %1, |%2|, |%3|" : "=v"(mn) : "v"(mn), "v"(A[r]), "v"(B[r]));
+  }
+  const bool fast = mx <= DIV_FAST_HI && mn >= DIV_FAST_LO;  // false for NaN
+  if (__builtin_amdgcn_ballot_w64(!fast) == 0) {
+    UNR for (int r = 0; r < R; r += 2) {
+      const F2 a = {A[r], A[r + 1]}, b = {B[r], B[r + 1]};
+      const F2 c = SWAP ? div2_inrange(b, a) : div2_inrange(a, b);
+      A[r] = c.x;
+      A[r + 1] = c.y;
+    }
+  } else {
+    UNR for (int r = 0; r < R; r += 2) {
+      const F2 a = {A[r], A[r + 1]}, b = {B[r], B[r + 1]};
+      const F2 c = SWAP ? div2_dev(b, a) : div2_dev(a, b);
+      A[r] = c.x;
+      A[r + 1] = c.y;
+    }
+  }
+}
+
 // Specialised binary operator over a lane's rows: A = A op B (SWAP: A = B op A).  Float32 + - * /
-// run on packed row pairs (v_pk_add_f32 / v_pk_mul_f32, div2_dev: each lane rounded exactly as
+// run on packed row pairs (v_pk_add_f32 / v_pk_mul_f32, div_rows: each lane rounded exactly as
 // the scalar instruction would); the rest row by row.
 typedef F2 PkF32;
 template <typename T, int SB> __device__ __attribute__((always_inline)) inline T sb_apply(T a, T b) {
@@ -333,15 +375,16 @@ template <typename T, int SB> __device__ __attribute__((always_inline)) inline T
 }
 template <typename T, int R, int SB, bool SWAP>
 __device__ __attribute__((always_inline)) inline void bin_rows(T (&A)[R], const T (&B)[R]) {
-  if constexpr (std::is_same<T, float>::value && R % 2 == 0 &&
-                (SB == SB_ADD || SB == SB_SUB || SB == SB_MUL || SB == SB_DIV)) {
+  if constexpr (std::is_same<T, float>::value && R % 2 == 0 && SB == SB_DIV) {
+    div_rows<R, SWAP>(A, B);
+  } else if constexpr (std::is_same<T, float>::value && R % 2 == 0 &&
+                       (SB == SB_ADD || SB == SB_SUB || SB == SB_MUL)) {
     UNR for (int r = 0; r < R; r += 2) {
       const PkF32 a = {A[r], A[r + 1]}, b = {B[r], B[r + 1]};
       PkF32 c;
       if constexpr (SB == SB_ADD) c = SWAP ? b + a : a + b;
       else if constexpr (SB == SB_SUB) c = SWAP ? b - a : a - b;
-      else if constexpr (SB == SB_MUL) c = SWAP ? b * a : a * b;
-      else c = SWAP ? div2_dev(b, a) : div2_dev(a, b);
+      else c = SWAP ? b * a : a * b;
       A[r] = c.x;
       A[r + 1] = c.y;
     }

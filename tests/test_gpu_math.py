@@ -126,3 +126,69 @@ def test_device_float32_exp_bits_equal_oracle(ctx, oracle):
     nan = np.isnan(x)
     assert np.array_equal(np.isnan(got), nan)
     assert np.array_equal(got[~nan].view(np.uint32), ref[~nan].view(np.uint32))
+
+
+def test_device_float32_trig_bits_equal_oracle(ctx, oracle):
+    """Device Float32 sin / cos (no per-row range select: one max |x| per lane decides whether the
+    scalar path redoes the large / Inf / NaN rows) return the oracle's srm_sinf / srm_cosf bits on
+    every 256th bit pattern of the float range."""
+    x = (np.arange(0, 2**32, 256, dtype=np.uint64).astype(np.uint32)).view(np.float32)
+    for name in ("sin", "cos"):
+        got = _device(ctx, name, x)
+        ref = oracle.srm(name, x)
+        nan = np.isnan(ref)
+        assert np.array_equal(np.isnan(got), nan), name
+        assert np.array_equal(got[~nan].view(np.uint32), ref[~nan].view(np.uint32)), name
+
+
+def _div_operands(n):
+    """Division operand pairs: whole tiles inside the in-range fast path (|n|, |d| in [2^-40, 2^40]),
+    whole tiles of arbitrary bit patterns (zeros, subnormals, Inf, NaN, huge), and tiles that mix one
+    stray value into in-range rows (the wave falls back to the full division)."""
+    def inrange(k):
+        return (RNG.choice([-1, 1], k) * 2.0 ** RNG.uniform(-40, 40, k)).astype(np.float32)
+
+    def anybits(k):
+        return RNG.integers(0, 2**32, k, dtype=np.uint64).astype(np.uint32).view(np.float32)
+
+    q = n // 4
+    a = np.concatenate([inrange(q), anybits(q), inrange(q), inrange(q)])
+    b = np.concatenate([inrange(q), anybits(q), inrange(q), inrange(q)])
+    stray = np.array([0.0, -0.0, np.inf, np.nan, 1e-41, 3e38, 2.0**41, 2.0**-41], dtype=np.float32)
+    pos = 2 * q + RNG.choice(q, 64, replace=False)
+    a[pos[:32]] = RNG.choice(stray, 32)
+    b[pos[32:]] = RNG.choice(stray, 32)
+    a[3 * q:3 * q + 8], b[3 * q:3 * q + 8] = 2.0**40, 2.0**-40   # the range boundaries themselves
+    a[3 * q + 8:3 * q + 16], b[3 * q + 8:3 * q + 16] = -2.0**-40, -2.0**40
+    return a, b
+
+
+def test_device_float32_division_bits_equal_ieee(ctx):
+    """Float32 `/` (srhip_eval.hip div_rows: the range-free division for waves whose operands are all in
+    [2^-40, 2^40], the full v_div_scale / v_div_fixup sequence otherwise) is IEEE division bit for bit
+    (numpy's float32 division) in every instruction form: A / X, X / A, A / c, c / A, A / S, S / A."""
+    import srhip
+
+    n = 1 << 20
+    a, b = _div_operands(n)
+    one = np.ones(n, dtype=np.float32)
+    X = np.stack([a, b, one])
+    opts = srhip.Options(binary_operators=("+", "-", "*", "/"), unary_operators=())
+    x1, x2, x3 = srhip.Node("x1"), srhip.Node("x2"), srhip.Node("x3")
+    c = np.float32(0.3716)
+    trees = [x1 / x2,                      # A / X
+             x1 / (x2 * x3),               # X / A
+             x1 / srhip.Node(val=c),       # A / c
+             srhip.Node(val=c) / x2,       # c / A
+             (x1 * x3) / (x2 * x3),        # S / A or A / S
+             (x2 * x3) / ((x1 * x3) * x3)]
+    refs = [a / b, a / b, a / c, c / b, a / b, b / a]
+    nodes, offs = srhip.flatten(trees, opts, np.float32)
+    prog = srhip.Program(ctx, nodes, offs, opts, np.float32)
+    pred, _ = prog.eval_predict(srhip.DeviceDataset(ctx, X))
+    for t, ref in enumerate(refs):
+        got = pred[t]
+        nan = np.isnan(ref)
+        assert np.array_equal(np.isnan(got), nan), t
+        bad = np.nonzero(got[~nan].view(np.uint32) != ref[~nan].view(np.uint32))[0]
+        assert len(bad) == 0, (t, len(bad), a[~nan][bad[:4]], b[~nan][bad[:4]], got[~nan][bad[:4]], ref[~nan][bad[:4]])
