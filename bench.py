@@ -43,6 +43,10 @@ def parse():
     ap.add_argument("--iterations", type=int, default=0,
                     help="c1/c3: search iterations (default: c1 2 of the config's 40, c3 1)")
     ap.add_argument("--ncycles", type=int, default=0, help="c1/c3: ncycles_per_iteration (default 550)")
+    ap.add_argument("--parallelism", default="multithreading", choices=("multithreading", "multiprocessing"),
+                    help="c1/c3: islands as threads of one process, or in worker processes (:multiprocessing)")
+    ap.add_argument("--procs", type=int, default=0, help="c1/c3 multiprocessing: worker processes "
+                    "(default min(populations per GPU, 16))")
     return ap.parse_args()
 
 
@@ -429,8 +433,11 @@ def bench_search(args):
     d = srhip.Dataset(X, y)
     if dist is not None:
         dist.barrier()
+    mp = args.parallelism == "multiprocessing"
+    procs = args.procs or min(npops // world, 16)
+    skw = dict(parallelism=args.parallelism, procs=procs, devices=[local_rank]) if mp else {}
     t0 = time.perf_counter()
-    res = S.equation_search(d, None, opts, niterations=iters)
+    res = S.equation_search(d, None, opts, niterations=iters, **skw)
     dt = time.perf_counter() - t0
     if dist is not None:
         import torch
@@ -442,7 +449,7 @@ def bench_search(args):
     best = float(min(m.loss for m in front))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_search_baseline(args, c1, X, y, opts, iters, dt)
+        cpu = cpu_search_baseline(args, c1, X, y, opts, iters, dt, skw)
     if rank == 0:
         print(json.dumps({
             "metric": ("C1 equation_search (README example)" if c1 else "C3 equation_search 10M x 10 F32 islands")
@@ -454,11 +461,17 @@ def bench_search(args):
             "config": {"workload": ("C1: X=randn(2,100) F64, + * / - cos exp, populations=20" if c1 else
                                     f"C3: 10M rows x 10 features F32, {npops} populations ({npops // world} per GPU)"),
                        "iterations": iters, "populations": npops, "ncycles_per_iteration": S.search_option(opts, "ncycles_per_iteration"),
-                       "parallelism": f"islands{world}" if world > 1 else "single"},
+                       "parallelism": (f"islands{world}" if world > 1 else "single")
+                                      + (f", {procs} worker processes per GPU" if mp else ", island threads")},
             "search": {"wall_s": dt, "num_evals": res.num_evals, "evals_per_s": res.num_evals / dt,
                        "node_rows": res.node_rows, "best_loss": best,
                        "baseline_loss": float(np.mean((y.astype(np.float64) - y.mean()) ** 2)),
-                       "coalescer": res.coalescer_stats},
+                       "coalescer": res.coalescer_stats,
+                       # interpreter time (HIP events) / wall time: how busy the search keeps the GPU;
+                       # worker time (compile + upload + launch + wait) / wall time
+                       "device_busy_frac": res.coalescer_stats.get("kernel_ms", 0.0) / (dt * 1e3),
+                       "coalescer_busy_frac": res.coalescer_stats.get("busy_ms", 0.0) / (dt * 1e3),
+                       "coalesce_wait_us": int(os.environ.get("SRHIP_COALESCE_WAIT_US", "50"))},
             "cpu_baseline": cpu,
         }))
     if dist is not None:
@@ -466,9 +479,35 @@ def bench_search(args):
         dist.destroy_process_group()
 
 
-def cpu_search_baseline(args, c1, X, y, opts, iters, gpu_dt):
-    """c1: the same search (same options and seed) with the oracle scorer on the host, bounded to
-    ~cpu_seconds of iterations; c3: the oracle's multithreaded population eval on a row sample."""
+def _oracle_scorer_factory(worker, dataset, options):
+    """cpu_baseline leg of c1 under --parallelism multiprocessing: each worker scores with the oracle."""
+    return _OracleScorer(dataset, options)
+
+
+class _OracleScorer:
+    """score_func through the oracle (bench cpu_baseline only)."""
+
+    def __init__(self, d, o):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+
+        self.d, self.o, self.node_rows, self.orc = d, o, 0, oracle
+
+    def score(self, tree, complexity=None, idx=None):
+        import srhip
+
+        nodes, offs = srhip.flatten([tree], self.o, self.d.X.dtype)
+        le, _, ok, _ = self.orc.eval_loss_batch(nodes, offs, self.o.binop_codes, self.o.unaop_codes,
+                                                self.d.X, self.d.y, nthreads=1)
+        self.node_rows += len(nodes) * self.d.n
+        loss = float(le[0]) if ok[0] else float("inf")
+        return srhip.loss_to_score(loss, self.d.use_baseline, self.d.baseline_loss, tree, self.o,
+                                   complexity), loss
+
+
+def cpu_search_baseline(args, c1, X, y, opts, iters, gpu_dt, skw=None):
+    """c1: the same search (same options and seed, same island parallelism) with the oracle scorer on
+    the host, bounded to 1 iteration; c3: the oracle's multithreaded population eval on a row sample."""
     import numpy as np
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -477,22 +516,17 @@ def cpu_search_baseline(args, c1, X, y, opts, iters, gpu_dt):
     from srhip import search as S
 
     if c1:
-        class OracleScorer:
-            def __init__(self, d, o):
-                self.d, self.o, self.node_rows = d, o, 0
-
-            def score(self, tree, complexity=None, idx=None):
-                nodes, offs = srhip.flatten([tree], self.o, self.d.X.dtype)
-                le, _, ok, _ = oracle.eval_loss_batch(nodes, offs, self.o.binop_codes, self.o.unaop_codes,
-                                                      self.d.X, self.d.y, nthreads=1)
-                self.node_rows += len(nodes) * self.d.n
-                loss = float(le[0]) if ok[0] else float("inf")
-                return srhip.loss_to_score(loss, self.d.use_baseline, self.d.baseline_loss, tree, self.o,
-                                           complexity), loss
-
         d = srhip.Dataset(X, y)
         d.baseline_loss, d.use_baseline = float(np.mean((y - y.mean()) ** 2)), True
-        sc = OracleScorer(d, opts)
+        if skw:
+            # same worker processes, each scoring with the oracle (constant optimisation stays on the device)
+            t0 = time.perf_counter()
+            res = S.equation_search(d, None, opts, niterations=1, scorer_factory=_oracle_scorer_factory, **skw)
+            dt = time.perf_counter() - t0
+            return {"value": res.node_rows / dt, "unit": "node-row evals/s", "cores": skw["procs"], "kind": "port",
+                    "sample": f"1 iteration of the same search in {skw['procs']} worker processes with the oracle "
+                              f"(oracle/sr_oracle.c) as every worker's scorer, {dt:.1f} s"}
+        sc = _OracleScorer(d, opts)
         t0 = time.perf_counter()
         S.equation_search(d, None, opts, niterations=1, scorer=sc)
         dt = time.perf_counter() - t0

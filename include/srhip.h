@@ -285,6 +285,10 @@ int srhip_batcher_eval(srhip_batcher* b, const srhip_node* nodes, int64_t nnodes
 /* requests served, device launches, largest batch */
 int srhip_batcher_stats(const srhip_batcher* b, int64_t* nrequests, int64_t* nlaunches,
                         int64_t* max_batch_seen);
+/* worker wall time spent inside flushes (compile + upload + launch + wait, ms) and the summed
+ * interpreter-kernel time of its launches (HIP events, ms): kernel_ms / elapsed wall time is the
+ * device-busy fraction of a search (bench C1 / C3) */
+int srhip_batcher_timing(const srhip_batcher* b, double* busy_ms, double* kernel_ms);
 /* drains the queue (pending requests are evaluated), joins the worker */
 void srhip_batcher_destroy(srhip_batcher* b);
 

@@ -282,18 +282,17 @@ SRM_FN double srm_tan(double x) {
 }
 
 /* ---- Float32 ---------------------------------------------------------------------------------
- * Every Float32 function evaluates in Float64 and rounds once (as Julia Base does for Float32
- * sin/cos/exp: Float64 kernels, one rounding), so results are correctly rounded except when the
- * Float64 value lies within ~2^-40 relative of a Float32 rounding boundary.
+ * Float32 sin / cos / tan / log evaluate in Float64 and round once (as Julia Base does for Float32
+ * trigonometry: Float64 kernels, one rounding), so results are correctly rounded except when the
+ * Float64 value lies within the kernel's error (2^-35 sin/cos, 2^-34 tan) of a rounding boundary.
  *   sinf/cosf, |x| < 2^28 pi/2: x = k pi + y with k an integer (sin) or half-integer (cos),
- *     pi as a double pair and two fmas, |y| <= pi/2; then sin y = y P(y^2) with one degree-6
- *     polynomial (relative error < 2^-43) and the sign of (-1)^k.  One polynomial and no quadrant
+ *     pi as a double pair and two fmas, |y| <= pi/2; then sin y = y P(y^2) with one degree-5
+ *     polynomial (relative error < 2^-35) and the sign of (-1)^k.  One polynomial and no quadrant
  *     select: a SIMD lane pays for every branch of a per-row case analysis.
  *   tanf, and sinf/cosf for |x| >= 2^28 pi/2: the FreeBSD s_tanf.c / s_cosf.c scheme (reduction to
  *     [-pi/4, pi/4] by quadrant, Payne-Hanek when large, the degree-4 __kernel_cosdf/sindf
  *     polynomials, |error| < 2^-34).
- *   expf: x = k ln2 + r in Float64 (ln2 as a double pair, fma), degree-8 polynomial (< 2^-40),
- *     exact scaling by 2^k, one rounding.
+ *   expf: Julia's own Float32 algorithm (srm_expf below), not a widened one.
  *   logf: srm_log on the widened value (exact: every float is a normal double). */
 /* __kernel_cosdf / __kernel_sindf coefficients (FreeBSD k_cosf.c / k_sinf.c, |error| < 2^-34 on
  * [-pi/4, pi/4]), evaluated by fma Horner as cos y = Q_C(z), sin y = y Q_S(z), z = y^2,
@@ -344,14 +343,16 @@ SRM_FN float srm_trigf_finish(int kind, int n, double y) {
   const double r = ((n & 1) ^ kind) ? s : c;
   return (float)((q & 2) ? -r : r);
 }
-/* sin y / y = P(y^2) on |y| <= pi/2 (+1e-4): minimax on relative error, < 2^-43.5 */
+/* sin y / y = P(y^2) on |y| <= pi/2 (+1e-4): degree-5 minimax on relative error, < 2^-35.3 (Remez,
+ * regenerated in tests/test_math_accuracy.py) -- the accuracy class of Julia's own Float32 kernels
+ * (FreeBSD __kernel_sindf < 2^-37.5, __kernel_cosdf < 2^-34.1).  A Float32 result differs from the
+ * correctly rounded one only within ~2^-35 relative of a rounding boundary (< 0.1 % of arguments). */
 SRM_FN double srm_psin(double z) {
-  double p = 1.54087455323602e-10;
-  p = srm_fma(p, z, -2.503013916297275e-08);
-  p = srm_fma(p, z, 2.7556951471409603e-06);
-  p = srm_fma(p, z, -0.0001984126670887231);
-  p = srm_fma(p, z, 0.008333333320988472);
-  p = srm_fma(p, z, -0.16666666666503963);
+  double p = -2.388876069481213e-08;
+  p = srm_fma(p, z, 2.752537618509206e-06);
+  p = srm_fma(p, z, -0.0001984086805341283);
+  p = srm_fma(p, z, 0.00833333110744034);
+  p = srm_fma(p, z, -0.16666666626122995);
   return srm_fma(p, z, 1.0);
 }
 SRM_FN uint32_t srm_bitsf(float x) { uint32_t u; __builtin_memcpy(&u, &x, 4); return u; }

@@ -59,6 +59,7 @@ struct srhip_batcher {
   bool stop = false;
   int64_t n_requests = 0, max_seen = 0;
   std::atomic<int64_t> n_launches{0};
+  double busy_ms = 0.0, kernel_ms = 0.0;  // worker: wall time inside flushes, interpreter time (HIP events)
   std::thread worker;
   srhip_program* slot = nullptr;  // the long-lived program every flush recompiles (worker thread only)
 
@@ -99,6 +100,10 @@ void launch_group(srhip_batcher* b, const std::vector<Request*>& reqs, std::vect
   std::vector<uint8_t> ok(n);
   int rc = run_slot_program(b, std::move(nodes), std::move(offs), idx, loss.data(), ok.data());
   b->n_launches++;
+  if (rc == SRHIP_OK) {
+    const double k = srhip_last_kernel_ms(b->ctx);
+    if (k > 0.0) b->kernel_ms += k;  // written by the worker thread only, read under mu after flush
+  }
   if (rc != SRHIP_OK && n > 1 && rc != SRHIP_ERR_DEVICE) {
     // a malformed / unsupported tree fails the whole program: attribute errors per request
     for (const Request* r : reqs) launch_group(b, std::vector<Request*>{const_cast<Request*>(r)}, out);
@@ -118,14 +123,17 @@ void launch_group(srhip_batcher* b, const std::vector<Request*>& reqs, std::vect
 }  // namespace
 
 void srhip_batcher::flush(std::vector<Request>& batch) {
+  const auto t0 = std::chrono::steady_clock::now();
   // group by row subset (most searches: one group, idx empty)
   std::map<std::vector<int64_t>, std::vector<Request*>> groups;
   for (Request& r : batch) groups[r.idx].push_back(&r);
   std::vector<std::pair<uint64_t, Result>> out;
   out.reserve(batch.size());
   for (auto& g : groups) launch_group(this, g.second, out);
+  const double dt = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   {
     std::lock_guard<std::mutex> lk(mu);
+    busy_ms += dt;
     for (auto& kv : out) results[kv.first] = std::move(kv.second);
     n_requests += (int64_t)batch.size();
     max_seen = std::max<int64_t>(max_seen, (int64_t)batch.size());
@@ -251,6 +259,14 @@ int srhip_batcher_stats(const srhip_batcher* b, int64_t* nrequests, int64_t* nla
   if (nrequests) *nrequests = b->n_requests;
   if (nlaunches) *nlaunches = b->n_launches.load();
   if (max_batch_seen) *max_batch_seen = b->max_seen;
+  return SRHIP_OK;
+}
+
+int srhip_batcher_timing(const srhip_batcher* b, double* busy_ms, double* kernel_ms) {
+  if (!b) return fail(SRHIP_ERR_INVALID, "null batcher");
+  std::lock_guard<std::mutex> lk(const_cast<srhip_batcher*>(b)->mu);
+  if (busy_ms) *busy_ms = b->busy_ms;
+  if (kernel_ms) *kernel_ms = b->kernel_ms;
   return SRHIP_OK;
 }
 

@@ -168,16 +168,26 @@ __device__ __attribute__((always_inline)) inline F2 expf2_dev(F2 x) {
 // cos / sin: no per-row range test or select.  Large, Inf and NaN rows reduce to garbage; one
 // NaN-propagating max |x| over the lane's rows (v_maximum3_f32, half an instruction per row) tells
 // whether any row needs the scalar path, which redoes exactly the rows with !(|x| < 2^28 pi/2) from
-// the inputs (Inf / NaN -> NaN as srm_trigf).  tan (KIND 2): Inf / NaN handled inline, finite large
-// rows redone the same way.
+// the inputs (Inf / NaN -> NaN as srm_trigf).  Measured against a per-row v_cmp + v_cndmask that
+// marks the rows by keeping x (one instruction fewer per row, as the inputs need not stay live):
+// the select form was 1-2 % slower on C2 (scripts/ab.sh, round 2).  tan (KIND 2): Inf / NaN handled
+// inline, finite large rows redone the same way.
 // Smallest float above SRM_PIO2F_BIG (not itself a float): for every float a,
 // (double)|a| < SRM_PIO2F_BIG  <=>  |a| < SRM_PIO2F_BIG_F.
 #define SRM_PIO2F_BIG_F 421657440.0f
+template <int R>
+__device__ __attribute__((noinline)) RV<float, R> trigf_fix_tan(RV<float, R> v, RV<float, R> res) {
+  UNR for (int r = 0; r < R; ++r) {
+    const float x = v[r];
+    if (x - x == 0.0f && srm_pio2f_is_big((double)x)) res[r] = srm_trigf(2, x);
+  }
+  return res;
+}
 template <int R, int KIND>
 __device__ __attribute__((noinline)) RV<float, R> trigf_fix(RV<float, R> v, RV<float, R> res) {
   UNR for (int r = 0; r < R; ++r) {
     const float x = v[r];
-    if (srm_pio2f_is_big((double)x)) res[r] = srm_trigf(KIND, x);  // Inf / NaN: x - x
+    if (!(__builtin_fabsf(x) < SRM_PIO2F_BIG_F)) res[r] = srm_trigf(KIND, x);  // Inf / NaN: x - x
   }
   return res;
 }
@@ -198,10 +208,10 @@ __device__ __attribute__((always_inline)) inline RV<float, R> trigf_rows(RV<floa
       res[r] = fin ? f : x - x;
       if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
     }
-    if (big) res = trigf_fix<R, KIND>(v, res);
+    if (big) res = trigf_fix_tan<R>(v, res);
   } else {
-    float mx = 0.0f;
     static_assert(R % 2 == 0, "row pairs");
+    float mx = 0.0f;
     UNR for (int r = 0; r < R; r += 2)
       asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(v[r]), "v"(v[r + 1]));
     UNR for (int r = 0; r < R; ++r) {

@@ -105,6 +105,7 @@ SIGNATURES = {
     "srhip_batcher_eval": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, ctypes.POINTER(_dbl),
                                           ctypes.POINTER(ctypes.c_uint8)]),
     "srhip_batcher_stats": (ctypes.c_int, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
+    "srhip_batcher_timing": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "srhip_batcher_destroy": (None, [_vp]),
     "srhip_last_kernel_ms": (_dbl, [_vp]),
     "srhip_program_stats": (ctypes.c_int, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64),

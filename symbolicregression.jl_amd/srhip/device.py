@@ -323,7 +323,9 @@ class Coalescer:
     def stats(self) -> dict:
         a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         check(_lib.load().srhip_batcher_stats(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
-        return dict(requests=a.value, launches=b.value, max_batch=c.value)
+        busy, kern = ctypes.c_double(), ctypes.c_double()
+        check(_lib.load().srhip_batcher_timing(self.handle, ctypes.byref(busy), ctypes.byref(kern)))
+        return dict(requests=a.value, launches=b.value, max_batch=c.value, busy_ms=busy.value, kernel_ms=kern.value)
 
     def close(self):
         if getattr(self, "handle", None):

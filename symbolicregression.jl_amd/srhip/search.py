@@ -421,12 +421,20 @@ class DeviceScorer:
     """score_func (src/LossFunctions.jl:161-174) for one tree at a time, served by the native
     coalescer so concurrent islands share device launches."""
 
-    def __init__(self, dataset: Dataset, options, nclients: int = 0, max_batch: int = 256, max_wait_us: int = 300):
+    def __init__(self, dataset: Dataset, options, nclients: int = 0, max_batch: int = 256, max_wait_us=None,
+                 ctx=None, device_dataset=None):
+        """``ctx`` / ``device_dataset``: score on an existing context and resident dataset (a
+        :multiprocessing worker's, see task_island_iteration) instead of a new context and upload."""
+        import os
+
         from .device import Coalescer, Context
 
+        if max_wait_us is None:  # (tuning) SRHIP_COALESCE_WAIT_US
+            max_wait_us = int(os.environ.get("SRHIP_COALESCE_WAIT_US", "50"))
         self.dataset, self.options = dataset, options
-        self.ctx = Context(options.device)
-        self.ds = dataset.device(self.ctx)
+        self._own_ctx = ctx is None
+        self.ctx = Context(options.device) if ctx is None else ctx
+        self.ds = dataset.device(self.ctx) if device_dataset is None else device_dataset
         self.coalescer = Coalescer(self.ctx, self.ds, options, options.elementwise_loss, max_batch=max_batch,
                                    max_wait_us=max_wait_us, nclients=nclients)
         self.L = dataset.loss_type.type
@@ -448,8 +456,9 @@ class DeviceScorer:
 
     def close(self):
         self.coalescer.close()
-        self.dataset.release_device(self.ctx)
-        self.ctx.close()
+        if self._own_ctx:
+            self.dataset.release_device(self.ctx)
+            self.ctx.close()
 
 
 # ---- one mutation / crossover (src/Mutate.jl) ----------------------------------------------------
@@ -692,8 +701,127 @@ class SearchResult:
         return self.hall_of_fame.pareto_frontier()
 
 
+# ---- :multiprocessing islands (src/SymbolicRegression.jl:964-987) ----------
+def _worker_search(worker, key, meta, options, factory):
+    """The worker-process side of an island task: a host Dataset over the shared-memory arrays with
+    the worker's resident device copy attached (no second upload), and one scorer per dataset --
+    a coalescer on the worker's own context (one client: max_wait 0), or ``factory``'s."""
+    cache = worker.__dict__.setdefault("search", {})
+    if worker.backend == "srhip":
+        options.device = worker.device
+    st = cache.get(key)
+    if st is None:
+        X, y, w = worker.arrays[key]
+        d = Dataset(X, y, w, loss_type=meta["loss_type"])
+        d.X_units, d.y_units = meta["X_units"], meta["y_units"]
+        dev = None
+        if worker.backend == "srhip":
+            dev = worker.datasets[key]
+            d._dev[(id(worker.ctx), worker.ctx.device)] = dev
+        if factory is not None:
+            sc = factory(worker, d, options)
+        else:
+            sc = DeviceScorer(d, options, nclients=1, max_wait_us=0, ctx=worker.ctx, device_dataset=dev)
+        st = cache[key] = (d, sc)
+    d, sc = st
+    if "baseline_loss" in meta:
+        d.baseline_loss, d.use_baseline = meta["baseline_loss"], meta["use_baseline"]
+    return d, sc
+
+
+def _scorer_counters(sc):
+    c = sc.coalescer.stats() if hasattr(sc, "coalescer") else {}
+    return float(getattr(sc, "node_rows", 0)), c
+
+
+def _counter_delta(before, after):
+    (r0, c0), (r1, c1) = before, after
+    return r1 - r0, {k: c1[k] - c0.get(k, 0) for k in c1 if k != "max_batch"} | (
+        {"max_batch": c1["max_batch"]} if "max_batch" in c1 else {})
+
+
+def task_search_baseline(worker, ds, key, meta, options, factory=None):
+    """update_baseline_loss! on the worker's resident dataset: (baseline_loss, use_baseline)."""
+    d, sc = _worker_search(worker, key, meta, options, factory)
+    if factory is None:
+        update_baseline_loss(d, options)
+        return d.baseline_loss, d.use_baseline
+    _, loss = sc.score(Node(val=d.avg_y))  # the same constant tree through the factory's scorer
+    if np.isfinite(loss):
+        return d.loss_type.type(loss), True
+    return d.loss_type.type(1), False
+
+
+def task_score_trees(worker, ds, key, meta, options, trees, factory=None):
+    """score_func of each tree (an initial population): ([(score, loss)], counter deltas)."""
+    _, sc = _worker_search(worker, key, meta, options, factory)
+    before = _scorer_counters(sc)
+    out = [sc.score(t) for t in trees]
+    return out, _counter_delta(before, _scorer_counters(sc))
+
+
+def task_island_iteration(worker, ds, key, meta, options, k, rng, num_evals, pop, curmaxsize, stats,
+                          factory=None):
+    """One island iteration (s_r_cycle + optimize_and_simplify_population) in a worker process:
+    (pop, best_seen, rng, num_evals, counter deltas)."""
+    from .utils import advance_birth_order
+
+    d, sc = _worker_search(worker, key, meta, options, factory)
+    advance_birth_order(max([m.birth for m in pop], default=-1))
+    isl = Island(k, d, options, sc, rng, d.X.dtype)
+    isl.num_evals = num_evals
+    before = _scorer_counters(sc)
+    pop, best_seen = isl.run_iteration(pop, curmaxsize, stats)
+    return pop, best_seen, isl.rng, isl.num_evals, _counter_delta(before, _scorer_counters(sc))
+
+
+class _MPIslands:
+    """Head-process side: the dataset registered once on the pool, island k pinned to worker
+    k % procs (its scorer and resident dataset stay on that worker), counters summed."""
+
+    def __init__(self, pool, dataset, options, factory):
+        self.pool, self.options, self.factory = pool, options, factory
+        self.key = pool.register_dataset(dataset.X, dataset.y, dataset.weights)
+        self.meta = dict(loss_type=dataset.loss_type, X_units=dataset.X_units, y_units=dataset.y_units)
+        bl, ub = pool.submit(task_search_baseline, self.key, self.meta, options, factory, dataset=self.key,
+                             worker=0).result()
+        dataset.baseline_loss, dataset.use_baseline = bl, ub
+        self.meta.update(baseline_loss=bl, use_baseline=ub)
+        self.node_rows = 0.0
+        self.cstats = {}
+
+    def _add(self, delta):
+        rows, c = delta
+        self.node_rows += rows
+        for name, v in c.items():
+            self.cstats[name] = max(self.cstats.get(name, 0), v) if name == "max_batch" else self.cstats.get(name, 0) + v
+
+    def score_trees(self, k, trees):
+        return self.pool.submit(task_score_trees, self.key, self.meta, self.options, trees, self.factory,
+                                dataset=self.key, worker=k % self.pool.nprocs)
+
+    def scores(self, fut):
+        out, delta = fut.result()
+        self._add(delta)
+        return out
+
+    def iterate(self, isl, pop, curmaxsize, stats):
+        return self.pool.submit(task_island_iteration, self.key, self.meta, self.options, isl.k, isl.rng,
+                                isl.num_evals, pop, curmaxsize, stats, self.factory, dataset=self.key,
+                                worker=isl.k % self.pool.nprocs)
+
+    def collect(self, isl, fut):
+        from .utils import advance_birth_order
+
+        pop, best_seen, isl.rng, isl.num_evals, delta = fut.result()
+        self._add(delta)
+        advance_birth_order(max([m.birth for m in pop], default=-1))
+        return pop, best_seen
+
+
 def equation_search(X, y, options, niterations: int = 10, weights=None, seed=None, scorer=None,
-                    verbosity: int = 0, distributed=None, group=None) -> SearchResult:
+                    verbosity: int = 0, distributed=None, group=None, parallelism: str = "multithreading",
+                    procs=None, devices=None, worker_backend: str = "srhip", scorer_factory=None) -> SearchResult:
     """equation_search (src/SymbolicRegression.jl:357-1000) for one output, populations as
     concurrent island threads, every score through the device.  ``scorer`` (testing hook):
     any object with ``score(tree, complexity=None) -> (score, loss)``; default: the device
@@ -706,7 +834,19 @@ def equation_search(X, y, options, niterations: int = 10, weights=None, seed=Non
     tables (:func:`srhip.parallel.exchange_members`, an all-gather over RCCL / xGMI), fold the
     remote members into their hall of fame, all-reduce the adaptive-parsimony size counts, and
     migrate from the global candidate set (src/Migration.jl:16-38).  Islands run in lock step
-    across ranks; every rank returns the same global hall of fame."""
+    across ranks; every rank returns the same global hall of fame.
+
+    ``parallelism="multiprocessing"`` (the reference's `:multiprocessing` with `procs` workers,
+    src/SymbolicRegression.jl:964-987): every island's iteration runs in a
+    worker process of a :class:`srhip.workers.GPUWorkerPool` (``procs`` workers, default
+    min(populations, 16); worker i on ``devices[i % len(devices)]``).  The dataset is copied once into
+    shared memory and uploaded once per worker; a task carries one population (node tables) and the
+    island's RNG, and returns the evolved population, its best_seen, the RNG and its counters.  Each
+    worker scores through its own coalescer on its resident dataset, so islands no longer share one
+    interpreter lock.  Island state and processing order are those of the threaded mode, so a
+    deterministic search returns the same hall of fame either way (tests/test_gpu_search.py).
+    ``worker_backend="host"`` + ``scorer_factory(worker, dataset, options)`` (testing hook): the same
+    process machinery without a GPU (tests/test_search.py)."""
     from . import parallel
 
     dataset = X if isinstance(X, Dataset) else Dataset(X, y, weights)
@@ -723,26 +863,45 @@ def equation_search(X, y, options, niterations: int = 10, weights=None, seed=Non
     rngs = [np.random.default_rng(s) for s in ss.spawn(npops + 1)]
     head_rng = rngs[-1] if not dist_mode else np.random.default_rng([int(base_seed or 0), rank, 7919])
     local = [k for k in range(npops) if k % ws == rank]
-    own_scorer = scorer is None
-    if own_scorer:
-        if dist_mode:
-            import os
+    mp_mode = parallelism == "multiprocessing"
+    if parallelism not in ("multithreading", "multiprocessing"):
+        raise ValueError(f"parallelism {parallelism!r}")
+    if mp_mode and scorer is not None:
+        raise ValueError("parallelism='multiprocessing' scores on the workers: use scorer_factory, not scorer")
+    own_scorer = scorer is None and not mp_mode
+    if dist_mode:
+        import os
 
-            options.device = int(os.environ.get("LOCAL_RANK", options.device))
+        options.device = int(os.environ.get("LOCAL_RANK", options.device))
+    pool = mpx = None
+    if own_scorer:
         update_baseline_loss(dataset, options)
         scorer = DeviceScorer(dataset, options, nclients=len(local))
+    elif mp_mode:
+        from .workers import GPUWorkerPool
+
+        nprocs = int(procs or min(len(local), 16))
+        pool = GPUWorkerPool(nprocs, devices=devices if devices is not None else
+                             ([options.device] if worker_backend == "srhip" else None), backend=worker_backend)
+        mpx = _MPIslands(pool, dataset, options, scorer_factory)
     try:
         islands = {k: Island(k, dataset, options, scorer, rngs[k], dtype) for k in local}
         # initial populations: gen_random_tree(3, ...) scored (src/Population.jl:40-63)
         pops = {}
+        init = {}
         for k in local:
             isl = islands[k]
             trees = [gen_random_tree(3, options, dataset.nfeatures, dtype, isl.rng) for _ in range(psize)]
+            if mp_mode:
+                init[k] = (trees, mpx.score_trees(k, trees))
+                continue
             members = []
             for t in trees:
                 sc, lo = scorer.score(t)
                 members.append(PopMember(t, sc, lo))
             pops[k] = members
+        for k, (trees, fut) in init.items():
+            pops[k] = [PopMember(t, sc, lo) for t, (sc, lo) in zip(trees, mpx.scores(fut))]
         stats = RunningSearchStatistics(options)
         hof = HallOfFame(options)
         best_sub_pops = {k: [] for k in local}
@@ -813,14 +972,22 @@ def equation_search(X, y, options, niterations: int = 10, weights=None, seed=Non
             curmaxsize = get_cur_maxsize(options, total_cycles, cycles_remaining)
 
         with ThreadPoolExecutor(max_workers=max(1, len(local))) as ex:
+            def submit(k):
+                if mp_mode:
+                    return mpx.iterate(islands[k], pops[k], curmaxsize, stats)
+                return ex.submit(islands[k].run_iteration, pops[k], curmaxsize, stats)
+
+            def result(k, fut):
+                return mpx.collect(islands[k], fut) if mp_mode else fut.result()
+
             if det:
                 for it in range(niterations):
-                    futs = {k: ex.submit(islands[k].run_iteration, pops[k], curmaxsize, stats) for k in local}
+                    futs = {k: submit(k) for k in local}
                     if dist_mode:
-                        process_distributed({k: f.result() for k, f in futs.items()}, it)
+                        process_distributed({k: result(k, f) for k, f in futs.items()}, it)
                     else:
                         for k in local:
-                            pop, best_seen = futs[k].result()
+                            pop, best_seen = result(k, futs[k])
                             process(k, pop, best_seen)
                     if verbosity and rank == 0:
                         print(f"iteration {it + 1}/{niterations}: best loss "
@@ -828,29 +995,34 @@ def equation_search(X, y, options, niterations: int = 10, weights=None, seed=Non
             else:
                 # asynchronous like the reference: a finished population is processed and re-dispatched
                 remaining = {k: niterations for k in local}
-                running = {ex.submit(islands[k].run_iteration, pops[k], curmaxsize, stats): k for k in local}
+                running = {submit(k): k for k in local}
                 from concurrent.futures import FIRST_COMPLETED, wait
 
                 while running:
                     done, _ = wait(list(running), return_when=FIRST_COMPLETED)
                     for f in done:
                         k = running.pop(f)
-                        pop, best_seen = f.result()
+                        pop, best_seen = result(k, f)
                         process(k, pop, best_seen)
                         remaining[k] -= 1
                         if remaining[k] > 0:
-                            running[ex.submit(islands[k].run_iteration, pops[k], curmaxsize, stats)] = k
+                            running[submit(k)] = k
                         elif own_scorer:
                             # one client fewer: the coalescer stops waiting for this island
                             scorer.coalescer.set_clients(sum(1 for r in remaining.values() if r > 0))
         num_evals += sum(isl.num_evals for isl in islands.values())
         if dist_mode:
             num_evals = float(parallel.allreduce_np(np.array([num_evals]), "sum", group)[0])
-        cstats = scorer.coalescer.stats() if own_scorer else {}
-        node_rows = float(getattr(scorer, "node_rows", 0))
+        if mp_mode:
+            cstats, node_rows = mpx.cstats, mpx.node_rows
+        else:
+            cstats = scorer.coalescer.stats() if own_scorer else {}
+            node_rows = float(getattr(scorer, "node_rows", 0))
         if dist_mode:
             node_rows = float(parallel.allreduce_np(np.array([node_rows]), "sum", group)[0])
         return SearchResult(hof, [pops[k] for k in local], num_evals, cstats, node_rows)
     finally:
         if own_scorer:
             scorer.close()
+        if pool is not None:
+            pool.close()

@@ -94,3 +94,20 @@ def test_device_search_finds_readme_equation():
     losses, _ = srhip.eval_loss_batch([m.tree for m in front], d, o)
     for m, l in zip(front, losses):
         assert abs(l - m.loss) <= 1e-12 * max(1.0, abs(l)) or (np.isinf(l) and np.isinf(m.loss))
+
+
+def test_device_search_multiprocessing_equals_threads():
+    """parallelism='multiprocessing' on the device: 4 islands in 2 worker
+    processes, each scoring through its own coalescer on its resident dataset and optimising
+    constants on its own context, return the threaded device search's hall of fame exactly."""
+    X, y = _data()
+    o = srhip.Options(populations=4, population_size=20, ncycles_per_iteration=40, maxsize=15,
+                      deterministic=True, seed=5, **OPS)
+    threaded = S.equation_search(X, y, o, niterations=2)
+    mp = S.equation_search(X, y, o, niterations=2, parallelism="multiprocessing", procs=2, devices=[0])
+    f0 = [(srhip.string_tree(m.tree, o), m.loss) for m in threaded.pareto_frontier()]
+    f1 = [(srhip.string_tree(m.tree, o), m.loss) for m in mp.pareto_frontier()]
+    assert f0 == f1
+    assert mp.num_evals == threaded.num_evals
+    assert mp.coalescer_stats["requests"] == threaded.coalescer_stats["requests"]
+    assert mp.node_rows == threaded.node_rows

@@ -169,3 +169,29 @@ def test_float32_vs_glibc_widened_large_sample(oracle, name):
     u = _ulps32(got, ref)
     assert u.max() <= 1
     assert np.mean(u > 0) < F32_DIFFER.get(name, 0.01)
+
+
+def test_float32_sine_kernel_error():
+    """srm_psin (the Float32 sin / cos fast path's sin(y)/y = P(y^2) on |y| <= pi/2 + 1e-4) is the
+    degree-5 relative minimax its header comment states: max relative error < 2^-35 on a dense grid
+    (mpmath reference), evaluated exactly as the header's fma Horner scheme."""
+    import re
+
+    src = open(__import__("os").path.join(__import__("os").path.dirname(__file__), "..", "include",
+                                          "srhip_math.h")).read()
+    body = src[src.index("SRM_FN double srm_psin(double z) {"):]
+    body = body[:body.index("}")]
+    coef = [float(c) for c in re.findall(r"(-?\d\.\d+e[-+]\d+|-?0\.\d+)", body)]
+    assert len(coef) == 5, coef
+    mpmath.mp.prec = 100
+    ys = np.linspace(1e-6, np.pi / 2 + 1e-4, 4001)
+    worst = 0.0
+    for y in ys:
+        z = float(y) * float(y)
+        p = coef[0]
+        for c in coef[1:]:
+            p = math.fma(p, z, c) if hasattr(math, "fma") else p * z + c
+        p = p * z + 1.0
+        exact = mpmath.sin(mpmath.mpf(float(y))) / mpmath.mpf(float(y))
+        worst = max(worst, abs(float((p - exact) / exact)))
+    assert worst < 2.0 ** -35, worst

@@ -180,3 +180,33 @@ def test_search_host_logic_deterministic(oracle):
     assert f0 == f1
     best = min(m.loss for m in runs[0].pareto_frontier())
     assert best < 0.5 * np.mean((y - y.mean()) ** 2)
+
+
+def oracle_scorer_factory(worker, dataset, options):
+    """scorer_factory of the :multiprocessing test (module level: workers import it by name)."""
+    import oracle as orc
+
+    return OracleScorer(dataset, options, orc)
+
+
+def test_search_multiprocessing_equals_threads(oracle):
+    """parallelism='multiprocessing' (islands in GPUWorkerPool processes, the
+    dataset resident per worker, populations and RNGs shipped per iteration) returns exactly the
+    threaded search's hall of fame: same seeds, same island state, same processing order."""
+    X, y = _data()
+    o = srhip.Options(populations=4, population_size=20, ncycles_per_iteration=30, maxsize=15,
+                      deterministic=True, seed=3, should_optimize_constants=False, **OPS)
+    base = np.float64(np.mean((y - y.mean()) ** 2))
+    d = srhip.Dataset(X, y)
+    d.baseline_loss, d.use_baseline = base, True
+    threaded = S.equation_search(d, None, o, niterations=2, scorer=OracleScorer(d, o, oracle))
+    d2 = srhip.Dataset(X, y)
+    mp = S.equation_search(d2, None, o, niterations=2, parallelism="multiprocessing", procs=2,
+                           worker_backend="host", scorer_factory=oracle_scorer_factory)
+    assert d2.baseline_loss == base and d2.use_baseline
+    f0 = [(srhip.string_tree(m.tree, o), m.loss, m.score) for m in threaded.pareto_frontier()]
+    f1 = [(srhip.string_tree(m.tree, o), m.loss, m.score) for m in mp.pareto_frontier()]
+    assert f0 == f1
+    assert mp.num_evals == threaded.num_evals
+    for p0, p1 in zip(threaded.populations, mp.populations):
+        assert [srhip.string_tree(m.tree, o) for m in p0] == [srhip.string_tree(m.tree, o) for m in p1]
