@@ -119,30 +119,39 @@ def main():
     kern_ms = float(np.mean(kms))
     achieved = flops / (kern_ms * 1e-3) / 1e12
 
+    def timed_steps(pr):
+        """(seconds for args.steps evaluations after the warmup, max over ranks; mean kernel ms)"""
+        for _ in range(args.warmup):
+            pr.eval_loss(ds, loss)
+        barrier()
+        t0 = time.perf_counter()
+        km = []
+        for _ in range(args.steps):
+            pr.eval_loss(ds, loss)
+            km.append(ctx.last_kernel_ms())
+        barrier()
+        d = time.perf_counter() - t0
+        if dist is not None:
+            import torch
+
+            tt = torch.tensor([d], dtype=torch.float64, device=f"cuda:{local_rank}")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            d = float(tt.item())
+        return d, float(np.mean(km))
+
     # the same population without derived columns: every node of every tree evaluated by its own
     # instruction (the headline counts the U(X[f]) reads served from shared LDS columns as evaluated
     # nodes; DESIGN.md §3.1) -- reported beside it
     os.environ["SRHIP_NO_DERIVE"] = "1"
     p_plain = srhip.Program(ctx, nodes, offs, opts, np.float32)
     del os.environ["SRHIP_NO_DERIVE"]
-    for _ in range(args.warmup):
-        p_plain.eval_loss(ds, loss)
-    barrier()
-    t0 = time.perf_counter()
-    kms_plain = []
-    for _ in range(args.steps):
-        p_plain.eval_loss(ds, loss)
-        kms_plain.append(ctx.last_kernel_ms())
-    barrier()
-    dt_plain = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-
-        tt = torch.tensor([dt_plain], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt_plain = float(tt.item())
-    kern_plain = float(np.mean(kms_plain))
+    dt_plain, kern_plain = timed_steps(p_plain)
     p_plain.close()
+    # ... and without the early exit of failed trees (every row of every tree evaluated; the headline
+    # counts the skipped rows of trees that failed as evaluated, like the reference's early return)
+    os.environ["SRHIP_NO_EARLY_EXIT"] = "1"
+    dt_full, kern_full = timed_steps(prog)
+    del os.environ["SRHIP_NO_EARLY_EXIT"]
 
     # end-to-end per population (host compile of 1024 fresh trees + upload + eval)
     t0 = time.perf_counter()
@@ -205,6 +214,9 @@ def main():
                 "no_derive": {"value": work * world * args.steps / dt_plain, "kernel_ms": kern_plain,
                               "frac": flops / (kern_plain * 1e-3) / 1e12 / PEAK_FP32_TFLOPS,
                               "note": "SRHIP_NO_DERIVE=1: no derived columns, every node evaluated per tree"},
+                "no_early_exit": {"value": work * world * args.steps / dt_full, "kernel_ms": kern_full,
+                                  "frac": flops / (kern_full * 1e-3) / 1e12 / PEAK_FP32_TFLOPS,
+                                  "note": "SRHIP_NO_EARLY_EXIT=1: failed trees evaluated on every row"},
             },
         }
         print(json.dumps(out))

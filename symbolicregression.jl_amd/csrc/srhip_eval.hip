@@ -161,6 +161,30 @@ __device__ __attribute__((always_inline)) inline F2 expf2_dev(F2 x) {
   return out;
 }
 
+// The same exp for waves whose inputs all satisfy |x| <= 87 (EXPF_FAST_MAX): no clamp; n = rint(x log2 e)
+// by adding and removing 1.5 * 2^23 (the same ties-to-even rounding of the same Float32 product), and
+// 2^n (a normal float for |n| <= 126) built in the exponent field from the low bits of that sum, one
+// multiply instead of v_cvt_i32 + v_ldexp (both round the exact p 2^n once).  tools/check_expf.c
+// proves it bit-identical to srm_expf on every float in range.
+constexpr float EXPF_FAST_MAX = 87.0f;
+__device__ __attribute__((always_inline)) inline F2 expf2_fast(F2 x) {
+  const F2 t = x * (F2)(SRM_EXPF_LOG2E) + (F2)(12582912.0f);
+  const F2 n = t - (F2)(12582912.0f);
+  F2 r = __builtin_elementwise_fma(n, (F2)(SRM_EXPF_NLN2_HI), x);
+  r = __builtin_elementwise_fma(n, (F2)(SRM_EXPF_NLN2_LO), r);
+  F2 p = __builtin_elementwise_fma(r, (F2)(SRM_EXPF_C6), (F2)(SRM_EXPF_C5));
+  p = __builtin_elementwise_fma(r, p, (F2)(SRM_EXPF_C4));
+  p = __builtin_elementwise_fma(r, p, (F2)(SRM_EXPF_C3));
+  p = __builtin_elementwise_fma(r, p, (F2)(0.5f));
+  p = __builtin_elementwise_fma(r, p, (F2)(1.0f));
+  p = __builtin_elementwise_fma(r, p, (F2)(1.0f));
+  // (opaque per row: left to itself the compiler built one scale and broadcast it to both rows)
+  float s0, s1;
+  asm("v_lshl_add_u32 %0, %1, 23, 1.0" : "=v"(s0) : "v"(t.x));
+  asm("v_lshl_add_u32 %0, %1, 23, 1.0" : "=v"(s1) : "v"(t.y));
+  return p * (F2){s0, s1};
+}
+
 // Float32 cos/sin/tan over a lane's R rows.  Every row takes the fast path; rows outside it are
 // redone by the scalar srm_trigf out of line, once per call and only if some row needs it.  The
 // same pieces as the scalar srm_trigf (include/srhip_math.h), so the values are bit-identical.
@@ -229,10 +253,22 @@ __device__ __attribute__((noinline)) RV<T, R> heavy_un(RV<T, R> v) {
   if constexpr (SRHIP_TRIG_ROWS && std::is_same<T, float>::value && (U == UN_COS || U == UN_SIN || U == UN_TAN))
     return trigf_rows<R, U == UN_COS ? 0 : (U == UN_SIN ? 1 : 2)>(v);
   if constexpr (std::is_same<T, float>::value && U == UN_EXP && R % 2 == 0) {
-    UNR for (int r = 0; r < R; r += 2) {
-      const F2 e = expf2_dev((F2){v[r], v[r + 1]});
-      v[r] = e.x;
-      v[r + 1] = e.y;
+    // one NaN-propagating max |x| per row pair decides for the whole wave (false for NaN)
+    float mx = 0.0f;
+    UNR for (int r = 0; r < R; r += 2)
+      asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(v[r]), "v"(v[r + 1]));
+    if (__builtin_amdgcn_ballot_w64(!(mx <= EXPF_FAST_MAX)) == 0) {
+      UNR for (int r = 0; r < R; r += 2) {
+        const F2 e = expf2_fast((F2){v[r], v[r + 1]});
+        v[r] = e.x;
+        v[r + 1] = e.y;
+      }
+    } else {
+      UNR for (int r = 0; r < R; r += 2) {
+        const F2 e = expf2_dev((F2){v[r], v[r + 1]});
+        v[r] = e.x;
+        v[r + 1] = e.y;
+      }
     }
     return v;
   }
@@ -712,6 +748,17 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
 
     LAccT<T> lacc = 0;
     CT M = 0;
+    // another row block already saw this tree fail in this launch: nothing here can change its
+    // result (did_succeed = false, loss L(Inf)); NaN partials and check statistic stand in
+    bool failed = false;
+    if constexpr (MODE == MODE_LOSS && !kIsInt<T>) {
+      if (p.early_exit) {
+        int f = 0;
+        if (lane == 0)
+          f = __hip_atomic_load(p.fail_flag + group_base + ti, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        failed = __builtin_amdgcn_readfirstlane(f) == p.epoch;
+      }
+    }
     if constexpr (DERIVED) {
       if (p.nd > 0) {  // check statistics of the derived columns this tree reads
         uint64_t msk = p.dmask[tree];
@@ -730,7 +777,12 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
     // write-back
     LAccT<T>* lslab = reinterpret_cast<LAccT<T>*>(p.slab_loss) +
                       ((int64_t)rb * p.ntrees + group_base + ti) * __builtin_amdgcn_readfirstlane(p.cpb);
-    for (int tile = 0; tile < ntiles; ++tile) {
+    if (failed) {
+      if (lane == WAVE_LAST)
+        for (int c = 0; c < p.cpb; ++c) lslab[c] = (LAccT<T>)NAN;
+      M = (CT)NAN;
+    }
+    for (int tile = 0; tile < (failed ? 0 : ntiles); ++tile) {
       const int64_t row0 = row_base + (int64_t)tile * TILE;
       if (row0 >= p.nvalid) break;  // whole tile is padding
       const T* xt = xsrc + (int64_t)tile * TILE;
@@ -833,6 +885,18 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
     break;
           SRHIP_UNOPS(SRHIP_UN_CASE)
 #undef SRHIP_UN_CASE
+          case H_COS_NC:
+            if constexpr (un_ok<T>(UN_COS)) {
+              apply_un<T, R, UN_COS>(A);
+              if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);
+            }
+            break;
+          case H_SIN_NC:
+            if constexpr (un_ok<T>(UN_SIN)) {
+              apply_un<T, R, UN_SIN>(A);
+              if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);
+            }
+            break;
 #undef SRHIP_K_CASES
           default: break;
         }
@@ -843,10 +907,25 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
         loss_tile<T, R>(p, A, ysrc + (int64_t)tile * TILE, wsrc + (int64_t)tile * TILE, lane, row0, lacc);
         constexpr int CH = sizeof(T) == 8 ? LOSS_CHUNK_8B : LOSS_CHUNK_4B;
         static_assert(CH % TILE == 0, "a loss chunk is whole tiles");
-        if ((tile + 1) % (CH / TILE) == 0 || row0 + TILE >= p.nvalid) {  // chunk done (or last valid tile)
+        const bool flushed = (tile + 1) % (CH / TILE) == 0 || row0 + TILE >= p.nvalid;
+        if (flushed) {  // chunk done (or last valid tile)
           const LAccT<T> s = wave_sum(lacc);
           if (lane == WAVE_LAST) lslab[tile / (CH / TILE)] = s;
           lacc = 0;
+        }
+        if constexpr (!kIsInt<T>) {
+          // Early return (DynamicExpressions returns at the first bad array): a non-finite check
+          // statistic in any lane means did_succeed = false for the whole tree (the host decision
+          // fails every tree whose statistic is non-finite), so its remaining tiles in this row
+          // block cannot change any result.  The unwritten loss chunks get NaN (never read: a failed
+          // tree's loss is L(Inf)); M keeps the non-finite value the host sees.
+          if (p.early_exit && __builtin_amdgcn_ballot_w64(!(M < (CT)INFINITY)) != 0) {
+            if (lane == WAVE_LAST) {
+              for (int c = tile / (CH / TILE) + (flushed ? 1 : 0); c < p.cpb; ++c) lslab[c] = (LAccT<T>)NAN;
+              __hip_atomic_store(p.fail_flag + group_base + ti, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            break;
+          }
         }
       } else if constexpr (MODE == MODE_PRED) {
         store_pred<T, R>(p, A, tree, lane, row0);

@@ -80,6 +80,7 @@ static double op_cost(uint32_t h) {
     return sb == SB_DIV ? 10.0 : 2.0;
   }
   if (h < H_UN0) return 120.0;
+  if (h >= H_UNNC0) return 30.0;  // cos / sin without the check fold
   const int u = h - H_UN0;
   switch (u) {
     case UN_NEG: case UN_SQUARE: case UN_CUBE: case UN_ABS: case UN_RELU: case UN_SIGN:
@@ -424,7 +425,11 @@ template <typename T> class TreeCompiler {
     const srhip_node& n = nd_[i];
     if (n.degree == 1) {
       emit(n.l, base, i);
-      push_op(h_un(classify_unop(unaop(i))), 0, 0, i, parent);
+      const int u = classify_unop(unaop(i));
+      // cos / sin of an operator output need no check fold of their own (srhip_isa.h H_UNNC0); the
+      // gradient program keeps every fold
+      const bool nc = !grad_ && !leafish(n.l) && (u == UN_COS || u == UN_SIN);
+      push_op(nc ? (u == UN_COS ? H_COS_NC : H_SIN_NC) : h_un(u), 0, 0, i, parent);
       return;
     }
     int sb, hb;
@@ -1124,6 +1129,18 @@ static void finalize_precise(const srhip_program& P, const int32_t* trees, int32
 
 }  // namespace
 
+int srhip::next_fail_epoch(srhip_ctx* ctx, int64_t n, int32_t** flags, int32_t* epoch) {
+  const void* before = ctx->fail_flag.p;
+  HIP_TRY(ctx->fail_flag.ensure((size_t)std::max<int64_t>(n, 1) * sizeof(int32_t)));
+  if (ctx->fail_flag.p != before || ctx->epoch == INT32_MAX) {  // fresh buffer (or wrap): no stale epochs
+    HIP_TRY(hipMemsetAsync(ctx->fail_flag.p, 0, ctx->fail_flag.bytes, ctx->stream));
+    ctx->epoch = 0;
+  }
+  *flags = (int32_t*)ctx->fail_flag.p;
+  *epoch = ++ctx->epoch;
+  return SRHIP_OK;
+}
+
 int srhip::decide_tree(const TreeInfo& I, const srhip_program& P, int64_t nfeat, const double* sums, double chk) {
   return decide_info(I, P.dtype, P.ntrees, nfeat, sums, chk);
 }
@@ -1248,6 +1265,11 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   a.has_y = mode == MODE_LOSS ? 1 : 0;
   a.max_steps = use_d ? P->dmax_len : P->max_len;
   a.debug_stop = debug_stop();
+  a.early_exit = mode == MODE_LOSS && early_exit_on() ? 1 : 0;
+  if (a.early_exit) {
+    const int rc = next_fail_epoch(ctx, nl, &a.fail_flag, &a.epoch);
+    if (rc) return rc;
+  }
   if (trace_on()) {
     HIP_TRY(ctx->h_dbg.ensure(64 * sizeof(int32_t), hipHostMallocCoherent));
     memset(ctx->h_dbg.p, 0xff, 64 * sizeof(int32_t));

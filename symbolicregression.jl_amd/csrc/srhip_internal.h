@@ -37,6 +37,12 @@ inline int debug_stop() {
   static const int v = [] { const char* e = getenv("SRHIP_DEBUG_STOP"); return e ? atoi(e) : 0; }();
   return v;
 }
+// SRHIP_NO_EARLY_EXIT=1: interpreter waves evaluate every row of a failed tree (read per launch, so
+// a test can compare both settings in one process)
+inline bool early_exit_on() {
+  const char* e = getenv("SRHIP_NO_EARLY_EXIT");
+  return !(e && *e && *e != '0');
+}
 #define HIP_TRY(expr)                                                                             \
   do {                                                                                            \
     if (trace_on()) { fprintf(stderr, "[srhip] %s:%d %s\n", __FILE__, __LINE__, #expr); fflush(stderr); } \
@@ -117,6 +123,8 @@ struct srhip_ctx {
   srhip::DevBuf vX, vy, vw, vidx, vstats;  // gathered views (batching idx)
   srhip::DevBuf g_chunks, g_slab, g_red;   // constant-gradient launches
   srhip::HostBuf h_loss, h_chk, h_stats, h_prec, h_dbg;
+  srhip::DevBuf fail_flag;  // [order slots] int32: launch epoch in which the tree was seen to fail
+  int32_t epoch = 0;        // interpreter launches so far (MODE_LOSS with early exit)
 };
 
 struct srhip_dataset {
@@ -226,6 +234,9 @@ LaunchPlan plan_launch(const srhip_ctx* ctx, int dtype, int64_t ncols, bool weig
 // did_succeed decision of tree t from partials in the srhip_eval_loss_partials layout:
 // 0 ok, 1 fail, 2 undecided (only the sums' feature / row-count entries are read)
 int decide_tree(const TreeInfo& I, const srhip_program& P, int64_t nfeat, const double* sums, double chk);
+// the context's failed-tree marks for one early-exit launch over n trees / chunks: a fresh epoch
+// (> 0) that no stale mark can equal; the marks are zeroed on the stream when (re)allocated
+int next_fail_epoch(srhip_ctx* ctx, int64_t n, int32_t** flags, int32_t* epoch);
 int check_eval_args(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss);
 int run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
              const int64_t* idx, int64_t nidx, double* out_loss, void* out_pred, uint8_t* out_ok);

@@ -72,6 +72,11 @@ struct EvalArgs {
   const uint32_t* dspec;    // [nd] (U << 16) | feature of each derived column
   const uint64_t* dmask;    // [program trees] bit d: the tree reads derived column d
   int32_t* dbg;             // SRHIP_TRACE: host-coherent progress words of block (0,0) wave 0, else nullptr
+  int32_t early_exit;       // MODE_LOSS: a wave stops a tree's row block once its check statistic is
+                            // non-finite (the tree has failed: DynamicExpressions' early return) and
+                            // marks the tree failed for the row blocks that have not started it
+  int32_t epoch;            // this launch's mark (> 0; fail_flag[slot] == epoch: failed in this launch)
+  int32_t* fail_flag;       // [ntrees] by order slot
 };
 
 int rows_per_lane(int dtype);

@@ -77,6 +77,9 @@ def eval_loss_sharded(prog, nfeatures: int, partials, precise=None, group=None):
     """
     sums, chk = partials()
     sums = allreduce_np(sums, "sum", group)
+    # any non-finite statistic fails its tree; +Inf survives every backend's MAX (a NaN may not:
+    # fmax-style reductions drop it)
+    chk = np.where(np.isfinite(chk), chk, np.inf)
     chk = allreduce_np(chk, "max" if prog.chk_reduce_op() == "max" else "sum", group)
     loss, ok, status = prog.finalize(nfeatures, sums, chk)
     undecided = np.nonzero(status == 2)[0].astype(np.int32)

@@ -71,6 +71,27 @@ def test_c2_plain_program_equals_derived(ctx, monkeypatch):
     assert np.array_equal(aok, bok) and np.array_equal(a.view(np.uint64), b.view(np.uint64))
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_early_exit_equals_full_evaluation(ctx, monkeypatch, dtype):
+    """A wave stops a tree's row block once the check statistic is non-finite (the reference's
+    early return); SRHIP_NO_EARLY_EXIT=1 evaluates every row.  Both give the same bits and masks,
+    on the C2 population (216 of 1024 trees fail, most of them on every row block)."""
+    sr = _sr()
+    from srhip import workloads
+
+    opts, X, y, trees, nodes, offs = workloads.c2(rows=200_000)
+    if dtype == np.float64:
+        X, y = X.astype(np.float64), y.astype(np.float64)
+        nodes, offs = sr.flatten(trees, opts, np.float64)
+    ds = sr.DeviceDataset(ctx, X, y)
+    prog = sr.Program(ctx, nodes, offs, opts, dtype)
+    a, aok = prog.eval_loss(ds, sr.L2DistLoss())
+    monkeypatch.setenv("SRHIP_NO_EARLY_EXIT", "1")
+    b, bok = prog.eval_loss(ds, sr.L2DistLoss())
+    assert (~aok).sum() > 100
+    assert np.array_equal(aok, bok) and np.array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
 def test_c3_shape_matches_oracle(ctx, oracle):
     """C3's dataset (10 features x 10M rows F32) with its 64-tree population."""
     sr = _sr()

@@ -1,6 +1,7 @@
 /* Exhaustive check of the Float32 exp (include/srhip_math.h srm_expf) over all 2^32 inputs:
  *  (1) the device formulation (srhip_eval.hip expf_rows: NaN-propagating clamp to [-104, 89] instead
  *      of the branches, v_cvt_i32_f32 semantics, v_ldexp_f32) returns the same bits as srm_expf;
+ *      and so does the range-free form of waves whose inputs all lie in [-87, 87] (dev_expf_fast);
  *  (2) accuracy against glibc's double exp rounded to Float32: max ULP distance and the share of
  *      inputs whose result differs.
  * Build: gcc -O2 -march=x86-64-v3 -ffp-contract=off -fopenmp tools/check_expf.c -lm -o /tmp/check_expf */
@@ -36,6 +37,27 @@ static float dev_expf(float x0) {
   p = fmaf(r, p, 1.0f);
   return ldexpf(p, cvt_i32(n));
 }
+/* the device's range-free form for waves whose every |x| <= SRM_EXPF_FAST_MAX (srhip_eval.hip
+ * expf2_fast): n by adding and subtracting 1.5 * 2^23 (the same ties-to-even rounding of the same
+ * product as rintf), 2^n built in the exponent field from the low bits of the rounded sum, one
+ * multiply instead of ldexp (both round the exact p 2^n once) */
+#define SRM_EXPF_FAST_MAX 87.0f
+static float dev_expf_fast(float x) {
+  const float prod = x * SRM_EXPF_LOG2E;
+  const float t = prod + 12582912.0f;
+  const float n = t - 12582912.0f;
+  float r = fmaf(n, SRM_EXPF_NLN2_HI, x);
+  r = fmaf(n, SRM_EXPF_NLN2_LO, r);
+  float p = SRM_EXPF_C6;
+  p = fmaf(r, p, SRM_EXPF_C5);
+  p = fmaf(r, p, SRM_EXPF_C4);
+  p = fmaf(r, p, SRM_EXPF_C3);
+  p = fmaf(r, p, 0.5f);
+  p = fmaf(r, p, 1.0f);
+  p = fmaf(r, p, 1.0f);
+  const float scale = from_u((to_u(t) << 23) + 0x3F800000u);
+  return p * scale;
+}
 static int64_t ordered(float f) {
   const int32_t i = (int32_t)to_u(f);
   return i < 0 ? (int64_t)INT32_MIN - i : i;
@@ -52,6 +74,7 @@ int main(void) {
       continue;
     }
     if (to_u(a) != to_u(d)) ++mism;
+    if (fabsf(x) <= SRM_EXPF_FAST_MAX && to_u(a) != to_u(dev_expf_fast(x))) ++mism;
     const float cr = (float)exp((double)x);
     const long long u = llabs(ordered(a) - ordered(cr));
     ++total;
