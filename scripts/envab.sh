@@ -1,17 +1,17 @@
 #!/bin/bash
-# A/B over environment settings of one build: the bench once per "NAME=VALUE[,NAME=VALUE]" in ENVS
-# ("-" = defaults).  usage: ENVS="- SRHIP_NO_DERIVE=1" scripts/envab.sh [bench args]
+# Same-box A/B of environment settings on one build: ENVS="A=1 B=2;A=0" (';' separates settings), REPS runs each.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
+mkdir -p gpurun_out/envab
 export TMPDIR=/tmp
-i=0
-for e in ${ENVS:--}; do
-  i=$((i + 1))
-  envs=()
-  [ "$e" = "-" ] || IFS=',' read -ra envs <<< "$e"
-  env "${envs[@]}" timeout -k 10 200 python -u bench.py --steps 10 --warmup 3 --no-cpu "$@" > gpurun_out/envab_$i.log 2>&1
-  rc=$?
-  echo "[$e] rc=$rc $(python3 -c "import json,sys; d=json.loads(open('gpurun_out/envab_$i.log').read().strip().splitlines()[-1]); print('kernel_ms=%.3f ms_per_step=%.3f frac=%.4f' % (d['roofline']['kernel_ms'], d['ms_per_step'], d['roofline']['frac']))" 2>&1)"
-  [ $rc -eq 0 ] || exit $rc
+IFS=';' read -ra SETS <<< "${ENVS}"
+for rep in $(seq 1 ${REPS:-3}); do
+  i=0
+  for e in "${SETS[@]}"; do
+    i=$((i+1))
+    env $e timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-cpu ${BENCH_ARGS:-} > gpurun_out/envab/$i.$rep.json 2> gpurun_out/envab/$i.$rep.err
+    rc=$?
+    echo "[$e] rep=$rep rc=$rc $(python3 -c "import json,sys; d=json.loads(open('gpurun_out/envab/$i.$rep.json').read().strip().splitlines()[-1]); r=d['roofline']; x=d.get('extra',{}); print('kernel_ms=%.4f no_ee=%.4f derived=%.4f ms_step=%.3f' % (r['kernel_ms'], x.get('no_early_exit',{}).get('kernel_ms',0), x.get('derived_columns',{}).get('kernel_ms',0), d['ms_per_step']))" 2>&1)"
+    [ $rc -eq 0 ] || exit $rc
+  done
 done

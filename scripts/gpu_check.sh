@@ -16,7 +16,7 @@ timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > gpurun_out/bench.lo
 rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log
 [ $rc -eq 0 ] || exit $rc
 if [ "${PROFILE:-1}" = "1" ]; then
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu > gpurun_out/prof.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu --headline-only > gpurun_out/prof.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -1 gpurun_out/prof.log
 fi
 exit 0

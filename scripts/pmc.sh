@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu}
+ARGS=${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu --headline-only}
 i=0
 while read -r counters; do
   [ -z "$counters" ] && continue

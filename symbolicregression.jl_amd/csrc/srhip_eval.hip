@@ -337,6 +337,22 @@ __device__ __attribute__((always_inline)) inline void apply_heavy(T (&A)[R], con
   UNR for (int r = 0; r < R; ++r) A[r] = a[r];
 }
 
+// Check accumulator: max |v| over every operator output (NaN-propagating, v_maximum3_f32) for
+// Float32; sum of |v| * 2^-512 for Float64 (Inf/NaN propagate, cannot overflow otherwise).
+template <typename T> struct Chk {
+  using type = T;
+};
+// Float32: one v_maximum3_f32 per two rows, chained through M (the compiler's reassociation into
+// a pairwise tree costs R/2 + 2 instructions instead of R/2).
+template <int R> __device__ __attribute__((always_inline)) inline void chk_update(float& M, const float (&A)[R]) {
+  UNR for (int r = 0; r < R; r += 2)
+    asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(M) : "v"(M), "v"(A[r]), "v"(A[r + 1]));
+}
+template <int R> __device__ __attribute__((always_inline)) inline void chk_update(double& M, const double (&A)[R]) {
+  UNR for (int r = 0; r < R; ++r) M = __builtin_fma(__builtin_fabs(A[r]), 0x1p-512, M);
+}
+template <int R> __device__ __attribute__((always_inline)) inline void chk_update(int32_t&, const int32_t (&)[R]) {}
+
 // IEEE Float32 division of two rows: the compiler's own a / b expansion (v_div_scale of the
 // denominator and of the numerator, v_rcp, Newton refinement, v_div_fmas with the numerator's scale
 // flag, v_div_fixup for the special cases), with its five fma / mul steps on packed row pairs
@@ -380,12 +396,26 @@ constexpr float DIV_FAST_LO = 0x1p-40f, DIV_FAST_HI = 0x1p40f;
 // A = A / B (SWAP: B / A) over a lane's rows: the whole wave takes div2_inrange when every operand
 // of every lane is in its range (one NaN-propagating v_maximum3 and v_minimum3 of |a|, |b| per row,
 // a ballot), else the full div2_dev.  C2's population: ~5 % of (division node, tile) pairs fall back.
-template <int R, bool SWAP>
-__device__ __attribute__((always_inline)) inline void div_rows(float (&A)[R], const float (&B)[R]) {
+// M (CHK): the check statistic is folded on the full path only -- an in-range quotient is finite
+// with |q| <= 2^80, so its column sum cannot overflow (rows < 2^46) and the host decision (which
+// bounds every folded output's sum by max|v| x rows) is unchanged.
+// CONSTB: B is one wave-uniform constant, so only A's rows need the range test.
+template <int R, bool SWAP, bool CHK, bool CONSTB = false>
+__device__ __attribute__((always_inline)) inline void div_rows(float (&A)[R], const float (&B)[R], float& M) {
   float mx = 0.0f, mn = __builtin_inff();
-  UNR for (int r = 0; r < R; ++r) {
-    asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(A[r]), "v"(B[r]));
-    asm("v_minimum3_f32 %0, %1, |%2|, |%3|" : "=v"(mn) : "v"(mn), "v"(A[r]), "v"(B[r]));
+  if constexpr (CONSTB) {
+    UNR for (int r = 0; r < R; r += 2) {
+      asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(A[r]), "v"(A[r + 1]));
+      asm("v_minimum3_f32 %0, %1, |%2|, |%3|" : "=v"(mn) : "v"(mn), "v"(A[r]), "v"(A[r + 1]));
+    }
+    const float c = __builtin_fabsf(B[0]);
+    mx = __builtin_elementwise_maximum(mx, c);
+    mn = __builtin_elementwise_minimum(mn, c);
+  } else {
+    UNR for (int r = 0; r < R; ++r) {
+      asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(A[r]), "v"(B[r]));
+      asm("v_minimum3_f32 %0, %1, |%2|, |%3|" : "=v"(mn) : "v"(mn), "v"(A[r]), "v"(B[r]));
+    }
   }
   const bool fast = mx <= DIV_FAST_HI && mn >= DIV_FAST_LO;  // false for NaN
   if (__builtin_amdgcn_ballot_w64(!fast) == 0) {
@@ -402,6 +432,7 @@ __device__ __attribute__((always_inline)) inline void div_rows(float (&A)[R], co
       A[r] = c.x;
       A[r + 1] = c.y;
     }
+    if constexpr (CHK) chk_update<R>(M, A);
   }
 }
 
@@ -422,7 +453,8 @@ template <typename T, int SB> __device__ __attribute__((always_inline)) inline T
 template <typename T, int R, int SB, bool SWAP>
 __device__ __attribute__((always_inline)) inline void bin_rows(T (&A)[R], const T (&B)[R]) {
   if constexpr (std::is_same<T, float>::value && R % 2 == 0 && SB == SB_DIV) {
-    div_rows<R, SWAP>(A, B);
+    float unused = 0.0f;
+    div_rows<R, SWAP, false>(A, B, unused);
   } else if constexpr (std::is_same<T, float>::value && R % 2 == 0 &&
                        (SB == SB_ADD || SB == SB_SUB || SB == SB_MUL)) {
     UNR for (int r = 0; r < R; r += 2) {
@@ -444,22 +476,22 @@ __device__ __attribute__((always_inline)) inline void bin_rows_c(T (&A)[R], T c)
   UNR for (int r = 0; r < R; ++r) B[r] = c;
   bin_rows<T, R, SB, SWAP>(A, B);
 }
-
-// Check accumulator: max |v| over every operator output (NaN-propagating, v_maximum3_f32) for
-// Float32; sum of |v| * 2^-512 for Float64 (Inf/NaN propagate, cannot overflow otherwise).
-template <typename T> struct Chk {
-  using type = T;
-};
-// Float32: one v_maximum3_f32 per two rows, chained through M (the compiler's reassociation into
-// a pairwise tree costs R/2 + 2 instructions instead of R/2).
-template <int R> __device__ __attribute__((always_inline)) inline void chk_update(float& M, const float (&A)[R]) {
-  UNR for (int r = 0; r < R; r += 2)
-    asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(M) : "v"(M), "v"(A[r]), "v"(A[r + 1]));
+// the interpreter's operator forms: the operation and the check fold of its output
+template <typename T, int R, int SB, bool SWAP, bool CONSTB = false>
+__device__ __attribute__((always_inline)) inline void bin_rows_chk(T (&A)[R], const T (&B)[R], typename Chk<T>::type& M) {
+  if constexpr (std::is_same<T, float>::value && R % 2 == 0 && SB == SB_DIV) {
+    div_rows<R, SWAP, true, CONSTB>(A, B, M);
+  } else {
+    bin_rows<T, R, SB, SWAP>(A, B);
+    chk_update<R>(M, A);
+  }
 }
-template <int R> __device__ __attribute__((always_inline)) inline void chk_update(double& M, const double (&A)[R]) {
-  UNR for (int r = 0; r < R; ++r) M = __builtin_fma(__builtin_fabs(A[r]), 0x1p-512, M);
+template <typename T, int R, int SB, bool SWAP>
+__device__ __attribute__((always_inline)) inline void bin_rows_c_chk(T (&A)[R], T c, typename Chk<T>::type& M) {
+  T B[R];
+  UNR for (int r = 0; r < R; ++r) B[r] = c;
+  bin_rows_chk<T, R, SB, SWAP, true>(A, B, M);
 }
-template <int R> __device__ __attribute__((always_inline)) inline void chk_update(int32_t&, const int32_t (&)[R]) {}
 
 template <typename T> using LAccT = typename std::conditional<kIsInt<T>, long long, double>::type;
 
@@ -713,6 +745,20 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
   KDBG("[k] staged, ntiles=%d rb_rows=%d nvalid=%ld max_steps=%d\n", ntiles, p.rb_rows, (long)p.nvalid, p.max_steps);
   __shared__ int next_tree;  // the group's next unclaimed tree (waves claim trees dynamically)
   if (threadIdx.x == 0) next_tree = EVAL_WAVES;
+  // failed-tree marks of the group's first FLAG_SNAP trees as this workgroup starts (one coherent
+  // load per thread, in parallel, instead of a memory round trip per wave and tree): workgroups that
+  // start after another row block saw a tree fail skip it.  A stale snapshot only skips less.
+  constexpr int FLAG_SNAP = 2048;
+  constexpr bool SNAP = MODE == MODE_LOSS && !kIsInt<T>;
+  __shared__ uint8_t failed_snap[SNAP ? FLAG_SNAP : 1];
+  const int snap_base = p.group_off ? p.group_off[blockIdx.y] : (int)blockIdx.y * p.trees_per_group;
+  const int snap_n = p.group_off ? p.group_off[blockIdx.y + 1] - snap_base
+                                 : min(p.trees_per_group, p.ntrees - snap_base);
+  if constexpr (SNAP) {
+    if (p.early_exit)
+      for (int i = threadIdx.x; i < min(snap_n, FLAG_SNAP); i += blockDim.x)
+        failed_snap[i] = __hip_atomic_load(p.fail_flag + snap_base + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.epoch;
+  }
   __syncthreads();
   constexpr bool DERIVED = XLDS && !kIsInt<T> && MODE != MODE_PRECISE;
   __shared__ CT dchk[DERIVED ? DERIVE_MAX : 1];
@@ -751,13 +797,8 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
     // another row block already saw this tree fail in this launch: nothing here can change its
     // result (did_succeed = false, loss L(Inf)); NaN partials and check statistic stand in
     bool failed = false;
-    if constexpr (MODE == MODE_LOSS && !kIsInt<T>) {
-      if (p.early_exit) {
-        int f = 0;
-        if (lane == 0)
-          f = __hip_atomic_load(p.fail_flag + group_base + ti, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        failed = __builtin_amdgcn_readfirstlane(f) == p.epoch;
-      }
+    if constexpr (SNAP) {
+      if (p.early_exit && ti < FLAG_SNAP) failed = __builtin_amdgcn_readfirstlane(failed_snap[ti]) != 0;
     }
     if constexpr (DERIVED) {
       if (p.nd > 0) {  // check statistics of the derived columns this tree reads
@@ -820,8 +861,7 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       T xv[R];                                                                                     \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
-      bin_rows<T, R, SB_##NAME, false>(A, xv);                                                     \
-      chk_update<R>(M, A);                                                                         \
+      bin_rows_chk<T, R, SB_##NAME, false>(A, xv, M);                                              \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
@@ -829,33 +869,28 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       T xv[R];                                                                                     \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
-      bin_rows<T, R, SB_##NAME, true>(A, xv);                                                      \
-      chk_update<R>(M, A);                                                                         \
+      bin_rows_chk<T, R, SB_##NAME, true>(A, xv, M);                                               \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
   case h_spec(SB_##NAME, SPEC_AC):                                                                 \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
-      bin_rows_c<T, R, SB_##NAME, false>(A, imm_as<T>(ins.imm));                                   \
-      chk_update<R>(M, A);                                                                         \
+      bin_rows_c_chk<T, R, SB_##NAME, false>(A, imm_as<T>(ins.imm), M);                            \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
   case h_spec(SB_##NAME, SPEC_CA):                                                                 \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
-      bin_rows_c<T, R, SB_##NAME, true>(A, imm_as<T>(ins.imm));                                    \
-      chk_update<R>(M, A);                                                                         \
+      bin_rows_c_chk<T, R, SB_##NAME, true>(A, imm_as<T>(ins.imm), M);                             \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
     SRHIP_K_CASES(h_spec(SB_##NAME, SPEC_SA0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
-      bin_rows<T, R, SB_##NAME, true>(A, S[k]);                                                    \
-      chk_update<R>(M, A);                                                                         \
+      bin_rows_chk<T, R, SB_##NAME, true>(A, S[k], M);                                             \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     })                                                                                             \
     SRHIP_K_CASES(h_spec(SB_##NAME, SPEC_AS0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
-      bin_rows<T, R, SB_##NAME, false>(A, S[k]);                                                   \
-      chk_update<R>(M, A);                                                                         \
+      bin_rows_chk<T, R, SB_##NAME, false>(A, S[k], M);                                            \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     })
           SRHIP_SPEC_BINOPS(SRHIP_SPEC_CASE)

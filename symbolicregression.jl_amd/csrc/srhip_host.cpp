@@ -526,8 +526,10 @@ int compile_derived_t(srhip_program& P) {
   std::stable_sort(cnt.begin(), cnt.end(), [](const std::pair<uint32_t, int>& a, const std::pair<uint32_t, int>& b) {
     return a.second > b.second;
   });
+  static const int dmax_env = [] { const char* e = getenv("SRHIP_DERIVE_MAX"); return e ? atoi(e) : -1; }();
+  const int dmax = dmax_env >= 0 ? std::min(dmax_env, DERIVE_MAX) : DERIVE_MAX;
   for (const auto& e : cnt)
-    if (e.second >= DERIVE_MIN_USES && (int)P.dspec.size() < DERIVE_MAX) P.dspec.push_back(e.first);
+    if (e.second >= DERIVE_MIN_USES && (int)P.dspec.size() < dmax) P.dspec.push_back(e.first);
   if (P.dspec.empty()) return SRHIP_OK;
   for (int32_t t = 0; t < P.ntrees; ++t) {
     const int64_t b = P.offsets[t], e = P.offsets[t + 1];
@@ -1204,6 +1206,16 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     const size_t budget = ((dtype == SRHIP_F32 && R == R_F32_WIDE) || EVAL_WAVES >= 12) ? 80 * 1024 - 512 : 64 * 1024 - 512;
     L = plan_launch(ctx, dtype, P->maxfeat + nd, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R, budget);
     use_d = L.xlds;
+    // ... and only when its columns do not shrink the row block: a wave's early exit of a failed tree
+    // saves the rest of its row block, and shorter blocks lose more than the shared columns save
+    // (C2, one MI355X: 10 columns at 1024-row blocks 1.56 ms, plain program at 2048 rows 1.41 ms)
+    const char* always = getenv("SRHIP_DERIVE_ALWAYS");  // (tests: the derived program whatever the blocks)
+    if (use_d && !(always && *always && *always != '0')) {
+      const int Kp = kvariant(P->kmax);
+      const LaunchPlan Lp = plan_launch(ctx, dtype, P->maxfeat, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(),
+                                        64 * pick_rows_per_lane(dtype, Kp, mode, v.m));
+      if (Lp.xlds && Lp.rb_rows > L.rb_rows) use_d = false;
+    }
   }
   if (!use_d) {
     K = kvariant(P->kmax);

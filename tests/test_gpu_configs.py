@@ -56,14 +56,18 @@ def test_c2_bench_population_matches_oracle(ctx, oracle):
 
 
 def test_c2_plain_program_equals_derived(ctx, monkeypatch):
-    """The headline counts derived-column reads as evaluated nodes; the plain
-    program (SRHIP_NO_DERIVE=1) evaluates every node and returns the same bits."""
+    """Derived columns (forced with SRHIP_DERIVE_ALWAYS=1 -- C2's launch prefers the
+    plain program's longer row blocks) return the same bits as the plain program (SRHIP_NO_DERIVE=1),
+    which evaluates every node."""
     sr = _sr()
     from srhip import workloads
 
     opts, X, y, _, nodes, offs = workloads.c2()
     ds = sr.DeviceDataset(ctx, X, y)
-    a, aok = sr.Program(ctx, nodes, offs, opts, np.float32).eval_loss(ds, sr.L2DistLoss())
+    monkeypatch.setenv("SRHIP_DERIVE_ALWAYS", "1")
+    dprog = sr.Program(ctx, nodes, offs, opts, np.float32)
+    assert len(dprog.derived_columns()) == 10
+    a, aok = dprog.eval_loss(ds, sr.L2DistLoss())
     monkeypatch.setenv("SRHIP_NO_DERIVE", "1")
     plain = sr.Program(ctx, nodes, offs, opts, np.float32)
     assert plain.derived_columns() == []
