@@ -40,11 +40,6 @@ struct GradArgs {
   // per-row modes: out_der[row + j][nvalid] for the components c0 + j < end (the values come from the
   // evaluator, which also decides did_succeed)
   void* out_der;
-  // value-only loss launches (KT = 0): a wave stops at the first tile whose check statistic is
-  // non-finite (the point fails: L(Inf)) and marks the chunk, so row blocks that start it later skip it
-  int32_t early_exit;
-  int32_t epoch;
-  int32_t* fail_flag;  // [nchunks]
 };
 
 // kt = tangent components per chunk: 4 or GRAD_KT (the slab / reduced layout stride is kt + 2)

@@ -257,20 +257,7 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
     double gacc[KT > 0 ? KT : 1];
     UNR for (int j = 0; j < KT; ++j) gacc[j] = 0.0;
     T M = T(0);
-    constexpr bool EE = GM == GMODE_LOSS && KT == 0;
-    bool failed = false;
-    if constexpr (EE) {
-      if (p.early_exit) {  // another row block already saw this point fail in this launch
-        int f = 0;
-        if (lane == 0) f = __hip_atomic_load(p.fail_flag + chunk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        failed = __builtin_amdgcn_readfirstlane(f) == p.epoch;
-        if (failed) {
-          M = T(NAN);
-          lacc = NAN;
-        }
-      }
-    }
-    for (int tile = 0; tile < (failed ? 0 : ntiles); ++tile) {
+    for (int tile = 0; tile < ntiles; ++tile) {
       const int tb = tile * 64 * R;  // block-relative first row of the tile
       if (row_base + tb >= p.nvalid) break;
       // rows up to ld are finite replicas; masked at the loss
@@ -377,14 +364,6 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
           }
           lacc += (double)l;
           UNR for (int j = 0; j < KT; ++j) gacc[j] += (double)(dl * A[r].d[j]);
-        }
-      }
-      if constexpr (EE) {
-        // non-finite statistic in any lane: the point has failed (the host returns L(Inf) and reads
-        // no gradient of a value-only point), the rest of this row block cannot change that
-        if (p.early_exit && __builtin_amdgcn_ballot_w64(!(M < T(INFINITY))) != 0) {
-          if (lane == 0) __hip_atomic_store(p.fail_flag + chunk, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
         }
       }
     }

@@ -896,25 +896,32 @@ int srhip::compile_program(srhip_program& P) {
 
 int srhip::upload_program(srhip_program& P, bool sync) {
   HIP_TRY(hipSetDevice(P.ctx->device));
-  HIP_TRY(P.d_code.ensure(P.code.size() * sizeof(Ins)));
-  HIP_TRY(P.d_off.ensure(std::max<size_t>(1, P.prog_off.size()) * sizeof(int32_t)));
-  HIP_TRY(hipMemcpyAsync(P.d_code.p, P.code.data(), P.code.size() * sizeof(Ins), hipMemcpyHostToDevice, P.ctx->stream));
-  if (!P.prog_off.empty())
-    HIP_TRY(hipMemcpyAsync(P.d_off.p, P.prog_off.data(), P.prog_off.size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                           P.ctx->stream));
-  if (!P.dspec.empty()) {
-    HIP_TRY(P.d_dcode.ensure(P.dcode.size() * sizeof(Ins)));
-    HIP_TRY(P.d_doff.ensure(P.dprog_off.size() * sizeof(int32_t)));
-    HIP_TRY(P.d_dspec.ensure(P.dspec.size() * sizeof(uint32_t)));
-    HIP_TRY(P.d_dmask.ensure(P.dmask.size() * sizeof(uint64_t)));
-    HIP_TRY(hipMemcpyAsync(P.d_dcode.p, P.dcode.data(), P.dcode.size() * sizeof(Ins), hipMemcpyHostToDevice, P.ctx->stream));
-    HIP_TRY(hipMemcpyAsync(P.d_doff.p, P.dprog_off.data(), P.dprog_off.size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                           P.ctx->stream));
-    HIP_TRY(hipMemcpyAsync(P.d_dspec.p, P.dspec.data(), P.dspec.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                           P.ctx->stream));
-    HIP_TRY(hipMemcpyAsync(P.d_dmask.p, P.dmask.data(), P.dmask.size() * sizeof(uint64_t), hipMemcpyHostToDevice,
-                           P.ctx->stream));
-  }
+  // one host image and one copy (each hipMemcpyAsync costs a few us of API time and a blit on the
+  // stream: the coalescer uploads a small program per flush)
+  auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
+  const bool der = !P.dspec.empty();
+  const size_t n_code = P.code.size() * sizeof(Ins), n_off = P.prog_off.size() * sizeof(int32_t);
+  const size_t n_dcode = der ? P.dcode.size() * sizeof(Ins) : 0, n_doff = der ? P.dprog_off.size() * sizeof(int32_t) : 0;
+  const size_t n_dspec = der ? P.dspec.size() * sizeof(uint32_t) : 0, n_dmask = der ? P.dmask.size() * sizeof(uint64_t) : 0;
+  const size_t o_off = al(n_code), o_dcode = o_off + al(n_off), o_doff = o_dcode + al(n_dcode);
+  const size_t o_dspec = o_doff + al(n_doff), o_dmask = o_dspec + al(n_dspec), total = std::max<size_t>(16, o_dmask + al(n_dmask));
+  P.blob.assign(total, 0);
+  uint8_t* h = P.blob.data();
+  if (n_code) memcpy(h, P.code.data(), n_code);
+  if (n_off) memcpy(h + o_off, P.prog_off.data(), n_off);
+  if (n_dcode) memcpy(h + o_dcode, P.dcode.data(), n_dcode);
+  if (n_doff) memcpy(h + o_doff, P.dprog_off.data(), n_doff);
+  if (n_dspec) memcpy(h + o_dspec, P.dspec.data(), n_dspec);
+  if (n_dmask) memcpy(h + o_dmask, P.dmask.data(), n_dmask);
+  HIP_TRY(P.d_prog.ensure(total));
+  HIP_TRY(hipMemcpyAsync(P.d_prog.p, h, total, hipMemcpyHostToDevice, P.ctx->stream));
+  const uint8_t* d = (const uint8_t*)P.d_prog.p;
+  P.code_dev = (const Ins*)d;
+  P.off_dev = (const int32_t*)(d + o_off);
+  P.dcode_dev = der ? (const Ins*)(d + o_dcode) : nullptr;
+  P.doff_dev = der ? (const int32_t*)(d + o_doff) : nullptr;
+  P.dspec_dev = der ? (const uint32_t*)(d + o_dspec) : nullptr;
+  P.dmask_dev = der ? (const uint64_t*)(d + o_dmask) : nullptr;
   if (sync) HIP_TRY(hipStreamSynchronize(P.ctx->stream));
   return SRHIP_OK;
 }
@@ -1245,17 +1252,17 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   const int cpb = L.rb_rows / loss_chunk(dtype);  // loss chunks per row block (row blocks are whole chunks)
   HIP_TRY(ctx->slab_loss.ensure((size_t)nl * L.nrb * cpb * 8));
   HIP_TRY(ctx->slab_chk.ensure((size_t)nl * L.nrb * 8));
-  HIP_TRY(ctx->red_loss.ensure((size_t)nt * 8));
-  HIP_TRY(ctx->red_chk.ensure((size_t)nt * 8));
-  HIP_TRY(ctx->h_loss.ensure((size_t)nt * 8));
-  HIP_TRY(ctx->h_chk.ensure((size_t)nt * 8));
+  // the reduction writes the per-tree results straight into coherent pinned host memory (no
+  // device-to-host copies on the stream)
+  HIP_TRY(ctx->h_loss.ensure((size_t)nt * 8, hipHostMallocCoherent));
+  HIP_TRY(ctx->h_chk.ensure((size_t)nt * 8, hipHostMallocCoherent));
   EvalArgs a{};
-  a.code = (const Ins*)(use_d ? P->d_dcode.p : P->d_code.p);
-  a.prog_off = (const int32_t*)(use_d ? P->d_doff.p : P->d_off.p);
+  a.code = use_d ? P->dcode_dev : P->code_dev;
+  a.prog_off = use_d ? P->doff_dev : P->off_dev;
   a.order = (const int32_t*)d_order;
   a.nd = use_d ? nd : 0;
-  a.dspec = use_d ? (const uint32_t*)P->d_dspec.p : nullptr;
-  a.dmask = use_d ? (const uint64_t*)P->d_dmask.p : nullptr;
+  a.dspec = use_d ? P->dspec_dev : nullptr;
+  a.dmask = use_d ? P->dmask_dev : nullptr;
   a.X = v.X;
   a.y = v.y;
   a.w = weighted ? v.w : nullptr;
@@ -1323,12 +1330,8 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   }
   HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, nch, cpb,
                         dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p, L.nrb, nl, (const int32_t*)d_order,
-                        mode == MODE_LOSS ? ctx->red_loss.p : nullptr, dtype == SRHIP_I32 ? nullptr : ctx->red_chk.p,
+                        mode == MODE_LOSS ? ctx->h_loss.p : nullptr, dtype == SRHIP_I32 ? nullptr : ctx->h_chk.p,
                         ctx->stream));
-  if (mode == MODE_LOSS)
-    HIP_TRY(hipMemcpyAsync(ctx->h_loss.p, ctx->red_loss.p, (size_t)nt * 8, hipMemcpyDeviceToHost, ctx->stream));
-  if (dtype != SRHIP_I32)
-    HIP_TRY(hipMemcpyAsync(ctx->h_chk.p, ctx->red_chk.p, (size_t)nt * 8, hipMemcpyDeviceToHost, ctx->stream));
   if (mode == MODE_PRED)
     HIP_TRY(hipMemcpyAsync(out_pred, pred.p, (size_t)nt * v.m * es, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -1359,8 +1362,8 @@ static int eval_precise(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pro
   HIP_TRY(ctx->order_prec.ensure((size_t)nu * sizeof(int32_t)));
   HIP_TRY(hipMemcpyAsync(ctx->order_prec.p, trees, (size_t)nu * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
   EvalArgs a{};
-  a.code = (const Ins*)(grad ? P->d_gcode.p : P->d_code.p);
-  a.prog_off = (const int32_t*)(grad ? P->d_goff.p : P->d_off.p);
+  a.code = grad ? (const Ins*)P->d_gcode.p : P->code_dev;
+  a.prog_off = grad ? (const int32_t*)P->d_goff.p : P->off_dev;
   a.order = (const int32_t*)ctx->order_prec.p;
   a.X = v.X;
   a.ld = v.ld;

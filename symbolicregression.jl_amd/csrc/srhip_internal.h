@@ -119,7 +119,7 @@ struct srhip_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   int num_cu = 256;
-  srhip::DevBuf slab_loss, slab_chk, red_loss, red_chk, slab_prec, order_prec;
+  srhip::DevBuf slab_loss, slab_chk, slab_prec, order_prec;
   srhip::DevBuf vX, vy, vw, vidx, vstats;  // gathered views (batching idx)
   srhip::DevBuf g_chunks, g_slab, g_red;   // constant-gradient launches
   srhip::HostBuf h_loss, h_chk, h_stats, h_prec, h_dbg;
@@ -152,7 +152,12 @@ struct srhip_program {
   int32_t kmax = 0, max_ops = 0, max_len = 0;
   int64_t total_nodes = 0, total_ops = 0;
   int32_t maxfeat = 0;  // largest feature index any tree reads (the columns a launch stages)
-  srhip::DevBuf d_code, d_off;
+  // device copy of the evaluation program, one buffer and one upload (upload_program):
+  // [code | prog_off | dcode | dprog_off | dspec | dmask], 16-byte aligned sections
+  srhip::DevBuf d_prog;
+  std::vector<uint8_t> blob;  // its host image (alive until the next upload)
+  const srhip::Ins* code_dev = nullptr;
+  const int32_t* off_dev = nullptr;
   // derived-column program (srhip_isa.h): the same trees with U(X[f]) leaves reading LDS columns;
   // used by loss / prediction launches whose staging fits LDS, the plain program otherwise
   std::vector<uint32_t> dspec;  // [nd] (U << 16) | (feature - 1)
@@ -161,7 +166,10 @@ struct srhip_program {
   std::vector<int32_t> dprog_off;
   std::vector<double> dcost;
   int32_t dkmax = 0, dmax_len = 0;
-  srhip::DevBuf d_dcode, d_doff, d_dspec, d_dmask;
+  const srhip::Ins* dcode_dev = nullptr;
+  const int32_t* doff_dev = nullptr;
+  const uint32_t* dspec_dev = nullptr;
+  const uint64_t* dmask_dev = nullptr;
   // launch schedule cache: the cost-sorted tree order of the last plan (groups, tpg, derived),
   // resident on the device; a program evaluated again with the same plan skips the sort and upload
   mutable std::mutex ord_mu;

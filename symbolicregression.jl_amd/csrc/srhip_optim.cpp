@@ -230,11 +230,6 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     a.loss_p0 = loss->p0;
     a.weighted = weighted ? 1 : 0;
     a.max_steps = P->gmax_len;
-    if (ps.kt == 0 && early_exit_on()) {
-      a.early_exit = 1;
-      const int rc = next_fail_epoch(ctx, nch, &a.fail_flag, &a.epoch);
-      if (rc) return rc;
-    }
     if (first) HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));  // srhip_last_kernel_ms: the gradient kernels
     first = false;
     HIP_TRY(launch_grad(dtype, K, ps.kt, a, dim3(ps.L.nrb, ps.L.groups), ctx->stream));

@@ -332,12 +332,10 @@ def test_speculative_trials_equal_sequential(ctx, dtype, monkeypatch, capfd):
     ds = sr.DeviceDataset(ctx, X, y)
     loss = sr.L2DistLoss()
     res = {}
-    # (speculative slots, value-only trials): the plain pipeline first; ("256", "1n"): value-only
-    # launches without their early exit of failed points (SRHIP_NO_EARLY_EXIT=1)
-    for spec, vt in (("0", "0"), ("0", "1"), ("256", "0"), ("256", "1"), ("256", "1n")):
+    # (speculative slots, value-only trials): the plain pipeline first
+    for spec, vt in (("0", "0"), ("0", "1"), ("256", "0"), ("256", "1")):
         monkeypatch.setenv("SRHIP_OPTIM_SPEC", spec)
-        monkeypatch.setenv("SRHIP_OPTIM_VALUE_TRIALS", vt[0])
-        monkeypatch.setenv("SRHIP_NO_EARLY_EXIT", "1" if vt == "1n" else "0")
+        monkeypatch.setenv("SRHIP_OPTIM_VALUE_TRIALS", vt)
         monkeypatch.setenv("SRHIP_OPTIM_TIMING", "2")
         prog = sr.Program(ctx, nodes, offs, opts, dtype)
         out, improved, fcalls = prog.optimize_constants(ds, loss, iterations=8, nrestarts=2, seed=5)
@@ -349,7 +347,7 @@ def test_speculative_trials_equal_sequential(ctx, dtype, monkeypatch, capfd):
         res[spec, vt, "used"] = int(m[-1][1])
     assert res["0", "0", "used"] == 0 and res["256", "1", "used"] > 0 and res["256", "0", "used"] > 0
     a = res["0", "0"]
-    for key in (("0", "1"), ("256", "0"), ("256", "1"), ("256", "1n")):
+    for key in (("0", "1"), ("256", "0"), ("256", "1")):
         b = res[key]
         assert np.array_equal(a[0].view(np.uint64), b[0].view(np.uint64)), key
         assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]), key
