@@ -524,7 +524,8 @@ class _OracleScorer:
 
 def cpu_search_baseline(args, c1, X, y, opts, iters, gpu_dt, skw=None):
     """c1: the same search (same options and seed, same island parallelism) with the oracle scorer on
-    the host, bounded to 1 iteration; c3: the oracle's multithreaded population eval on a row sample."""
+    the host, over the device run's iterations (threaded islands; 1 iteration with worker processes); c3: the
+    oracle's multithreaded population eval on a row sample."""
     import numpy as np
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -543,12 +544,14 @@ def cpu_search_baseline(args, c1, X, y, opts, iters, gpu_dt, skw=None):
             return {"value": res.node_rows / dt, "unit": "node-row evals/s", "cores": skw["procs"], "kind": "port",
                     "sample": f"1 iteration of the same search in {skw['procs']} worker processes with the oracle "
                               f"(oracle/sr_oracle.c) as every worker's scorer, {dt:.1f} s"}
+        # the same iterations as the device run: tree sizes grow over a search, and the oracle's cost
+        # per evaluation grows with them while the device's (latency-bound at 100 rows) does not
         sc = _OracleScorer(d, opts)
         t0 = time.perf_counter()
-        S.equation_search(d, None, opts, niterations=1, scorer=sc)
+        S.equation_search(d, None, opts, niterations=iters, scorer=sc)
         dt = time.perf_counter() - t0
         return {"value": sc.node_rows / dt, "unit": "node-row evals/s", "cores": 1, "kind": "port",
-                "sample": f"1 iteration of the same search (20 populations, Python islands) with the "
+                "sample": f"{iters} iteration(s) of the same search (20 populations, Python islands) with the "
                           f"oracle (oracle/sr_oracle.c) as scorer, {dt:.1f} s"}
     from srhip import workloads
 

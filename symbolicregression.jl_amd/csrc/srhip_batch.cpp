@@ -81,7 +81,7 @@ int run_slot_program(srhip_batcher* b, std::vector<srhip_node>&& nodes, std::vec
   P.offsets = std::move(offs);
   int rc = compile_program(P);
   if (rc) return rc;
-  rc = upload_program(P, false);
+  rc = upload_program(P, false, true);  // uploaded with the launch's tree order, one copy
   if (rc) return rc;
   return srhip_eval_loss(b->ctx, b->ds, &P, &b->loss, idx.empty() ? nullptr : idx.data(), (int64_t)idx.size(), loss, ok);
 }

@@ -818,10 +818,12 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
     // write-back
     LAccT<T>* lslab = reinterpret_cast<LAccT<T>*>(p.slab_loss) +
                       ((int64_t)rb * p.ntrees + group_base + ti) * __builtin_amdgcn_readfirstlane(p.cpb);
+    LAccT<T> csum = 0;  // fused launches: this lane's share of the tree's chunk sums
     if (failed) {
       if (lane == WAVE_LAST)
         for (int c = 0; c < p.cpb; ++c) lslab[c] = (LAccT<T>)NAN;
       M = (CT)NAN;
+      csum = (LAccT<T>)NAN;
     }
     for (int tile = 0; tile < (failed ? 0 : ntiles); ++tile) {
       const int64_t row0 = row_base + (int64_t)tile * TILE;
@@ -945,7 +947,12 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
         const bool flushed = (tile + 1) % (CH / TILE) == 0 || row0 + TILE >= p.nvalid;
         if (flushed) {  // chunk done (or last valid tile)
           const LAccT<T> s = wave_sum(lacc);
-          if (lane == WAVE_LAST) lslab[tile / (CH / TILE)] = s;
+          const int ci = tile / (CH / TILE);
+          if (lane == WAVE_LAST) lslab[ci] = s;
+          if (p.fused) {  // reduce_kernel's lane-strided accumulation: lane c % 64 adds chunk c
+            const LAccT<T> sb = __shfl(s, WAVE_LAST);
+            if (lane == ci % 64) csum += sb;
+          }
           lacc = 0;
         }
         if constexpr (!kIsInt<T>) {
@@ -955,6 +962,7 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
           // block cannot change any result.  The unwritten loss chunks get NaN (never read: a failed
           // tree's loss is L(Inf)); M keeps the non-finite value the host sees.
           if (p.early_exit && __builtin_amdgcn_ballot_w64(!(M < (CT)INFINITY)) != 0) {
+            csum = (LAccT<T>)NAN;
             if (lane == WAVE_LAST) {
               for (int c = tile / (CH / TILE) + (flushed ? 1 : 0); c < p.cpb; ++c) lslab[c] = (LAccT<T>)NAN;
               __hip_atomic_store(p.fail_flag + group_base + ti, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -973,6 +981,30 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
     if constexpr (!kIsInt<T> && MODE != MODE_PRECISE) {
       M = wave_chk(M);
       if (lane == WAVE_LAST) reinterpret_cast<CT*>(p.slab_chk)[(int64_t)rb * p.ntrees + group_base + ti] = M;
+    }
+    if constexpr (MODE != MODE_PRECISE) {
+      if (p.fused) {  // the only row block: reduce_kernel's steps for this tree, same order, same bits
+        LAccT<T> s = csum;
+        CT m = 0;
+        if constexpr (!kIsInt<T>) {
+          const CT mb = __shfl(M, WAVE_LAST);  // reduce_kernel's lane 0 reads row block 0
+          if (lane == 0) {
+            if constexpr (sizeof(T) == 4) m = __builtin_elementwise_maximum(m, mb);
+            else m += mb;
+          }
+        }
+        UNR for (int o = 32; o > 0; o >>= 1) {
+          if (MODE == MODE_LOSS) s += __shfl_xor(s, o);
+          if constexpr (!kIsInt<T>) {
+            if constexpr (sizeof(T) == 4) m = __builtin_elementwise_maximum(m, __shfl_xor(m, o));
+            else m += __shfl_xor(m, o);
+          }
+        }
+        if (lane == 0) {
+          if (MODE == MODE_LOSS && p.fused_loss) reinterpret_cast<LAccT<T>*>(p.fused_loss)[tree] = s;
+          if (p.fused_chk) reinterpret_cast<CT*>(p.fused_chk)[tree] = m;
+        }
+      }
     }
     KMARK(8 + wave, 13);
     int claim = 0;

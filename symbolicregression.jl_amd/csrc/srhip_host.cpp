@@ -894,7 +894,19 @@ int srhip::compile_program(srhip_program& P) {
   }
 }
 
-int srhip::upload_program(srhip_program& P, bool sync) {
+// device pointers of the program's sections inside d_prog (blob_off layout)
+static void set_prog_pointers(const srhip_program& P) {
+  const uint8_t* d = (const uint8_t*)P.d_prog.p;
+  const bool der = !P.dspec.empty();
+  P.code_dev = (const Ins*)d;
+  P.off_dev = (const int32_t*)(d + P.blob_off[0]);
+  P.dcode_dev = der ? (const Ins*)(d + P.blob_off[1]) : nullptr;
+  P.doff_dev = der ? (const int32_t*)(d + P.blob_off[2]) : nullptr;
+  P.dspec_dev = der ? (const uint32_t*)(d + P.blob_off[3]) : nullptr;
+  P.dmask_dev = der ? (const uint64_t*)(d + P.blob_off[4]) : nullptr;
+}
+
+int srhip::upload_program(srhip_program& P, bool sync, bool defer) {
   HIP_TRY(hipSetDevice(P.ctx->device));
   // one host image and one copy (each hipMemcpyAsync costs a few us of API time and a blit on the
   // stream: the coalescer uploads a small program per flush)
@@ -913,15 +925,16 @@ int srhip::upload_program(srhip_program& P, bool sync) {
   if (n_doff) memcpy(h + o_doff, P.dprog_off.data(), n_doff);
   if (n_dspec) memcpy(h + o_dspec, P.dspec.data(), n_dspec);
   if (n_dmask) memcpy(h + o_dmask, P.dmask.data(), n_dmask);
+  const size_t offs[6] = {o_off, o_dcode, o_doff, o_dspec, o_dmask, total};
+  memcpy(P.blob_off, offs, sizeof(offs));
+  if (defer) {
+    P.upload_pending = true;
+    return SRHIP_OK;
+  }
+  P.upload_pending = false;
   HIP_TRY(P.d_prog.ensure(total));
   HIP_TRY(hipMemcpyAsync(P.d_prog.p, h, total, hipMemcpyHostToDevice, P.ctx->stream));
-  const uint8_t* d = (const uint8_t*)P.d_prog.p;
-  P.code_dev = (const Ins*)d;
-  P.off_dev = (const int32_t*)(d + o_off);
-  P.dcode_dev = der ? (const Ins*)(d + o_dcode) : nullptr;
-  P.doff_dev = der ? (const int32_t*)(d + o_doff) : nullptr;
-  P.dspec_dev = der ? (const uint32_t*)(d + o_dspec) : nullptr;
-  P.dmask_dev = der ? (const uint64_t*)(d + o_dmask) : nullptr;
+  set_prog_pointers(P);
   if (sync) HIP_TRY(hipStreamSynchronize(P.ctx->stream));
   return SRHIP_OK;
 }
@@ -1234,19 +1247,32 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   const std::vector<int32_t> goff = shape_groups(L, nl, ctx->num_cu);
   {
     std::lock_guard<std::mutex> g(P->ord_mu);
-    if (P->ord_key[0] != L.groups || P->ord_key[1] != L.tpg || P->ord_key[2] != (int)use_d || P->ord_goff != goff) {
+    if (P->upload_pending || P->ord_key[0] != L.groups || P->ord_key[1] != L.tpg || P->ord_key[2] != (int)use_d ||
+        P->ord_goff != goff) {
       std::vector<int32_t>& order = P->ord_host;  // lives in the program: the copy below is asynchronous
       order = make_order(*P, live, goff, use_d);
       order.insert(order.end(), goff.begin(), goff.end());  // the group offsets follow the order
-      HIP_TRY(P->d_order.ensure(order.size() * sizeof(int32_t)));
-      HIP_TRY(hipMemcpyAsync(P->d_order.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                             ctx->stream));
+      if (P->upload_pending) {  // deferred program upload: program and order in one copy
+        const size_t base = P->blob_off[5], bytes = order.size() * sizeof(int32_t);
+        P->blob.resize(base + bytes);
+        memcpy(P->blob.data() + base, order.data(), bytes);
+        HIP_TRY(P->d_prog.ensure(base + bytes));
+        HIP_TRY(hipMemcpyAsync(P->d_prog.p, P->blob.data(), base + bytes, hipMemcpyHostToDevice, ctx->stream));
+        set_prog_pointers(*P);
+        P->upload_pending = false;
+        P->ord_dev = (const uint8_t*)P->d_prog.p + base;
+      } else {
+        HIP_TRY(P->d_order.ensure(order.size() * sizeof(int32_t)));
+        HIP_TRY(hipMemcpyAsync(P->d_order.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                               ctx->stream));
+        P->ord_dev = P->d_order.p;
+      }
       P->ord_key[0] = L.groups;
       P->ord_key[1] = L.tpg;
       P->ord_key[2] = (int)use_d;
       P->ord_goff = goff;
     }
-    d_order = P->d_order.p;
+    d_order = P->ord_dev;
   }
   const int nch = (int)((v.m + loss_chunk(dtype) - 1) / loss_chunk(dtype));
   const int cpb = L.rb_rows / loss_chunk(dtype);  // loss chunks per row block (row blocks are whole chunks)
@@ -1284,6 +1310,14 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   a.has_y = mode == MODE_LOSS ? 1 : 0;
   a.max_steps = use_d ? P->dmax_len : P->max_len;
   a.debug_stop = debug_stop();
+  // one row block: the waves finish the per-tree reduction themselves (SRHIP_NO_FUSED_REDUCE=1: the
+  // reduce kernel instead; read per launch)
+  const char* nofuse = getenv("SRHIP_NO_FUSED_REDUCE");
+  if (L.nrb == 1 && !(nofuse && *nofuse && *nofuse != '0')) {
+    a.fused = 1;
+    a.fused_loss = mode == MODE_LOSS ? ctx->h_loss.p : nullptr;
+    a.fused_chk = dtype == SRHIP_I32 ? nullptr : ctx->h_chk.p;
+  }
   a.early_exit = mode == MODE_LOSS && early_exit_on() ? 1 : 0;
   if (a.early_exit) {
     const int rc = next_fail_epoch(ctx, nl, &a.fail_flag, &a.epoch);
@@ -1328,10 +1362,11 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       }
     }
   }
-  HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, nch, cpb,
-                        dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p, L.nrb, nl, (const int32_t*)d_order,
-                        mode == MODE_LOSS ? ctx->h_loss.p : nullptr, dtype == SRHIP_I32 ? nullptr : ctx->h_chk.p,
-                        ctx->stream));
+  if (!a.fused)
+    HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, nch, cpb,
+                          dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p, L.nrb, nl, (const int32_t*)d_order,
+                          mode == MODE_LOSS ? ctx->h_loss.p : nullptr, dtype == SRHIP_I32 ? nullptr : ctx->h_chk.p,
+                          ctx->stream));
   if (mode == MODE_PRED)
     HIP_TRY(hipMemcpyAsync(out_pred, pred.p, (size_t)nt * v.m * es, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));

@@ -154,10 +154,14 @@ struct srhip_program {
   int32_t maxfeat = 0;  // largest feature index any tree reads (the columns a launch stages)
   // device copy of the evaluation program, one buffer and one upload (upload_program):
   // [code | prog_off | dcode | dprog_off | dspec | dmask], 16-byte aligned sections
-  srhip::DevBuf d_prog;
-  std::vector<uint8_t> blob;  // its host image (alive until the next upload)
-  const srhip::Ins* code_dev = nullptr;
-  const int32_t* off_dev = nullptr;
+  // upload_program(P, sync, defer = true) only builds the image: the next evaluation appends its tree
+  // order and uploads both with one copy (the coalescer's per-flush program)
+  mutable srhip::DevBuf d_prog;
+  mutable std::vector<uint8_t> blob;  // its host image (alive until the next upload)
+  mutable bool upload_pending = false;
+  mutable size_t blob_off[6] = {0, 0, 0, 0, 0, 0};  // section offsets: off, dcode, doff, dspec, dmask, end
+  mutable const srhip::Ins* code_dev = nullptr;
+  mutable const int32_t* off_dev = nullptr;
   // derived-column program (srhip_isa.h): the same trees with U(X[f]) leaves reading LDS columns;
   // used by loss / prediction launches whose staging fits LDS, the plain program otherwise
   std::vector<uint32_t> dspec;  // [nd] (U << 16) | (feature - 1)
@@ -166,16 +170,17 @@ struct srhip_program {
   std::vector<int32_t> dprog_off;
   std::vector<double> dcost;
   int32_t dkmax = 0, dmax_len = 0;
-  const srhip::Ins* dcode_dev = nullptr;
-  const int32_t* doff_dev = nullptr;
-  const uint32_t* dspec_dev = nullptr;
-  const uint64_t* dmask_dev = nullptr;
+  mutable const srhip::Ins* dcode_dev = nullptr;
+  mutable const int32_t* doff_dev = nullptr;
+  mutable const uint32_t* dspec_dev = nullptr;
+  mutable const uint64_t* dmask_dev = nullptr;
   // launch schedule cache: the cost-sorted tree order of the last plan (groups, tpg, derived),
   // resident on the device; a program evaluated again with the same plan skips the sort and upload
   mutable std::mutex ord_mu;
   mutable int ord_key[3] = {-1, -1, -1};
   mutable std::vector<int32_t> ord_goff;  // group offsets of that plan (appended to d_order)
   mutable std::vector<int32_t> ord_host;  // the uploaded order (kept alive: its copy is asynchronous)
+  mutable const void* ord_dev = nullptr;  // where it lives on the device (d_order, or inside d_prog)
   mutable srhip::DevBuf d_order;
   // gradient program (constants not folded, constant leaves carry their get_constants index);
   // compiled on first use by the constant-gradient path
@@ -233,7 +238,7 @@ bool spec_instantiate(srhip_program& P, int32_t slot, int32_t t, const double* c
                       int64_t& hi);
 // sync = false: the copies stay queued on the context's stream (the caller's next evaluation, which
 // synchronises before returning, must follow before P's host code changes again)
-int upload_program(srhip_program& P, bool sync = true);
+int upload_program(srhip_program& P, bool sync = true, bool defer = false);
 int make_view(srhip_ctx* ctx, const srhip_dataset* ds, const int64_t* idx, int64_t nidx, bool need_y, View& v);
 int gathered_weight_sum(srhip_ctx* ctx, const srhip_dataset* ds, int64_t nidx, View& v);
 // ncols: feature (+ derived) columns staged; lds_budget: bytes of LDS a workgroup may use

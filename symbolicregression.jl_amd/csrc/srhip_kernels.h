@@ -77,6 +77,12 @@ struct EvalArgs {
                             // marks the tree failed for the row blocks that have not started it
   int32_t epoch;            // this launch's mark (> 0; fail_flag[slot] == epoch: failed in this launch)
   int32_t* fail_flag;       // [ntrees] by order slot
+  // single-row-block launches (nrb == 1, small datasets): each wave finishes its tree's reduction
+  // itself, in reduce_kernel's order, and writes the results to these (coherent pinned host) arrays
+  // indexed by tree; no reduce launch
+  int32_t fused;
+  void* fused_loss;         // [program trees] LAccT (MODE_LOSS) or nullptr
+  void* fused_chk;          // [program trees] check statistic type, or nullptr (Int32)
 };
 
 int rows_per_lane(int dtype);

@@ -169,6 +169,36 @@ def test_random_population_losses(ctx, oracle, dtype, n, weighted):
     assert np.all(np.isinf(dl[~dok]))
 
 
+@pytest.mark.parametrize("dtype,n", [(np.float32, 100), (np.float64, 100), (np.float32, 2000), (np.float64, 1000)])
+def test_fused_single_block_reduction_equals_reduce_kernel(ctx, oracle, dtype, n, monkeypatch):
+    """Single-row-block launches (small datasets, C1's 100 rows) finish each tree's reduction in the
+    interpreter wave, in the reduce kernel's order: the same bits as the reduce kernel
+    (SRHIP_NO_FUSED_REDUCE=1), the oracle's losses, and the coalescer's deferred one-copy upload."""
+    sr = _sr()
+    opts = sr.Options(**OPS_C2)
+    trees, nodes, offs = _population(sr, opts, 96, 2, dtype, seed=21, max_size=20)
+    X, y, _ = _data(2, n, dtype, seed=22)
+    ds = _ds(ctx, X, y, None)
+    prog = sr.Program(ctx, nodes, offs, opts, dtype)
+    a, aok = prog.eval_loss(ds, sr.L2DistLoss())
+    monkeypatch.setenv("SRHIP_NO_FUSED_REDUCE", "1")
+    b, bok = prog.eval_loss(ds, sr.L2DistLoss())
+    monkeypatch.delenv("SRHIP_NO_FUSED_REDUCE")
+    assert np.array_equal(aok, bok) and np.array_equal(a.view(np.uint64), b.view(np.uint64))
+    ol, _, ook, _ = oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, X, y, None, 0, 0.0)
+    assert np.array_equal(aok, ook)
+    tol = F32_REL if dtype == np.float32 else F64_REL
+    assert not [t for t in np.nonzero(ook)[0] if _rel(a[t], ol[t]) > tol]
+    # the coalescer (deferred upload: program and tree order in one copy) scores the same bits
+    co = sr.Coalescer(ctx, ds, opts, sr.L2DistLoss(), max_wait_us=0)
+    try:
+        for t in range(0, 96, 7):
+            loss, ok = co.score_loss(nodes[offs[t]:offs[t + 1]])
+            assert bool(ok) == bool(aok[t]) and (not ok or np.float64(loss).view(np.uint64) == a[t:t + 1].view(np.uint64)[0])
+    finally:
+        co.close()
+
+
 def test_random_population_predictions(ctx, oracle):
     sr = _sr()
     opts = sr.Options(binary_operators=("+", "-", "*", "/"), unary_operators=("cos", "sin", "exp"))
