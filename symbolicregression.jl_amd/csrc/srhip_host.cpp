@@ -25,6 +25,7 @@
 #include <memory>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -531,18 +532,62 @@ int compile_derived_t(srhip_program& P) {
   for (const auto& e : cnt)
     if (e.second >= DERIVE_MIN_USES && (int)P.dspec.size() < dmax) P.dspec.push_back(e.first);
   if (P.dspec.empty()) return SRHIP_OK;
+  std::vector<TreeInfo> dinfo(P.ntrees);
+  const int rc = compile_trees<T>(P, P.dcode, dinfo, " (derived program)", [&](int32_t t, TreeCompiler<T>& tc) {
+    if (t >= 0) tc.set_derived(&P.dspec, P.maxfeat);
+    else P.dmask[-1 - t] = tc.dmask();
+  });
+  if (rc) return rc;
   for (int32_t t = 0; t < P.ntrees; ++t) {
-    const int64_t b = P.offsets[t], e = P.offsets[t + 1];
-    TreeCompiler<T> tc(P.nodes.data() + b, e - b, P, 0);
-    tc.set_derived(&P.dspec, P.maxfeat);
-    TreeInfo ti;
-    int rc = tc.compile(ti, P.dcode);
-    if (rc) return fail(rc, "tree %d (derived program): %s", (int)t, g_err.c_str());
+    const TreeInfo& ti = dinfo[t];
     P.dprog_off[t] = ti.code_begin;
-    P.dmask[t] = tc.dmask();
     P.dcost[t] = ti.cost;
     P.dkmax = std::max(P.dkmax, ti.need);
     P.dmax_len = std::max(P.dmax_len, ti.code_len);
+  }
+  return SRHIP_OK;
+}
+
+// Compile trees [0, P.ntrees) into `code` / `info` (code_begin absolute), `body(t, tc)` configuring
+// each TreeCompiler; large populations are split into contiguous ranges compiled on worker threads
+// (per-thread code vectors concatenated in tree order: the same bytes as one sequential pass).
+template <typename T, typename Setup>
+int compile_trees(srhip_program& P, std::vector<Ins>& code, std::vector<TreeInfo>& info, const char* what, Setup setup) {
+  const int32_t n = P.ntrees;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const int W = (int)std::min<int64_t>({(int64_t)8, (int64_t)hw, (int64_t)n / 128});
+  auto run = [&](int32_t t0, int32_t t1, std::vector<Ins>& out, std::string& err) -> int {
+    for (int32_t t = t0; t < t1; ++t) {
+      const int64_t b = P.offsets[t], e = P.offsets[t + 1];
+      TreeCompiler<T> tc(P.nodes.data() + b, e - b, P, 0);
+      setup(t, tc);
+      const int rc = tc.compile(info[t], out);
+      if (rc) {
+        err = "tree " + std::to_string(t) + what + ": " + g_err;
+        return rc;
+      }
+      setup(-1 - t, tc);  // after-compile hook (derived masks)
+    }
+    return SRHIP_OK;
+  };
+  if (W <= 1) {
+    std::string err;
+    const int rc = run(0, n, code, err);
+    return rc ? fail(rc, "%s", err.c_str()) : SRHIP_OK;
+  }
+  std::vector<std::vector<Ins>> part(W);
+  std::vector<std::string> errs(W);
+  std::vector<int> rcs(W, SRHIP_OK);
+  std::vector<std::thread> th;
+  for (int w = 0; w < W; ++w)
+    th.emplace_back([&, w] { rcs[w] = run((int32_t)((int64_t)n * w / W), (int32_t)((int64_t)n * (w + 1) / W), part[w], errs[w]); });
+  for (auto& x : th) x.join();
+  for (int w = 0; w < W; ++w)
+    if (rcs[w]) return fail(rcs[w], "%s", errs[w].c_str());
+  for (int w = 0; w < W; ++w) {
+    const int32_t base = (int32_t)code.size();
+    for (int32_t t = (int32_t)((int64_t)n * w / W); t < (int32_t)((int64_t)n * (w + 1) / W); ++t) info[t].code_begin += base;
+    code.insert(code.end(), part[w].begin(), part[w].end());
   }
   return SRHIP_OK;
 }
@@ -557,11 +602,9 @@ int compile_program_t(srhip_program& P) {
   P.max_len = 0;
   P.total_nodes = 0;
   P.total_ops = 0;
+  const int rc = compile_trees<T>(P, P.code, P.info, "", [](int32_t, TreeCompiler<T>&) {});
+  if (rc) return rc;
   for (int32_t t = 0; t < P.ntrees; ++t) {
-    const int64_t b = P.offsets[t], e = P.offsets[t + 1];
-    TreeCompiler<T> tc(P.nodes.data() + b, e - b, P, 0);
-    int rc = tc.compile(P.info[t], P.code);
-    if (rc) return fail(rc, "tree %d: %s", (int)t, g_err.c_str());
     P.prog_off[t] = P.info[t].code_begin;
     P.kmax = std::max(P.kmax, P.info[t].need);
     P.max_ops = std::max(P.max_ops, (int32_t)P.info[t].op_sumcheck.size());
