@@ -68,8 +68,16 @@ def main():
         import torch
         import torch.distributed as dist
 
+        # (rehearsal on fewer GPUs than ranks: SRHIP_BENCH_BACKEND=gloo, ranks share devices round-robin)
+        backend = os.environ.get("SRHIP_BENCH_BACKEND", "nccl")
+        if backend != "nccl":
+            local_rank %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
+    red_dev = f"cuda:{local_rank}" if os.environ.get("SRHIP_BENCH_BACKEND", "nccl") == "nccl" else "cpu"
 
     import numpy as np
 
@@ -114,7 +122,7 @@ def main():
     if dist is not None:
         import torch
 
-        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
+        tt = torch.tensor([dt], dtype=torch.float64, device=red_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms_per_step = dt * 1e3 / args.steps
@@ -137,7 +145,7 @@ def main():
         if dist is not None:
             import torch
 
-            tt = torch.tensor([d], dtype=torch.float64, device=f"cuda:{local_rank}")
+            tt = torch.tensor([d], dtype=torch.float64, device=red_dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             d = float(tt.item())
         return d, float(np.mean(km))
@@ -488,7 +496,7 @@ def bench_search(args):
                        # worker time (compile + upload + launch + wait) / wall time
                        "device_busy_frac": res.coalescer_stats.get("kernel_ms", 0.0) / (dt * 1e3),
                        "coalescer_busy_frac": res.coalescer_stats.get("busy_ms", 0.0) / (dt * 1e3),
-                       "coalesce_wait_us": int(os.environ.get("SRHIP_COALESCE_WAIT_US", "50"))},
+                       "coalesce_wait_us": int(os.environ.get("SRHIP_COALESCE_WAIT_US", "0"))},
             "cpu_baseline": cpu,
         }))
     if dist is not None:
