@@ -658,7 +658,7 @@ __device__ __attribute__((always_inline)) inline void derive_columns(const EvalA
                                                                      typename Chk<T>::type* dchk) {
   using CT = typename Chk<T>::type;
   constexpr int DV = 16 / sizeof(T);
-  __shared__ CT part[EVAL_WAVES][DERIVE_MAX];
+  __shared__ CT part[EVAL_WAVES_MAX][DERIVE_MAX];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int d = 0; d < p.nd; ++d) {
     const uint32_t spec = __builtin_amdgcn_readfirstlane(p.dspec[d]);
@@ -698,7 +698,8 @@ __device__ __attribute__((always_inline)) inline void derive_columns(const EvalA
 //   MODE_PRED: prediction rows -> out_pred[tree][row], check partial -> slab
 // ------------------------------------------------------------------------------------------------
 template <typename T, int R, int K, int MODE, bool XLDS>
-__global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
+__global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p) {
+  constexpr int WAVES = eval_waves(R, K);
   using O = OpsT<T>;
   using CT = typename Chk<T>::type;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -744,7 +745,7 @@ __global__ __launch_bounds__(64 * EVAL_WAVES) void eval_kernel(EvalArgs p) {
   }
   KDBG("[k] staged, ntiles=%d rb_rows=%d nvalid=%ld max_steps=%d\n", ntiles, p.rb_rows, (long)p.nvalid, p.max_steps);
   __shared__ int next_tree;  // the group's next unclaimed tree (waves claim trees dynamically)
-  if (threadIdx.x == 0) next_tree = EVAL_WAVES;
+  if (threadIdx.x == 0) next_tree = WAVES;
   // failed-tree marks of the group's first FLAG_SNAP trees as this workgroup starts (one coherent
   // load per thread, in parallel, instead of a memory round trip per wave and tree): workgroups that
   // start after another row block saw a tree fail skip it.  A stale snapshot only skips less.
@@ -1121,7 +1122,7 @@ static hipError_t launch_eval_t(const EvalArgs& a, dim3 grid, size_t lds, hipStr
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(kern, grid, dim3(64 * EVAL_WAVES), lds, s, a);
+  hipLaunchKernelGGL(kern, grid, dim3(64 * eval_waves(R, K)), lds, s, a);
   return hipGetLastError();
 }
 

@@ -1038,7 +1038,7 @@ int srhip::make_view(srhip_ctx* ctx, const srhip_dataset* ds, const int64_t* idx
 }
 
 LaunchPlan srhip::plan_launch(const srhip_ctx* ctx, int dtype, int64_t nxcols, bool weighted, bool with_y, int64_t m,
-                              int32_t ntrees, int tile, size_t budget) {
+                              int32_t ntrees, int tile, size_t budget, int waves) {
   LaunchPlan L;
   ntrees = std::max<int32_t>(1, ntrees);  // every tree may have failed statically
   m = std::max<int64_t>(1, m);
@@ -1058,7 +1058,7 @@ LaunchPlan srhip::plan_launch(const srhip_ctx* ctx, int dtype, int64_t nxcols, b
   L.nrb = (int)((m + rb - 1) / rb);
   const int target_blocks = 4 * ctx->num_cu;
   int g = (target_blocks + L.nrb - 1) / L.nrb;
-  const int max_g = std::max(1, ntrees / (2 * EVAL_WAVES));
+  const int max_g = std::max(1, ntrees / (2 * waves));
   g = std::max(1, std::min(g, max_g));
   L.groups = g;
   L.tpg = (ntrees + g - 1) / g;
@@ -1262,28 +1262,36 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   bool use_d = false;
   int K = 0, R = 0;
   LaunchPlan L{};
+  // LDS a workgroup may stage: the 16-wave variant runs one workgroup per CU (160 KB, less the
+  // kernel's static arrays); 8-wave workgroups run two (derived-column programs) or more
+  auto lds_budget = [](int r, int k, bool derived) -> size_t {
+    if (eval_waves(r, k) >= 16) return 152 * 1024;
+    return derived ? 64 * 1024 - 512 : 64 * 1024 - 64;
+  };
   if (nd > 0 && mode != MODE_PRECISE) {
     K = kvariant(P->dkmax);
     R = pick_rows_per_lane(dtype, K, mode, v.m);
-    // two workgroups per CU: the R = 16 variant's registers (or >= 12-wave workgroups) allow no more
-    const size_t budget = ((dtype == SRHIP_F32 && R == R_F32_WIDE) || EVAL_WAVES >= 12) ? 80 * 1024 - 512 : 64 * 1024 - 512;
-    L = plan_launch(ctx, dtype, P->maxfeat + nd, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R, budget);
+    L = plan_launch(ctx, dtype, P->maxfeat + nd, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R,
+                    lds_budget(R, K, true), eval_waves(R, K));
     use_d = L.xlds;
-    // ... and only when its columns do not shrink the row block: a wave's early exit of a failed tree
-    // saves the rest of its row block, and shorter blocks lose more than the shared columns save
-    // (C2, one MI355X: 10 columns at 1024-row blocks 1.56 ms, plain program at 2048 rows 1.41 ms)
+    // ... and only when its columns leave the row block at least two tiles long (or as long as the
+    // plain program's): a wave's early exit of a failed tree saves the rest of its row block, and
+    // one-tile blocks lose more than the shared columns save (C2, one MI355X: 10 columns at
+    // 1024-row blocks 1.56 ms vs the plain program at 2048 rows 1.41 ms with 8-wave workgroups; with
+    // 16-wave workgroups 10 columns at 2048 rows 1.30 ms vs plain at 4096 rows 1.35 ms)
     const char* always = getenv("SRHIP_DERIVE_ALWAYS");  // (tests: the derived program whatever the blocks)
     if (use_d && !(always && *always && *always != '0')) {
-      const int Kp = kvariant(P->kmax);
+      const int Kp = kvariant(P->kmax), Rp = pick_rows_per_lane(dtype, Kp, mode, v.m);
       const LaunchPlan Lp = plan_launch(ctx, dtype, P->maxfeat, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(),
-                                        64 * pick_rows_per_lane(dtype, Kp, mode, v.m));
-      if (Lp.xlds && Lp.rb_rows > L.rb_rows) use_d = false;
+                                        64 * Rp, lds_budget(Rp, Kp, false), eval_waves(Rp, Kp));
+      if (Lp.xlds && L.rb_rows < std::min(Lp.rb_rows, 2 * 64 * R)) use_d = false;
     }
   }
   if (!use_d) {
     K = kvariant(P->kmax);
     R = pick_rows_per_lane(dtype, K, mode, v.m);
-    L = plan_launch(ctx, dtype, P->maxfeat, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R);
+    L = plan_launch(ctx, dtype, P->maxfeat, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R,
+                    lds_budget(R, K, false), eval_waves(R, K));
   }
   const int nl = (int)live.size();
   const void* d_order;

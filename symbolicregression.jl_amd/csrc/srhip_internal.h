@@ -243,7 +243,7 @@ int make_view(srhip_ctx* ctx, const srhip_dataset* ds, const int64_t* idx, int64
 int gathered_weight_sum(srhip_ctx* ctx, const srhip_dataset* ds, int64_t nidx, View& v);
 // ncols: feature (+ derived) columns staged; lds_budget: bytes of LDS a workgroup may use
 LaunchPlan plan_launch(const srhip_ctx* ctx, int dtype, int64_t ncols, bool weighted, bool with_y, int64_t m,
-                       int32_t ntrees, int rows_per_tile, size_t lds_budget = 64 * 1024 - 64);
+                       int32_t ntrees, int rows_per_tile, size_t lds_budget = 64 * 1024 - 64, int waves = EVAL_WAVES);
 // did_succeed decision of tree t from partials in the srhip_eval_loss_partials layout:
 // 0 ok, 1 fail, 2 undecided (only the sums' feature / row-count entries are read)
 int decide_tree(const TreeInfo& I, const srhip_program& P, int64_t nfeat, const double* sums, double chk);

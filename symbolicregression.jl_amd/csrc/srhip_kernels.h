@@ -11,6 +11,13 @@ namespace srhip {
 #define SRHIP_EVAL_WAVES 8
 #endif
 constexpr int EVAL_WAVES = SRHIP_EVAL_WAVES;  // wavefronts per workgroup of the interpreter kernel
+// ... except the wide Float32 variant (R = 16, K = 2: the C2 / C3 kernel), which runs 16-wave
+// workgroups, one per CU, over 4096-row blocks: twice the rows per staged block and per tree (the
+// early exit of failed trees saves more of each block), the same 4 waves per SIMD (C2, one MI355X:
+// 1.47 -> 1.34 ms)
+constexpr int EVAL_WAVES_WIDE = 16;
+constexpr int eval_waves(int R, int K) { return (R == 16 && K <= 2) ? EVAL_WAVES_WIDE : EVAL_WAVES; }
+constexpr int EVAL_WAVES_MAX = EVAL_WAVES_WIDE > EVAL_WAVES ? EVAL_WAVES_WIDE : EVAL_WAVES;
 #ifndef SRHIP_R_F32
 #define SRHIP_R_F32 8
 #endif
