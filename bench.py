@@ -29,8 +29,10 @@ PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 vector peak
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default: c2 20, c4 10)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps first (default: c2 30 -- the GPU reaches its steady clocks over the "
+                         "first ~50 ms of work -- c4 3)")
     ap.add_argument("--ntrees", type=int, default=1024)
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
@@ -50,7 +52,12 @@ def parse():
                     help="c1/c3: islands as threads of one process, or in worker processes (:multiprocessing)")
     ap.add_argument("--procs", type=int, default=0, help="c1/c3 multiprocessing: worker processes "
                     "(default min(populations per GPU, 16))")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 20 if args.config == "c2" else 10
+    if args.warmup is None:
+        args.warmup = 30 if args.config == "c2" else 3
+    return args
 
 
 def main():
@@ -150,16 +157,14 @@ def main():
             d = float(tt.item())
         return d, float(np.mean(km))
 
-    # the same population without derived columns (the headline launch shares U(X[f]) columns
-    # across trees, counted as evaluated nodes): every node of every tree evaluated by
-    # its own instruction -- reported beside it
-    dt_plain = kern_plain = dt_full = kern_full = float("nan")
+    # the same population with derived columns forced on (the launch picks the plain program for C2:
+    # every node of every tree evaluated by its own instruction, over longer row blocks; DESIGN.md
+    # §3.1) -- reported beside it
+    dt_derived = kern_derived = dt_full = kern_full = float("nan")
     if not args.headline_only:
-        os.environ["SRHIP_NO_DERIVE"] = "1"
-        p_plain = srhip.Program(ctx, nodes, offs, opts, np.float32)
-        del os.environ["SRHIP_NO_DERIVE"]
-        dt_plain, kern_plain = timed_steps(p_plain)
-        p_plain.close()
+        os.environ["SRHIP_DERIVE_ALWAYS"] = "1"
+        dt_derived, kern_derived = timed_steps(prog)
+        del os.environ["SRHIP_DERIVE_ALWAYS"]
     # ... and without the early exit of failed trees (every row of every tree evaluated; the headline
     # counts the skipped rows of trees that failed as evaluated, like the reference's early return)
     if not args.headline_only:
@@ -225,11 +230,10 @@ def main():
             "cpu_baseline": cpu,
             "extra": {
                 "compile_ms_1024_trees": compile_ms, "end_to_end_ms_per_population": e2e_ms,
-                "no_derive": {"value": work * world * args.steps / dt_plain, "kernel_ms": kern_plain,
-                              "frac": flops / (kern_plain * 1e-3) / 1e12 / PEAK_FP32_TFLOPS,
-                              "note": "SRHIP_NO_DERIVE=1: no shared U(X[f]) columns, every node evaluated by "
-                                      "its own instruction (4096-row blocks; the headline's derived-column "
-                                      "program runs 2048-row blocks)"},
+                "derived_columns": {"value": work * world * args.steps / dt_derived, "kernel_ms": kern_derived,
+                                    "frac": flops / (kern_derived * 1e-3) / 1e12 / PEAK_FP32_TFLOPS,
+                                    "note": "SRHIP_DERIVE_ALWAYS=1: shared U(X[f]) columns in LDS (2048-row "
+                                            "blocks); the headline runs the plain program (4096-row blocks)"},
                 "no_early_exit": {"value": work * world * args.steps / dt_full, "kernel_ms": kern_full,
                                   "frac": flops / (kern_full * 1e-3) / 1e12 / PEAK_FP32_TFLOPS,
                                   "note": "SRHIP_NO_EARLY_EXIT=1: failed trees evaluated on every row"},

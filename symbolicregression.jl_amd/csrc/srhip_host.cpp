@@ -1274,17 +1274,17 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     L = plan_launch(ctx, dtype, P->maxfeat + nd, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R,
                     lds_budget(R, K, true), eval_waves(R, K));
     use_d = L.xlds;
-    // ... and only when its columns leave the row block at least two tiles long (or as long as the
-    // plain program's): a wave's early exit of a failed tree saves the rest of its row block, and
-    // one-tile blocks lose more than the shared columns save (C2, one MI355X: 10 columns at
-    // 1024-row blocks 1.56 ms vs the plain program at 2048 rows 1.41 ms with 8-wave workgroups; with
-    // 16-wave workgroups 10 columns at 2048 rows 1.30 ms vs plain at 4096 rows 1.35 ms)
+    // ... and only when its columns do not shrink the row block: a wave's early exit of a failed tree
+    // saves the rest of its row block, and shorter blocks lose more than the shared columns save
+    // (C2, one MI355X, warm, separate processes: 10 columns at 2048-row blocks 1.29 ms vs the plain
+    // program at 4096 rows 1.27 ms with 16-wave workgroups; 1.56 vs 1.41 ms at 1024 / 2048 rows with
+    // 8-wave workgroups)
     const char* always = getenv("SRHIP_DERIVE_ALWAYS");  // (tests: the derived program whatever the blocks)
     if (use_d && !(always && *always && *always != '0')) {
       const int Kp = kvariant(P->kmax), Rp = pick_rows_per_lane(dtype, Kp, mode, v.m);
       const LaunchPlan Lp = plan_launch(ctx, dtype, P->maxfeat, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(),
                                         64 * Rp, lds_budget(Rp, Kp, false), eval_waves(Rp, Kp));
-      if (Lp.xlds && L.rb_rows < std::min(Lp.rb_rows, 2 * 64 * R)) use_d = false;
+      if (Lp.xlds && Lp.rb_rows > L.rb_rows) use_d = false;
     }
   }
   if (!use_d) {

@@ -56,9 +56,9 @@ def test_c2_bench_population_matches_oracle(ctx, oracle):
 
 
 def test_c2_plain_program_equals_derived(ctx, monkeypatch):
-    """Derived columns (SRHIP_DERIVE_ALWAYS=1 makes sure the launch uses them whatever
-    the row-block rule decides) return the same bits as the plain program (SRHIP_NO_DERIVE=1), which
-    evaluates every node."""
+    """Derived columns (forced with SRHIP_DERIVE_ALWAYS=1 -- C2's launch prefers the
+    plain program's longer row blocks) return the same bits as the plain program (SRHIP_NO_DERIVE=1),
+    which evaluates every node."""
     sr = _sr()
     from srhip import workloads
 
