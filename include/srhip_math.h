@@ -387,7 +387,7 @@ SRM_FN float srm_tanf(float x) { return srm_trigf(2, x); }
  * p 2^N with one rounding (Julia's subnormal / N = 128 rescalings are that same single rounding);
  * x > 88.72284 -> Inf, x < -103.97208 -> 0.  Max error 1 ULP (tests/test_math_accuracy.py; every
  * Float32 input is checked by tools/check_expf.c).  The device runs the same operations two rows per
- * packed instruction (srhip_eval.hip expf_rows), proven bit-identical by the same exhaustive check. */
+ * packed instruction (srhip_eval_impl.h expf2_dev), proven bit-identical by the same exhaustive check. */
 #define SRM_EXPF_LOG2E 1.442695f
 #define SRM_EXPF_NLN2_HI (-0.6931472f)
 #define SRM_EXPF_NLN2_LO 1.9046542e-9f

@@ -1,1019 +1,11 @@
-// srhip_eval.hip — gfx950 kernels of the batched expression evaluator.
-//
-// Hot kernel: eval_kernel<T, R, K, MODE, XLDS>.  One workgroup owns a block of RB dataset rows
-// (staged once into LDS: X[f][RB], y, w) and its waves interpret many trees over those rows.
-// A wave holds R rows per lane (64*R rows = one tile) in VGPRs; the bytecode is wave-uniform
-// and read with scalar loads, so the interpreter's dispatch runs on the SALU/branch unit while
-// the VALU does the arithmetic.  MUST be compiled with
-//     -mllvm -structurizecfg-skip-uniform-regions=true
-// so the uniform opcode switch lowers to a scalar branch tree with in-place VGPR updates
-// (without it, the CFG structurizer inserts R phi copies per case per dispatch).
-//
-// Replaces (reference): DynamicExpressions.eval_tree_array's array-at-a-time recursion (one
-// Vector{T}(n) per node + an isfinite(sum) pass per child array) and LossFunctions' mean/sum
-// (src/LossFunctions.jl:13-33, 45-75).  See DESIGN.md for the did_succeed mapping.
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-
-#include <algorithm>
-#include <type_traits>
-
-#include "srhip_isa.h"
-#include "srhip_kernels.h"
-#include "srhip_ops.h"
-
-#define UNR _Pragma("unroll")
-// SRHIP_KDEBUG builds (diagnostic only): lane 0 of wave 0 of block (0,0) printfs its progress.
-#ifdef SRHIP_KDEBUG
-#define KDBG(...) do { if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) printf(__VA_ARGS__); } while (0)
-#else
-#define KDBG(...) do { } while (0)
-#endif
-// Progress words for SRHIP_TRACE runs: lane 0 of wave 0 of block (0,0) stores (slot, value) to
-// host-coherent memory with system scope, so the host can read them while the kernel runs.
-#define KMARK(slot, val)                                                                       \
-  do {                                                                                         \
-    if (p.dbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                      \
-      __hip_atomic_store(p.dbg + (slot), (int32_t)(val), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
-  } while (0)
-#ifndef SRHIP_HEAVY_ILP
-#define SRHIP_HEAVY_ILP 1  // rows a heavy operator body may interleave
-#endif
-#ifndef SRHIP_TRIG_ROWS
-#define SRHIP_TRIG_ROWS 1  // Float32 cos/sin/tan batched over the rows (trigf_rows)
-#endif
-#ifndef SRHIP_ROW_FENCE
-#define SRHIP_ROW_FENCE() __builtin_amdgcn_sched_barrier(0)
-#endif
+// srhip_eval.hip — gfx950 kernels of the batched expression evaluator: the per-tree partial
+// reduction, the batching gather, feature statistics, and the launch dispatch of the interpreter
+// (eval_kernel, srhip_eval_impl.h), whose variants are instantiated by the translation units
+// srhip_eval_{f32,f64}_{loss,pred,precise}.hip, srhip_eval_f32w.hip and srhip_eval_i32.hip.
+#include "srhip_eval_impl.h"
+#include "srhip_eval_variants.h"
 
 namespace srhip {
-
-template <typename T> constexpr bool kIsInt = std::is_same<T, int32_t>::value;
-
-template <typename T>
-using OpsT = typename std::conditional<kIsInt<T>, IOps, FOps<typename std::conditional<kIsInt<T>, float, T>::type>>::type;
-
-// Which handlers exist for T (Int32 trees: ring ops and comparisons only).
-template <typename T> __device__ constexpr bool sb_ok(int sb) {
-  return !kIsInt<T> || sb != SB_DIV;
-}
-template <typename T> __device__ constexpr bool hb_ok(int) { return !kIsInt<T>; }
-template <typename T> __device__ constexpr bool un_ok(int u) {
-  return !kIsInt<T> || u == UN_NEG || u == UN_SQUARE || u == UN_CUBE || u == UN_ABS ||
-         u == UN_RELU || u == UN_SIGN;
-}
-
-// 16-byte vector of T
-template <typename T> struct Vec16;
-template <> struct Vec16<float> { typedef float __attribute__((ext_vector_type(4))) type; };
-template <> struct Vec16<int32_t> { typedef int32_t __attribute__((ext_vector_type(4))) type; };
-template <> struct Vec16<double> { typedef double __attribute__((ext_vector_type(2))) type; };
-
-// Rows of one tile owned by a lane: register r holds tile row
-//   (r / VEC) * 64 * VEC + lane * VEC + (r % VEC)        (VEC = 16 / sizeof(T))
-// so every access to a column is one 16-byte load per lane, contiguous across the wave.
-template <typename T, int R>
-__device__ __attribute__((always_inline)) inline void load_rows(const T* base, int lane, T (&v)[R]) {
-  constexpr int VEC = 16 / sizeof(T);
-  using V = typename Vec16<T>::type;
-  UNR for (int j = 0; j < R / VEC; ++j) {
-    const V q = reinterpret_cast<const V*>(base)[j * 64 + lane];
-    UNR for (int e = 0; e < VEC; ++e) v[j * VEC + e] = q[e];
-  }
-}
-
-#if defined(__HIP_DEVICE_COMPILE__)
-typedef const __attribute__((address_space(4))) Ins CIns;  // constant address space: scalar loads
-#else
-typedef const Ins CIns;
-#endif
-
-template <typename T> __device__ __attribute__((always_inline)) inline T imm_as(uint64_t bits) {
-  if constexpr (sizeof(T) == 8) {
-    return __builtin_bit_cast(T, bits);
-  } else {
-    return __builtin_bit_cast(T, (uint32_t)bits);
-  }
-}
-
-// ---- heavy operators: one out-of-line body per (T, R, op), called by every kernel variant ----
-// Transcendentals are 20-60 VALU instructions per row; inlining them R times into every handler of
-// every kernel variant made a ~700k-instruction kernel whose hot loop thrashed the instruction
-// cache (SQ_IFETCH ~ 0.4 x SQ_INSTS).  Out of line, the dispatch loop and the cheap handlers stay
-// compact and each heavy body exists once; the R rows travel in VGPRs (vector argument/return).
-template <typename T, int R> struct RowVec { typedef T type __attribute__((ext_vector_type(R))); };
-template <typename T, int R> using RV = typename RowVec<T, R>::type;
-
-// v_cvt_i32_f64 as an opaque instruction: saturating for out-of-range input and 0 for NaN (the C++
-// conversion of such values is undefined, and the compiler may exploit that).
-__device__ __attribute__((always_inline)) inline int cvt_i32_sat(double k) {
-  int m;
-  asm("v_cvt_i32_f64 %0, %1" : "=v"(m) : "v"(k));
-  return m;
-}
-
-// srm_sincosf_fast (include/srhip_math.h) for the device rows, bit-identical for every finite x:
-// the sign (-1)^(m+1) of cos is a free negation modifier on the product plus the bit of m, and
-// Inf / NaN need no select: they reach here unreduced and come out of the reduction as NaN.
-template <int KIND>
-__device__ __attribute__((always_inline)) inline float sincosf_dev(double x) {
-  const double invpi = 0.3183098861837907, pi_hi = 3.141592653589793, pi_lo = 1.2246467991473532e-16;
-  double k = __builtin_rint(__builtin_fma(x, invpi, KIND == 0 ? -0.5 : 0.0));
-  const int m = cvt_i32_sat(k);
-  if (KIND == 0) k += 0.5;
-  const double y = __builtin_fma(-k, pi_lo, __builtin_fma(-k, pi_hi, x));
-  const double p = srm_psin(y * y);
-  const float r = KIND == 0 ? (float)(-y * p) : (float)(y * p);
-  // sign flip by m's low bit: adding m << 31 is the xor on the sign bit (the carry leaves the word),
-  // one v_lshl_add_u32 instead of a shift and an xor
-  uint32_t o;
-  asm("v_lshl_add_u32 %0, %1, 31, %2" : "=v"(o) : "v"(m), "v"(__builtin_bit_cast(uint32_t, r)));
-  return __builtin_bit_cast(float, o);
-}
-
-// Julia's Float32 exp (include/srhip_math.h srm_expf) on two rows per instruction: the clamp to
-// [-104, 89] (NaN-propagating minimum / maximum) replaces srm_expf's Inf / 0 branches and every other
-// step is the same Float32 operation, packed (v_pk_mul_f32, v_pk_fma_f32); v_cvt_i32_f32 saturates and
-// maps NaN to 0, v_ldexp_f32 rounds once.  tools/check_expf.c proves this formulation bit-identical
-// to srm_expf on all 2^32 inputs (NaN in, NaN out).
-typedef float F2 __attribute__((ext_vector_type(2)));
-__device__ __attribute__((always_inline)) inline int cvt_i32_f32(float x) {
-  int m;
-  asm("v_cvt_i32_f32 %0, %1" : "=v"(m) : "v"(x));
-  return m;
-}
-__device__ __attribute__((always_inline)) inline F2 expf2_dev(F2 x) {
-  x = __builtin_elementwise_minimum(__builtin_elementwise_maximum(x, (F2)(-104.0f)), (F2)(89.0f));
-  F2 n = x * (F2)(SRM_EXPF_LOG2E);
-  n.x = __builtin_rintf(n.x);
-  n.y = __builtin_rintf(n.y);
-  F2 r = __builtin_elementwise_fma(n, (F2)(SRM_EXPF_NLN2_HI), x);
-  r = __builtin_elementwise_fma(n, (F2)(SRM_EXPF_NLN2_LO), r);
-  F2 p = __builtin_elementwise_fma(r, (F2)(SRM_EXPF_C6), (F2)(SRM_EXPF_C5));
-  p = __builtin_elementwise_fma(r, p, (F2)(SRM_EXPF_C4));
-  p = __builtin_elementwise_fma(r, p, (F2)(SRM_EXPF_C3));
-  p = __builtin_elementwise_fma(r, p, (F2)(0.5f));
-  p = __builtin_elementwise_fma(r, p, (F2)(1.0f));
-  p = __builtin_elementwise_fma(r, p, (F2)(1.0f));
-  F2 out;
-  out.x = __builtin_ldexpf(p.x, cvt_i32_f32(n.x));
-  out.y = __builtin_ldexpf(p.y, cvt_i32_f32(n.y));
-  return out;
-}
-
-// The same exp for waves whose inputs all satisfy |x| <= 87 (EXPF_FAST_MAX): no clamp; n = rint(x log2 e)
-// by adding and removing 1.5 * 2^23 (the same ties-to-even rounding of the same Float32 product), and
-// 2^n (a normal float for |n| <= 126) built in the exponent field from the low bits of that sum, one
-// multiply instead of v_cvt_i32 + v_ldexp (both round the exact p 2^n once).  tools/check_expf.c
-// proves it bit-identical to srm_expf on every float in range.
-constexpr float EXPF_FAST_MAX = 87.0f;
-__device__ __attribute__((always_inline)) inline F2 expf2_fast(F2 x) {
-  const F2 t = x * (F2)(SRM_EXPF_LOG2E) + (F2)(12582912.0f);
-  const F2 n = t - (F2)(12582912.0f);
-  F2 r = __builtin_elementwise_fma(n, (F2)(SRM_EXPF_NLN2_HI), x);
-  r = __builtin_elementwise_fma(n, (F2)(SRM_EXPF_NLN2_LO), r);
-  F2 p = __builtin_elementwise_fma(r, (F2)(SRM_EXPF_C6), (F2)(SRM_EXPF_C5));
-  p = __builtin_elementwise_fma(r, p, (F2)(SRM_EXPF_C4));
-  p = __builtin_elementwise_fma(r, p, (F2)(SRM_EXPF_C3));
-  p = __builtin_elementwise_fma(r, p, (F2)(0.5f));
-  p = __builtin_elementwise_fma(r, p, (F2)(1.0f));
-  p = __builtin_elementwise_fma(r, p, (F2)(1.0f));
-  // (opaque per row: left to itself the compiler built one scale and broadcast it to both rows)
-  float s0, s1;
-  asm("v_lshl_add_u32 %0, %1, 23, 1.0" : "=v"(s0) : "v"(t.x));
-  asm("v_lshl_add_u32 %0, %1, 23, 1.0" : "=v"(s1) : "v"(t.y));
-  return p * (F2){s0, s1};
-}
-
-// Float32 cos/sin/tan over a lane's R rows.  Every row takes the fast path; rows outside it are
-// redone by the scalar srm_trigf out of line, once per call and only if some row needs it.  The
-// same pieces as the scalar srm_trigf (include/srhip_math.h), so the values are bit-identical.
-// (A call inside the batched body would pin its live rows to callee-saved, high-numbered VGPRs.)
-// cos / sin: no per-row range test or select.  Large, Inf and NaN rows reduce to garbage; one
-// NaN-propagating max |x| over the lane's rows (v_maximum3_f32, half an instruction per row) tells
-// whether any row needs the scalar path, which redoes exactly the rows with !(|x| < 2^28 pi/2) from
-// the inputs (Inf / NaN -> NaN as srm_trigf).  Measured against a per-row v_cmp + v_cndmask that
-// marks the rows by keeping x (one instruction fewer per row, as the inputs need not stay live):
-// the select form was 1-2 % slower on C2 (scripts/ab.sh, round 2).  tan (KIND 2): Inf / NaN handled
-// inline, finite large rows redone the same way.
-// Smallest float above SRM_PIO2F_BIG (not itself a float): for every float a,
-// (double)|a| < SRM_PIO2F_BIG  <=>  |a| < SRM_PIO2F_BIG_F.
-#define SRM_PIO2F_BIG_F 421657440.0f
-template <int R>
-__device__ __attribute__((noinline)) RV<float, R> trigf_fix_tan(RV<float, R> v, RV<float, R> res) {
-  UNR for (int r = 0; r < R; ++r) {
-    const float x = v[r];
-    if (x - x == 0.0f && srm_pio2f_is_big((double)x)) res[r] = srm_trigf(2, x);
-  }
-  return res;
-}
-template <int R, int KIND>
-__device__ __attribute__((noinline)) RV<float, R> trigf_fix(RV<float, R> v, RV<float, R> res) {
-  UNR for (int r = 0; r < R; ++r) {
-    const float x = v[r];
-    if (!(__builtin_fabsf(x) < SRM_PIO2F_BIG_F)) res[r] = srm_trigf(KIND, x);  // Inf / NaN: x - x
-  }
-  return res;
-}
-template <int R, int KIND>
-__device__ __attribute__((always_inline)) inline RV<float, R> trigf_rows(RV<float, R> v) {
-  RV<float, R> res;
-  if constexpr (KIND == 2) {
-    bool big = false;
-    UNR for (int r = 0; r < R; ++r) {
-      const float x = v[r];
-      const bool fin = __builtin_isfinite(x);
-      const double xd = (double)x;
-      const bool b = srm_pio2f_is_big(xd);  // also true for Inf / NaN
-      big |= b && fin;
-      double y;
-      const int n = srm_rem_pio2f_fast(b ? 0.0 : xd, &y);
-      const float f = srm_trigf_finish(KIND, n, y);
-      res[r] = fin ? f : x - x;
-      if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
-    }
-    if (big) res = trigf_fix_tan<R>(v, res);
-  } else {
-    static_assert(R % 2 == 0, "row pairs");
-    float mx = 0.0f;
-    UNR for (int r = 0; r < R; r += 2)
-      asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(v[r]), "v"(v[r + 1]));
-    UNR for (int r = 0; r < R; ++r) {
-      res[r] = sincosf_dev<KIND>((double)v[r]);
-      if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
-    }
-    if (!(mx < SRM_PIO2F_BIG_F)) res = trigf_fix<R, KIND>(v, res);
-  }
-  return res;
-}
-
-template <typename T, int R, int U>
-__device__ __attribute__((noinline)) RV<T, R> heavy_un(RV<T, R> v) {
-  using O = OpsT<T>;
-  if constexpr (SRHIP_TRIG_ROWS && std::is_same<T, float>::value && (U == UN_COS || U == UN_SIN || U == UN_TAN))
-    return trigf_rows<R, U == UN_COS ? 0 : (U == UN_SIN ? 1 : 2)>(v);
-  if constexpr (std::is_same<T, float>::value && U == UN_EXP && R % 2 == 0) {
-    // one NaN-propagating max |x| per row pair decides for the whole wave (false for NaN)
-    float mx = 0.0f;
-    UNR for (int r = 0; r < R; r += 2)
-      asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(v[r]), "v"(v[r + 1]));
-    if (__builtin_amdgcn_ballot_w64(!(mx <= EXPF_FAST_MAX)) == 0) {
-      UNR for (int r = 0; r < R; r += 2) {
-        const F2 e = expf2_fast((F2){v[r], v[r + 1]});
-        v[r] = e.x;
-        v[r + 1] = e.y;
-      }
-    } else {
-      UNR for (int r = 0; r < R; r += 2) {
-        const F2 e = expf2_dev((F2){v[r], v[r + 1]});
-        v[r] = e.x;
-        v[r + 1] = e.y;
-      }
-    }
-    return v;
-  }
-  UNR for (int r = 0; r < R; ++r) {
-    T x = v[r];
-    switch (U) {
-#define X_(NAME, FN) case UN_##NAME: if constexpr (un_ok<T>(UN_##NAME)) x = O::FN(x); break;
-      SRHIP_UNOPS(X_)
-#undef X_
-      default: break;
-    }
-    v[r] = x;
-    if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();  // rows in groups: bounds the callee's registers
-  }
-  return v;
-}
-// heavy binary: a op b per row
-template <typename T, int R, int HB>
-__device__ __attribute__((noinline)) RV<T, R> heavy_bin(RV<T, R> a, RV<T, R> b) {
-  using O = OpsT<T>;
-  UNR for (int r = 0; r < R; ++r) {
-    T x = a[r];
-    switch (HB) {
-#define X_(NAME, FN) case HB_##NAME: if constexpr (hb_ok<T>(HB_##NAME)) x = O::FN(a[r], b[r]); break;
-      SRHIP_HEAVY_BINOPS(X_)
-#undef X_
-      default: break;
-    }
-    a[r] = x;
-    if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
-  }
-  return a;
-}
-// "Wide" unary operators: OCML bodies with ~70-100 live VGPRs.  A kernel's register budget is the
-// max over every callee it can reach, so only the K = K_MAX variant carries them; with them the
-// common variants would drop from 5 to 4 waves per SIMD.  Programs whose operator table has one
-// of them launch K_MAX (the host's variant choice).
-constexpr bool un_wide(int u) { return un_wide_op(u); }
-
-// unary operators cheap enough to inline into the handler (a few VALU instructions per row)
-template <int U> constexpr bool un_inline() { return un_cheap(U); }
-template <typename T, int R, int U>
-__device__ __attribute__((always_inline)) inline void apply_un(T (&A)[R]) {
-  if constexpr (un_inline<U>()) {
-    using O = OpsT<T>;
-    UNR for (int r = 0; r < R; ++r) {
-      switch (U) {
-#define X_(NAME, FN) case UN_##NAME: if constexpr (un_ok<T>(UN_##NAME)) A[r] = O::FN(A[r]); break;
-        SRHIP_UNOPS(X_)
-#undef X_
-        default: break;
-      }
-    }
-  } else {
-    RV<T, R> v;
-    UNR for (int r = 0; r < R; ++r) v[r] = A[r];
-    v = heavy_un<T, R, U>(v);
-    UNR for (int r = 0; r < R; ++r) A[r] = v[r];
-  }
-}
-template <typename T, int R, int HB>
-__device__ __attribute__((always_inline)) inline void apply_heavy(T (&A)[R], const T (&X)[R], const T (&Y)[R]) {
-  RV<T, R> a, b;
-  UNR for (int r = 0; r < R; ++r) { a[r] = X[r]; b[r] = Y[r]; }
-  a = heavy_bin<T, R, HB>(a, b);
-  UNR for (int r = 0; r < R; ++r) A[r] = a[r];
-}
-
-// Check accumulator: max |v| over every operator output (NaN-propagating, v_maximum3_f32) for
-// Float32; sum of |v| * 2^-512 for Float64 (Inf/NaN propagate, cannot overflow otherwise).
-template <typename T> struct Chk {
-  using type = T;
-};
-// Float32: one v_maximum3_f32 per two rows, chained through M (the compiler's reassociation into
-// a pairwise tree costs R/2 + 2 instructions instead of R/2).
-template <int R> __device__ __attribute__((always_inline)) inline void chk_update(float& M, const float (&A)[R]) {
-  UNR for (int r = 0; r < R; r += 2)
-    asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(M) : "v"(M), "v"(A[r]), "v"(A[r + 1]));
-}
-template <int R> __device__ __attribute__((always_inline)) inline void chk_update(double& M, const double (&A)[R]) {
-  UNR for (int r = 0; r < R; ++r) M = __builtin_fma(__builtin_fabs(A[r]), 0x1p-512, M);
-}
-template <int R> __device__ __attribute__((always_inline)) inline void chk_update(int32_t&, const int32_t (&)[R]) {}
-
-// IEEE Float32 division of two rows: the compiler's own a / b expansion (v_div_scale of the
-// denominator and of the numerator, v_rcp, Newton refinement, v_div_fmas with the numerator's scale
-// flag, v_div_fixup for the special cases), with its five fma / mul steps on packed row pairs
-// (v_pk_fma_f32, v_pk_mul_f32 round each lane exactly as the scalar instructions): the same bits as
-// n / d, 8 instead of 11 VALU instructions per row.
-__device__ __attribute__((always_inline)) inline F2 div2_dev(F2 n, F2 d) {
-  bool unused0, unused1, f0, f1;
-  const F2 ds = {__builtin_amdgcn_div_scalef(n.x, d.x, false, &unused0),
-                 __builtin_amdgcn_div_scalef(n.y, d.y, false, &unused1)};
-  F2 r = {__builtin_amdgcn_rcpf(ds.x), __builtin_amdgcn_rcpf(ds.y)};
-  const F2 e = __builtin_elementwise_fma(-ds, r, (F2)(1.0f));
-  r = __builtin_elementwise_fma(e, r, r);
-  const F2 ns = {__builtin_amdgcn_div_scalef(n.x, d.x, true, &f0), __builtin_amdgcn_div_scalef(n.y, d.y, true, &f1)};
-  F2 q = ns * r;
-  const F2 e2 = __builtin_elementwise_fma(-ds, q, ns);
-  q = __builtin_elementwise_fma(e2, r, q);
-  const F2 e3 = __builtin_elementwise_fma(-ds, q, ns);
-  F2 out;
-  out.x = __builtin_amdgcn_div_fixupf(__builtin_amdgcn_div_fmasf(e3.x, r.x, q.x, f0), d.x, n.x);
-  out.y = __builtin_amdgcn_div_fixupf(__builtin_amdgcn_div_fmasf(e3.y, r.y, q.y, f1), d.y, n.y);
-  return out;
-}
-
-// The same division without its range machinery, for operands with |n|, |d| in [2^-40, 2^40]:
-// there v_div_scale returns its operand unchanged with no scale flag (exponent difference < 96, no
-// denormal divisor, reciprocal or quotient, numerator exponent > 23), so v_div_fmas is a plain fma,
-// and v_div_fixup passes a finite normal quotient through -- the identical operation sequence on the
-// same values, 4 instead of 8 VALU instructions per row.
-__device__ __attribute__((always_inline)) inline F2 div2_inrange(F2 n, F2 d) {
-  F2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-  const F2 e = __builtin_elementwise_fma(-d, r, (F2)(1.0f));
-  r = __builtin_elementwise_fma(e, r, r);
-  F2 q = n * r;
-  const F2 e2 = __builtin_elementwise_fma(-d, q, n);
-  q = __builtin_elementwise_fma(e2, r, q);
-  const F2 e3 = __builtin_elementwise_fma(-d, q, n);
-  return __builtin_elementwise_fma(e3, r, q);
-}
-constexpr float DIV_FAST_LO = 0x1p-40f, DIV_FAST_HI = 0x1p40f;
-
-// A = A / B (SWAP: B / A) over a lane's rows: the whole wave takes div2_inrange when every operand
-// of every lane is in its range (one NaN-propagating v_maximum3 and v_minimum3 of |a|, |b| per row,
-// a ballot), else the full div2_dev.  C2's population: ~5 % of (division node, tile) pairs fall back.
-// M (CHK): the check statistic is folded on the full path only -- an in-range quotient is finite
-// with |q| <= 2^80, so its column sum cannot overflow (rows < 2^46) and the host decision (which
-// bounds every folded output's sum by max|v| x rows) is unchanged.
-// CONSTB: B is one wave-uniform constant, so only A's rows need the range test.
-template <int R, bool SWAP, bool CHK, bool CONSTB = false>
-__device__ __attribute__((always_inline)) inline void div_rows(float (&A)[R], const float (&B)[R], float& M) {
-  float mx = 0.0f, mn = __builtin_inff();
-  if constexpr (CONSTB) {
-    UNR for (int r = 0; r < R; r += 2) {
-      asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(A[r]), "v"(A[r + 1]));
-      asm("v_minimum3_f32 %0, %1, |%2|, |%3|" : "=v"(mn) : "v"(mn), "v"(A[r]), "v"(A[r + 1]));
-    }
-    const float c = __builtin_fabsf(B[0]);
-    mx = __builtin_elementwise_maximum(mx, c);
-    mn = __builtin_elementwise_minimum(mn, c);
-  } else {
-    UNR for (int r = 0; r < R; ++r) {
-      asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(A[r]), "v"(B[r]));
-      asm("v_minimum3_f32 %0, %1, |%2|, |%3|" : "=v"(mn) : "v"(mn), "v"(A[r]), "v"(B[r]));
-    }
-  }
-  const bool fast = mx <= DIV_FAST_HI && mn >= DIV_FAST_LO;  // false for NaN
-  if (__builtin_amdgcn_ballot_w64(!fast) == 0) {
-    UNR for (int r = 0; r < R; r += 2) {
-      const F2 a = {A[r], A[r + 1]}, b = {B[r], B[r + 1]};
-      const F2 c = SWAP ? div2_inrange(b, a) : div2_inrange(a, b);
-      A[r] = c.x;
-      A[r + 1] = c.y;
-    }
-  } else {
-    UNR for (int r = 0; r < R; r += 2) {
-      const F2 a = {A[r], A[r + 1]}, b = {B[r], B[r + 1]};
-      const F2 c = SWAP ? div2_dev(b, a) : div2_dev(a, b);
-      A[r] = c.x;
-      A[r + 1] = c.y;
-    }
-    if constexpr (CHK) chk_update<R>(M, A);
-  }
-}
-
-// Specialised binary operator over a lane's rows: A = A op B (SWAP: A = B op A).  Float32 + - * /
-// run on packed row pairs (v_pk_add_f32 / v_pk_mul_f32, div_rows: each lane rounded exactly as
-// the scalar instruction would); the rest row by row.
-typedef F2 PkF32;
-template <typename T, int SB> __device__ __attribute__((always_inline)) inline T sb_apply(T a, T b) {
-  using O = OpsT<T>;
-  switch (SB) {
-#define X_(NAME, FN) case SB_##NAME: if constexpr (sb_ok<T>(SB_##NAME)) return O::FN(a, b); break;
-    SRHIP_SPEC_BINOPS(X_)
-#undef X_
-    default: break;
-  }
-  return a;
-}
-template <typename T, int R, int SB, bool SWAP>
-__device__ __attribute__((always_inline)) inline void bin_rows(T (&A)[R], const T (&B)[R]) {
-  if constexpr (std::is_same<T, float>::value && R % 2 == 0 && SB == SB_DIV) {
-    float unused = 0.0f;
-    div_rows<R, SWAP, false>(A, B, unused);
-  } else if constexpr (std::is_same<T, float>::value && R % 2 == 0 &&
-                       (SB == SB_ADD || SB == SB_SUB || SB == SB_MUL)) {
-    UNR for (int r = 0; r < R; r += 2) {
-      const PkF32 a = {A[r], A[r + 1]}, b = {B[r], B[r + 1]};
-      PkF32 c;
-      if constexpr (SB == SB_ADD) c = SWAP ? b + a : a + b;
-      else if constexpr (SB == SB_SUB) c = SWAP ? b - a : a - b;
-      else c = SWAP ? b * a : a * b;
-      A[r] = c.x;
-      A[r + 1] = c.y;
-    }
-  } else {
-    UNR for (int r = 0; r < R; ++r) A[r] = SWAP ? sb_apply<T, SB>(B[r], A[r]) : sb_apply<T, SB>(A[r], B[r]);
-  }
-}
-template <typename T, int R, int SB, bool SWAP>
-__device__ __attribute__((always_inline)) inline void bin_rows_c(T (&A)[R], T c) {
-  T B[R];
-  UNR for (int r = 0; r < R; ++r) B[r] = c;
-  bin_rows<T, R, SB, SWAP>(A, B);
-}
-// the interpreter's operator forms: the operation and the check fold of its output
-template <typename T, int R, int SB, bool SWAP, bool CONSTB = false>
-__device__ __attribute__((always_inline)) inline void bin_rows_chk(T (&A)[R], const T (&B)[R], typename Chk<T>::type& M) {
-  if constexpr (std::is_same<T, float>::value && R % 2 == 0 && SB == SB_DIV) {
-    div_rows<R, SWAP, true, CONSTB>(A, B, M);
-  } else {
-    bin_rows<T, R, SB, SWAP>(A, B);
-    chk_update<R>(M, A);
-  }
-}
-template <typename T, int R, int SB, bool SWAP>
-__device__ __attribute__((always_inline)) inline void bin_rows_c_chk(T (&A)[R], T c, typename Chk<T>::type& M) {
-  T B[R];
-  UNR for (int r = 0; r < R; ++r) B[r] = c;
-  bin_rows_chk<T, R, SB, SWAP, true>(A, B, M);
-}
-
-template <typename T> using LAccT = typename std::conditional<kIsInt<T>, long long, double>::type;
-
-
-// Wave reductions on DPP lane moves (no LDS round trip per step): quad butterflies, half-row and
-// row mirrors, then row_bcast15 / row_bcast31 fold the four rows into lane WAVE_LAST.  Only that
-// lane's result is meaningful; the order is fixed, so results are deterministic.
-constexpr int WAVE_LAST = 63;
-template <int CTRL, int ROWS = 0xf>
-__device__ __attribute__((always_inline)) inline uint32_t dpp32(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
-}
-template <int CTRL, int ROWS = 0xf, typename U>
-__device__ __attribute__((always_inline)) inline U dpp(U v) {
-  if constexpr (sizeof(U) == 8) {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const uint64_t r = (uint64_t)dpp32<CTRL, ROWS>((uint32_t)b) | ((uint64_t)dpp32<CTRL, ROWS>((uint32_t)(b >> 32)) << 32);
-    return __builtin_bit_cast(U, r);
-  } else {
-    return __builtin_bit_cast(U, dpp32<CTRL, ROWS>(__builtin_bit_cast(uint32_t, v)));
-  }
-}
-template <typename U, typename F>
-__device__ __attribute__((always_inline)) inline U wave_fold(U v, F op) {
-  v = op(v, dpp<0xB1>(v));       // quad_perm [1,0,3,2]
-  v = op(v, dpp<0x4E>(v));       // quad_perm [2,3,0,1]
-  v = op(v, dpp<0x141>(v));      // row_half_mirror
-  v = op(v, dpp<0x140>(v));      // row_mirror: every lane of a row holds the row's fold
-  v = op(v, dpp<0x142, 0xa>(v)); // row_bcast15 -> rows 1, 3
-  v = op(v, dpp<0x143, 0xc>(v)); // row_bcast31 -> rows 2, 3: lane 63 holds the wave's fold
-  return v;
-}
-__device__ __attribute__((always_inline)) inline double wave_sum(double v) {
-  return wave_fold(v, [](double a, double b) { return a + b; });
-}
-__device__ __attribute__((always_inline)) inline double wave_sum_d(double v) { return wave_sum(v); }
-__device__ __attribute__((always_inline)) inline long long wave_sum(long long v) {
-  return wave_fold(v, [](long long a, long long b) { return a + b; });
-}
-__device__ __attribute__((always_inline)) inline float wave_chk(float v) {
-  return wave_fold(v, [](float a, float b) { return __builtin_elementwise_maximum(a, b); });
-}
-__device__ __attribute__((always_inline)) inline double wave_chk(double v) { return wave_sum(v); }
-__device__ __attribute__((always_inline)) inline int32_t wave_chk(int32_t v) { return v; }
-
-// MODE_PRECISE: exact per-(tree, operator node, row block) sums, used only for the rare trees
-// whose fast max|v| bound cannot decide DynamicExpressions' isfinite(sum(array)) checks.
-// One wave owns a (tree, row block), so plain read-modify-write of its slab entry is race-free.
-template <typename T, int R>
-__device__ __attribute__((always_inline)) inline void precise_hook(const EvalArgs& p, uint32_t a, const T (&A)[R],
-                                                                   int ti, int rb, int lane, int64_t row0) {
-  if constexpr (!kIsInt<T>) {
-    const uint32_t opidx = a >> 16;
-    if (opidx == 0) return;
-    constexpr int VEC = 16 / sizeof(T);
-    double s = 0.0;
-    UNR for (int r = 0; r < R; ++r) {
-      const int64_t row = row0 + (r / VEC) * 64 * VEC + lane * VEC + (r % VEC);
-      const double v = sizeof(T) == 8 ? (double)A[r] * 0x1p-64 : (double)A[r];
-      s += row < p.nvalid ? v : 0.0;
-    }
-    s = wave_sum_d(s);
-    if (lane == WAVE_LAST) {
-      double* slot = reinterpret_cast<double*>(p.slab_prec) + ((int64_t)ti * p.prec_stride + (opidx - 1)) * p.nrb + rb;
-      *slot += s;
-    }
-  }
-}
-
-// Per-tile loss epilogue for a given loss kind (KIND < 0: runtime kind).
-template <typename T, int R>
-__device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& p, const T (&A)[R], const T* ybase,
-                                                                const T* wbase, int lane, int64_t row0,
-                                                                LAccT<T>& lacc) {
-  T yv[R];
-  load_rows<T, R>(ybase, lane, yv);
-  constexpr int VEC = 16 / sizeof(T);
-  const bool full = row0 + 64 * R <= p.nvalid;  // wave-uniform
-  if constexpr (kIsInt<T>) {
-    UNR for (int r = 0; r < R; ++r) {
-      int32_t l = loss_elem_int(p.loss_kind, IOps::sub(A[r], yv[r]));
-      long long c = (long long)l;
-      if (!full) {
-        const int64_t row = row0 + (r / VEC) * 64 * VEC + lane * VEC + (r % VEC);
-        c = row < p.nvalid ? c : 0;
-      }
-      lacc += c;
-    }
-  } else {
-    T wv[R];
-    if (p.weighted) load_rows<T, R>(wbase, lane, wv);
-    const T p0 = (T)p.loss_p0;
-    T lv[R];
-    if (p.loss_kind == SRHIP_LOSS_L2) {
-      UNR for (int r = 0; r < R; ++r) lv[r] = A[r];
-      bin_rows<T, R, SB_SUB, false>(lv, yv);
-      T dv[R];
-      UNR for (int r = 0; r < R; ++r) dv[r] = lv[r];
-      bin_rows<T, R, SB_MUL, false>(lv, dv);
-    } else if (p.loss_kind == SRHIP_LOSS_L1) {
-      UNR for (int r = 0; r < R; ++r) lv[r] = m_abs(A[r] - yv[r]);
-    } else {
-      UNR for (int r = 0; r < R; ++r) lv[r] = loss_elem<T>(p.loss_kind, A[r] - yv[r], p0);
-    }
-    if (p.weighted) {
-      // padded rows carry w = 0 and a replicated (finite when ok) prediction
-      UNR for (int r = 0; r < R; ++r) lacc += (double)(wv[r] * lv[r]);
-    } else if (full) {
-      UNR for (int r = 0; r < R; ++r) lacc += (double)lv[r];
-    } else {
-      UNR for (int r = 0; r < R; ++r) {
-        const int64_t row = row0 + (r / VEC) * 64 * VEC + lane * VEC + (r % VEC);
-        lacc += row < p.nvalid ? (double)lv[r] : 0.0;
-      }
-    }
-  }
-}
-
-template <typename T, int R>
-__device__ __attribute__((always_inline)) inline void store_pred(const EvalArgs& p, const T (&A)[R], int tree, int lane,
-                                                                 int64_t row0) {
-  constexpr int VEC = 16 / sizeof(T);
-  using V = typename Vec16<T>::type;
-  T* out = reinterpret_cast<T*>(p.out_pred) + (int64_t)tree * p.nvalid;
-  UNR for (int j = 0; j < R / VEC; ++j) {
-    const int64_t row = row0 + j * 64 * VEC + lane * VEC;
-    if (row + VEC <= p.nvalid && ((p.nvalid % VEC) == 0)) {
-      V q;
-      UNR for (int e = 0; e < VEC; ++e) q[e] = A[j * VEC + e];
-      *reinterpret_cast<V*>(out + row) = q;
-    } else {
-      UNR for (int e = 0; e < VEC; ++e)
-        if (row + e < p.nvalid) out[row + e] = A[j * VEC + e];
-    }
-  }
-}
-
-// Derived columns (srhip_isa.h): U(X[f]) for this workgroup's rows, computed once into LDS column
-// nfeat + d by the same out-of-line operator bodies the interpreter calls (rows are independent
-// and -ffp-contract=off, so the values are bit-identical to evaluating U inside a tree).  The
-// column's check statistic over the block's rows (max |v| for Float32, sum |v| 2^-512 for
-// Float64) lands in dchk[d]; a tree that reads the column folds it into its own statistic, exactly
-// as its U instruction would have.
-template <typename T, int R>
-__device__ __attribute__((noinline)) RV<T, R> derive_un(int u, RV<T, R> v) {
-  switch (u) {
-#define X_(NAME, FN)                                                                     \
-  case UN_##NAME:                                                                        \
-    if constexpr (un_ok<T>(UN_##NAME) && un_derivable(UN_##NAME)) return heavy_un<T, R, UN_##NAME>(v); \
-    break;
-    SRHIP_UNOPS(X_)
-#undef X_
-    default: break;
-  }
-  return v;
-}
-
-// A thread takes one 16-byte vector (DV rows) of a column per call; each wave folds its column
-// statistic with DPP and parks it in LDS, and one barrier after all columns lets the first nd
-// threads fold the wave partials in wave order (fixed: deterministic).  (DV = 2 for Float32 kept all
-// 512 threads busy but cost more VALU in call overhead; the kernel is VALU-issue bound.)
-template <typename T>
-__device__ __attribute__((always_inline)) inline void derive_columns(const EvalArgs& p, T* lx, int rbb,
-                                                                     typename Chk<T>::type* dchk) {
-  using CT = typename Chk<T>::type;
-  constexpr int DV = 16 / sizeof(T);
-  __shared__ CT part[EVAL_WAVES_MAX][DERIVE_MAX];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int d = 0; d < p.nd; ++d) {
-    const uint32_t spec = __builtin_amdgcn_readfirstlane(p.dspec[d]);
-    const int u = (int)(spec >> 16), f = (int)(spec & 0xffff);
-    const T* src = lx + (int64_t)f * rbb;
-    T* dst = lx + (int64_t)(p.nfeat + d) * rbb;
-    CT m = 0;
-    for (int c = threadIdx.x; c < rbb / DV; c += blockDim.x) {
-      RV<T, DV> v = reinterpret_cast<const RV<T, DV>*>(src)[c];
-      v = derive_un<T, DV>(u, v);
-      reinterpret_cast<RV<T, DV>*>(dst)[c] = v;
-      UNR for (int e = 0; e < DV; ++e) {
-        if constexpr (sizeof(T) == 4) m = __builtin_elementwise_maximum(m, __builtin_fabsf(v[e]));
-        else m = __builtin_fma(__builtin_fabs(v[e]), 0x1p-512, m);
-      }
-    }
-    m = wave_chk(m);
-    if (lane == WAVE_LAST) part[wave][d] = m;
-  }
-  __syncthreads();
-  if ((int)threadIdx.x < p.nd) {
-    const int d = threadIdx.x;
-    CT t = part[0][d];
-    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
-      if constexpr (sizeof(T) == 4) t = __builtin_elementwise_maximum(t, part[w][d]);
-      else t += part[w][d];
-    }
-    dchk[d] = t;
-  }
-  __syncthreads();
-}
-
-// ------------------------------------------------------------------------------------------------
-// The interpreter kernel.
-//   grid.x = row blocks (RB rows each), grid.y = tree groups; block = WAVES wavefronts.
-//   MODE_LOSS: fused loss partial + check partial per (tree, row block) -> slabs
-//   MODE_PRED: prediction rows -> out_pred[tree][row], check partial -> slab
-// ------------------------------------------------------------------------------------------------
-template <typename T, int R, int K, int MODE, bool XLDS>
-__global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p) {
-  constexpr int WAVES = eval_waves(R, K);
-  using O = OpsT<T>;
-  using CT = typename Chk<T>::type;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  KMARK(0, 1);
-  if (p.debug_stop == 1) return;
-  constexpr int TILE = 64 * R;
-  const int lane = threadIdx.x & 63;
-  const int rb = blockIdx.x;
-  const int64_t row_base = (int64_t)rb * p.rb_rows;
-  const int ntiles = p.rb_rows / TILE;
-
-  // ---- stage this block's rows of X (and y, w) into LDS ----
-  const T* xsrc;
-  const T* ysrc;
-  const T* wsrc;
-  int64_t xstride;
-  if constexpr (XLDS) {
-    T* lx = reinterpret_cast<T*>(smem);
-    const int rbb = p.rb_rows;
-    const int ncols = p.nfeat + (p.has_y ? 1 : 0) + (p.weighted ? 1 : 0);
-    using V = typename Vec16<T>::type;
-    constexpr int VEC = 16 / sizeof(T);
-    const int vec_per_col = rbb / VEC;
-    const T* gX = reinterpret_cast<const T*>(p.X);
-    const T* gy = reinterpret_cast<const T*>(p.y);
-    const T* gw = reinterpret_cast<const T*>(p.w);
-    for (int i = threadIdx.x; i < ncols * vec_per_col; i += blockDim.x) {
-      const int c = i / vec_per_col;
-      const int v = i - c * vec_per_col;
-      const T* src = c < p.nfeat ? gX + (int64_t)c * p.ld : (c == p.nfeat ? gy : gw);
-      const int lc = c < p.nfeat ? c : c + p.nd;  // LDS column: derived columns follow the features
-      reinterpret_cast<V*>(lx + (int64_t)lc * rbb)[v] = reinterpret_cast<const V*>(src + row_base)[v];
-    }
-    xsrc = lx;
-    ysrc = lx + (int64_t)(p.nfeat + p.nd) * rbb;
-    wsrc = lx + (int64_t)(p.nfeat + p.nd + 1) * rbb;
-    xstride = rbb;
-  } else {
-    xsrc = reinterpret_cast<const T*>(p.X) + row_base;
-    ysrc = reinterpret_cast<const T*>(p.y) + row_base;
-    wsrc = reinterpret_cast<const T*>(p.w) + row_base;
-    xstride = p.ld;
-  }
-  KDBG("[k] staged, ntiles=%d rb_rows=%d nvalid=%ld max_steps=%d\n", ntiles, p.rb_rows, (long)p.nvalid, p.max_steps);
-  __shared__ int next_tree;  // the group's next unclaimed tree (waves claim trees dynamically)
-  if (threadIdx.x == 0) next_tree = WAVES;
-  // failed-tree marks of the group's first FLAG_SNAP trees as this workgroup starts (one coherent
-  // load per thread, in parallel, instead of a memory round trip per wave and tree): workgroups that
-  // start after another row block saw a tree fail skip it.  A stale snapshot only skips less.
-  constexpr int FLAG_SNAP = 2048;
-  constexpr bool SNAP = MODE == MODE_LOSS && !kIsInt<T>;
-  __shared__ uint8_t failed_snap[SNAP ? FLAG_SNAP : 1];
-  const int snap_base = p.group_off ? p.group_off[blockIdx.y] : (int)blockIdx.y * p.trees_per_group;
-  const int snap_n = p.group_off ? p.group_off[blockIdx.y + 1] - snap_base
-                                 : min(p.trees_per_group, p.ntrees - snap_base);
-  if constexpr (SNAP) {
-    if (p.early_exit)
-      for (int i = threadIdx.x; i < min(snap_n, FLAG_SNAP); i += blockDim.x)
-        failed_snap[i] = __hip_atomic_load(p.fail_flag + snap_base + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.epoch;
-  }
-  __syncthreads();
-  constexpr bool DERIVED = XLDS && !kIsInt<T> && MODE != MODE_PRECISE;
-  __shared__ CT dchk[DERIVED ? DERIVE_MAX : 1];
-  if constexpr (DERIVED) {
-    if (p.nd > 0) derive_columns<T>(p, reinterpret_cast<T*>(smem), p.rb_rows, dchk);
-  }
-  KMARK(0, 2);
-  if (p.debug_stop == 2) return;
-
-  // tree group of this workgroup: uniform, or the host's tail-shaped sizes (group_off)
-  const int group_base = p.group_off ? __builtin_amdgcn_readfirstlane(p.group_off[blockIdx.y])
-                                     : (int)blockIdx.y * p.trees_per_group;
-  const int group_n = p.group_off ? __builtin_amdgcn_readfirstlane(p.group_off[blockIdx.y + 1]) - group_base
-                                  : min(p.trees_per_group, p.ntrees - group_base);
-
-  // the group's trees are in descending estimated cost (host make_order): wave w starts with tree w,
-  // then each wave claims the next unclaimed tree from an LDS counter as it finishes one — longest
-  // first, so the waves of a workgroup end within about one cheap tree of each other (a static
-  // round-robin left up to the cost spread idle at every workgroup's end).  The counter only grows:
-  // every wave leaves the loop once it passes group_n.
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const CIns* code = (const CIns*)(uintptr_t)p.code;
-  KMARK(8 + wave, 10);
-  for (int ti = wave; ti < group_n;) {
-    KMARK(8 + wave, 11);
-    const int tree = __builtin_amdgcn_readfirstlane(p.order[group_base + ti]);
-    const int pc0 = __builtin_amdgcn_readfirstlane(p.prog_off[tree]);
-    const int max_steps = __builtin_amdgcn_readfirstlane(p.max_steps);
-    KDBG("[k] ti=%d tree=%d pc0=%d group_n=%d\n", ti, tree, pc0, group_n);
-    KMARK(0, 3);
-    KMARK(1, tree);
-    if (p.debug_stop == 3) break;  // (diagnostic) skip the trees; a continue would not claim the next one
-
-    LAccT<T> lacc = 0;
-    CT M = 0;
-    // another row block already saw this tree fail in this launch: nothing here can change its
-    // result (did_succeed = false, loss L(Inf)); NaN partials and check statistic stand in
-    bool failed = false;
-    if constexpr (SNAP) {
-      if (p.early_exit && ti < FLAG_SNAP) failed = __builtin_amdgcn_readfirstlane(failed_snap[ti]) != 0;
-    }
-    if constexpr (DERIVED) {
-      if (p.nd > 0) {  // check statistics of the derived columns this tree reads
-        uint64_t msk = p.dmask[tree];
-        msk = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(msk >> 32)) << 32) |
-              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)msk);
-        while (msk) {
-          const int d = __builtin_ctzll(msk);
-          msk &= msk - 1;
-          if constexpr (sizeof(T) == 4) M = __builtin_elementwise_maximum(M, dchk[d]);
-          else if (lane == WAVE_LAST) M += dchk[d];  // a wave sum follows: count the column once
-        }
-      }
-    }
-    // loss slab layout [row block][order slot][chunk of the block] (p.cpb chunks per block): a
-    // workgroup's partials are one contiguous range (its group's slots), so L2 lines fill before
-    // write-back
-    LAccT<T>* lslab = reinterpret_cast<LAccT<T>*>(p.slab_loss) +
-                      ((int64_t)rb * p.ntrees + group_base + ti) * __builtin_amdgcn_readfirstlane(p.cpb);
-    LAccT<T> csum = 0;  // fused launches: this lane's share of the tree's chunk sums
-    if (failed) {
-      if (lane == WAVE_LAST)
-        for (int c = 0; c < p.cpb; ++c) lslab[c] = (LAccT<T>)NAN;
-      M = (CT)NAN;
-      csum = (LAccT<T>)NAN;
-    }
-    for (int tile = 0; tile < (failed ? 0 : ntiles); ++tile) {
-      const int64_t row0 = row_base + (int64_t)tile * TILE;
-      if (row0 >= p.nvalid) break;  // whole tile is padding
-      const T* xt = xsrc + (int64_t)tile * TILE;
-      T A[R], S[K][R];
-      UNR for (int r = 0; r < R; ++r) A[r] = T(0);
-      UNR for (int k = 0; k < K; ++k) UNR for (int r = 0; r < R; ++r) S[k][r] = T(0);
-      // The program is read through the constant address space with a wave-uniform pc, so every
-      // instruction is one s_load_dwordx4 (scalar cache), prefetched one instruction ahead.
-      const CIns* prog = code + pc0;
-      Ins nxt = prog[0];
-      // bounded: a malformed program ends after max_steps instructions instead of hanging
-      for (int step = 0; step < max_steps; ++step) {
-        const Ins ins = nxt;
-        nxt = prog[step + 1];
-        KDBG("[k]   tile=%d step=%d h=%u a=%u\n", tile, step, ins.h, ins.a);
-        if (ins.h == H_END) break;
-        switch (ins.h) {
-          case H_LOADF: load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A); break;
-          case H_LOADC: { const T c = imm_as<T>(ins.imm); UNR for (int r = 0; r < R; ++r) A[r] = c; break; }
-#define SRHIP_K_CASES(BASE, ...)                                                            \
-  case BASE + 0: if constexpr (0 < K) { constexpr int k = 0; __VA_ARGS__ } break;                 \
-  case BASE + 1: if constexpr (1 < K) { constexpr int k = 1; __VA_ARGS__ } break;                 \
-  case BASE + 2: if constexpr (2 < K) { constexpr int k = 2; __VA_ARGS__ } break;                 \
-  case BASE + 3: if constexpr (3 < K) { constexpr int k = 3; __VA_ARGS__ } break;                 \
-  case BASE + 4: if constexpr (4 < K) { constexpr int k = 4; __VA_ARGS__ } break;                 \
-  case BASE + 5: if constexpr (5 < K) { constexpr int k = 5; __VA_ARGS__ } break;                 \
-  case BASE + 6: if constexpr (6 < K) { constexpr int k = 6; __VA_ARGS__ } break;                 \
-  case BASE + 7: if constexpr (7 < K) { constexpr int k = 7; __VA_ARGS__ } break;
-          SRHIP_K_CASES(H_PUSH0, { UNR for (int r = 0; r < R; ++r) S[k][r] = A[r]; })
-          SRHIP_K_CASES(H_SLOADF0, { load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, S[k]); })
-          SRHIP_K_CASES(H_SLOADC0, { const T c = imm_as<T>(ins.imm); UNR for (int r = 0; r < R; ++r) S[k][r] = c; })
-
-#define SRHIP_SPEC_CASE(NAME, FN)                                                                  \
-  case h_spec(SB_##NAME, SPEC_AF):                                                                 \
-    if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
-      T xv[R];                                                                                     \
-      load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
-      bin_rows_chk<T, R, SB_##NAME, false>(A, xv, M);                                              \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
-    }                                                                                              \
-    break;                                                                                         \
-  case h_spec(SB_##NAME, SPEC_FA):                                                                 \
-    if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
-      T xv[R];                                                                                     \
-      load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
-      bin_rows_chk<T, R, SB_##NAME, true>(A, xv, M);                                               \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
-    }                                                                                              \
-    break;                                                                                         \
-  case h_spec(SB_##NAME, SPEC_AC):                                                                 \
-    if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
-      bin_rows_c_chk<T, R, SB_##NAME, false>(A, imm_as<T>(ins.imm), M);                            \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
-    }                                                                                              \
-    break;                                                                                         \
-  case h_spec(SB_##NAME, SPEC_CA):                                                                 \
-    if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
-      bin_rows_c_chk<T, R, SB_##NAME, true>(A, imm_as<T>(ins.imm), M);                             \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
-    }                                                                                              \
-    break;                                                                                         \
-    SRHIP_K_CASES(h_spec(SB_##NAME, SPEC_SA0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
-      bin_rows_chk<T, R, SB_##NAME, true>(A, S[k], M);                                             \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
-    })                                                                                             \
-    SRHIP_K_CASES(h_spec(SB_##NAME, SPEC_AS0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
-      bin_rows_chk<T, R, SB_##NAME, false>(A, S[k], M);                                            \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
-    })
-          SRHIP_SPEC_BINOPS(SRHIP_SPEC_CASE)
-#undef SRHIP_SPEC_CASE
-
-#define SRHIP_HEAVY_CASE(NAME, FN)                                                              \
-    SRHIP_K_CASES(h_heavy(HB_##NAME, HEAVY_SA0), if constexpr (hb_ok<T>(HB_##NAME)) {           \
-      apply_heavy<T, R, HB_##NAME>(A, S[k], A);                                                 \
-      chk_update<R>(M, A);                                                                      \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);  \
-    })                                                                                          \
-    SRHIP_K_CASES(h_heavy(HB_##NAME, HEAVY_AS0), if constexpr (hb_ok<T>(HB_##NAME)) {           \
-      apply_heavy<T, R, HB_##NAME>(A, A, S[k]);                                                 \
-      chk_update<R>(M, A);                                                                      \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);  \
-    })
-          SRHIP_HEAVY_BINOPS(SRHIP_HEAVY_CASE)
-#undef SRHIP_HEAVY_CASE
-
-#define SRHIP_UN_CASE(NAME, FN)                                                  \
-  case h_un(UN_##NAME):                                                          \
-    if constexpr (un_ok<T>(UN_##NAME) && (K == K_MAX || !un_wide(UN_##NAME))) {  \
-      apply_un<T, R, UN_##NAME>(A);                                              \
-      chk_update<R>(M, A);                                                       \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0); \
-    }                                                                            \
-    break;
-          SRHIP_UNOPS(SRHIP_UN_CASE)
-#undef SRHIP_UN_CASE
-          case H_COS_NC:
-            if constexpr (un_ok<T>(UN_COS)) {
-              apply_un<T, R, UN_COS>(A);
-              if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);
-            }
-            break;
-          case H_SIN_NC:
-            if constexpr (un_ok<T>(UN_SIN)) {
-              apply_un<T, R, UN_SIN>(A);
-              if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);
-            }
-            break;
-#undef SRHIP_K_CASES
-          default: break;
-        }
-      }
-      KDBG("[k]   tile %d done\n", tile);
-      KMARK(0, 4);
-      if constexpr (MODE == MODE_LOSS) {
-        loss_tile<T, R>(p, A, ysrc + (int64_t)tile * TILE, wsrc + (int64_t)tile * TILE, lane, row0, lacc);
-        constexpr int CH = sizeof(T) == 8 ? LOSS_CHUNK_8B : LOSS_CHUNK_4B;
-        static_assert(CH % TILE == 0, "a loss chunk is whole tiles");
-        const bool flushed = (tile + 1) % (CH / TILE) == 0 || row0 + TILE >= p.nvalid;
-        if (flushed) {  // chunk done (or last valid tile)
-          const LAccT<T> s = wave_sum(lacc);
-          const int ci = tile / (CH / TILE);
-          if (lane == WAVE_LAST) lslab[ci] = s;
-          if (p.fused) {  // reduce_kernel's lane-strided accumulation: lane c % 64 adds chunk c
-            const LAccT<T> sb = __shfl(s, WAVE_LAST);
-            if (lane == ci % 64) csum += sb;
-          }
-          lacc = 0;
-        }
-        if constexpr (!kIsInt<T>) {
-          // Early return (DynamicExpressions returns at the first bad array): a non-finite check
-          // statistic in any lane means did_succeed = false for the whole tree (the host decision
-          // fails every tree whose statistic is non-finite), so its remaining tiles in this row
-          // block cannot change any result.  The unwritten loss chunks get NaN (never read: a failed
-          // tree's loss is L(Inf)); M keeps the non-finite value the host sees.
-          if (p.early_exit && __builtin_amdgcn_ballot_w64(!(M < (CT)INFINITY)) != 0) {
-            csum = (LAccT<T>)NAN;
-            if (lane == WAVE_LAST) {
-              for (int c = tile / (CH / TILE) + (flushed ? 1 : 0); c < p.cpb; ++c) lslab[c] = (LAccT<T>)NAN;
-              __hip_atomic_store(p.fail_flag + group_base + ti, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            break;
-          }
-        }
-      } else if constexpr (MODE == MODE_PRED) {
-        store_pred<T, R>(p, A, tree, lane, row0);
-      }
-    }
-    KDBG("[k] tree %d tiles done\n", tree);
-    KMARK(0, 5);
-    KMARK(8 + wave, 12);
-    // ---- wave reduction, one partial per (tree, row block) ----
-    if constexpr (!kIsInt<T> && MODE != MODE_PRECISE) {
-      M = wave_chk(M);
-      if (lane == WAVE_LAST) reinterpret_cast<CT*>(p.slab_chk)[(int64_t)rb * p.ntrees + group_base + ti] = M;
-    }
-    if constexpr (MODE != MODE_PRECISE) {
-      if (p.fused) {  // the only row block: reduce_kernel's steps for this tree, same order, same bits
-        LAccT<T> s = csum;
-        CT m = 0;
-        if constexpr (!kIsInt<T>) {
-          const CT mb = __shfl(M, WAVE_LAST);  // reduce_kernel's lane 0 reads row block 0
-          if (lane == 0) {
-            if constexpr (sizeof(T) == 4) m = __builtin_elementwise_maximum(m, mb);
-            else m += mb;
-          }
-        }
-        UNR for (int o = 32; o > 0; o >>= 1) {
-          if (MODE == MODE_LOSS) s += __shfl_xor(s, o);
-          if constexpr (!kIsInt<T>) {
-            if constexpr (sizeof(T) == 4) m = __builtin_elementwise_maximum(m, __shfl_xor(m, o));
-            else m += __shfl_xor(m, o);
-          }
-        }
-        if (lane == 0) {
-          if (MODE == MODE_LOSS && p.fused_loss) reinterpret_cast<LAccT<T>*>(p.fused_loss)[tree] = s;
-          if (p.fused_chk) reinterpret_cast<CT*>(p.fused_chk)[tree] = m;
-        }
-      }
-    }
-    KMARK(8 + wave, 13);
-    int claim = 0;
-    if (lane == 0) claim = atomicAdd(&next_tree, 1);
-    ti = __builtin_amdgcn_readfirstlane(claim);
-  }
-  KMARK(8 + wave, 14);
-}
 
 // Per-tree reduction of the partials, fixed order (deterministic): one wavefront per order slot
 // (slab layout of eval_kernel: loss [row block][slot][chunk of the block], check [row block][slot]);
@@ -1115,40 +107,6 @@ __global__ void feature_stats_final(const FeatStat* __restrict__ part, int nb, i
 // ------------------------------------------------------------------------------------------------
 // host-side launchers (called from srhip_host.cpp)
 // ------------------------------------------------------------------------------------------------
-template <typename T, int R, int K, int MODE, bool XLDS>
-static hipError_t launch_eval_t(const EvalArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-  auto kern = eval_kernel<T, R, K, MODE, XLDS>;
-  if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(kern, grid, dim3(64 * eval_waves(R, K)), lds, s, a);
-  return hipGetLastError();
-}
-
-template <typename T, int R, int MODE, bool XLDS>
-static hipError_t launch_eval_k(const EvalArgs& a, int K, dim3 grid, size_t lds, hipStream_t s) {
-  if (K <= 2) return launch_eval_t<T, R, 2, MODE, XLDS>(a, grid, lds, s);
-  if (K <= 4) return launch_eval_t<T, R, 4, MODE, XLDS>(a, grid, lds, s);
-  return launch_eval_t<T, R, 8, MODE, XLDS>(a, grid, lds, s);
-}
-
-template <typename T, int R>
-static hipError_t launch_eval_m(const EvalArgs& a, int K, int mode, bool xlds, dim3 grid, size_t lds, hipStream_t s) {
-  if (mode == MODE_LOSS)
-    return xlds ? launch_eval_k<T, R, MODE_LOSS, true>(a, K, grid, lds, s)
-                : launch_eval_k<T, R, MODE_LOSS, false>(a, K, grid, lds, s);
-  if (mode == MODE_PRED)
-    return xlds ? launch_eval_k<T, R, MODE_PRED, true>(a, K, grid, lds, s)
-                : launch_eval_k<T, R, MODE_PRED, false>(a, K, grid, lds, s);
-  if constexpr (!kIsInt<T>) {
-    // precise mode: rare path, K_MAX stack, global feature reads
-    (void)xlds;
-    return launch_eval_t<T, R, K_MAX, MODE_PRECISE, false>(a, grid, lds, s);
-  }
-  return hipErrorInvalidValue;
-}
-
 int rows_per_lane(int dtype) { return dtype == SRHIP_F64 ? R_F64 : R_F32; }
 
 int pick_rows_per_lane(int dtype, int K, int mode, int64_t m) {
@@ -1163,16 +121,20 @@ hipError_t launch_eval(int dtype, const EvalArgs& a, int R, int K, int mode, boo
                        hipStream_t s) {
   if (R != pick_rows_per_lane(dtype, K, mode, a.nvalid)) return hipErrorInvalidValue;
   if (R == R_F32_WIDE && R != R_F32) {  // Float32, K = 2, loss or prediction
-    if (mode == MODE_LOSS)
-      return xlds ? launch_eval_t<float, R_F32_WIDE, 2, MODE_LOSS, true>(a, grid, lds, s)
-                  : launch_eval_t<float, R_F32_WIDE, 2, MODE_LOSS, false>(a, grid, lds, s);
-    return xlds ? launch_eval_t<float, R_F32_WIDE, 2, MODE_PRED, true>(a, grid, lds, s)
-                : launch_eval_t<float, R_F32_WIDE, 2, MODE_PRED, false>(a, grid, lds, s);
+    if (mode != MODE_LOSS && mode != MODE_PRED) return hipErrorInvalidValue;
+    return launch_eval_f32w(a, mode, xlds, grid, lds, s);
   }
   switch (dtype) {
-    case SRHIP_F32: return launch_eval_m<float, R_F32>(a, K, mode, xlds, grid, lds, s);
-    case SRHIP_F64: return launch_eval_m<double, R_F64>(a, K, mode, xlds, grid, lds, s);
-    case SRHIP_I32: return launch_eval_m<int32_t, R_F32>(a, K, mode, xlds, grid, lds, s);
+    case SRHIP_F32:
+      return mode == MODE_LOSS ? launch_eval_f32_loss(a, K, xlds, grid, lds, s)
+           : mode == MODE_PRED ? launch_eval_f32_pred(a, K, xlds, grid, lds, s)
+                               : launch_eval_f32_precise(a, grid, lds, s);
+    case SRHIP_F64:
+      return mode == MODE_LOSS ? launch_eval_f64_loss(a, K, xlds, grid, lds, s)
+           : mode == MODE_PRED ? launch_eval_f64_pred(a, K, xlds, grid, lds, s)
+                               : launch_eval_f64_precise(a, grid, lds, s);
+    case SRHIP_I32:
+      return mode == MODE_PRECISE ? hipErrorInvalidValue : launch_eval_i32(a, K, mode, xlds, grid, lds, s);
     default: return hipErrorInvalidValue;
   }
 }

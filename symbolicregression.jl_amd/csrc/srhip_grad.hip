@@ -8,7 +8,7 @@
 // same bytecode interpreter as the evaluator (the "gradient program": constants not folded, each
 // constant leaf tagged with its index).  A "chunk" is (tree, first constant c0): trees with more
 // than KT constants take several chunks.  One lane owns one row (R = 1); values and tangents
-// live in VGPRs.  Operator values are computed by the same functions as srhip_eval.hip, so the
+// live in VGPRs.  Operator values are computed by the same functions as srhip_eval_impl.h, so the
 // loss equals srhip_eval_loss's.
 #include <hip/hip_runtime.h>
 #include <stdint.h>

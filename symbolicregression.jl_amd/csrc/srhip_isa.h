@@ -1,5 +1,5 @@
 // srhip_isa.h — the device bytecode ("postfix accumulator/stack machine") shared by the host
-// compiler (srhip_compile.cpp) and the gfx950 interpreter (srhip_eval.hip).
+// compiler (srhip_compile.cpp) and the gfx950 interpreter (srhip_eval_impl.h).
 //
 // Machine model (one wavefront, R rows per lane, all state in VGPRs):
 //   A      accumulator: the value of the subexpression being evaluated (R values per lane)

@@ -1,4 +1,4 @@
-// srhip_kernels.h — kernel argument blocks and launcher declarations (host <-> srhip_eval.hip).
+// srhip_kernels.h — kernel argument blocks and launcher declarations (host <-> srhip_eval.hip and the srhip_eval_<slice>.hip variant units).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -118,7 +118,7 @@ def test_device_special_values(ctx):
 
 
 def test_device_float32_exp_bits_equal_oracle(ctx, oracle):
-    """The packed device exp (srhip_eval.hip expf2_dev) returns the oracle's srm_expf bits on 16.7M
+    """The packed device exp (srhip_eval_impl.h expf2_dev) returns the oracle's srm_expf bits on 16.7M
     inputs: every 256th bit pattern of the whole float range (all exponents, both signs, NaN / Inf)."""
     x = (np.arange(0, 2**32, 256, dtype=np.uint64).astype(np.uint32)).view(np.float32)
     got = _device(ctx, "exp", x)
@@ -164,7 +164,7 @@ def _div_operands(n):
 
 
 def test_device_float32_division_bits_equal_ieee(ctx):
-    """Float32 `/` (srhip_eval.hip div_rows: the range-free division for waves whose operands are all in
+    """Float32 `/` (srhip_eval_impl.h div_rows: the range-free division for waves whose operands are all in
     [2^-40, 2^40], the full v_div_scale / v_div_fixup sequence otherwise) is IEEE division bit for bit
     (numpy's float32 division) in every instruction form: A / X, X / A, A / c, c / A, A / S, S / A."""
     import srhip

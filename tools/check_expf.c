@@ -1,5 +1,5 @@
 /* Exhaustive check of the Float32 exp (include/srhip_math.h srm_expf) over all 2^32 inputs:
- *  (1) the device formulation (srhip_eval.hip expf_rows: NaN-propagating clamp to [-104, 89] instead
+ *  (1) the device formulation (srhip_eval_impl.h expf2_dev: NaN-propagating clamp to [-104, 89] instead
  *      of the branches, v_cvt_i32_f32 semantics, v_ldexp_f32) returns the same bits as srm_expf;
  *      and so does the range-free form of waves whose inputs all lie in [-87, 87] (dev_expf_fast);
  *  (2) accuracy against glibc's double exp rounded to Float32: max ULP distance and the share of
@@ -37,7 +37,7 @@ static float dev_expf(float x0) {
   p = fmaf(r, p, 1.0f);
   return ldexpf(p, cvt_i32(n));
 }
-/* the device's range-free form for waves whose every |x| <= SRM_EXPF_FAST_MAX (srhip_eval.hip
+/* the device's range-free form for waves whose every |x| <= SRM_EXPF_FAST_MAX (srhip_eval_impl.h
  * expf2_fast): n by adding and subtracting 1.5 * 2^23 (the same ties-to-even rounding of the same
  * product as rintf), 2^n built in the exponent field from the low bits of the rounded sum, one
  * multiply instead of ldexp (both round the exact p 2^n once) */
