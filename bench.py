@@ -120,33 +120,44 @@ def main():
         prog.eval_loss(ds, loss)
     barrier()
     t0 = time.perf_counter()
-    kms = []
+    kms, works = [], []
     for _ in range(args.steps):
         l, ok = prog.eval_loss(ds, loss)
         kms.append(ctx.last_kernel_ms())
+        works.append(ctx.last_work())
     barrier()
     dt = time.perf_counter() - t0
+    # work COUNTED on the device: the rows each tree was actually evaluated on (a failed tree -- the
+    # reference's early return -- stops at its failing tile and is skipped by later row blocks)
+    done_node_rows = float(sum(w["node_rows"] for w in works))
+    done_flops = float(sum(w["opnode_rows"] + 3 * w["tree_rows"] for w in works)) / args.steps
     if dist is not None:
         import torch
 
         tt = torch.tensor([dt], dtype=torch.float64, device=red_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+        tw = torch.tensor([done_node_rows], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(tw, op=dist.ReduceOp.SUM)
+        done_node_rows = float(tw.item())
     ms_per_step = dt * 1e3 / args.steps
-    value = work * world * args.steps / dt
+    value = done_node_rows / dt               # evaluated node-rows per second, all ranks
+    nominal_value = work * world * args.steps / dt
     kern_ms = float(np.mean(kms))
-    achieved = flops / (kern_ms * 1e-3) / 1e12
+    achieved = done_flops / (kern_ms * 1e-3) / 1e12
 
     def timed_steps(pr):
-        """(seconds for args.steps evaluations after the warmup, max over ranks; mean kernel ms)"""
+        """(seconds for args.steps evaluations after the warmup, max over ranks; mean kernel ms;
+        counted flops per launch; counted node-rows per launch)"""
         for _ in range(args.warmup):
             pr.eval_loss(ds, loss)
         barrier()
         t0 = time.perf_counter()
-        km = []
+        km, wk = [], []
         for _ in range(args.steps):
             pr.eval_loss(ds, loss)
             km.append(ctx.last_kernel_ms())
+            wk.append(ctx.last_work())
         barrier()
         d = time.perf_counter() - t0
         if dist is not None:
@@ -155,21 +166,25 @@ def main():
             tt = torch.tensor([d], dtype=torch.float64, device=red_dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             d = float(tt.item())
-        return d, float(np.mean(km))
+        fl = float(np.mean([w["opnode_rows"] + 3 * w["tree_rows"] for w in wk]))
+        nr = float(np.mean([w["node_rows"] for w in wk]))
+        return d, float(np.mean(km)), fl, nr
 
     # the same population with derived columns forced on (the launch picks the plain program for C2:
     # every node of every tree evaluated by its own instruction, over longer row blocks; DESIGN.md
     # §3.1) -- reported beside it
-    dt_derived = kern_derived = dt_full = kern_full = float("nan")
+    nan4 = (float("nan"),) * 4
+    dt_grid, kern_grid, fl_grid, nr_grid = nan4
+    dt_full, kern_full, fl_full, nr_full = nan4
+    # the same population through the round-2 grid launch (row blocks x tree groups, no probe)
     if not args.headline_only:
-        os.environ["SRHIP_DERIVE_ALWAYS"] = "1"
-        dt_derived, kern_derived = timed_steps(prog)
-        del os.environ["SRHIP_DERIVE_ALWAYS"]
-    # ... and without the early exit of failed trees (every row of every tree evaluated; the headline
-    # counts the skipped rows of trees that failed as evaluated, like the reference's early return)
+        os.environ["SRHIP_NO_PERSISTENT"] = "1"
+        dt_grid, kern_grid, fl_grid, nr_grid = timed_steps(prog)
+        del os.environ["SRHIP_NO_PERSISTENT"]
+    # ... and without the early exit of failed trees (every row of every tree evaluated)
     if not args.headline_only:
         os.environ["SRHIP_NO_EARLY_EXIT"] = "1"
-        dt_full, kern_full = timed_steps(prog)
+        dt_full, kern_full, fl_full, nr_full = timed_steps(prog)
         del os.environ["SRHIP_NO_EARLY_EXIT"]
 
     # end-to-end per population (host compile of 1024 fresh trees + upload + eval)
@@ -220,8 +235,12 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "kernel": kname,
+                # HIP events around the step's interpreter launches (probe + persistent main launch)
                 "kernel_ms": kern_ms,
-                "flops_per_launch": int(flops),
+                "launches_per_step": 2,
+                # counted on the device (srhip_last_work): evaluated operator-node rows + 3 x tree-rows
+                "flops_per_launch": int(done_flops),
+                "nominal_flops_per_launch": int(flops),
                 # SQ_ACTIVE_INST_VALU x 4 / (GRBM_GUI_ACTIVE x 1024 SIMDs) from the same PMC summary:
                 # the issue-slot bound the kernel actually runs against
                 "valu_issue_util": valu_issue,
@@ -230,12 +249,16 @@ def main():
             "cpu_baseline": cpu,
             "extra": {
                 "compile_ms_1024_trees": compile_ms, "end_to_end_ms_per_population": e2e_ms,
-                "derived_columns": {"value": work * world * args.steps / dt_derived, "kernel_ms": kern_derived,
-                                    "frac": flops / (kern_derived * 1e-3) / 1e12 / PEAK_FP32_TFLOPS,
-                                    "note": "SRHIP_DERIVE_ALWAYS=1: shared U(X[f]) columns in LDS (2048-row "
-                                            "blocks); the headline runs the plain program (4096-row blocks)"},
-                "no_early_exit": {"value": work * world * args.steps / dt_full, "kernel_ms": kern_full,
-                                  "frac": flops / (kern_full * 1e-3) / 1e12 / PEAK_FP32_TFLOPS,
+                # population scoring rate: every live tree's nodes x every row per step / step time (the
+                # rows a failed tree skipped counted as if evaluated)
+                "nominal_value": nominal_value,
+                "evaluated_fraction": done_node_rows / (work * world * args.steps),
+                "grid_launch": {"value": nr_grid * world * args.steps / dt_grid, "kernel_ms": kern_grid,
+                                "frac": fl_grid / (kern_grid * 1e-3) / 1e12 / PEAK_FP32_TFLOPS,
+                                "nominal_value": work * world * args.steps / dt_grid,
+                                "note": "SRHIP_NO_PERSISTENT=1: the round-2 launch (row blocks x tree groups)"},
+                "no_early_exit": {"value": nr_full * world * args.steps / dt_full, "kernel_ms": kern_full,
+                                  "frac": fl_full / (kern_full * 1e-3) / 1e12 / PEAK_FP32_TFLOPS,
                                   "note": "SRHIP_NO_EARLY_EXIT=1: failed trees evaluated on every row"},
             },
         }

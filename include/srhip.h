@@ -247,6 +247,12 @@ int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_prog
  * srhip_eval_predict, or the dual-number kernel of srhip_eval_loss_grad / the optimiser's last
  * gradient launch -- measured with HIP events recorded on the context's stream; < 0 if unavailable. */
 double srhip_last_kernel_ms(const srhip_ctx* ctx);
+/* Work of the last srhip_eval_loss / srhip_eval_loss_partials / srhip_eval_predict on this context,
+ * counted on the device (the rows each tree was actually evaluated on: a tree that failed -- the
+ * reference's early return -- stops at the failing tile): out[0] evaluated node-rows (count_nodes x
+ * rows), out[1] nominal node-rows (every live tree on every row), out[2] evaluated operator-node
+ * rows, out[3] evaluated tree-rows. */
+int srhip_last_work(const srhip_ctx* ctx, int64_t out[4]);
 /* Per-program work counters: sum over trees of count_nodes / operator nodes. */
 int srhip_program_stats(const srhip_program* prog, int64_t* total_nodes, int64_t* total_opnodes,
                         int32_t* max_stack);

@@ -15,12 +15,14 @@ template <typename LT, typename CT, bool CHK_MAX>
 __global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab_loss, int nch, int cpb,
                                                      const CT* __restrict__ slab_chk, int nrb, int nslots,
                                                      const int32_t* __restrict__ order, LT* __restrict__ out_loss,
-                                                     CT* __restrict__ out_chk) {
+                                                     CT* __restrict__ out_chk, const int32_t* __restrict__ slab_rows,
+                                                     int64_t* __restrict__ out_rows) {
   const int lane = threadIdx.x & 63;
   const int slot = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (slot >= nslots) return;
   LT s = 0;
   CT m = 0;
+  long long rows = 0;
   if (slab_loss)
     for (int c = lane; c < nch; c += 64) s += slab_loss[((int64_t)(c / cpb) * nslots + slot) * cpb + c % cpb];
   for (int i = lane; i < nrb; i += 64) {
@@ -28,16 +30,19 @@ __global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab
       const CT v = slab_chk[(int64_t)i * nslots + slot];
       if constexpr (CHK_MAX) m = __builtin_elementwise_maximum(m, v); else m += v;
     }
+    if (slab_rows) rows += slab_rows[(int64_t)i * nslots + slot];
   }
   UNR for (int o = 32; o > 0; o >>= 1) {
     if (slab_loss) s += __shfl_xor(s, o);
     if constexpr (CHK_MAX) m = __builtin_elementwise_maximum(m, __shfl_xor(m, o));
     else m += __shfl_xor(m, o);
+    if (slab_rows) rows += __shfl_xor(rows, o);
   }
   if (lane == 0) {
     const int tree = order[slot];
     if (out_loss) out_loss[tree] = s;
     if (out_chk) out_chk[tree] = m;
+    if (out_rows) out_rows[tree] = rows;
   }
 }
 
@@ -140,20 +145,24 @@ hipError_t launch_eval(int dtype, const EvalArgs& a, int R, int K, int mode, boo
 }
 
 hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, int cpb, const void* slab_chk, int nrb, int nslots,
-                         const int32_t* order, void* out_loss, void* out_chk, hipStream_t s) {
+                         const int32_t* order, void* out_loss, void* out_chk, hipStream_t s, const int32_t* slab_rows,
+                         int64_t* out_rows) {
   dim3 grid((nslots + 3) / 4), block(256);
   switch (dtype) {
     case SRHIP_F32:
       hipLaunchKernelGGL((reduce_kernel<double, float, true>), grid, block, 0, s, (const double*)slab_loss, nch, cpb,
-                         (const float*)slab_chk, nrb, nslots, order, (double*)out_loss, (float*)out_chk);
+                         (const float*)slab_chk, nrb, nslots, order, (double*)out_loss, (float*)out_chk, slab_rows,
+                         out_rows);
       break;
     case SRHIP_F64:
       hipLaunchKernelGGL((reduce_kernel<double, double, false>), grid, block, 0, s, (const double*)slab_loss, nch, cpb,
-                         (const double*)slab_chk, nrb, nslots, order, (double*)out_loss, (double*)out_chk);
+                         (const double*)slab_chk, nrb, nslots, order, (double*)out_loss, (double*)out_chk, slab_rows,
+                         out_rows);
       break;
     case SRHIP_I32:
       hipLaunchKernelGGL((reduce_kernel<long long, float, true>), grid, block, 0, s, (const long long*)slab_loss, nch,
-                         cpb, (const float*)nullptr, nrb, nslots, order, (long long*)out_loss, (float*)nullptr);
+                         cpb, (const float*)nullptr, nrb, nslots, order, (long long*)out_loss, (float*)nullptr,
+                         slab_rows, out_rows);
       break;
     default: return hipErrorInvalidValue;
   }

@@ -219,6 +219,34 @@ __device__ __attribute__((noinline)) RV<float, R> trigf_fix(RV<float, R> v, RV<f
   }
   return res;
 }
+// Float32 cos / sin of a lane's R rows as two leaf bodies: the handler tests the wave's rows first
+// (one NaN-propagating max |x| per row pair, a ballot) and calls trigf_fast -- every row in the
+// fast range, computed in place, no call inside, so no return-address save and no copy of the
+// inputs -- or, if any row of the wave is outside it (|x| >= 2^28 pi/2, Inf, NaN), trigf_slow,
+// which takes the scalar srm_trigf path for those rows.  The same values as trigf_rows.
+template <int R, int KIND>
+__device__ __attribute__((noinline)) RV<float, R> trigf_fast(RV<float, R> v) {
+  UNR for (int r = 0; r < R; ++r) {
+    v[r] = sincosf_dev<KIND>((double)v[r]);
+    if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
+  }
+  return v;
+}
+template <int R, int KIND>
+__device__ __attribute__((noinline)) RV<float, R> trigf_slow(RV<float, R> v) {
+  UNR for (int r = 0; r < R; ++r) {
+    const float x = v[r];
+    v[r] = __builtin_fabsf(x) < SRM_PIO2F_BIG_F ? sincosf_dev<KIND>((double)x) : srm_trigf(KIND, x);
+  }
+  return v;
+}
+template <int R> __device__ __attribute__((always_inline)) inline bool trigf_rows_fast(const float (&A)[R]) {
+  float mx = 0.0f;
+  UNR for (int r = 0; r < R; r += 2)
+    asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(A[r]), "v"(A[r + 1]));
+  return __builtin_amdgcn_ballot_w64(!(mx < SRM_PIO2F_BIG_F)) == 0;  // false for NaN
+}
+
 template <int R, int KIND>
 __device__ __attribute__((always_inline)) inline RV<float, R> trigf_rows(RV<float, R> v) {
   RV<float, R> res;
@@ -316,7 +344,13 @@ constexpr bool un_wide(int u) { return un_wide_op(u); }
 template <int U> constexpr bool un_inline() { return un_cheap(U); }
 template <typename T, int R, int U>
 __device__ __attribute__((always_inline)) inline void apply_un(T (&A)[R]) {
-  if constexpr (un_inline<U>()) {
+  if constexpr (SRHIP_TRIG_ROWS && std::is_same<T, float>::value && (U == UN_COS || U == UN_SIN) && R % 2 == 0) {
+    constexpr int KIND = U == UN_COS ? 0 : 1;
+    RV<T, R> v;
+    UNR for (int r = 0; r < R; ++r) v[r] = A[r];
+    v = trigf_rows_fast<R>(A) ? trigf_fast<R, KIND>(v) : trigf_slow<R, KIND>(v);
+    UNR for (int r = 0; r < R; ++r) A[r] = v[r];
+  } else if constexpr (un_inline<U>()) {
     using O = OpsT<T>;
     UNR for (int r = 0; r < R; ++r) {
       switch (U) {
@@ -603,12 +637,25 @@ __device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& 
     if (p.weighted) {
       // padded rows carry w = 0 and a replicated (finite when ok) prediction
       UNR for (int r = 0; r < R; ++r) lacc += (double)(wv[r] * lv[r]);
-    } else if (full) {
-      UNR for (int r = 0; r < R; ++r) lacc += (double)lv[r];
     } else {
-      UNR for (int r = 0; r < R; ++r) {
-        const int64_t row = row0 + (r / VEC) * 64 * VEC + lane * VEC + (r % VEC);
-        lacc += row < p.nvalid ? (double)lv[r] : 0.0;
+      if (!full) {
+        UNR for (int r = 0; r < R; ++r) {
+          const int64_t row = row0 + (r / VEC) * 64 * VEC + lane * VEC + (r % VEC);
+          lv[r] = row < p.nvalid ? lv[r] : T(0);
+        }
+      }
+      if constexpr (sizeof(T) == 4 && R % 4 == 0 && VEC == 4) {
+        // Float32: a lane's 4 consecutive rows (one 16-byte group: the same rows in every launch
+        // geometry) summed in Float32, (l0 + l1) + (l2 + l3) -- one packed add, one add -- then
+        // widened once: relative error <= 2^-23 for the non-negative distance losses, against the
+        // 1e-6 parity bar; one bit pattern per tree and dataset as before
+        UNR for (int r = 0; r < R; r += 4) {
+          const F2 a = {lv[r], lv[r + 2]}, b = {lv[r + 1], lv[r + 3]};
+          const F2 q = a + b;
+          lacc += (double)(q.x + q.y);
+        }
+      } else {
+        UNR for (int r = 0; r < R; ++r) lacc += (double)lv[r];
       }
     }
   }
@@ -695,23 +742,74 @@ __device__ __attribute__((always_inline)) inline void derive_columns(const EvalA
   __syncthreads();
 }
 
+// Derived columns for one row block, a wave per (column, tile): the wave runs the interpreter's own
+// R-row operator body over one tile of the source feature (the same call the U instruction makes,
+// so the values are the same bits), stores it into the column and parks the tile's check statistic
+// in LDS; after one barrier the first nd threads fold each column's tiles in tile order.
+template <typename T, int R>
+__device__ __attribute__((always_inline)) inline void derive_columns_tiles(const EvalArgs& p, T* lx, int rbb,
+                                                                           typename Chk<T>::type* dchk) {
+  using CT = typename Chk<T>::type;
+  constexpr int TILE = 64 * R, VEC = 16 / sizeof(T);
+  constexpr int MAX_TILES = ROW_ALIGN / TILE > 0 ? ROW_ALIGN / TILE : 1;
+  __shared__ CT part[DERIVE_MAX][MAX_TILES];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nwaves = blockDim.x >> 6;
+  const int ntiles = rbb / TILE;
+  for (int item = wave; item < p.nd * ntiles; item += nwaves) {
+    const int d = item / ntiles, j = item - d * ntiles;
+    const uint32_t spec = __builtin_amdgcn_readfirstlane(p.dspec[d]);
+    const int u = (int)(spec >> 16), f = (int)(spec & 0xffff);
+    T v[R];
+    load_rows<T, R>(lx + (int64_t)f * rbb + (int64_t)j * TILE, lane, v);
+    RV<T, R> rv;
+    UNR for (int r = 0; r < R; ++r) rv[r] = v[r];
+    rv = derive_un<T, R>(u, rv);
+    CT m = 0;
+    using V = typename Vec16<T>::type;
+    T* dst = lx + (int64_t)(p.nfeat + d) * rbb + (int64_t)j * TILE;
+    UNR for (int q = 0; q < R / VEC; ++q) {
+      V o;
+      UNR for (int e = 0; e < VEC; ++e) {
+        o[e] = rv[q * VEC + e];
+        if constexpr (sizeof(T) == 4) m = __builtin_elementwise_maximum(m, __builtin_fabsf(o[e]));
+        else m = __builtin_fma(__builtin_fabs(o[e]), 0x1p-512, m);
+      }
+      reinterpret_cast<V*>(dst)[q * 64 + lane] = o;
+    }
+    m = wave_chk(m);
+    if (lane == WAVE_LAST) part[d][j] = m;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < p.nd) {
+    const int d = threadIdx.x;
+    CT t = part[d][0];
+    for (int j = 1; j < ntiles; ++j) {
+      if constexpr (sizeof(T) == 4) t = __builtin_elementwise_maximum(t, part[d][j]);
+      else t += part[d][j];
+    }
+    dchk[d] = t;
+  }
+  __syncthreads();
+}
+
 // ------------------------------------------------------------------------------------------------
 // The interpreter kernel.
 //   grid.x = row blocks (RB rows each), grid.y = tree groups; block = WAVES wavefronts.
 //   MODE_LOSS: fused loss partial + check partial per (tree, row block) -> slabs
 //   MODE_PRED: prediction rows -> out_pred[tree][row], check partial -> slab
 // ------------------------------------------------------------------------------------------------
+// One (row block, tree group) of the launch: stage the block, derive its columns, interpret the
+// group's trees over it.  rb = row block, gy = tree group (grid.y; 0 in persistent launches, whose
+// one group is the whole population).
 template <typename T, int R, int K, int MODE, bool XLDS>
-__global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p) {
+__device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs& p, unsigned char* smem, const int rb,
+                                                                 const int gy) {
   constexpr int WAVES = eval_waves(R, K);
   using O = OpsT<T>;
   using CT = typename Chk<T>::type;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  KMARK(0, 1);
-  if (p.debug_stop == 1) return;
   constexpr int TILE = 64 * R;
   const int lane = threadIdx.x & 63;
-  const int rb = blockIdx.x;
   const int64_t row_base = (int64_t)rb * p.rb_rows;
   const int ntiles = p.rb_rows / TILE;
 
@@ -756,8 +854,8 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
   constexpr int FLAG_SNAP = 2048;
   constexpr bool SNAP = MODE == MODE_LOSS && !kIsInt<T>;
   __shared__ uint8_t failed_snap[SNAP ? FLAG_SNAP : 1];
-  const int snap_base = p.group_off ? p.group_off[blockIdx.y] : (int)blockIdx.y * p.trees_per_group;
-  const int snap_n = p.group_off ? p.group_off[blockIdx.y + 1] - snap_base
+  const int snap_base = p.group_off ? p.group_off[gy] : gy * p.trees_per_group;
+  const int snap_n = p.group_off ? p.group_off[gy + 1] - snap_base
                                  : min(p.trees_per_group, p.ntrees - snap_base);
   if constexpr (SNAP) {
     if (p.early_exit)
@@ -768,15 +866,17 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
   constexpr bool DERIVED = XLDS && !kIsInt<T> && MODE != MODE_PRECISE;
   __shared__ CT dchk[DERIVED ? DERIVE_MAX : 1];
   if constexpr (DERIVED) {
-    if (p.nd > 0) derive_columns<T>(p, reinterpret_cast<T*>(smem), p.rb_rows, dchk);
+    if (p.nd > 0) {
+      if (p.persistent) derive_columns_tiles<T, R>(p, reinterpret_cast<T*>(smem), p.rb_rows, dchk);
+      else derive_columns<T>(p, reinterpret_cast<T*>(smem), p.rb_rows, dchk);
+    }
   }
   KMARK(0, 2);
-  if (p.debug_stop == 2) return;
+  if (p.debug_stop == 2) return;  // (diagnostic runs are never persistent)
 
   // tree group of this workgroup: uniform, or the host's tail-shaped sizes (group_off)
-  const int group_base = p.group_off ? __builtin_amdgcn_readfirstlane(p.group_off[blockIdx.y])
-                                     : (int)blockIdx.y * p.trees_per_group;
-  const int group_n = p.group_off ? __builtin_amdgcn_readfirstlane(p.group_off[blockIdx.y + 1]) - group_base
+  const int group_base = p.group_off ? __builtin_amdgcn_readfirstlane(p.group_off[gy]) : gy * p.trees_per_group;
+  const int group_n = p.group_off ? __builtin_amdgcn_readfirstlane(p.group_off[gy + 1]) - group_base
                                   : min(p.trees_per_group, p.ntrees - group_base);
 
   // the group's trees are in descending estimated cost (host make_order): wave w starts with tree w,
@@ -824,6 +924,7 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
     LAccT<T>* lslab = reinterpret_cast<LAccT<T>*>(p.slab_loss) +
                       ((int64_t)rb * p.ntrees + group_base + ti) * __builtin_amdgcn_readfirstlane(p.cpb);
     LAccT<T> csum = 0;  // fused launches: this lane's share of the tree's chunk sums
+    int rows_done = 0;  // valid rows this wave evaluated the tree on (the launch's work count)
     if (failed) {
       if (lane == WAVE_LAST)
         for (int c = 0; c < p.cpb; ++c) lslab[c] = (LAccT<T>)NAN;
@@ -833,6 +934,7 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
     for (int tile = 0; tile < (failed ? 0 : ntiles); ++tile) {
       const int64_t row0 = row_base + (int64_t)tile * TILE;
       if (row0 >= p.nvalid) break;  // whole tile is padding
+      rows_done += (int)min((int64_t)TILE, p.nvalid - row0);
       const T* xt = xsrc + (int64_t)tile * TILE;
       T A[R], S[K][R];
       UNR for (int r = 0; r < R; ++r) A[r] = T(0);
@@ -987,6 +1089,7 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
       M = wave_chk(M);
       if (lane == WAVE_LAST) reinterpret_cast<CT*>(p.slab_chk)[(int64_t)rb * p.ntrees + group_base + ti] = M;
     }
+    if (p.slab_rows && lane == WAVE_LAST) p.slab_rows[(int64_t)rb * p.ntrees + group_base + ti] = rows_done;
     if constexpr (MODE != MODE_PRECISE) {
       if (p.fused) {  // the only row block: reduce_kernel's steps for this tree, same order, same bits
         LAccT<T> s = csum;
@@ -1008,6 +1111,7 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
         if (lane == 0) {
           if (MODE == MODE_LOSS && p.fused_loss) reinterpret_cast<LAccT<T>*>(p.fused_loss)[tree] = s;
           if (p.fused_chk) reinterpret_cast<CT*>(p.fused_chk)[tree] = m;
+          if (p.fused_rows) p.fused_rows[tree] = rows_done;
         }
       }
     }
@@ -1017,6 +1121,36 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
     ti = __builtin_amdgcn_readfirstlane(claim);
   }
   KMARK(8 + wave, 14);
+}
+
+// ------------------------------------------------------------------------------------------------
+// The interpreter kernel.
+//   grid.x = row blocks (RB rows each), grid.y = tree groups; block = WAVES wavefronts.
+//   Persistent launches (p.persistent, one tree group): grid.x workgroups, each claims row blocks
+//   block0, block0 + 1, ... from the counter p.block_ctr (zeroed before the launch) and interprets
+//   the whole population over each, until the blocks run out -- every workgroup leaves the loop on
+//   the same claimed index, so the grid always drains.
+//   MODE_LOSS: fused loss partial + check partial per (tree, row block) -> slabs
+//   MODE_PRED: prediction rows -> out_pred[tree][row], check partial -> slab
+// ------------------------------------------------------------------------------------------------
+template <typename T, int R, int K, int MODE, bool XLDS>
+__global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  KMARK(0, 1);
+  if (p.debug_stop == 1) return;
+  if (p.persistent) {
+    __shared__ int claimed;
+    for (;;) {
+      if (threadIdx.x == 0) claimed = atomicAdd(p.block_ctr, 1) + p.block0;
+      __syncthreads();
+      const int rb = __builtin_amdgcn_readfirstlane(claimed);
+      if (rb >= p.nrb) break;
+      eval_block<T, R, K, MODE, XLDS>(p, smem, rb, 0);
+      __syncthreads();  // every wave is done with this block's LDS (and has read `claimed`)
+    }
+  } else {
+    eval_block<T, R, K, MODE, XLDS>(p, smem, blockIdx.x, blockIdx.y);
+  }
 }
 
 // ---- launch helpers, instantiated by the per-variant translation units ----

@@ -114,6 +114,7 @@ template <typename T> class TreeCompiler {
     int rc = validate(0, 0);
     if (rc) return rc;
     info.nnodes = count_nodes(0);
+    info.nops = count_opnodes(0);
     info.nconst = count_constants(0);
     cidx_.assign(nn_, -1);
     dcolv_.assign(dspec_ && !grad_ ? nn_ : 0, -1);
@@ -217,6 +218,12 @@ template <typename T> class TreeCompiler {
     return rc;
   }
 
+  int32_t count_opnodes(int64_t i) const {  // operator nodes (degree >= 1), as count_nodes walks them
+    const srhip_node& n = nd_[i];
+    if (n.degree == 0) return 0;
+    if (n.degree == 1) return 1 + count_opnodes(n.l);
+    return 1 + count_opnodes(n.l) + count_opnodes(n.r);
+  }
   int32_t count_nodes(int64_t i) const {
     const srhip_node& n = nd_[i];
     if (n.degree == 0) return 1;
@@ -1268,7 +1275,51 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     if (eval_waves(r, k) >= 16) return 152 * 1024;
     return derived ? 64 * 1024 - 512 : 64 * 1024 - 64;
   };
-  if (nd > 0 && mode != MODE_PRECISE) {
+  // Persistent launch (the wide Float32 variant's loss launches): one workgroup per CU claims short
+  // row blocks from a counter and interprets the WHOLE population over each -- the dataset is read
+  // from HBM once, every derived column is computed once per row block for all trees, and the tail
+  // is one short block instead of a wave of workgroups.  A probe launch first evaluates the leading
+  // row blocks with many small tree groups, so trees that fail there (DynamicExpressions' early
+  // return: did_succeed = false whatever the other rows hold) are skipped by every later block.
+  // SRHIP_NO_PERSISTENT=1: the grid launch; SRHIP_PRB_ROWS: row-block rows (default 2048: C2, one
+  // MI355X, same box: 1024 rows 1.31 ms, 2048 1.19, 4096 1.35, grid launch 1.33);
+  // SRHIP_PROBE_BLOCKS: probe row blocks (default 4).
+  static const bool no_persistent = [] { const char* e = getenv("SRHIP_NO_PERSISTENT"); return e && *e && *e != '0'; }();
+  static const int prb_env = [] { const char* e = getenv("SRHIP_PRB_ROWS"); return e ? atoi(e) : 0; }();
+  static const int probe_env = [] { const char* e = getenv("SRHIP_PROBE_BLOCKS"); return e ? atoi(e) : -1; }();
+  bool persistent = false;
+  int probe_blocks = 0;
+  {
+    const int Kp = kvariant(P->kmax);
+    persistent = !no_persistent && mode == MODE_LOSS && debug_stop() == 0 && dtype == SRHIP_F32 &&
+                 pick_rows_per_lane(dtype, Kp, mode, v.m) == R_F32_WIDE && R_F32_WIDE != R_F32 &&
+                 (nd == 0 || kvariant(P->dkmax) == Kp);
+    if (persistent) {
+      K = Kp;
+      R = R_F32_WIDE;
+      const int tile = 64 * R;
+      int rb = prb_env >= tile && prb_env <= ROW_ALIGN && (prb_env & (prb_env - 1)) == 0 ? prb_env : 2048;
+      rb = std::max(rb, std::max(tile, loss_chunk(dtype)));
+      const size_t es = dtype_size(dtype);
+      const int base_cols = P->maxfeat + 1 + (weighted ? 1 : 0);
+      use_d = nd > 0 && (size_t)(base_cols + nd) * rb * es <= lds_budget(R, K, true);
+      const int ncols = base_cols + (use_d ? nd : 0);
+      if ((size_t)ncols * rb * es > lds_budget(R, K, false)) {
+        persistent = false;  // the block does not fit LDS: grid launch over global reads
+        use_d = false;
+      } else {
+        L.rb_rows = rb;
+        L.xlds = true;
+        L.lds = (size_t)ncols * rb * es + 16;
+        L.nrb = (int)((v.m + rb - 1) / rb);
+        L.groups = 1;
+        L.tpg = (int)live.size();
+        probe_blocks = probe_env >= 0 ? probe_env : 4;
+        probe_blocks = L.nrb >= 16 * std::max(1, probe_blocks) ? probe_blocks : 0;
+      }
+    }
+  }
+  if (!persistent && nd > 0 && mode != MODE_PRECISE) {
     K = kvariant(P->dkmax);
     R = pick_rows_per_lane(dtype, K, mode, v.m);
     L = plan_launch(ctx, dtype, P->maxfeat + nd, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R,
@@ -1287,7 +1338,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       if (Lp.xlds && Lp.rb_rows > L.rb_rows) use_d = false;
     }
   }
-  if (!use_d) {
+  if (!persistent && !use_d) {
     K = kvariant(P->kmax);
     R = pick_rows_per_lane(dtype, K, mode, v.m);
     L = plan_launch(ctx, dtype, P->maxfeat, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R,
@@ -1295,7 +1346,9 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   }
   const int nl = (int)live.size();
   const void* d_order;
-  const std::vector<int32_t> goff = shape_groups(L, nl, ctx->num_cu);
+  // persistent launches: one group, the order globally by descending cost (the probe's uniform
+  // groups of one tree per wave are consecutive slots of it)
+  const std::vector<int32_t> goff = persistent ? std::vector<int32_t>{0, nl} : shape_groups(L, nl, ctx->num_cu);
   {
     std::lock_guard<std::mutex> g(P->ord_mu);
     if (P->upload_pending || P->ord_key[0] != L.groups || P->ord_key[1] != L.tpg || P->ord_key[2] != (int)use_d ||
@@ -1333,6 +1386,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   // device-to-host copies on the stream)
   HIP_TRY(ctx->h_loss.ensure((size_t)nt * 8, hipHostMallocCoherent));
   HIP_TRY(ctx->h_chk.ensure((size_t)nt * 8, hipHostMallocCoherent));
+  HIP_TRY(ctx->h_rows.ensure((size_t)nt * 8, hipHostMallocCoherent));
   EvalArgs a{};
   a.code = use_d ? P->dcode_dev : P->code_dev;
   a.prog_off = use_d ? P->doff_dev : P->off_dev;
@@ -1368,6 +1422,10 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     a.fused = 1;
     a.fused_loss = mode == MODE_LOSS ? ctx->h_loss.p : nullptr;
     a.fused_chk = dtype == SRHIP_I32 ? nullptr : ctx->h_chk.p;
+    a.fused_rows = (int64_t*)ctx->h_rows.p;
+  } else {
+    HIP_TRY(ctx->slab_rows.ensure((size_t)nl * L.nrb * sizeof(int32_t)));
+    a.slab_rows = (int32_t*)ctx->slab_rows.p;
   }
   a.early_exit = mode == MODE_LOSS && early_exit_on() ? 1 : 0;
   if (a.early_exit) {
@@ -1385,8 +1443,35 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     a.out_pred = pred.p;
   }
   dim3 grid(L.nrb, (unsigned)goff.size() - 1);
+  if (persistent) HIP_TRY(ctx->block_ctr.ensure(sizeof(int32_t)));
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
-  HIP_TRY(launch_eval(dtype, a, R, K, mode, L.xlds, grid, L.lds, ctx->stream));
+  if (persistent) {
+    if (probe_blocks > 0) {
+      // leading row blocks, one tree per wave (uniform groups of consecutive slots), with the plain
+      // program: a probe workgroup serves 16 trees, too few to pay for deriving columns (the values,
+      // partials and slots are the same either way)
+      EvalArgs q = a;
+      q.group_off = nullptr;
+      q.trees_per_group = eval_waves(R, K);
+      q.code = P->code_dev;
+      q.prog_off = P->off_dev;
+      q.max_steps = P->max_len;
+      q.nd = 0;
+      q.dspec = nullptr;
+      q.dmask = nullptr;
+      const size_t qlds = (size_t)(P->maxfeat + 1 + (weighted ? 1 : 0)) * L.rb_rows * es + 16;
+      const dim3 pgrid(probe_blocks, (unsigned)((nl + q.trees_per_group - 1) / q.trees_per_group));
+      HIP_TRY(launch_eval(dtype, q, R, K, mode, true, pgrid, qlds, ctx->stream));
+    }
+    HIP_TRY(hipMemsetAsync(ctx->block_ctr.p, 0, sizeof(int32_t), ctx->stream));
+    a.persistent = 1;
+    a.block0 = probe_blocks;
+    a.block_ctr = (int32_t*)ctx->block_ctr.p;
+    const int wgs = std::max(1, std::min(L.nrb - probe_blocks, ctx->num_cu));
+    HIP_TRY(launch_eval(dtype, a, R, K, mode, true, dim3(wgs, 1), L.lds, ctx->stream));
+  } else {
+    HIP_TRY(launch_eval(dtype, a, R, K, mode, L.xlds, grid, L.lds, ctx->stream));
+  }
   HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
   ctx->timed = true;
   if (trace_on()) {  // poll the kernel's progress words for up to 10 s, then abort loudly
@@ -1417,7 +1502,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, nch, cpb,
                           dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p, L.nrb, nl, (const int32_t*)d_order,
                           mode == MODE_LOSS ? ctx->h_loss.p : nullptr, dtype == SRHIP_I32 ? nullptr : ctx->h_chk.p,
-                          ctx->stream));
+                          ctx->stream, a.slab_rows, (int64_t*)ctx->h_rows.p));
   if (mode == MODE_PRED)
     HIP_TRY(hipMemcpyAsync(out_pred, pred.p, (size_t)nt * v.m * es, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -1426,6 +1511,15 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       sums[2 * (size_t)t] = dtype == SRHIP_I32 ? (double)((long long*)ctx->h_loss.p)[t] : ((double*)ctx->h_loss.p)[t];
     if (dtype == SRHIP_F32) chk[t] = ((float*)ctx->h_chk.p)[t];
     else if (dtype == SRHIP_F64) chk[t] = ((double*)ctx->h_chk.p)[t];
+  }
+  // the launch's work, counted on the device (rows each tree was evaluated on)
+  for (int i = 0; i < 4; ++i) ctx->work[i] = 0;
+  for (int32_t t : live) {
+    const int64_t rows = ((const int64_t*)ctx->h_rows.p)[t];
+    ctx->work[0] += rows * P->info[t].nnodes;
+    ctx->work[1] += v.m * P->info[t].nnodes;
+    ctx->work[2] += rows * P->info[t].nops;
+    ctx->work[3] += rows;
   }
   return SRHIP_OK;
 }
@@ -1838,6 +1932,12 @@ double srhip_last_kernel_ms(const srhip_ctx* ctx) {
   float ms = -1.0f;
   if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) != hipSuccess) return -1.0;
   return (double)ms;
+}
+
+int srhip_last_work(const srhip_ctx* ctx, int64_t* out) {
+  if (!ctx || !out) return fail(SRHIP_ERR_INVALID, "null argument");
+  for (int i = 0; i < 4; ++i) out[i] = ctx->work[i];
+  return SRHIP_OK;
 }
 
 int srhip_program_stats(const srhip_program* P, int64_t* total_nodes, int64_t* total_opnodes, int32_t* max_stack) {

@@ -125,6 +125,13 @@ struct srhip_ctx {
   srhip::HostBuf h_loss, h_chk, h_stats, h_prec, h_dbg;
   srhip::DevBuf fail_flag;  // [order slots] int32: launch epoch in which the tree was seen to fail
   int32_t epoch = 0;        // interpreter launches so far (MODE_LOSS with early exit)
+  srhip::DevBuf block_ctr;  // persistent launches: the row-block counter (one int32, zeroed per launch)
+  srhip::DevBuf slab_rows;  // [row block][order slot] valid rows evaluated
+  srhip::HostBuf h_rows;    // [program trees] int64 rows evaluated per tree (coherent pinned)
+  // work of the last srhip_eval_loss / srhip_eval_predict on this context (srhip_last_work):
+  // evaluated node-rows, nominal node-rows (every live tree on every row), evaluated operator-node
+  // rows, evaluated tree-rows
+  int64_t work[4] = {0, 0, 0, 0};
 };
 
 struct srhip_dataset {

@@ -90,6 +90,13 @@ struct EvalArgs {
   int32_t fused;
   void* fused_loss;         // [program trees] LAccT (MODE_LOSS) or nullptr
   void* fused_chk;          // [program trees] check statistic type, or nullptr (Int32)
+  // persistent launches (one tree group, the whole population): grid.x workgroups claim row blocks
+  // block0 .. nrb-1 from *block_ctr (zeroed before the launch)
+  int32_t persistent;
+  int32_t block0;
+  int32_t* block_ctr;
+  int32_t* slab_rows;       // [nrb][ntrees] valid rows each (row block, order slot) evaluated, or nullptr
+  int64_t* fused_rows;      // fused launches: [program trees] rows evaluated (coherent pinned host), or nullptr
 };
 
 int rows_per_lane(int dtype);
@@ -99,8 +106,10 @@ hipError_t launch_eval(int dtype, const EvalArgs& a, int R, int K, int mode, boo
                        hipStream_t s);
 // per-tree reduction of eval_kernel's slabs: nslots order slots, cpb loss chunks per row block, results
 // at out[order[slot]]
+// slab_rows (optional): [nrb][nslots] rows evaluated, summed per tree into out_rows (int64)
 hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, int cpb, const void* slab_chk, int nrb, int nslots,
-                         const int32_t* order, void* out_loss, void* out_chk, hipStream_t s);
+                         const int32_t* order, void* out_loss, void* out_chk, hipStream_t s,
+                         const int32_t* slab_rows = nullptr, int64_t* out_rows = nullptr);
 hipError_t launch_gather(int dtype, const void* X, const void* y, const void* w, int64_t ld_src, int nfeat,
                          const int64_t* idx, int64_t m, int64_t ld_dst, void* Xd, void* yd, void* wd, hipStream_t s);
 hipError_t launch_feature_stats(int dtype, const void* X, int64_t ld, int64_t m, int nfeat, FeatStat* out,

@@ -108,6 +108,7 @@ SIGNATURES = {
     "srhip_batcher_timing": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "srhip_batcher_destroy": (None, [_vp]),
     "srhip_last_kernel_ms": (_dbl, [_vp]),
+    "srhip_last_work": (ctypes.c_int, [_vp, ctypes.POINTER(_i64)]),
     "srhip_program_stats": (ctypes.c_int, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
                                            ctypes.POINTER(_i32)]),
     "srhip_program_derived": (ctypes.c_int, [_vp, ctypes.POINTER(_i32), _vp, _i32]),

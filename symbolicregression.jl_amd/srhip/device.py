@@ -29,6 +29,15 @@ class Context:
     def last_kernel_ms(self) -> float:
         return float(self._lib.srhip_last_kernel_ms(self.handle))
 
+    def last_work(self) -> dict:
+        """Work of the last evaluation launch, counted on the device (srhip_last_work): node-rows
+        evaluated, nominal node-rows (every live tree on every row), operator-node rows and tree-rows
+        evaluated.  A failed tree (the reference's early return) stops at its failing tile."""
+        out = (ctypes.c_int64 * 4)()
+        check(self._lib.srhip_last_work(self.handle, out))
+        return {"node_rows": int(out[0]), "nominal_node_rows": int(out[1]), "opnode_rows": int(out[2]),
+                "tree_rows": int(out[3])}
+
     def close(self):
         if self.handle:
             self._lib.srhip_ctx_destroy(self.handle)

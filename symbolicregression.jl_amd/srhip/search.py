@@ -40,7 +40,8 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from .api import compute_complexity, loss_to_score, optimize_constants, update_baseline_loss
+from .api import (compute_complexity, dimensional_regularization, loss_to_score, optimize_constants,
+                  update_baseline_loss)
 from .dataset import Dataset
 from .node import Node, count_constants, count_depth, count_nodes, flatten, string_tree
 from .random_trees import make_random_leaf
@@ -453,6 +454,10 @@ class DeviceScorer:
             self.trees_scored += 1
             self.node_rows += len(nodes) * (self.dataset.n if idx is None else len(idx))
         loss = self.L(loss) if ok else self.L(np.inf)
+        if ok and self.dataset.has_units():
+            # score_func -> eval_loss(regularization=true) adds the units penalty to a finite loss
+            # (src/LossFunctions.jl:70-71), as eval_loss / eval_loss_batch do
+            loss = self.L(loss + dimensional_regularization(tree, self.dataset, self.options))
         score = loss_to_score(loss, self.dataset.use_baseline, self.dataset.baseline_loss, tree, self.options,
                               complexity)
         return score, loss

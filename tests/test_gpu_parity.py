@@ -417,7 +417,10 @@ def test_c2_shape_subset_matches_oracle(ctx, oracle):
 
 
 def test_row_permutation_invariance_and_determinism(ctx):
-    """Loss is invariant (to rounding) under a row permutation; repeated calls are bit-identical."""
+    """Loss is invariant (to rounding) under a row permutation; repeated calls are bit-identical.
+    Float32 losses sum each lane's 4 consecutive rows in Float32 before widening (relative error
+    <= 2^-23, srhip_eval_impl.h loss_tile), so a permutation moves the loss at that level -- inside
+    the 1e-6 parity bar, and far inside the reference's own sequential Float32 sum."""
     sr = _sr()
     opts = sr.Options(**OPS_C2)
     _, nodes, offs = _population(sr, opts, 64, 5, np.float32, seed=41)
@@ -430,7 +433,7 @@ def test_row_permutation_invariance_and_determinism(ctx):
     assert np.array_equal(a, a2)
     assert np.array_equal(aok, bok)
     for t in np.nonzero(aok)[0]:
-        assert _rel(a[t], b[t]) < 1e-9
+        assert _rel(a[t], b[t]) < 2.5e-7
 
 
 def test_set_constants_matches_fresh_compile(ctx):

@@ -111,3 +111,23 @@ def test_device_search_multiprocessing_equals_threads():
     assert mp.num_evals == threaded.num_evals
     assert mp.coalescer_stats["requests"] == threaded.coalescer_stats["requests"]
     assert mp.node_rows == threaded.node_rows
+
+
+def test_device_scorer_adds_units_penalty():
+    """The search's scorer (score_func -> eval_loss(regularization=true), src/LossFunctions.jl:70-71,
+    161-174) adds dimensional_regularization like eval_loss does: a violating tree's coalesced loss
+    equals eval_loss on the units dataset, penalty included; a conforming tree pays nothing."""
+    X = np.random.default_rng(5).standard_normal((3, 1000))
+    y = np.cos(X[2] * 2.1 - 0.2) + 0.5
+    opts = srhip.Options(binary_operators=("-", "*", "/", "+"), unary_operators=("cos",))
+    ds = srhip.Dataset(X, y, X_units=["m", "1", "kg"], y_units="1")
+    x1, x2 = srhip.Node("x1"), srhip.Node("x2")
+    good, bad = srhip.cos(3.2 * x1) - x2, srhip.cos(x1) + x2
+    sc = S.DeviceScorer(ds, opts)
+    try:
+        for tree, pen in ((good, 0.0), (bad, 1000.0)):
+            _, loss = sc.score(tree)
+            assert loss == srhip.eval_loss(tree, ds, opts), srhip.string_tree(tree, opts)
+            assert loss - srhip.eval_loss(tree, ds, opts, regularization=False) == pytest.approx(pen)
+    finally:
+        sc.close()
