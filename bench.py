@@ -42,6 +42,12 @@ def parse():
                          "per-kernel average must be the headline kernel's alone")
     ap.add_argument("--binops", default="+,-,*,/", help="(tuning) binary operators of the C2 population")
     ap.add_argument("--unaops", default="cos,exp", help="(tuning) unary operators of the C2 population")
+    ap.add_argument("--mode", default="islands", choices=("islands", "rowshard"),
+                    help="c2 over N ranks: islands (each rank its own population; every step ends with the "
+                         "migration all-gather of each rank's best trees) or rowshard (one population, the "
+                         "C3-shape 10 x 10M dataset's rows sharded over the ranks, one all-reduce of the "
+                         "per-tree partials per step: strong scaling)")
+    ap.add_argument("--migrate-k", type=int, default=12, help="islands: trees each rank sends per step (topn)")
     ap.add_argument("--config", default="c2", choices=("c2", "c4", "c1", "c3"),
                     help="c2 (default, the headline metric); c4: batched constant optimisation; c1 / c3: "
                          "equation_search (README example / 10M x 10 islands over the ranks)")
@@ -66,6 +72,8 @@ def main():
         return bench_c4(args)
     if args.config in ("c1", "c3"):
         return bench_search(args)
+    if args.mode == "rowshard":
+        return bench_rowshard(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -118,15 +126,26 @@ def main():
 
     for _ in range(args.warmup):
         prog.eval_loss(ds, loss)
+    from srhip import parallel
+
+    def migrate(l):
+        """islands: every step ends with the migration exchange (the best args.migrate_k trees of
+        every rank reach every rank: one all_gather_into_tensor over RCCL)"""
+        if dist is not None:
+            parallel.migrate_topk(nodes, offs, l, args.migrate_k, 30)
+
     barrier()
+    parallel.timer.reset()
     t0 = time.perf_counter()
     kms, works = [], []
     for _ in range(args.steps):
         l, ok = prog.eval_loss(ds, loss)
         kms.append(ctx.last_kernel_ms())
         works.append(ctx.last_work())
+        migrate(l)
     barrier()
     dt = time.perf_counter() - t0
+    coll_s, coll_calls = parallel.timer.seconds, parallel.timer.calls
     # work COUNTED on the device: the rows each tree was actually evaluated on (a failed tree -- the
     # reference's early return -- stops at its failing tile and is skipped by later row blocks)
     done_node_rows = float(sum(w["node_rows"] for w in works))
@@ -226,6 +245,11 @@ def main():
                 "parallelism": f"islands{world}" if world > 1 else "single",
                 "trees_ok": int(ok.sum()),
             },
+            # N > 1: the per-step migration exchange (parallel.migrate_topk), wall time on rank 0
+            "collective": None if dist is None else {
+                "op": f"all_gather_into_tensor of each rank's {args.migrate_k} best trees (node tables + losses)",
+                "backend": dist.get_backend(), "ranks": world, "calls_per_step": coll_calls / args.steps,
+                "ms_per_step": coll_s * 1e3 / args.steps},
             "roofline": {
                 "bound": "valu",
                 "achieved": achieved,
@@ -266,6 +290,93 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def bench_rowshard(args):
+    """c2 --mode rowshard: ONE population of 1024 random trees over the C3-shape dataset (10 features
+    x 10M rows F32, workloads.c3_shard), its rows sharded over the ranks (SURVEY.md 8(e) "very large
+    row counts"): a step = srhip_eval_loss_partials on this rank's rows + the fused all-reduce of the
+    per-tree partials (parallel.allreduce_partials: SUM / MAX over RCCL) + the did_succeed decision,
+    identical on every rank.  Strong scaling: the total work is fixed."""
+    import numpy as np
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    backend = os.environ.get("SRHIP_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local_rank %= max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_rank)
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
+    import srhip
+    from srhip import parallel, workloads
+
+    n = 10_000_000 if args.rows == 1_000_000 else args.rows
+    lo, hi = parallel.shard_rows(n, rank, world)
+    X, y = workloads.c3_shard(lo, hi)
+    opts, trees, nodes, offs = workloads.rowshard_population(args.ntrees)
+    ctx = srhip.get_context(local_rank)
+    ds = srhip.DeviceDataset(ctx, X, y)
+    prog = srhip.Program(ctx, nodes, offs, opts, np.float32)
+    loss = srhip.L2DistLoss()
+    st = prog.stats()
+    nfeat = X.shape[0]
+
+    def step():
+        return parallel.eval_loss_sharded(prog, nfeat, lambda: prog.eval_loss_partials(ds, loss),
+                                          precise=lambda tr: prog.eval_precise_partials(ds, tr))
+
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+    dist.barrier()
+    parallel.timer.reset()
+    t0 = time.perf_counter()
+    kms, done = [], 0.0
+    for _ in range(args.steps):
+        l, ok = step()
+        kms.append(ctx.last_kernel_ms())
+        done += ctx.last_work()["node_rows"]
+    ctx.synchronize()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    coll_s = parallel.timer.seconds
+    red = torch.device("cuda", local_rank) if backend == "nccl" else torch.device("cpu")
+    tt = torch.tensor([dt, coll_s, float(np.mean(kms))], dtype=torch.float64, device=red)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    tw = torch.tensor([done], dtype=torch.float64, device=red)
+    dist.all_reduce(tw, op=dist.ReduceOp.SUM)
+    dt, coll_max, kern_max = (float(v) for v in tt.cpu().numpy())
+    if rank == 0:
+        print(json.dumps({
+            "metric": "tree-node x row evals/sec (whole node), 1k trees x 10M rows f32 row-sharded over the ranks",
+            "value": float(tw.item()) / dt, "unit": "node-row evals/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (X ~ N(0,1) 10 x 10M in seeded 2^20-row chunks, C3's formula for y)",
+            "config": {"workload": f"rowshard: {args.ntrees} random trees (size<=30) x {n} rows x 10 features F32, "
+                                   f"rows split over {world} rank(s), fused L2",
+                       "rows_per_rank": hi - lo, "nodes": int(st["total_nodes"]), "parallelism": f"rowshard{world}",
+                       "trees_ok": int(ok.sum())},
+            "nominal_value": st["total_nodes"] * n * args.steps / dt,
+            "kernel_ms_max_over_ranks": kern_max,
+            "collective": {"op": "all_reduce SUM (per-tree loss sums, feature stats) + all_reduce MAX (check "
+                                 "statistics) on one buffer", "backend": dist.get_backend(), "ranks": world,
+                           "ms_per_step_max_over_ranks": coll_max * 1e3 / args.steps},
+        }))
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 def pmc_summary(kname, pattern="*pmc_c2*.json"):

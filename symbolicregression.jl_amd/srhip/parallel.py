@@ -68,6 +68,45 @@ def allreduce_np(a: np.ndarray, op: str = "sum", group=None) -> np.ndarray:
     return t.cpu().numpy()
 
 
+class CollectiveTimer:
+    """Wall time spent in this module's collectives (host copies included), for the bench."""
+
+    def __init__(self):
+        self.seconds = 0.0
+        self.calls = 0
+
+    def reset(self):
+        self.seconds, self.calls = 0.0, 0
+
+
+timer = CollectiveTimer()
+
+
+def allreduce_partials(sums: np.ndarray, chk: np.ndarray, chk_op: str, group=None):
+    """The row-shard exchange of eval_loss_partials in ONE device buffer [sums | chk] (one host->device
+    copy, the two all-reduces issued back to back on it -- SUM over the sums, MAX (Float32) or SUM
+    over the check statistics -- and one copy back).  A non-finite check statistic is sent as +Inf,
+    which every backend's MAX keeps (an fmax-style reduction may drop a NaN)."""
+    import time
+
+    import torch
+
+    dist = _dist()
+    t0 = time.perf_counter()
+    ns = len(sums)
+    chk = np.where(np.isfinite(chk), chk, np.inf)
+    buf = torch.from_numpy(np.concatenate([np.asarray(sums, dtype=np.float64), chk])).to(_device(group))
+    w1 = dist.all_reduce(buf[:ns], op=dist.ReduceOp.SUM, group=group, async_op=True)
+    w2 = dist.all_reduce(buf[ns:], op=dist.ReduceOp.MAX if chk_op == "max" else dist.ReduceOp.SUM, group=group,
+                         async_op=True)
+    w1.wait()
+    w2.wait()
+    out = buf.cpu().numpy()
+    timer.seconds += time.perf_counter() - t0
+    timer.calls += 1
+    return out[:ns].copy(), out[ns:].copy()
+
+
 def eval_loss_sharded(prog, nfeatures: int, partials, precise=None, group=None):
     """Row-sharded eval_loss for every tree of ``prog``.
 
@@ -76,11 +115,7 @@ def eval_loss_sharded(prog, nfeatures: int, partials, precise=None, group=None):
     ``prog.eval_precise_partials(shard, trees)``.  Returns (loss[T], ok[T]) identical on all ranks.
     """
     sums, chk = partials()
-    sums = allreduce_np(sums, "sum", group)
-    # any non-finite statistic fails its tree; +Inf survives every backend's MAX (a NaN may not:
-    # fmax-style reductions drop it)
-    chk = np.where(np.isfinite(chk), chk, np.inf)
-    chk = allreduce_np(chk, "max" if prog.chk_reduce_op() == "max" else "sum", group)
+    sums, chk = allreduce_partials(sums, chk, "max" if prog.chk_reduce_op() == "max" else "sum", group)
     loss, ok, status = prog.finalize(nfeatures, sums, chk)
     undecided = np.nonzero(status == 2)[0].astype(np.int32)
     if len(undecided):
@@ -165,4 +200,57 @@ def exchange_members(trees, scores, losses, options, dtype, group=None):
         ts = unflatten(nd, of, options) if len(of) > 1 else []
         v = v.reshape(-1, 2)
         out.extend((t, float(v[i, 0]), float(v[i, 1])) for i, t in enumerate(ts))
+    return out
+
+
+def migrate_topk(nodes: np.ndarray, offsets: np.ndarray, losses: np.ndarray, k: int, max_nodes: int, group=None):
+    """Migration exchange with a fixed-size payload: this rank's k best trees (by loss; did_succeed
+    trees first) travel as node tables plus their losses in one packed buffer of
+    k x max_nodes node records, so the exchange is ONE all_gather_into_tensor with no size
+    round (src/Migration.jl:16-38: every population's best members reach every other).  Trees
+    longer than max_nodes are skipped.  Returns [(nodes, offsets, losses)] by rank."""
+    import time
+
+    import torch
+
+    dist = _dist()
+    t0 = time.perf_counter()
+    ws = dist.get_world_size(group)
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    offsets = np.asarray(offsets, dtype=np.int64)
+    losses = np.asarray(losses, dtype=np.float64)
+    order = np.argsort(np.where(np.isfinite(losses), losses, np.inf), kind="stable")
+    sel = [int(t) for t in order if offsets[t + 1] - offsets[t] <= max_nodes][:k]
+    rec = NODE_DTYPE.itemsize
+    # [count, offsets (k + 1) int64, losses k f64, nodes k * max_nodes records]
+    head = 8 * (1 + (k + 1) + k)
+    payload = np.zeros(head + k * max_nodes * rec, dtype=np.uint8)
+    hdr = payload[:head].view(np.int64)
+    hdr[0] = len(sel)
+    offs_out = hdr[1:k + 2]
+    loss_out = payload[8 * (k + 2):head].view(np.float64)
+    cur = 0
+    body = payload[head:]
+    for i, t in enumerate(sel):
+        a, b = int(offsets[t]), int(offsets[t + 1])
+        body[cur * rec:(cur + b - a) * rec] = nodes[a:b].view(np.uint8)
+        offs_out[i] = cur
+        loss_out[i] = losses[t]
+        cur += b - a
+    offs_out[len(sel)] = cur
+    dev = _device(group)
+    src = torch.from_numpy(payload).to(dev)
+    dst = torch.empty(ws * len(payload), dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(dst, src, group=group)
+    allb = dst.cpu().numpy().reshape(ws, len(payload))
+    out = []
+    for r in range(ws):
+        h = allb[r, :head].copy().view(np.int64)
+        cnt = int(h[0])
+        of = h[1:cnt + 2].copy()
+        ls = allb[r, 8 * (k + 2):head].copy().view(np.float64)[:cnt]
+        nd = allb[r, head:head + int(of[-1]) * rec].copy().view(NODE_DTYPE)
+        out.append((nd, of, ls))
+    timer.seconds += time.perf_counter() - t0
+    timer.calls += 1
     return out

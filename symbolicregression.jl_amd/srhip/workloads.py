@@ -52,6 +52,33 @@ def c3_data(rows: int = 10_000_000):
     return X, y
 
 
+def c3_shard(lo: int, hi: int, nfeat: int = 10):
+    """Rows [lo, hi) of the row-sharded C3-shape dataset (bench.py --mode rowshard): generated in
+    fixed 2^20-row chunks, chunk c from seed 100 + c, so a shard's rows do not depend on how many
+    ranks share the dataset.  X ~ N(0,1) nfeat x rows F32, y as c3_data's formula."""
+    step = 1 << 20
+    X = np.empty((nfeat, hi - lo), dtype=np.float32)
+    for c in range(lo // step, (hi + step - 1) // step):
+        a, b = c * step, (c + 1) * step
+        Xc = np.random.default_rng(100 + c).standard_normal((nfeat, step)).astype(np.float32)
+        s0, s1 = max(a, lo), min(b, hi)
+        X[:, s0 - lo:s1 - lo] = Xc[:, s0 - a:s1 - a]
+    y = np.empty(hi - lo, dtype=np.float32)
+    for a in range(0, hi - lo, step):
+        Xd = X[:, a:a + step].astype(np.float64)
+        y[a:a + step] = 2 * np.cos(Xd[3]) + Xd[0] ** 2 - 2 + 0.5 * Xd[6] * Xd[2] - np.exp(Xd[9] / 4)
+    return X, y
+
+
+def rowshard_population(ntrees: int = 1024, nfeat: int = 10):
+    """bench.py --mode rowshard's population: random trees (size U{1..30}, C3's operators) over
+    nfeat features, seed 7."""
+    opts = Options(**C3_OPS)
+    trees = random_population(ntrees, opts, nfeat, np.float32, seed=7, max_size=30)
+    nodes, offs = flatten(trees, opts, np.float32)
+    return opts, trees, nodes, offs
+
+
 def c3_population(opts=None, ntrees: int = 64):
     """The 64-tree population (size <= 20, the search's default maxsize) C3's CPU baseline scores."""
     opts = opts or Options(**C3_OPS)

@@ -184,3 +184,72 @@ def test_island_search_gloo_world2():
 
     X, y = _data(100, seed=3)
     assert min(l for _, l in f0) < 0.5 * np.mean((y - y.mean()) ** 2)
+
+
+def _migrate_rank_main(rank, world, port, q):
+    """One rank of the bench's per-step exchanges: migrate_topk (fixed-size all-gather) and
+    allreduce_partials (one buffer, SUM + MAX)."""
+    try:
+        sys.path[:0] = [os.path.join(ROOT, "symbolicregression.jl_amd")]
+        import torch.distributed as dist
+
+        import srhip
+        from srhip.parallel import allreduce_partials, migrate_topk
+
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        opts = srhip.Options(**OPS)
+        trees = srhip.random_population(20 + 5 * rank, opts, 3, np.float32, seed=200 + rank, max_size=25)
+        nodes, offs = srhip.flatten(trees, opts, np.float32)
+        losses = np.random.default_rng(300 + rank).uniform(0, 10, len(trees))
+        losses[::4] = np.inf  # failed trees never migrate ahead of finite ones
+        got = migrate_topk(nodes, offs, losses, k=6, max_nodes=20)
+        sums = np.arange(7, dtype=np.float64) * (rank + 1)
+        chk = np.array([1.0 + rank, np.nan if rank == 1 else 2.0, 3.0 - rank])
+        rs, rc = allreduce_partials(sums, chk, "max")
+        q.put((rank, [(g[0].tobytes(), g[1], g[2]) for g in got], rs, rc))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # surface the failure to the parent
+        import traceback
+
+        q.put((rank, traceback.format_exc() + repr(e), None, None))
+
+
+def test_migrate_topk_and_fused_allreduce_gloo_world2():
+    """The multi-GPU bench's collectives at world size 2: every rank receives every rank's 6 best
+    trees (finite losses first, trees over 20 nodes skipped) bit for bit with their losses, and the
+    one-buffer partials all-reduce sums the sums and takes the max of the check statistics (a NaN
+    sent as +Inf)."""
+    import multiprocessing as mp
+
+    import srhip
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_migrate_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    res.sort(key=lambda r: r[0])
+    for r in res:
+        assert r[2] is not None, r[1]
+    opts = srhip.Options(**OPS)
+    for rank in range(2):
+        trees = srhip.random_population(20 + 5 * rank, opts, 3, np.float32, seed=200 + rank, max_size=25)
+        nodes, offs = srhip.flatten(trees, opts, np.float32)
+        losses = np.random.default_rng(300 + rank).uniform(0, 10, len(trees))
+        losses[::4] = np.inf
+        order = np.argsort(losses, kind="stable")
+        sel = [t for t in order if offs[t + 1] - offs[t] <= 20][:6]
+        want = b"".join(nodes[offs[t]:offs[t + 1]].tobytes() for t in sel)
+        for _, got, _, _ in res:
+            nd, of, ls = got[rank]
+            assert nd == want
+            assert np.array_equal(ls, losses[sel])
+            assert np.array_equal(np.diff(of), [offs[t + 1] - offs[t] for t in sel])
+    for _, _, rs, rc in res:
+        assert np.array_equal(rs, np.arange(7, dtype=np.float64) * 3)
+        assert np.array_equal(rc, [2.0, np.inf, 3.0])
