@@ -79,15 +79,16 @@ def _backtracking(phi, phi0, dphi0, c1=1e-4, rho_hi=0.5, rho_lo=0.1, iterations=
         it += 1
         if it > iterations:
             return None, None
+        # LineSearches.jl's expressions with Julia's association: x^2 = x*x, x^3 = x*x*x (literal powers)
         if it == 1:
             with np.errstate(all="ignore"):
-                a_tmp = -(dphi0 * a2 ** 2) / np.float64(2 * (phix1 - phi0 - dphi0 * a2))
+                a_tmp = -(np.float64(dphi0) * (a2 * a2)) / np.float64(2 * (phix1 - phi0 - dphi0 * a2))
         else:
             with np.errstate(all="ignore"):  # IEEE like Julia: a1 == a2 (alpha underflowed) gives Inf / NaN
-                div = np.float64(1.0) / np.float64(a1 ** 2 * a2 ** 2 * (a2 - a1))
-            e1, e0 = phix1 - phi0 - dphi0 * a2, phix0 - phi0 - dphi0 * a1
-            a = (a1 ** 2 * e1 - a2 ** 2 * e0) * div
-            b = (-a1 ** 3 * e1 + a2 ** 3 * e0) * div
+                div = np.float64(1.0) / np.float64((a1 * a1) * (a2 * a2) * (a2 - a1))
+                e1, e0 = phix1 - phi0 - dphi0 * a2, phix0 - phi0 - dphi0 * a1
+                a = ((a1 * a1) * e1 - (a2 * a2) * e0) * div
+                b = (-(a1 * a1 * a1) * e1 + (a2 * a2 * a2) * e0) * div
             with np.errstate(all="ignore"):
                 if abs(a) <= np.finfo(float).eps:
                     a_tmp = np.float64(dphi0) / np.float64(2 * b)
@@ -204,3 +205,180 @@ def reference_outcome(tree_nodes, binops, unaops, X, y, w=None, iterations=8, rt
     _, l4, _ = optimize_constants(tree_nodes, binops, unaops, X, y, w, iterations, nrestarts=0, fd_scale=4.0)
     stable = l1 == l4 or abs(l1 - l4) <= rtol * abs(l1) + 1e-12
     return l1, bool(stable)
+
+
+# ---- exact-gradient mode ------------------------------------------------------------------------
+# libsrhip differentiates the objective exactly (forward-mode dual numbers) where the reference
+# differentiates by finite differences.  This mode restates the same optimiser -- Optim's BFGS /
+# Newton with LineSearches' BackTracking, in the arithmetic order of their source (Optim bfgs.jl
+# update_h!: c1 = (dx'dg + dg'u) / (dx'dg)^2, c2 = 1 / dx'dg; direction s = -invH g; the 1x1 Newton
+# Hessian as the central difference of the exact gradient with step cbrt(eps) max(1, |c|), made
+# positive like cholesky!(Positive, H)) -- over the oracle's exact gradient (oracle.loss_grad), so
+# the device optimiser's state machine is compared with no finite-difference noise on either side.
+
+def _grad_fn(tree_nodes, binops, unaops, X, y, w, order):
+    def g(c):
+        nd = tree_nodes.copy()
+        for k, i in enumerate(order):
+            nd[i]["val"] = c[k]
+        return oracle.loss_grad(nd, binops, unaops, X, y, w)
+    return g
+
+
+def _maxabs(v):
+    m = 0.0
+    for e in v:
+        m = max(m, abs(float(e)))
+    return m
+
+
+def bfgs_exact(f, grad, x0, iterations=8, g_tol=1e-8):
+    """(x, f(x), objective calls) -- Optim.BFGS(linesearch=BackTracking()) with the exact gradient."""
+    x = np.asarray(x0, dtype=np.float64).copy()
+    n = len(x)
+    fx = f(x)
+    calls = 1
+    if not np.isfinite(fx):
+        return x, fx, calls
+    g = grad(x)
+    H = [[1.0 if i == j else 0.0 for j in range(n)] for i in range(n)]
+    if _maxabs(g) <= g_tol:
+        return x, fx, calls
+    for _ in range(iterations):
+        s = [0.0] * n
+        dphi0 = 0.0
+        for i in range(n):
+            acc = 0.0
+            for j in range(n):
+                acc += H[i][j] * g[j]
+            s[i] = -acc
+            dphi0 += g[i] * s[i]
+        if not dphi0 < 0:
+            H = [[1.0 if i == j else 0.0 for j in range(n)] for i in range(n)]
+            dphi0 = 0.0
+            for i in range(n):
+                s[i] = -g[i]
+                dphi0 -= g[i] * g[i]
+        nc = [0]
+
+        def phi(a):
+            nc[0] += 1
+            return f(np.array([x[i] + a * s[i] for i in range(n)]))
+
+        a, fnew = _backtracking(phi, fx, dphi0)
+        calls += nc[0]
+        if a is None:
+            break
+        xn = np.array([x[i] + a * s[i] for i in range(n)])
+        gn = grad(xn)
+        dx = [a * s[i] for i in range(n)]
+        dg = [gn[i] - g[i] for i in range(n)]
+        dxdg = 0.0
+        for i in range(n):
+            dxdg += dx[i] * dg[i]
+        if dxdg > 0.0:
+            u = [0.0] * n
+            dgu = 0.0
+            for i in range(n):
+                acc = 0.0
+                for j in range(n):
+                    acc += H[i][j] * dg[j]
+                u[i] = acc
+                dgu += dg[i] * acc
+            c1 = (dxdg + dgu) / (dxdg * dxdg)
+            c2 = 1.0 / dxdg
+            for i in range(n):
+                for j in range(n):
+                    H[i][j] += c1 * dx[i] * dx[j] - c2 * (u[i] * dx[j] + dx[i] * u[j])
+        fold = fx
+        x, fx, g = xn, fnew, gn
+        if fx == fold or _maxabs(g) <= g_tol:
+            break
+    return x, fx, calls
+
+
+def newton_exact(f, grad, x0, iterations=8, g_tol=1e-8):
+    """(x, f(x), objective calls) -- Optim.Newton(linesearch=BackTracking()) for one constant, exact
+    gradient, Hessian = central difference of the exact gradient."""
+    x = np.asarray(x0, dtype=np.float64).copy()
+    fx = f(x)
+    calls = 1
+    if not np.isfinite(fx):
+        return x, fx, calls
+    g = grad(x)
+    if _maxabs(g) <= g_tol:
+        return x, fx, calls
+    for it in range(iterations):
+        e = 6.055454452393343e-06 * max(1.0, abs(float(x[0])))  # cbrt(eps(Float64))
+        xp, xm = np.array([x[0] + e]), np.array([x[0] - e])
+        fp, fm = f(xp), f(xm)
+        h = (grad(xp)[0] - grad(xm)[0]) / (2.0 * e) if np.isfinite(fp) and np.isfinite(fm) else np.nan
+        hp = abs(h) if (np.isfinite(h) and h != 0.0) else 1.0  # cholesky!(Positive, [h])
+        s0 = -g[0] / hp
+        dphi0 = g[0] * s0
+        nc = [0]
+
+        def phi(a):
+            nc[0] += 1
+            return f(np.array([x[0] + a * s0]))
+
+        a, fnew = _backtracking(phi, fx, dphi0)
+        calls += nc[0]
+        if a is None:
+            break
+        xn = np.array([x[0] + a * s0])
+        fold = fx
+        x, fx = xn, fnew
+        g = grad(x)
+        if fx == fold or _maxabs(g) <= g_tol:
+            break
+    return x, fx, calls
+
+
+def _devorder_fns(tree_nodes, binops, unaops, X, y, w, order):
+    """(f, grad) with libsrhip's row-sum order (oracle.loss_grad_devorder) and the value oracle's
+    did_succeed (f = Inf where the tree fails, as eval_loss returns L(Inf))."""
+    offs = np.array([0, len(tree_nodes)], dtype=np.int64)
+    cache = {}
+
+    def both(c):
+        key = np.asarray(c, dtype=np.float64).tobytes()
+        if key not in cache:
+            nd = tree_nodes.copy()
+            for k, i in enumerate(order):
+                nd[i]["val"] = c[k]
+            _, _, ok, _ = oracle.eval_loss_batch(nd, offs, binops, unaops, X, y, w, 0, 0.0, nthreads=1)
+            lv, g = oracle.loss_grad_devorder(nd, binops, unaops, X, y, w)
+            cache.clear()
+            cache[key] = (lv if ok[0] and np.isfinite(lv) else np.inf, g)
+        return cache[key]
+
+    return (lambda c: both(c)[0]), (lambda c: both(c)[1])
+
+
+def optimize_constants_exact(tree_nodes, binops, unaops, X, y, w=None, iterations=8, starts=None,
+                             device_order=False):
+    """(constants, loss, improved, objective calls) for one Float64 tree -- the reference procedure
+    (src/ConstantOptimization.jl:22-81: Newton for one constant, BFGS otherwise, best of the starts,
+    accepted only if it beats the baseline) with the exact gradient.  ``starts``: the start points
+    (default: the tree's own constants only).  ``device_order``: the objective and gradient summed
+    in libsrhip's row order instead of exactly, so that a line search deciding at the rounding
+    noise decides as the device does."""
+    f, order = _loss_fn(tree_nodes, binops, unaops, X, y, w)
+    grad = _grad_fn(tree_nodes, binops, unaops, X, y, w, order)
+    if device_order:  # sums in libsrhip's row order: the same objective bits as the device's
+        f, grad = _devorder_fns(tree_nodes, binops, unaops, X, y, w, order)
+    x0 = np.array([tree_nodes[i]["val"] for i in order], dtype=np.float64)
+    if len(x0) == 0:
+        return x0, f(x0), False, 0
+    algorithm = newton_exact if len(x0) == 1 else bfgs_exact
+    baseline = f(x0)
+    best_x, best_f, calls = x0, np.inf, 0
+    for xs in (starts if starts is not None else [x0]):
+        xr, fr, c = algorithm(f, grad, np.asarray(xs, dtype=np.float64), iterations)
+        calls += c
+        if fr < best_f:
+            best_x, best_f = xr, fr
+    if best_f < baseline:
+        return best_x, best_f, True, calls
+    return x0, baseline, False, calls

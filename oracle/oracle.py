@@ -104,6 +104,46 @@ def eval_loss_batch(nodes, offsets, binops, unaops, X, y, w=None, kind=0, p0=0.0
     return le, lr, ok.astype(bool), used
 
 
+def loss_grad(nodes, binops, unaops, X, y, w=None, kind=0):
+    """Exact d loss / d constants (get_constants order) of ONE Float64 tree by forward-mode dual
+    numbers (sr_oracle_grad.h); kind 0 = L2, 1 = L1."""
+    lib = load()
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    w = None if w is None else np.ascontiguousarray(w, dtype=np.float64)
+    nodes = np.ascontiguousarray(nodes)
+    b = np.ascontiguousarray(binops, dtype=np.int32)
+    u = np.ascontiguousarray(unaops, dtype=np.int32)
+    out = np.empty(64, dtype=np.float64)
+    fn = _setup(lib.oracle_loss_grad_f64, ctypes.c_int,
+                [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                 ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p])
+    nc = fn(_p(nodes), len(nodes), _p(b), _p(u), _p(X), _p(y), _p(w), X.shape[1], int(kind), _p(out))
+    if nc < 0:
+        raise ValueError("too many constants for the gradient oracle")
+    return out[:nc].copy()
+
+
+def loss_grad_devorder(nodes, binops, unaops, X, y, w=None, kind=0, rb=256):
+    """(loss, gradient) of ONE Float64 tree -- the loss value and exact gradient summed in libsrhip's
+    dual-number kernel's row order (sr_oracle_grad.h dev_order_sum; no did_succeed decision)."""
+    lib = load()
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    w = None if w is None else np.ascontiguousarray(w, dtype=np.float64)
+    nodes = np.ascontiguousarray(nodes)
+    b = np.ascontiguousarray(binops, dtype=np.int32)
+    u = np.ascontiguousarray(unaops, dtype=np.int32)
+    out = np.empty(65, dtype=np.float64)
+    fn = _setup(lib.oracle_loss_grad_devorder_f64, ctypes.c_int,
+                [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                 ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p])
+    nc = fn(_p(nodes), len(nodes), _p(b), _p(u), _p(X), _p(y), _p(w), X.shape[1], int(kind), int(rb), _p(out))
+    if nc < 0:
+        raise ValueError("too many constants for the gradient oracle")
+    return float(out[0]), out[1:nc + 1].copy()
+
+
 def scalar_bin(op, a, b, dtype):
     lib = load()
     sfx = _SFX[np.dtype(dtype)]

@@ -308,3 +308,5 @@ static int32_t loss_i32(int kind, int32_t d, int32_t p0) { (void)p0; return kind
 #undef SFX
 #undef IS_INT
 #undef OVF_T
+
+#include "sr_oracle_grad.h"

@@ -302,13 +302,15 @@ constexpr int LS_ITERFINITEMAX = 52, LS_ITERATIONS = 1000;
 double backtrack_step(LineSearch& s) {
   const double rho_hi = 0.5, rho_lo = 0.1;
   double a_tmp;
+  // LineSearches.jl's expressions with Julia's association (x^2 = x*x, x^3 = x*x*x as literal powers)
   if (s.iter == 1) {
-    a_tmp = -(s.dphi0 * s.a2 * s.a2) / (2.0 * (s.phix1 - s.phi0 - s.dphi0 * s.a2));
+    a_tmp = -(s.dphi0 * (s.a2 * s.a2)) / (2.0 * (s.phix1 - s.phi0 - s.dphi0 * s.a2));
   } else {
-    const double div = 1.0 / (s.a1 * s.a1 * s.a2 * s.a2 * (s.a2 - s.a1));
+    const double a1sq = s.a1 * s.a1, a2sq = s.a2 * s.a2;
+    const double div = 1.0 / (a1sq * a2sq * (s.a2 - s.a1));
     const double e1 = s.phix1 - s.phi0 - s.dphi0 * s.a2, e0 = s.phix0 - s.phi0 - s.dphi0 * s.a1;
-    const double a = (s.a1 * s.a1 * e1 - s.a2 * s.a2 * e0) * div;
-    const double b = (-s.a1 * s.a1 * s.a1 * e1 + s.a2 * s.a2 * s.a2 * e0) * div;
+    const double a = (a1sq * e1 - a2sq * e0) * div;
+    const double b = (-(s.a1 * s.a1 * s.a1) * e1 + (s.a2 * s.a2 * s.a2) * e0) * div;
     if (fabs(a) <= 2.220446049250313e-16) a_tmp = s.dphi0 / (2.0 * b);
     else a_tmp = (-b + sqrt(std::max(b * b - 3.0 * a * s.dphi0, 0.0))) / (3.0 * a);
   }

@@ -17,11 +17,16 @@ from .api import (
     eval_grad_tree_array,
     eval_tree_array,
     eval_tree_array_batch,
+    finalize_scores,
+    LossCache,
     optimize_constants,
     loss_to_score,
+    rescore_hall_of_fame,
+    rescore_population_batched,
     score_func,
     score_func_batch,
     score_func_batched,
+    trees_equal,
     update_baseline_loss,
 )
 from .dataset import Dataset

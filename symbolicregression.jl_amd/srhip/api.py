@@ -126,8 +126,10 @@ def eval_loss_batch(trees, dataset: Dataset, options, regularization: bool = Tru
         return out, np.isfinite(out)
     out, ok = _eval_loss_batch_device(trees, dataset, options, idx)
     if regularization and dataset.has_units():
+        # in the loss type L, as _eval_loss adds L(loss) + L(penalty) (src/LossFunctions.jl:70-72)
+        L = dataset.loss_type.type
         for t in np.nonzero(ok)[0]:
-            out[t] = out[t] + float(dimensional_regularization(trees[t], dataset, options))
+            out[t] = float(L(out[t]) + dimensional_regularization(trees[t], dataset, options))
     return out, ok
 
 
@@ -243,6 +245,80 @@ def score_func_batch(dataset: Dataset, members, options, idx=None):
     scores = np.array([loss_to_score(L(l), dataset.use_baseline, dataset.baseline_loss, t, options)
                        for l, t in zip(losses, trees)], dtype=dataset.loss_type)
     return scores, losses
+
+
+# ---- the batching-mode batch seams (options.batching): one launch per population ----------------
+def trees_equal(a: Node, b: Node) -> bool:
+    """DynamicExpressions' structural == on nodes (degree, operator, feature, constant value)."""
+    if a is b:
+        return True
+    if a is None or b is None or a.degree != b.degree:
+        return False
+    if a.degree == 0:
+        if a.constant != b.constant:
+            return False
+        return a.val == b.val if a.constant else a.feature == b.feature
+    if a.op != b.op or not trees_equal(a.l, b.l):
+        return False
+    return a.degree == 1 or trees_equal(a.r, b.r)
+
+
+class LossCache:
+    """s_r_cycle's loss_cache (src/SingleIteration.jl:47-50): per population slot, the tree last
+    scored on the cycle's fixed batch and that score."""
+
+    def __init__(self, n: int, L=np.float64):
+        self.oid = [None] * n
+        self.score = np.zeros(n, dtype=L)
+
+
+def rescore_population_batched(dataset: Dataset, members, options, idx, cache: LossCache, first_loop: bool):
+    """The batched re-score of s_r_cycle (src/SingleIteration.jl:64-82) for a whole population in ONE
+    device launch: on the first loop every member, afterwards every member whose tree differs from
+    its cache entry, is scored on the fixed batch ``idx`` (score_func_batched on each: eval_loss with
+    idx, regularization, loss_to_score with the member's complexity) by a single eval_loss_batch(idx)
+    launch; the others keep their cached score.  Returns (scores[n], number of trees evaluated)."""
+    members = list(members)
+    stale = [i for i, m in enumerate(members)
+             if first_loop or cache.oid[i] is None or not trees_equal(cache.oid[i], _tree_of(m))]
+    if stale:
+        scores, _ = score_func_batch(dataset, [members[i] for i in stale], options, idx=idx)
+        for i, sc in zip(stale, scores):
+            cache.oid[i] = _tree_of(members[i]).copy()
+            cache.score[i] = sc
+    return cache.score.copy(), len(stale)
+
+
+def finalize_scores(dataset: Dataset, members, options) -> float:
+    """finalize_scores (src/Population.jl:162-176): with options.batching every member's score and
+    loss are recomputed on the full dataset -- here one score_func_batch launch for the population
+    (members get .score / .loss).  Returns num_evals (pop.n, or 0 without batching)."""
+    members = list(members)
+    if not options.batching or not members:
+        return 0.0
+    scores, losses = score_func_batch(dataset, members, options)
+    for m, sc, lo in zip(members, scores, losses):
+        m.score, m.loss = sc, lo
+    return float(len(members))
+
+
+def rescore_hall_of_fame(dataset: Dataset, members, exists, options) -> float:
+    """_dispatch_s_r_cycle's best_seen re-score (src/SymbolicRegression.jl:1120-1127): with
+    options.batching each hall-of-fame entry's score and loss are recomputed on the full dataset --
+    one launch over the entries that exist (the reference also re-scores the placeholder entries,
+    whose values are never read; num_evals counts every entry as it does)."""
+    if not options.batching:
+        return 0.0
+    live = [m for m, e in zip(members, exists) if e and m is not None]
+    if live:
+        scores, losses = score_func_batch(dataset, live, options)
+        for m, sc, lo in zip(live, scores, losses):
+            m.score, m.loss = sc, lo
+    return float(len(members))
+
+
+def _tree_of(member):
+    return member.tree if hasattr(member, "tree") else member
 
 
 def update_baseline_loss(dataset: Dataset, options) -> None:

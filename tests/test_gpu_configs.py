@@ -192,11 +192,11 @@ def test_c4_gradient_vs_oracle_differences(ctx, oracle, c4):
 
 
 def test_c4_optimizer_outcome_vs_oracle(ctx, oracle, c4):
-    """The batched optimiser on C4 (512 trees x 100k F64, BFGS(8) + 2 restarts as bench.py runs
-    it): never worse than the baseline on any tree, improves most; and on a 32-tree sample, single
-    start, the device optimum matches or beats the reference procedure (oracle/optim.py,
-    finite-difference BFGS) on every tree whose reference optimum is resolved
-    (optim.reference_outcome; the unresolved ones are listed)."""
+    """C4's 512 trees, BFGS(8) / Newton + 2 restarts (the bench's call): never worse than the
+    baseline on any tree, improves most; and on a 32-tree sample, single start, the device optimum
+    equals the exact-gradient restatement's (oracle/optim.py optimize_constants_exact over the
+    oracle's dual-number gradient, row sums in the device's order) to 1e-12 relative on EVERY
+    sampled tree -- no exclusions."""
     import optim
 
     sr = _sr()
@@ -207,7 +207,6 @@ def test_c4_optimizer_outcome_vs_oracle(ctx, oracle, c4):
     out, improved, fcalls = prog.optimize_constants(ds, sr.L2DistLoss(), iterations=8, nrestarts=2, seed=7)
     assert np.all(out[base_ok] <= base[base_ok] * (1 + 1e-12))
     assert improved.sum() >= 0.6 * base_ok.sum()
-    # single start on a sample, against the oracle
     sample = [t for t in np.random.default_rng(10).permutation(len(offs) - 1) if base_ok[t]][:32]
     sub_nodes = np.concatenate([nodes[offs[t]:offs[t + 1]] for t in sample])
     sub_offs = np.concatenate([[0], np.cumsum([offs[t + 1] - offs[t] for t in sample])]).astype(np.int64)
@@ -216,17 +215,14 @@ def test_c4_optimizer_outcome_vs_oracle(ctx, oracle, c4):
 
     def orc(u):
         tn = sub_nodes[sub_offs[u]:sub_offs[u + 1]].copy()
-        return optim.reference_outcome(tn, opts.binop_codes, opts.unaop_codes, X, y)
+        return optim.optimize_constants_exact(tn, opts.binop_codes, opts.unaop_codes, X, y,
+                                               device_order=True)[1]
 
     with cf.ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
         ref = list(ex.map(orc, range(len(sample))))
-    unresolved = [int(sample[u]) for u in range(len(sample)) if not ref[u][1]]
-    lost = [(sample[u], dl[u], ref[u][0], base[sample[u]]) for u in range(len(sample))
-            if ref[u][1] and not dl[u] <= ref[u][0] * (1 + 1e-6) + 1e-12]
-    assert not lost, (lost, unresolved)
-    # size-20 trees with exp and / are often oscillatory at the difference step; at least 12 of the
-    # 32 sampled trees must still have a resolved reference optimum for the comparison to mean much
-    assert len(sample) - len(unresolved) >= 12, unresolved
+    off = [(int(sample[u]), dl[u], ref[u], base[sample[u]]) for u in range(len(sample))
+           if not (dl[u] == ref[u] or abs(dl[u] - ref[u]) <= 1e-12 * max(abs(dl[u]), abs(ref[u])))]
+    assert not off, off
 
 
 def test_c5_int32_population_1m_rows_bit_exact(ctx, oracle):

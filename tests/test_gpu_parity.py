@@ -515,3 +515,28 @@ def test_row_sharded_partials_match_single_device(ctx, oracle, dtype):
     assert np.array_equal(ok, ook)
     for t in np.nonzero(ok)[0]:
         assert _rel(loss[t], full_l[t]) < 1e-12
+
+
+def test_loss_in_reference_type_L(ctx, oracle):
+    """_eval_loss returns the dataset's loss type L (Float32 for Float32 data; _loss folds in T,
+    src/LossFunctions.jl:13-33,45-75): srhip.eval_loss / score_func return L scalars, and the
+    device's L-typed loss is the oracle's exact loss rounded to L -- equal, or one ULP of L apart
+    where the exact losses (within 1e-6) straddle a rounding boundary of L."""
+    sr = _sr()
+    opts = sr.Options(**OPS_C2)
+    trees, nodes, offs = _population(sr, opts, 160, 3, np.float32, seed=61)
+    X, y, _ = _data(3, 20000, np.float32, seed=62)
+    d = sr.Dataset(X, y)
+    dl, dok = sr.eval_loss_batch(trees, d, opts)
+    ol, _, ook, _ = oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, X, y, None, 0, 0.0)
+    assert np.array_equal(dok, ook)
+    live = np.nonzero(ook)[0]
+    dL, oL = dl[live].astype(np.float32), ol[live].astype(np.float32)
+    ulps = np.abs(dL.view(np.int32).astype(np.int64) - oL.view(np.int32).astype(np.int64))
+    assert np.all(ulps <= 1), live[ulps > 1]
+    assert np.mean(ulps == 0) >= 0.85  # the device's Float32 4-row group sums: <= 2^-23 from exact
+    for t in live[:20]:
+        v = sr.eval_loss(trees[t], d, opts)
+        assert isinstance(v, np.float32) and v == np.float32(dl[t])
+        s, l2 = sr.score_func(d, trees[t], opts)
+        assert isinstance(l2, np.float32) and isinstance(s, np.float32)
