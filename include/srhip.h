@@ -265,9 +265,11 @@ int srhip_program_derived(const srhip_program* prog, int32_t* count, uint32_t* s
 /* ---- Cross-population request coalescer (8(b) "Threading") ----------------
  * The reference scores one tree per mutation from every population task concurrently
  * (score_func in next_generation, src/Mutate.jl:268-274, under Threads.@spawn per population,
- * src/SymbolicRegression.jl:964-987 / src/SearchUtils.jl:121-122).  A batcher owns one context
- * and one device dataset; any number of threads submit single-tree score requests and block on
- * their ticket; one worker thread flushes the queue as ONE program + ONE srhip_eval_loss launch
+ * src/SymbolicRegression.jl:964-987 / src/SearchUtils.jl:121-122).  A batcher uses the caller's
+ * context and device dataset; any number of threads submit single-tree score requests and block on
+ * their ticket; worker threads (SRHIP_COALESCE_WORKERS, default 2: worker 0 on the caller's context,
+ * the others on contexts of their own on the same device, so one compiles and launches while
+ * another waits for its kernel) flush the queue as ONE program + ONE srhip_eval_loss launch
  * when max_batch requests are queued, when every registered client is waiting (nclients > 0), or
  * max_wait_us after the oldest request.  Requests with different row subsets (batching `idx`)
  * go to separate launches of the same flush.  Results are exactly those of srhip_eval_loss on
@@ -291,9 +293,10 @@ int srhip_batcher_eval(srhip_batcher* b, const srhip_node* nodes, int64_t nnodes
 /* requests served, device launches, largest batch */
 int srhip_batcher_stats(const srhip_batcher* b, int64_t* nrequests, int64_t* nlaunches,
                         int64_t* max_batch_seen);
-/* worker wall time spent inside flushes (compile + upload + launch + wait, ms) and the summed
- * interpreter-kernel time of its launches (HIP events, ms): kernel_ms / elapsed wall time is the
- * device-busy fraction of a search (bench C1 / C3) */
+/* worker wall time spent inside flushes (compile + upload + launch + wait, ms, summed over the
+ * workers) and the summed interpreter-kernel time of their launches (HIP events, ms): kernel_ms /
+ * elapsed wall time is the device-busy fraction of a search (bench C1 / C3; concurrent launches of
+ * two workers can overlap, so it is an upper bound) */
 int srhip_batcher_timing(const srhip_batcher* b, double* busy_ms, double* kernel_ms);
 /* drains the queue (pending requests are evaluated), joins the worker */
 void srhip_batcher_destroy(srhip_batcher* b);

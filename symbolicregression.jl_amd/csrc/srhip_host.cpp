@@ -1222,7 +1222,10 @@ int srhip::check_eval_args(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_
   if (!ctx || !ds || !P) return fail(SRHIP_ERR_INVALID, "null handle");
   if (!P->ctx) return fail(SRHIP_ERR_INVALID, "host-only program (created without a context) cannot be evaluated");
   if (ds->dtype != P->dtype) return fail(SRHIP_ERR_INVALID, "dataset dtype %d != program dtype %d", ds->dtype, P->dtype);
-  if (ds->ctx != ctx || P->ctx != ctx) return fail(SRHIP_ERR_INVALID, "handles belong to a different context");
+  // a dataset is read-only device memory after its (synchronised) upload: any context on its device
+  // may evaluate over it (the coalescer's worker contexts share the caller's dataset)
+  if (P->ctx != ctx) return fail(SRHIP_ERR_INVALID, "program belongs to a different context");
+  if (ds->ctx != ctx && ds->device != ctx->device) return fail(SRHIP_ERR_INVALID, "dataset is on another device");
   if (P->maxfeat > ds->nfeat)
     return fail(SRHIP_ERR_INVALID, "tree uses feature %d but dataset has %lld features", (int)P->maxfeat, (long long)ds->nfeat);
   if (mode == MODE_LOSS) {
