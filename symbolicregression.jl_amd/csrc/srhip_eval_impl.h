@@ -801,10 +801,13 @@ __device__ __attribute__((always_inline)) inline void derive_columns_tiles(const
 // ------------------------------------------------------------------------------------------------
 // One (row block, tree group) of the launch: stage the block, derive its columns, interpret the
 // group's trees over it.  rb = row block, gy = tree group (grid.y; 0 in persistent launches, whose
-// one group is the whole population).
+// one group is the whole population).  gstride > 1 (a persistent launch's tail items): the group is
+// the order slots gslice, gslice + gstride, ... -- an interleaved 1/gstride of the population, so
+// the slices of a block cost about the same.
 template <typename T, int R, int K, int MODE, bool XLDS>
 __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs& p, unsigned char* smem, const int rb,
-                                                                 const int gy) {
+                                                                 const int gy, const int gslice = 0,
+                                                                 const int gstride = 1) {
   constexpr int WAVES = eval_waves(R, K);
   using O = OpsT<T>;
   using CT = typename Chk<T>::type;
@@ -854,13 +857,15 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
   constexpr int FLAG_SNAP = 2048;
   constexpr bool SNAP = MODE == MODE_LOSS && !kIsInt<T>;
   __shared__ uint8_t failed_snap[SNAP ? FLAG_SNAP : 1];
-  const int snap_base = p.group_off ? p.group_off[gy] : gy * p.trees_per_group;
-  const int snap_n = p.group_off ? p.group_off[gy + 1] - snap_base
-                                 : min(p.trees_per_group, p.ntrees - snap_base);
+  const int gb0 = p.group_off ? p.group_off[gy] : gy * p.trees_per_group;
+  const int snap_base = gb0 + gslice;
+  const int snap_n = gstride > 1 ? (p.ntrees - gslice + gstride - 1) / gstride
+                                 : (p.group_off ? p.group_off[gy + 1] - gb0 : min(p.trees_per_group, p.ntrees - gb0));
   if constexpr (SNAP) {
     if (p.early_exit)
       for (int i = threadIdx.x; i < min(snap_n, FLAG_SNAP); i += blockDim.x)
-        failed_snap[i] = __hip_atomic_load(p.fail_flag + snap_base + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.epoch;
+        failed_snap[i] = __hip_atomic_load(p.fail_flag + snap_base + i * gstride, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT) == p.epoch;
   }
   __syncthreads();
   constexpr bool DERIVED = XLDS && !kIsInt<T> && MODE != MODE_PRECISE;
@@ -875,9 +880,8 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
   if (p.debug_stop == 2) return;  // (diagnostic runs are never persistent)
 
   // tree group of this workgroup: uniform, or the host's tail-shaped sizes (group_off)
-  const int group_base = p.group_off ? __builtin_amdgcn_readfirstlane(p.group_off[gy]) : gy * p.trees_per_group;
-  const int group_n = p.group_off ? __builtin_amdgcn_readfirstlane(p.group_off[gy + 1]) - group_base
-                                  : min(p.trees_per_group, p.ntrees - group_base);
+  const int group_base = __builtin_amdgcn_readfirstlane(snap_base);
+  const int group_n = __builtin_amdgcn_readfirstlane(snap_n);
 
   // the group's trees are in descending estimated cost (host make_order): wave w starts with tree w,
   // then each wave claims the next unclaimed tree from an LDS counter as it finishes one — longest
@@ -889,7 +893,8 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
   KMARK(8 + wave, 10);
   for (int ti = wave; ti < group_n;) {
     KMARK(8 + wave, 11);
-    const int tree = __builtin_amdgcn_readfirstlane(p.order[group_base + ti]);
+    const int slot = group_base + ti * gstride;  // order slot (uniform)
+    const int tree = __builtin_amdgcn_readfirstlane(p.order[slot]);
     const int pc0 = __builtin_amdgcn_readfirstlane(p.prog_off[tree]);
     const int max_steps = __builtin_amdgcn_readfirstlane(p.max_steps);
     KDBG("[k] ti=%d tree=%d pc0=%d group_n=%d\n", ti, tree, pc0, group_n);
@@ -922,7 +927,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
     // workgroup's partials are one contiguous range (its group's slots), so L2 lines fill before
     // write-back
     LAccT<T>* lslab = reinterpret_cast<LAccT<T>*>(p.slab_loss) +
-                      ((int64_t)rb * p.ntrees + group_base + ti) * __builtin_amdgcn_readfirstlane(p.cpb);
+                      ((int64_t)rb * p.ntrees + slot) * __builtin_amdgcn_readfirstlane(p.cpb);
     LAccT<T> csum = 0;  // fused launches: this lane's share of the tree's chunk sums
     int rows_done = 0;  // valid rows this wave evaluated the tree on (the launch's work count)
     if (failed) {
@@ -1072,7 +1077,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
             csum = (LAccT<T>)NAN;
             if (lane == WAVE_LAST) {
               for (int c = tile / (CH / TILE) + (flushed ? 1 : 0); c < p.cpb; ++c) lslab[c] = (LAccT<T>)NAN;
-              __hip_atomic_store(p.fail_flag + group_base + ti, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(p.fail_flag + slot, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             break;
           }
@@ -1087,9 +1092,9 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
     // ---- wave reduction, one partial per (tree, row block) ----
     if constexpr (!kIsInt<T> && MODE != MODE_PRECISE) {
       M = wave_chk(M);
-      if (lane == WAVE_LAST) reinterpret_cast<CT*>(p.slab_chk)[(int64_t)rb * p.ntrees + group_base + ti] = M;
+      if (lane == WAVE_LAST) reinterpret_cast<CT*>(p.slab_chk)[(int64_t)rb * p.ntrees + slot] = M;
     }
-    if (p.slab_rows && lane == WAVE_LAST) p.slab_rows[(int64_t)rb * p.ntrees + group_base + ti] = rows_done;
+    if (p.slab_rows && lane == WAVE_LAST) p.slab_rows[(int64_t)rb * p.ntrees + slot] = rows_done;
     if constexpr (MODE != MODE_PRECISE) {
       if (p.fused) {  // the only row block: reduce_kernel's steps for this tree, same order, same bits
         LAccT<T> s = csum;
@@ -1138,18 +1143,39 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   KMARK(0, 1);
   if (p.debug_stop == 1) return;
-  if (p.persistent) {
-    __shared__ int claimed;
-    for (;;) {
-      if (threadIdx.x == 0) claimed = atomicAdd(p.block_ctr, 1) + p.block0;
+  // items [0, nfull): whole row blocks block0 .. block0 + nfull - 1; then tail_slices items per
+  // remaining row block, each an interleaved slice of the population (the last round of a launch
+  // in finer pieces: the workgroups end within a slice of each other, not within a block).
+  // Grid launches run their one (blockIdx.x, blockIdx.y) item.  One call site: the interpreter
+  // body is inlined once.
+  __shared__ int claimed;
+  const int nfull = p.nrb - p.block0 - p.tail_blocks;
+  const int nitems = nfull + p.tail_blocks * p.tail_slices;
+  for (int it = 0;; ++it) {
+    int rb, gy = 0, gslice = 0, gstride = 1;
+    if (p.persistent) {
+      if (threadIdx.x == 0) claimed = atomicAdd(p.block_ctr, 1);
       __syncthreads();
-      const int rb = __builtin_amdgcn_readfirstlane(claimed);
-      if (rb >= p.nrb) break;
-      eval_block<T, R, K, MODE, XLDS>(p, smem, rb, 0);
-      __syncthreads();  // every wave is done with this block's LDS (and has read `claimed`)
+      const int item = __builtin_amdgcn_readfirstlane(claimed);
+      if (item >= nitems) break;
+      const int q = item - nfull;
+      const bool whole = item < nfull;
+      rb = p.block0 + (whole ? item : nfull + q / p.tail_slices);
+      gslice = whole ? 0 : q % p.tail_slices;
+      gstride = whole ? 1 : p.tail_slices;
+    } else {
+      if (it > 0) break;
+      rb = blockIdx.x;
+      if (p.grid_interleave) {  // grid.y workgroups share the population interleaved (the probe)
+        gslice = blockIdx.y;
+        gstride = gridDim.y;
+      } else {
+        gy = blockIdx.y;
+      }
     }
-  } else {
-    eval_block<T, R, K, MODE, XLDS>(p, smem, blockIdx.x, blockIdx.y);
+    eval_block<T, R, K, MODE, XLDS>(p, smem, rb, gy, gslice, gstride);
+    if (!p.persistent) break;
+    __syncthreads();  // every wave is done with this block's LDS (and has read `claimed`)
   }
 }
 

@@ -1453,9 +1453,13 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       // leading row blocks, one tree per wave (uniform groups of consecutive slots), with the plain
       // program: a probe workgroup serves 16 trees, too few to pay for deriving columns (the values,
       // partials and slots are the same either way)
+      // workgroup (b, g) of the probe takes slots g, g + G, g + 2G, ... (grid_interleave): each CU
+      // gets one of the most expensive trees and cheap ones, not 16 of the most expensive (which
+      // four waves per SIMD would share)
       EvalArgs q = a;
       q.group_off = nullptr;
       q.trees_per_group = eval_waves(R, K);
+      q.grid_interleave = 1;
       q.code = P->code_dev;
       q.prog_off = P->off_dev;
       q.max_steps = P->max_len;
@@ -1470,7 +1474,17 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     a.persistent = 1;
     a.block0 = probe_blocks;
     a.block_ctr = (int32_t*)ctx->block_ctr.p;
-    const int wgs = std::max(1, std::min(L.nrb - probe_blocks, ctx->num_cu));
+    const int nmain = L.nrb - probe_blocks;
+    const int wgs = std::max(1, std::min(nmain, ctx->num_cu));
+    // SRHIP_TAIL_SLICES = S > 1: the row blocks past the last whole round of workgroups are claimed
+    // as S interleaved population slices each (C2's 485 blocks on 256 workgroups leave 229 for a
+    // second round that idles 27 CUs for a block).  Default 1 (whole blocks): every slice restages
+    // the block and re-derives its columns, and that costs more than the idle CUs (C2, same box:
+    // S = 1 1.215 ms, 8 1.250, 16 1.278)
+    static const int slices_env = [] { const char* e = getenv("SRHIP_TAIL_SLICES"); return e ? atoi(e) : 1; }();
+    const int slices = std::max(1, std::min(slices_env, 64));
+    a.tail_slices = slices;
+    a.tail_blocks = slices > 1 && nmain > wgs && nl >= 16 * slices ? nmain % wgs : 0;
     HIP_TRY(launch_eval(dtype, a, R, K, mode, true, dim3(wgs, 1), L.lds, ctx->stream));
   } else {
     HIP_TRY(launch_eval(dtype, a, R, K, mode, L.xlds, grid, L.lds, ctx->stream));

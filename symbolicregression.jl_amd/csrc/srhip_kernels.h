@@ -94,6 +94,9 @@ struct EvalArgs {
   // block0 .. nrb-1 from *block_ctr (zeroed before the launch)
   int32_t persistent;
   int32_t block0;
+  int32_t tail_blocks;      // the last tail_blocks row blocks are claimed as tail_slices population slices each
+  int32_t tail_slices;
+  int32_t grid_interleave;  // grid launches: workgroup (x, y) takes order slots y, y + grid.y, ... (group_off unused)
   int32_t* block_ctr;
   int32_t* slab_rows;       // [nrb][ntrees] valid rows each (row block, order slot) evaluated, or nullptr
   int64_t* fused_rows;      // fused launches: [program trees] rows evaluated (coherent pinned host), or nullptr
