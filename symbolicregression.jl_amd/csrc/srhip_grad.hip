@@ -414,7 +414,11 @@ template <typename T> static size_t grad_lds_bytes(const GradArgs& a) {
 
 // rows per lane: value-only passes (no tangents) carry 4 rows per lane (one dispatch per 256-row
 // block); with tangents the register budget decides (GRAD_R)
-template <int KT, int K> constexpr int grad_rows() { return KT == 0 ? 4 : (KT <= 4 && K <= 4 ? GRAD_R : 1); }
+// (K = 2, the common shallow-stack population -- C4's size-20 trees all fit it -- leaves room for two
+// rows per lane with 4 tangents: half the dispatches per row at the same waves per SIMD)
+template <int KT, int K> constexpr int grad_rows() {
+  return KT == 0 ? 4 : (KT <= 4 && K <= 2 ? 2 : (KT <= 4 && K <= 4 ? GRAD_R : 1));
+}
 
 template <typename T, int KT, int K, int GM = GMODE_LOSS>
 static hipError_t launch_grad_t(const GradArgs& a, dim3 grid, hipStream_t s) {
@@ -453,10 +457,15 @@ hipError_t launch_grad(int dtype, int K, int kt, const GradArgs& a, dim3 grid, h
       if (kt == 0) return K <= 4 ? launch_grad_t<float, 0, 4>(a, grid, s) : launch_grad_t<float, 0, 8>(a, grid, s);
       if (kt == 4) return K <= 4 ? launch_grad_t<float, 4, 4>(a, grid, s) : launch_grad_t<float, 4, 8>(a, grid, s);
       return K <= 4 ? launch_grad_t<float, GRAD_KT, 4>(a, grid, s) : launch_grad_t<float, GRAD_KT, 8>(a, grid, s);
-    case SRHIP_F64:
-      if (kt == 0) return K <= 4 ? launch_grad_t<double, 0, 4>(a, grid, s) : launch_grad_t<double, 0, 8>(a, grid, s);
-      if (kt == 4) return K <= 4 ? launch_grad_t<double, 4, 4>(a, grid, s) : launch_grad_t<double, 4, 8>(a, grid, s);
-      return K <= 4 ? launch_grad_t<double, GRAD_KT, 4>(a, grid, s) : launch_grad_t<double, GRAD_KT, 8>(a, grid, s);
+    case SRHIP_F64:  // K = 2 variants for shallow-stack populations (fewer VGPRs: two rows per lane)
+      if (kt == 0)
+        return K <= 2 ? launch_grad_t<double, 0, 2>(a, grid, s)
+             : K <= 4 ? launch_grad_t<double, 0, 4>(a, grid, s) : launch_grad_t<double, 0, 8>(a, grid, s);
+      if (kt == 4)
+        return K <= 2 ? launch_grad_t<double, 4, 2>(a, grid, s)
+             : K <= 4 ? launch_grad_t<double, 4, 4>(a, grid, s) : launch_grad_t<double, 4, 8>(a, grid, s);
+      return K <= 2 ? launch_grad_t<double, GRAD_KT, 2>(a, grid, s)
+           : K <= 4 ? launch_grad_t<double, GRAD_KT, 4>(a, grid, s) : launch_grad_t<double, GRAD_KT, 8>(a, grid, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -203,7 +203,7 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
   HIP_TRY(ctx->g_chunks.ensure(chunk_n * sizeof(int32_t)));
   HIP_TRY(ctx->g_slab.ensure(slab_n * sizeof(double)));
   HIP_TRY(ctx->g_red.ensure(red_n * sizeof(double)));
-  const int K = P->gkmax <= 4 ? 4 : 8;
+  const int K = P->gkmax <= 2 ? 2 : (P->gkmax <= 4 ? 4 : 8);  // stack slots of the kernel variant
   bool first = true;
   for (Pass& ps : pass) {
     const int nch = (int)ps.chunks.size() / 2;
