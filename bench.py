@@ -2,13 +2,18 @@
 1024 random trees (size U{1..30}, ops + - * / cos exp) x 1M rows x 5 features, Float32, fused L2
 loss, one MI355X per rank.  A step = one srhip_eval_loss over the whole population (dataset
 and compiled population resident in HBM; per-step host work: launch, per-tree did_succeed
-decisions, 1024 losses back to the host).
+decisions, 1024 losses back to the host).  `value` counts the node-rows the device actually
+evaluated (srhip_last_work: a failed tree's skipped rows are not counted).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-seconds S]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-seconds S] [--mode islands|rowshard]
 
-N > 1 (launched by torch.distributed.run): each rank evaluates its own population on its own
-GPU (islands are independent, src/SymbolicRegression.jl:746-793): weak scaling, no collective on
-the data path; barrier + max-over-ranks timing via torch.distributed.
+N > 1 (launched by torch.distributed.run), --mode islands (default): each rank evaluates its own
+population on its own GPU (islands, src/SymbolicRegression.jl:746-793) and every step's results
+feed the migration exchange (src/Migration.jl:16-38): each rank's 12 best trees reach every rank
+through one RCCL all_gather_into_tensor, in flight during the next step's evaluation; weak
+scaling.  --mode rowshard: one population over a 10 x 10M dataset whose rows are sharded over the
+ranks, one fused all-reduce of the per-tree partials per step; strong scaling.  Barrier +
+max-over-ranks timing via torch.distributed.  --config c4 / c1 / c3: the other BASELINE configs.
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
@@ -128,21 +133,26 @@ def main():
         prog.eval_loss(ds, loss)
     from srhip import parallel
 
-    def migrate(l):
-        """islands: every step ends with the migration exchange (the best args.migrate_k trees of
-        every rank reach every rank: one all_gather_into_tensor over RCCL)"""
-        if dist is not None:
-            parallel.migrate_topk(nodes, offs, l, args.migrate_k, 30)
-
+    # islands: every step's evaluation is followed by the migration exchange of its results (the
+    # best args.migrate_k trees of every rank reach every rank: one all_gather_into_tensor over
+    # RCCL), issued in flight and collected after the next step's evaluation -- the all-gather runs
+    # on the collective's stream while the interpreter runs on the library's; the last one is
+    # collected inside the timed region
     barrier()
     parallel.timer.reset()
     t0 = time.perf_counter()
     kms, works = [], []
+    pending = None
     for _ in range(args.steps):
         l, ok = prog.eval_loss(ds, loss)
         kms.append(ctx.last_kernel_ms())
         works.append(ctx.last_work())
-        migrate(l)
+        if dist is not None:
+            if pending is not None:
+                pending.wait()
+            pending = parallel.migrate_topk_async(nodes, offs, l, args.migrate_k, 30)
+    if pending is not None:
+        pending.wait()
     barrier()
     dt = time.perf_counter() - t0
     coll_s, coll_calls = parallel.timer.seconds, parallel.timer.calls
@@ -247,7 +257,8 @@ def main():
             },
             # N > 1: the per-step migration exchange (parallel.migrate_topk), wall time on rank 0
             "collective": None if dist is None else {
-                "op": f"all_gather_into_tensor of each rank's {args.migrate_k} best trees (node tables + losses)",
+                "op": f"all_gather_into_tensor of each rank's {args.migrate_k} best trees (node tables + losses), "
+                      f"in flight during the next step's evaluation",
                 "backend": dist.get_backend(), "ranks": world, "calls_per_step": coll_calls / args.steps,
                 "ms_per_step": coll_s * 1e3 / args.steps},
             "roofline": {

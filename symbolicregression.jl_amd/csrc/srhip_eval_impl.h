@@ -891,7 +891,15 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const CIns* code = (const CIns*)(uintptr_t)p.code;
   KMARK(8 + wave, 10);
-  for (int ti = wave; ti < group_n;) {
+  // tile claims (the probe launch, R = 16: one tile = one loss chunk): a wave claims one (tree, tile)
+  // at a time, so the two tiles of a row block's costliest tree run on two waves at once; the check
+  // statistic and the row count then combine by atomics (max of non-negative float bits; NaN bits
+  // order above every finite and infinite value), each loss chunk is still written by one wave
+  const bool tile_claims = p.tile_claims != 0 && TILE % (sizeof(T) == 8 ? LOSS_CHUNK_8B : LOSS_CHUNK_4B) == 0;
+  const int nclaims = tile_claims ? group_n * ntiles : group_n;
+  for (int cl = wave; cl < nclaims;) {
+    const int ti = tile_claims ? cl / ntiles : cl;
+    const int tile0 = tile_claims ? cl - ti * ntiles : 0, tile_end = tile_claims ? tile0 + 1 : ntiles;
     KMARK(8 + wave, 11);
     const int slot = group_base + ti * gstride;  // order slot (uniform)
     const int tree = __builtin_amdgcn_readfirstlane(p.order[slot]);
@@ -932,11 +940,11 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
     int rows_done = 0;  // valid rows this wave evaluated the tree on (the launch's work count)
     if (failed) {
       if (lane == WAVE_LAST)
-        for (int c = 0; c < p.cpb; ++c) lslab[c] = (LAccT<T>)NAN;
+        for (int c = tile_claims ? tile0 : 0; c < (tile_claims ? tile_end : p.cpb); ++c) lslab[c] = (LAccT<T>)NAN;
       M = (CT)NAN;
       csum = (LAccT<T>)NAN;
     }
-    for (int tile = 0; tile < (failed ? 0 : ntiles); ++tile) {
+    for (int tile = tile0; tile < (failed ? tile0 : tile_end); ++tile) {
       const int64_t row0 = row_base + (int64_t)tile * TILE;
       if (row0 >= p.nvalid) break;  // whole tile is padding
       rows_done += (int)min((int64_t)TILE, p.nvalid - row0);
@@ -1076,7 +1084,8 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
           if (p.early_exit && __builtin_amdgcn_ballot_w64(!(M < (CT)INFINITY)) != 0) {
             csum = (LAccT<T>)NAN;
             if (lane == WAVE_LAST) {
-              for (int c = tile / (CH / TILE) + (flushed ? 1 : 0); c < p.cpb; ++c) lslab[c] = (LAccT<T>)NAN;
+              for (int c = tile / (CH / TILE) + (flushed ? 1 : 0); c < (tile_claims ? tile_end : p.cpb); ++c)
+                lslab[c] = (LAccT<T>)NAN;
               __hip_atomic_store(p.fail_flag + slot, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             break;
@@ -1092,9 +1101,20 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
     // ---- wave reduction, one partial per (tree, row block) ----
     if constexpr (!kIsInt<T> && MODE != MODE_PRECISE) {
       M = wave_chk(M);
-      if (lane == WAVE_LAST) reinterpret_cast<CT*>(p.slab_chk)[(int64_t)rb * p.ntrees + slot] = M;
+      CT* chk_at = reinterpret_cast<CT*>(p.slab_chk) + (int64_t)rb * p.ntrees + slot;
+      if (lane == WAVE_LAST) {
+        if constexpr (sizeof(CT) == 4) {
+          if (tile_claims) atomicMax(reinterpret_cast<unsigned*>(chk_at), __builtin_bit_cast(unsigned, __builtin_fabsf(M) == __builtin_fabsf(M) ? __builtin_fabsf(M) : M));
+          else *chk_at = M;
+        } else {
+          *chk_at = M;
+        }
+      }
     }
-    if (p.slab_rows && lane == WAVE_LAST) p.slab_rows[(int64_t)rb * p.ntrees + slot] = rows_done;
+    if (p.slab_rows && lane == WAVE_LAST) {
+      if (tile_claims) atomicAdd(p.slab_rows + (int64_t)rb * p.ntrees + slot, rows_done);
+      else p.slab_rows[(int64_t)rb * p.ntrees + slot] = rows_done;
+    }
     if constexpr (MODE != MODE_PRECISE) {
       if (p.fused) {  // the only row block: reduce_kernel's steps for this tree, same order, same bits
         LAccT<T> s = csum;
@@ -1123,7 +1143,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
     KMARK(8 + wave, 13);
     int claim = 0;
     if (lane == 0) claim = atomicAdd(&next_tree, 1);
-    ti = __builtin_amdgcn_readfirstlane(claim);
+    cl = __builtin_amdgcn_readfirstlane(claim);
   }
   KMARK(8 + wave, 14);
 }

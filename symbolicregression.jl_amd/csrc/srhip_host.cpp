@@ -1238,6 +1238,15 @@ int srhip::check_eval_args(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_
   return SRHIP_OK;
 }
 
+static bool env_flag(const char* name) {
+  const char* e = getenv(name);
+  return e && *e && *e != '0';
+}
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+
 // Device stage: one interpreter launch over the view + the per-tree reduction.  Fills the partials
 // (sums layout above; chk[T]) and, in MODE_PRED, out_pred.
 static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
@@ -1274,9 +1283,11 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   LaunchPlan L{};
   // LDS a workgroup may stage: the 16-wave variant runs one workgroup per CU (160 KB, less the
   // kernel's static arrays); 8-wave workgroups run two (derived-column programs) or more
-  auto lds_budget = [](int r, int k, bool derived) -> size_t {
-    if (eval_waves(r, k) >= 16) return 152 * 1024;
-    return derived ? 64 * 1024 - 512 : 64 * 1024 - 64;
+  // (the device's LDS per workgroup, read once per context, less 8 KB for the kernel's static arrays)
+  const size_t lds_dev = (size_t)ctx->lds_max;
+  auto lds_budget = [lds_dev](int r, int k, bool derived) -> size_t {
+    if (eval_waves(r, k) >= 16) return lds_dev - 8 * 1024;
+    return std::min<size_t>(lds_dev / 2, derived ? 64 * 1024 - 512 : 64 * 1024 - 64);
   };
   // Persistent launch (the wide Float32 variant's loss launches): one workgroup per CU claims short
   // row blocks from a counter and interprets the WHOLE population over each -- the dataset is read
@@ -1287,9 +1298,10 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   // SRHIP_NO_PERSISTENT=1: the grid launch; SRHIP_PRB_ROWS: row-block rows (default 2048: C2, one
   // MI355X, same box: 1024 rows 1.31 ms, 2048 1.19, 4096 1.35, grid launch 1.33);
   // SRHIP_PROBE_BLOCKS: probe row blocks (default 4).
-  static const bool no_persistent = [] { const char* e = getenv("SRHIP_NO_PERSISTENT"); return e && *e && *e != '0'; }();
-  static const int prb_env = [] { const char* e = getenv("SRHIP_PRB_ROWS"); return e ? atoi(e) : 0; }();
-  static const int probe_env = [] { const char* e = getenv("SRHIP_PROBE_BLOCKS"); return e ? atoi(e) : -1; }();
+  // (read per launch: tests and the bench toggle them inside one process)
+  const bool no_persistent = env_flag("SRHIP_NO_PERSISTENT");
+  const int prb_env = env_int("SRHIP_PRB_ROWS", 0);
+  const int probe_env = env_int("SRHIP_PROBE_BLOCKS", -1);
   bool persistent = false;
   int probe_blocks = 0;
   {
@@ -1460,6 +1472,14 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       q.group_off = nullptr;
       q.trees_per_group = eval_waves(R, K);
       q.grid_interleave = 1;
+      // one (tree, tile) per claim: the costliest tree's two tiles run on two waves at once (the
+      // probe's duration is that tree's); chk / rows of the probe blocks combine by atomics from 0
+      const bool no_tile_claims = env_flag("SRHIP_PROBE_TREE_CLAIMS");
+      if (!no_tile_claims) {
+        q.tile_claims = 1;
+        HIP_TRY(hipMemsetAsync(ctx->slab_chk.p, 0, (size_t)probe_blocks * nl * sizeof(float), ctx->stream));
+        HIP_TRY(hipMemsetAsync(ctx->slab_rows.p, 0, (size_t)probe_blocks * nl * sizeof(int32_t), ctx->stream));
+      }
       q.code = P->code_dev;
       q.prog_off = P->off_dev;
       q.max_steps = P->max_len;
@@ -1481,7 +1501,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     // second round that idles 27 CUs for a block).  Default 1 (whole blocks): every slice restages
     // the block and re-derives its columns, and that costs more than the idle CUs (C2, same box:
     // S = 1 1.215 ms, 8 1.250, 16 1.278)
-    static const int slices_env = [] { const char* e = getenv("SRHIP_TAIL_SLICES"); return e ? atoi(e) : 1; }();
+    const int slices_env = env_int("SRHIP_TAIL_SLICES", 1);
     const int slices = std::max(1, std::min(slices_env, 64));
     a.tail_slices = slices;
     a.tail_blocks = slices > 1 && nmain > wgs && nl >= 16 * slices ? nmain % wgs : 0;
@@ -1685,6 +1705,9 @@ int srhip_ctx_create(int device, srhip_ctx** out) {
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));
   c->num_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  int lds_max = 0;
+  if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && lds_max > 0)
+    c->lds_max = lds_max;
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
     return fail(SRHIP_ERR_UNSUPPORTED, "device %d is %s; libsrhip is built for gfx950 only", device, prop.gcnArchName);
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));

@@ -119,6 +119,7 @@ struct srhip_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   int num_cu = 256;
+  int lds_max = 160 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerBlock of the device
   srhip::DevBuf slab_loss, slab_chk, slab_prec, order_prec;
   srhip::DevBuf vX, vy, vw, vidx, vstats;  // gathered views (batching idx)
   srhip::DevBuf g_chunks, g_slab, g_red;   // constant-gradient launches

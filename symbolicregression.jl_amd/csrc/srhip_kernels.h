@@ -97,6 +97,7 @@ struct EvalArgs {
   int32_t tail_blocks;      // the last tail_blocks row blocks are claimed as tail_slices population slices each
   int32_t tail_slices;
   int32_t grid_interleave;  // grid launches: workgroup (x, y) takes order slots y, y + grid.y, ... (group_off unused)
+  int32_t tile_claims;      // a wave claims one (tree, tile) at a time (R = 16 probe; slab_chk / slab_rows zeroed first)
   int32_t* block_ctr;
   int32_t* slab_rows;       // [nrb][ntrees] valid rows each (row block, order slot) evaluated, or nullptr
   int64_t* fused_rows;      // fused launches: [program trees] rows evaluated (coherent pinned host), or nullptr

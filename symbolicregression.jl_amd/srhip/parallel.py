@@ -82,29 +82,54 @@ class CollectiveTimer:
 timer = CollectiveTimer()
 
 
+_bufs = {}
+
+
+def _staging(n: int, dtype, dev):
+    """Reused (pinned host, device) buffer pair of n elements for a collective's copies: no allocation
+    and no pageable-memory copy per call.  One exchange of a given size in flight at a time (an
+    async migration is collected before the next is issued)."""
+    import torch
+
+    key = (n, dtype, str(dev))
+    if key not in _bufs:
+        host = torch.empty(n, dtype=dtype, pin_memory=dev.type == "cuda")
+        _bufs[key] = (host, host if dev.type != "cuda" else torch.empty(n, dtype=dtype, device=dev))
+    return _bufs[key]
+
+
 def allreduce_partials(sums: np.ndarray, chk: np.ndarray, chk_op: str, group=None):
     """The row-shard exchange of eval_loss_partials in ONE device buffer [sums | chk] (one host->device
-    copy, the two all-reduces issued back to back on it -- SUM over the sums, MAX (Float32) or SUM
-    over the check statistics -- and one copy back).  A non-finite check statistic is sent as +Inf,
-    which every backend's MAX keeps (an fmax-style reduction may drop a NaN)."""
+    copy from a reused pinned buffer, the two all-reduces issued back to back on it -- SUM over the
+    sums, MAX (Float32) or SUM over the check statistics -- and one copy back).  A non-finite check
+    statistic is sent as +Inf, which every backend's MAX keeps (an fmax-style reduction may drop a
+    NaN)."""
     import time
 
     import torch
 
     dist = _dist()
     t0 = time.perf_counter()
-    ns = len(sums)
-    chk = np.where(np.isfinite(chk), chk, np.inf)
-    buf = torch.from_numpy(np.concatenate([np.asarray(sums, dtype=np.float64), chk])).to(_device(group))
+    ns, nc = len(sums), len(chk)
+    dev = _device(group)
+    host, buf = _staging(ns + nc, torch.float64, dev)
+    hv = host.numpy()
+    hv[:ns] = sums
+    hv[ns:] = np.where(np.isfinite(chk), chk, np.inf)
+    if buf is not host:
+        buf.copy_(host, non_blocking=True)
     w1 = dist.all_reduce(buf[:ns], op=dist.ReduceOp.SUM, group=group, async_op=True)
     w2 = dist.all_reduce(buf[ns:], op=dist.ReduceOp.MAX if chk_op == "max" else dist.ReduceOp.SUM, group=group,
                          async_op=True)
     w1.wait()
     w2.wait()
-    out = buf.cpu().numpy()
+    if buf is not host:
+        host.copy_(buf, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+    out = hv.copy()
     timer.seconds += time.perf_counter() - t0
     timer.calls += 1
-    return out[:ns].copy(), out[ns:].copy()
+    return out[:ns], out[ns:]
 
 
 def eval_loss_sharded(prog, nfeatures: int, partials, precise=None, group=None):
@@ -203,12 +228,48 @@ def exchange_members(trees, scores, losses, options, dtype, group=None):
     return out
 
 
-def migrate_topk(nodes: np.ndarray, offsets: np.ndarray, losses: np.ndarray, k: int, max_nodes: int, group=None):
-    """Migration exchange with a fixed-size payload: this rank's k best trees (by loss; did_succeed
-    trees first) travel as node tables plus their losses in one packed buffer of
-    k x max_nodes node records, so the exchange is ONE all_gather_into_tensor with no size
-    round (src/Migration.jl:16-38: every population's best members reach every other).  Trees
-    longer than max_nodes are skipped.  Returns [(nodes, offsets, losses)] by rank."""
+class _Pending:
+    """An in-flight migrate_topk exchange (migrate_topk_async): wait() -> [(nodes, offsets, losses)]."""
+
+    def __init__(self, work, dst, host_out, ws, head, k, payload_len, t_issue):
+        self.work, self.dst, self.host_out, self.ws = work, dst, host_out, ws
+        self.head, self.k, self.n, self.t_issue = head, k, payload_len, t_issue
+
+    def wait(self):
+        import time
+
+        import torch
+
+        t0 = time.perf_counter()
+        self.work.wait()
+        if self.host_out is not self.dst:
+            self.host_out.copy_(self.dst, non_blocking=True)
+            torch.cuda.current_stream(self.dst.device).synchronize()
+        allb = self.host_out.numpy().reshape(self.ws, self.n)
+        out = _unpack_topk(allb, self.ws, self.head, self.k)
+        timer.seconds += time.perf_counter() - t0
+        timer.calls += 1
+        return out
+
+
+def _unpack_topk(allb, ws, head, k):
+    rec = NODE_DTYPE.itemsize
+    out = []
+    for r in range(ws):
+        h = allb[r, :head].copy().view(np.int64)
+        cnt = int(h[0])
+        of = h[1:cnt + 2].copy()
+        ls = allb[r, 8 * (k + 2):head].copy().view(np.float64)[:cnt]
+        nd = allb[r, head:head + int(of[-1]) * rec].copy().view(NODE_DTYPE)
+        out.append((nd, of, ls))
+    return out
+
+
+def migrate_topk_async(nodes: np.ndarray, offsets: np.ndarray, losses: np.ndarray, k: int, max_nodes: int,
+                       group=None) -> _Pending:
+    """migrate_topk, issued and left in flight: the all-gather runs on the collective's own stream
+    while the caller's next evaluation runs on the library's; .wait() collects it.  The bench issues
+    step k's exchange after step k's evaluation and collects it after step k + 1's."""
     import time
 
     import torch
@@ -216,6 +277,19 @@ def migrate_topk(nodes: np.ndarray, offsets: np.ndarray, losses: np.ndarray, k: 
     dist = _dist()
     t0 = time.perf_counter()
     ws = dist.get_world_size(group)
+    payload, head = _pack_topk(nodes, offsets, losses, k, max_nodes)
+    dev = _device(group)
+    host_in, src = _staging(len(payload), torch.uint8, dev)
+    host_in.numpy()[:] = payload
+    if src is not host_in:
+        src.copy_(host_in, non_blocking=True)
+    host_out, dst = _staging(ws * len(payload), torch.uint8, dev)
+    work = dist.all_gather_into_tensor(dst, src, group=group, async_op=True)
+    timer.seconds += time.perf_counter() - t0
+    return _Pending(work, dst, host_out, ws, head, k, len(payload), t0)
+
+
+def _pack_topk(nodes, offsets, losses, k, max_nodes):
     nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
     offsets = np.asarray(offsets, dtype=np.int64)
     losses = np.asarray(losses, dtype=np.float64)
@@ -238,19 +312,13 @@ def migrate_topk(nodes: np.ndarray, offsets: np.ndarray, losses: np.ndarray, k: 
         loss_out[i] = losses[t]
         cur += b - a
     offs_out[len(sel)] = cur
-    dev = _device(group)
-    src = torch.from_numpy(payload).to(dev)
-    dst = torch.empty(ws * len(payload), dtype=torch.uint8, device=dev)
-    dist.all_gather_into_tensor(dst, src, group=group)
-    allb = dst.cpu().numpy().reshape(ws, len(payload))
-    out = []
-    for r in range(ws):
-        h = allb[r, :head].copy().view(np.int64)
-        cnt = int(h[0])
-        of = h[1:cnt + 2].copy()
-        ls = allb[r, 8 * (k + 2):head].copy().view(np.float64)[:cnt]
-        nd = allb[r, head:head + int(of[-1]) * rec].copy().view(NODE_DTYPE)
-        out.append((nd, of, ls))
-    timer.seconds += time.perf_counter() - t0
-    timer.calls += 1
-    return out
+    return payload, head
+
+
+def migrate_topk(nodes: np.ndarray, offsets: np.ndarray, losses: np.ndarray, k: int, max_nodes: int, group=None):
+    """Migration exchange with a fixed-size payload: this rank's k best trees (by loss; did_succeed
+    trees first) travel as node tables plus their losses in one packed buffer of
+    k x max_nodes node records, so the exchange is ONE all_gather_into_tensor with no size
+    round (src/Migration.jl:16-38: every population's best members reach every other).  Trees
+    longer than max_nodes are skipped.  Returns [(nodes, offsets, losses)] by rank."""
+    return migrate_topk_async(nodes, offsets, losses, k, max_nodes, group).wait()

@@ -713,7 +713,8 @@ class SearchResult:
 def _worker_search(worker, key, meta, options, factory):
     """The worker-process side of an island task: a host Dataset over the shared-memory arrays with
     the worker's resident device copy attached (no second upload), and one scorer per dataset --
-    a coalescer on the worker's own context (one client: max_wait 0), or ``factory``'s."""
+    a coalescer on a context of its own over the resident dataset (one client: max_wait 0), or
+    ``factory``'s."""
     cache = worker.__dict__.setdefault("search", {})
     if worker.backend == "srhip":
         options.device = worker.device
@@ -729,7 +730,10 @@ def _worker_search(worker, key, meta, options, factory):
         if factory is not None:
             sc = factory(worker, d, options)
         else:
-            sc = DeviceScorer(d, options, nclients=1, max_wait_us=0, ctx=worker.ctx, device_dataset=dev)
+            # the coalescer on a context of its own (over the worker's resident dataset: any context
+            # on its device may read it), not the worker's: api.optimize_constants / eval_loss on
+            # this thread use the worker's context, and the coalescer's worker threads never share it
+            sc = DeviceScorer(d, options, nclients=1, max_wait_us=0, device_dataset=dev)
         st = cache[key] = (d, sc)
     d, sc = st
     if "baseline_loss" in meta:

@@ -12,7 +12,11 @@ dataset is serialized into every task.  Here:
   uploads it to its device once, and tasks name the dataset by key -- a task carries only
   populations (node tables, a few KB);
 * a worker that died is respawned by ``ensure_workers`` (called before every submit) and re-attaches
-  every registered dataset from shared memory (no re-send from the head process);
+  every registered dataset from shared memory (no re-send from the head process); the tasks that
+  were in flight on the dead process fail with ``WorkerDied`` (tasks queued for its replacement are
+  untouched: reaping goes by process generation).  The pool does not resubmit them, and the island
+  search (srhip.search, :multiprocessing) does not either: a worker death ends that search with the
+  error, while the pool stays usable for the next call;
 * tasks are plain picklable functions ``fn(worker, dataset, *args)`` (module-level, like the
   reference's requirement that user functions be defined on the workers, `move_functions_to_workers`),
   run in submission order per worker; results come back as concurrent.futures.Future objects.
@@ -156,7 +160,8 @@ class GPUWorkerPool:
         self._procs = [None] * self.nprocs
         self._inbox = [None] * self.nprocs
         self._shared = {}  # key -> (_Shared X, y, w)
-        self._pending = {}  # tid -> (Future, worker)
+        self._pending = {}  # tid -> (Future, worker, generation of that worker's process)
+        self._gen = [0] * self.nprocs  # respawns of each worker slot
         self._lock = threading.Lock()
         self._tids = itertools.count()
         self._keys = itertools.count()
@@ -178,7 +183,9 @@ class GPUWorkerPool:
         p = self._mp.Process(target=_worker_main, args=(i, self.device_of(i), self.backend, self._inbox[i],
                                                          self._outbox, specs), daemon=True)
         p.start()
-        self._procs[i] = p
+        with self._lock:
+            self._procs[i] = p
+            self._gen[i] += 1
 
     def _read(self):
         while True:
@@ -193,7 +200,7 @@ class GPUWorkerPool:
                 return
             tid, worker, ok, res = msg
             with self._lock:
-                fut = self._pending.pop(tid, (None, None))[0] if tid is not None else None
+                fut = self._pending.pop(tid, (None, None, None))[0] if tid is not None else None
             if fut is None:
                 continue
             if ok:
@@ -202,12 +209,14 @@ class GPUWorkerPool:
                 fut.set_exception(RuntimeError(f"worker {worker} (device {self.device_of(worker)}):\n{res}"))
 
     def _reap(self):
-        """Fail the tasks of workers that died (they are respawned on the next submit)."""
-        dead = {i for i, p in enumerate(self._procs) if p is not None and not p.is_alive()}
-        if not dead:
-            return
+        """Fail the tasks of worker processes that died (the slots are respawned on the next submit).
+        Under the lock and by generation: a task queued for a slot's NEW process (respawned since the
+        old one died) is never failed for the old one's death."""
         with self._lock:
-            lost = [tid for tid, (_, w) in self._pending.items() if w in dead]
+            dead = {(i, self._gen[i]) for i, p in enumerate(self._procs) if p is not None and not p.is_alive()}
+            if not dead:
+                return
+            lost = [tid for tid, (_, w, g) in self._pending.items() if (w, g) in dead]
             futs = [self._pending.pop(tid)[0] for tid in lost]
         for f in futs:
             f.set_exception(WorkerDied("worker process died"))
@@ -240,7 +249,7 @@ class GPUWorkerPool:
         tid = next(self._tids)
         fut = Future()
         with self._lock:
-            self._pending[tid] = (fut, worker)
+            self._pending[tid] = (fut, worker, self._gen[worker])
         self._inbox[worker].put((kind, tid, payload))
         return fut
 
