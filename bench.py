@@ -512,7 +512,7 @@ def bench_c4(args):
     fin = np.isfinite(base)
     # HBM bytes of the profiled gradient variant (scripts/pmc_grad.sh over scripts/grad_bench.py: the
     # same 512 x 100k population, one full loss + gradient launch)
-    gname = "srhip::grad_kernel<double, 4, 4, 0, true, 1>"
+    gname = "srhip::grad_kernel<double, 4, 2, 0, true, 2>"
     gtraffic, gvalu, gsrc = pmc_summary(gname, "*pmc_grad_c4*.json")
     print(json.dumps({
         "metric": "C4 batched constant optimisation: wall time per optimize_constants over the population",
