@@ -83,6 +83,7 @@ struct srhip_batcher {
   int64_t n_requests = 0, max_seen = 0;
   std::atomic<int64_t> n_launches{0};
   std::vector<Worker> workers;
+  bool w0_busy = false;  // worker 0 is inside a flush (guarded by mu)
 
   void run(Worker& w);
   void flush(Worker& w, std::vector<Request>& batch);
@@ -174,10 +175,15 @@ void srhip_batcher::flush(Worker& w, std::vector<Request>& batch) {
 }
 
 void srhip_batcher::run(Worker& w) {
+  // Worker 0 takes every batch it can; the others only while worker 0 is inside a flush (a single
+  // client -- C1's latency-bound path -- then always meets worker 0 on the caller's context, and a
+  // second worker adds throughput only under load)
+  const bool first = &w == &workers[0];
   std::unique_lock<std::mutex> lk(mu);
   for (;;) {
-    cv_work.wait(lk, [&] { return stop || !queue.empty(); });
+    cv_work.wait(lk, [&] { return stop || (!queue.empty() && (first || w0_busy)); });
     if (queue.empty() && stop) return;
+    if (queue.empty()) continue;
     // gather: flush when full, when every registered client has a request queued, at the
     // deadline (clients that finished or are slow), or on stop
     const auto deadline = queue.front().t_submit + std::chrono::microseconds(max_wait_us);
@@ -193,9 +199,12 @@ void srhip_batcher::run(Worker& w) {
       batch.push_back(std::move(queue.front()));
       queue.pop_front();
     }
+    if (first) w0_busy = true;
+    if (first && !queue.empty()) cv_work.notify_all();  // the rest is for another worker
     lk.unlock();
     flush(w, batch);
     lk.lock();
+    if (first) w0_busy = false;
   }
 }
 
@@ -287,7 +296,8 @@ int srhip_batcher_submit(srhip_batcher* b, const srhip_node* nodes, int64_t nnod
     b->pending.emplace(r.ticket, r.pending);
     b->queue.push_back(std::move(r));
   }
-  b->cv_work.notify_one();
+  if (b->workers.size() > 1) b->cv_work.notify_all();  // worker 0 if idle, else another
+  else b->cv_work.notify_one();
   return SRHIP_OK;
 }
 

@@ -73,11 +73,16 @@ template <> struct Vec16<float> { typedef float __attribute__((ext_vector_type(4
 template <> struct Vec16<int32_t> { typedef int32_t __attribute__((ext_vector_type(4))) type; };
 template <> struct Vec16<double> { typedef double __attribute__((ext_vector_type(2))) type; };
 
+// A lane's R rows of one tile, as one vector value (a VGPR tuple): packed row-pair operations
+// (v_pk_*) read and write aligned sub-pairs of it in place.
+template <typename T, int R> struct RowVec { typedef T type __attribute__((ext_vector_type(R))); };
+template <typename T, int R> using RV = typename RowVec<T, R>::type;
+
 // Rows of one tile owned by a lane: register r holds tile row
 //   (r / VEC) * 64 * VEC + lane * VEC + (r % VEC)        (VEC = 16 / sizeof(T))
 // so every access to a column is one 16-byte load per lane, contiguous across the wave.
 template <typename T, int R>
-__device__ __attribute__((always_inline)) inline void load_rows(const T* base, int lane, T (&v)[R]) {
+__device__ __attribute__((always_inline)) inline void load_rows(const T* base, int lane, RV<T, R>& v) {
   constexpr int VEC = 16 / sizeof(T);
   using V = typename Vec16<T>::type;
   UNR for (int j = 0; j < R / VEC; ++j) {
@@ -105,8 +110,6 @@ template <typename T> __device__ __attribute__((always_inline)) inline T imm_as(
 // every kernel variant made a ~700k-instruction kernel whose hot loop thrashed the instruction
 // cache (SQ_IFETCH ~ 0.4 x SQ_INSTS).  Out of line, the dispatch loop and the cheap handlers stay
 // compact and each heavy body exists once; the R rows travel in VGPRs (vector argument/return).
-template <typename T, int R> struct RowVec { typedef T type __attribute__((ext_vector_type(R))); };
-template <typename T, int R> using RV = typename RowVec<T, R>::type;
 
 // v_cvt_i32_f64 as an opaque instruction: saturating for out-of-range input and 0 for NaN (the C++
 // conversion of such values is undefined, and the compiler may exploit that).
@@ -240,7 +243,7 @@ __device__ __attribute__((noinline)) RV<float, R> trigf_slow(RV<float, R> v) {
   }
   return v;
 }
-template <int R> __device__ __attribute__((always_inline)) inline bool trigf_rows_fast(const float (&A)[R]) {
+template <int R> __device__ __attribute__((always_inline)) inline bool trigf_rows_fast(const RV<float, R>& A) {
   float mx = 0.0f;
   UNR for (int r = 0; r < R; r += 2)
     asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(A[r]), "v"(A[r + 1]));
@@ -343,7 +346,7 @@ constexpr bool un_wide(int u) { return un_wide_op(u); }
 // unary operators cheap enough to inline into the handler (a few VALU instructions per row)
 template <int U> constexpr bool un_inline() { return un_cheap(U); }
 template <typename T, int R, int U>
-__device__ __attribute__((always_inline)) inline void apply_un(T (&A)[R]) {
+__device__ __attribute__((always_inline)) inline void apply_un(RV<T, R>& A) {
   if constexpr (SRHIP_TRIG_ROWS && std::is_same<T, float>::value && (U == UN_COS || U == UN_SIN) && R % 2 == 0) {
     constexpr int KIND = U == UN_COS ? 0 : 1;
     RV<T, R> v;
@@ -368,7 +371,7 @@ __device__ __attribute__((always_inline)) inline void apply_un(T (&A)[R]) {
   }
 }
 template <typename T, int R, int HB>
-__device__ __attribute__((always_inline)) inline void apply_heavy(T (&A)[R], const T (&X)[R], const T (&Y)[R]) {
+__device__ __attribute__((always_inline)) inline void apply_heavy(RV<T, R>& A, const RV<T, R>& X, const RV<T, R>& Y) {
   RV<T, R> a, b;
   UNR for (int r = 0; r < R; ++r) { a[r] = X[r]; b[r] = Y[r]; }
   a = heavy_bin<T, R, HB>(a, b);
@@ -382,14 +385,14 @@ template <typename T> struct Chk {
 };
 // Float32: one v_maximum3_f32 per two rows, chained through M (the compiler's reassociation into
 // a pairwise tree costs R/2 + 2 instructions instead of R/2).
-template <int R> __device__ __attribute__((always_inline)) inline void chk_update(float& M, const float (&A)[R]) {
+template <int R> __device__ __attribute__((always_inline)) inline void chk_update(float& M, const RV<float, R>& A) {
   UNR for (int r = 0; r < R; r += 2)
     asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(M) : "v"(M), "v"(A[r]), "v"(A[r + 1]));
 }
-template <int R> __device__ __attribute__((always_inline)) inline void chk_update(double& M, const double (&A)[R]) {
+template <int R> __device__ __attribute__((always_inline)) inline void chk_update(double& M, const RV<double, R>& A) {
   UNR for (int r = 0; r < R; ++r) M = __builtin_fma(__builtin_fabs(A[r]), 0x1p-512, M);
 }
-template <int R> __device__ __attribute__((always_inline)) inline void chk_update(int32_t&, const int32_t (&)[R]) {}
+template <int R> __device__ __attribute__((always_inline)) inline void chk_update(int32_t&, const RV<int32_t, R>&) {}
 
 // IEEE Float32 division of two rows: the compiler's own a / b expansion (v_div_scale of the
 // denominator and of the numerator, v_rcp, Newton refinement, v_div_fmas with the numerator's scale
@@ -439,7 +442,7 @@ constexpr float DIV_FAST_LO = 0x1p-40f, DIV_FAST_HI = 0x1p40f;
 // bounds every folded output's sum by max|v| x rows) is unchanged.
 // CONSTB: B is one wave-uniform constant, so only A's rows need the range test.
 template <int R, bool SWAP, bool CHK, bool CONSTB = false>
-__device__ __attribute__((always_inline)) inline void div_rows(float (&A)[R], const float (&B)[R], float& M) {
+__device__ __attribute__((always_inline)) inline void div_rows(RV<float, R>& A, const RV<float, R>& B, float& M) {
   float mx = 0.0f, mn = __builtin_inff();
   if constexpr (CONSTB) {
     UNR for (int r = 0; r < R; r += 2) {
@@ -478,6 +481,9 @@ __device__ __attribute__((always_inline)) inline void div_rows(float (&A)[R], co
 // run on packed row pairs (v_pk_add_f32 / v_pk_mul_f32, div_rows: each lane rounded exactly as
 // the scalar instruction would); the rest row by row.
 typedef F2 PkF32;
+#ifndef SRHIP_PK_BINOPS
+#define SRHIP_PK_BINOPS 1
+#endif
 template <typename T, int SB> __device__ __attribute__((always_inline)) inline T sb_apply(T a, T b) {
   using O = OpsT<T>;
   switch (SB) {
@@ -489,11 +495,11 @@ template <typename T, int SB> __device__ __attribute__((always_inline)) inline T
   return a;
 }
 template <typename T, int R, int SB, bool SWAP>
-__device__ __attribute__((always_inline)) inline void bin_rows(T (&A)[R], const T (&B)[R]) {
+__device__ __attribute__((always_inline)) inline void bin_rows(RV<T, R>& A, const RV<T, R>& B) {
   if constexpr (std::is_same<T, float>::value && R % 2 == 0 && SB == SB_DIV) {
     float unused = 0.0f;
     div_rows<R, SWAP, false>(A, B, unused);
-  } else if constexpr (std::is_same<T, float>::value && R % 2 == 0 &&
+  } else if constexpr (SRHIP_PK_BINOPS && std::is_same<T, float>::value && R % 2 == 0 &&
                        (SB == SB_ADD || SB == SB_SUB || SB == SB_MUL)) {
     UNR for (int r = 0; r < R; r += 2) {
       const PkF32 a = {A[r], A[r + 1]}, b = {B[r], B[r + 1]};
@@ -509,14 +515,14 @@ __device__ __attribute__((always_inline)) inline void bin_rows(T (&A)[R], const 
   }
 }
 template <typename T, int R, int SB, bool SWAP>
-__device__ __attribute__((always_inline)) inline void bin_rows_c(T (&A)[R], T c) {
-  T B[R];
+__device__ __attribute__((always_inline)) inline void bin_rows_c(RV<T, R>& A, T c) {
+  RV<T, R> B;
   UNR for (int r = 0; r < R; ++r) B[r] = c;
   bin_rows<T, R, SB, SWAP>(A, B);
 }
 // the interpreter's operator forms: the operation and the check fold of its output
 template <typename T, int R, int SB, bool SWAP, bool CONSTB = false>
-__device__ __attribute__((always_inline)) inline void bin_rows_chk(T (&A)[R], const T (&B)[R], typename Chk<T>::type& M) {
+__device__ __attribute__((always_inline)) inline void bin_rows_chk(RV<T, R>& A, const RV<T, R>& B, typename Chk<T>::type& M) {
   if constexpr (std::is_same<T, float>::value && R % 2 == 0 && SB == SB_DIV) {
     div_rows<R, SWAP, true, CONSTB>(A, B, M);
   } else {
@@ -525,8 +531,8 @@ __device__ __attribute__((always_inline)) inline void bin_rows_chk(T (&A)[R], co
   }
 }
 template <typename T, int R, int SB, bool SWAP>
-__device__ __attribute__((always_inline)) inline void bin_rows_c_chk(T (&A)[R], T c, typename Chk<T>::type& M) {
-  T B[R];
+__device__ __attribute__((always_inline)) inline void bin_rows_c_chk(RV<T, R>& A, T c, typename Chk<T>::type& M) {
+  RV<T, R> B;
   UNR for (int r = 0; r < R; ++r) B[r] = c;
   bin_rows_chk<T, R, SB, SWAP, true>(A, B, M);
 }
@@ -579,7 +585,7 @@ __device__ __attribute__((always_inline)) inline int32_t wave_chk(int32_t v) { r
 // whose fast max|v| bound cannot decide DynamicExpressions' isfinite(sum(array)) checks.
 // One wave owns a (tree, row block), so plain read-modify-write of its slab entry is race-free.
 template <typename T, int R>
-__device__ __attribute__((always_inline)) inline void precise_hook(const EvalArgs& p, uint32_t a, const T (&A)[R],
+__device__ __attribute__((always_inline)) inline void precise_hook(const EvalArgs& p, uint32_t a, const RV<T, R>& A,
                                                                    int ti, int rb, int lane, int64_t row0) {
   if constexpr (!kIsInt<T>) {
     const uint32_t opidx = a >> 16;
@@ -601,10 +607,10 @@ __device__ __attribute__((always_inline)) inline void precise_hook(const EvalArg
 
 // Per-tile loss epilogue for a given loss kind (KIND < 0: runtime kind).
 template <typename T, int R>
-__device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& p, const T (&A)[R], const T* ybase,
+__device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& p, const RV<T, R>& A, const T* ybase,
                                                                 const T* wbase, int lane, int64_t row0,
                                                                 LAccT<T>& lacc) {
-  T yv[R];
+  RV<T, R> yv;
   load_rows<T, R>(ybase, lane, yv);
   constexpr int VEC = 16 / sizeof(T);
   const bool full = row0 + 64 * R <= p.nvalid;  // wave-uniform
@@ -619,14 +625,14 @@ __device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& 
       lacc += c;
     }
   } else {
-    T wv[R];
+    RV<T, R> wv;
     if (p.weighted) load_rows<T, R>(wbase, lane, wv);
     const T p0 = (T)p.loss_p0;
-    T lv[R];
+    RV<T, R> lv;
     if (p.loss_kind == SRHIP_LOSS_L2) {
       UNR for (int r = 0; r < R; ++r) lv[r] = A[r];
       bin_rows<T, R, SB_SUB, false>(lv, yv);
-      T dv[R];
+      RV<T, R> dv;
       UNR for (int r = 0; r < R; ++r) dv[r] = lv[r];
       bin_rows<T, R, SB_MUL, false>(lv, dv);
     } else if (p.loss_kind == SRHIP_LOSS_L1) {
@@ -662,7 +668,7 @@ __device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& 
 }
 
 template <typename T, int R>
-__device__ __attribute__((always_inline)) inline void store_pred(const EvalArgs& p, const T (&A)[R], int tree, int lane,
+__device__ __attribute__((always_inline)) inline void store_pred(const EvalArgs& p, const RV<T, R>& A, int tree, int lane,
                                                                  int64_t row0) {
   constexpr int VEC = 16 / sizeof(T);
   using V = typename Vec16<T>::type;
@@ -760,7 +766,7 @@ __device__ __attribute__((always_inline)) inline void derive_columns_tiles(const
     const int d = item / ntiles, j = item - d * ntiles;
     const uint32_t spec = __builtin_amdgcn_readfirstlane(p.dspec[d]);
     const int u = (int)(spec >> 16), f = (int)(spec & 0xffff);
-    T v[R];
+    RV<T, R> v;
     load_rows<T, R>(lx + (int64_t)f * rbb + (int64_t)j * TILE, lane, v);
     RV<T, R> rv;
     UNR for (int r = 0; r < R; ++r) rv[r] = v[r];
@@ -949,7 +955,9 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
       if (row0 >= p.nvalid) break;  // whole tile is padding
       rows_done += (int)min((int64_t)TILE, p.nvalid - row0);
       const T* xt = xsrc + (int64_t)tile * TILE;
-      T A[R], S[K][R];
+      // (cleared per tile: with the registers left undefined or carried over, the allocator moved the
+      // accumulator off v0-v15, where the out-of-line operator bodies take and return it)
+      RV<T, R> A, S[K];
       UNR for (int r = 0; r < R; ++r) A[r] = T(0);
       UNR for (int k = 0; k < K; ++k) UNR for (int r = 0; r < R; ++r) S[k][r] = T(0);
       // The program is read through the constant address space with a wave-uniform pc, so every
@@ -981,7 +989,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
 #define SRHIP_SPEC_CASE(NAME, FN)                                                                  \
   case h_spec(SB_##NAME, SPEC_AF):                                                                 \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
-      T xv[R];                                                                                     \
+      RV<T, R> xv;                                                                                     \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
       bin_rows_chk<T, R, SB_##NAME, false>(A, xv, M);                                              \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
@@ -989,7 +997,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
     break;                                                                                         \
   case h_spec(SB_##NAME, SPEC_FA):                                                                 \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
-      T xv[R];                                                                                     \
+      RV<T, R> xv;                                                                                     \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
       bin_rows_chk<T, R, SB_##NAME, true>(A, xv, M);                                               \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
