@@ -33,13 +33,19 @@
 #else
 #define KDBG(...) do { } while (0)
 #endif
-// Progress words for SRHIP_TRACE runs: lane 0 of wave 0 of block (0,0) stores (slot, value) to
-// host-coherent memory with system scope, so the host can read them while the kernel runs.
+// Progress words for SRHIP_TRACE runs of SRHIP_KTRACE builds (make EXTRA=-DSRHIP_KTRACE, diagnostic
+// only): lane 0 of wave 0 of block (0,0) stores (slot, value) to host-coherent memory with system
+// scope, so the host can read them while the kernel runs.  Compiled out otherwise: the stores'
+// operands pinned v0-v1 and moved the accumulator off v0-v15 after every tile.
+#ifdef SRHIP_KTRACE
 #define KMARK(slot, val)                                                                       \
   do {                                                                                         \
     if (p.dbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                      \
       __hip_atomic_store(p.dbg + (slot), (int32_t)(val), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
   } while (0)
+#else
+#define KMARK(slot, val) do { } while (0)
+#endif
 #ifndef SRHIP_HEAVY_ILP
 #define SRHIP_HEAVY_ILP 1  // rows a heavy operator body may interleave
 #endif
@@ -481,6 +487,13 @@ __device__ __attribute__((always_inline)) inline void div_rows(RV<float, R>& A, 
 // run on packed row pairs (v_pk_add_f32 / v_pk_mul_f32, div_rows: each lane rounded exactly as
 // the scalar instruction would); the rest row by row.
 typedef F2 PkF32;
+// a - b on a row pair as v_pk_add_f32 with the second operand negated (the same IEEE result,
+// signed zeros included); the compiler otherwise splits a <2 x float> subtraction into two v_sub_f32
+__device__ __attribute__((always_inline)) inline F2 pk_sub(F2 a, F2 b) {
+  F2 c;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(c) : "v"(a), "v"(b));
+  return c;
+}
 #ifndef SRHIP_PK_BINOPS
 #define SRHIP_PK_BINOPS 1
 #endif
@@ -505,7 +518,7 @@ __device__ __attribute__((always_inline)) inline void bin_rows(RV<T, R>& A, cons
       const PkF32 a = {A[r], A[r + 1]}, b = {B[r], B[r + 1]};
       PkF32 c;
       if constexpr (SB == SB_ADD) c = SWAP ? b + a : a + b;
-      else if constexpr (SB == SB_SUB) c = SWAP ? b - a : a - b;
+      else if constexpr (SB == SB_SUB) c = SWAP ? pk_sub(b, a) : pk_sub(a, b);
       else c = SWAP ? b * a : a * b;
       A[r] = c.x;
       A[r + 1] = c.y;
@@ -544,9 +557,13 @@ template <typename T> using LAccT = typename std::conditional<kIsInt<T>, long lo
 // row mirrors, then row_bcast15 / row_bcast31 fold the four rows into lane WAVE_LAST.  Only that
 // lane's result is meaningful; the order is fixed, so results are deterministic.
 constexpr int WAVE_LAST = 63;
+// (v_mov_b32_dpp with an undefined old value: lanes of rows outside ROWS keep whatever the
+// destination held, which only feeds lanes whose results are never read -- lane WAVE_LAST's chain
+// reads row 3's own lanes, lane 47 before the bcast15 step and lane 31 after it; a zero old value
+// cost a v_mov per 32-bit half per step)
 template <int CTRL, int ROWS = 0xf>
 __device__ __attribute__((always_inline)) inline uint32_t dpp32(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, ROWS, 0xf, false);
 }
 template <int CTRL, int ROWS = 0xf, typename U>
 __device__ __attribute__((always_inline)) inline U dpp(U v) {
@@ -605,6 +622,14 @@ __device__ __attribute__((always_inline)) inline void precise_hook(const EvalArg
   }
 }
 
+// The other distance losses, out of line: their bodies call math routines, and inline they made
+// the allocator move the accumulator off the registers the operator bodies use for it.
+template <typename T, int R>
+__device__ __attribute__((noinline)) RV<T, R> loss_rows_generic(int kind, RV<T, R> a, RV<T, R> y, T p0) {
+  UNR for (int r = 0; r < R; ++r) a[r] = loss_elem<T>(kind, a[r] - y[r], p0);
+  return a;
+}
+
 // Per-tile loss epilogue for a given loss kind (KIND < 0: runtime kind).
 template <typename T, int R>
 __device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& p, const RV<T, R>& A, const T* ybase,
@@ -638,7 +663,7 @@ __device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& 
     } else if (p.loss_kind == SRHIP_LOSS_L1) {
       UNR for (int r = 0; r < R; ++r) lv[r] = m_abs(A[r] - yv[r]);
     } else {
-      UNR for (int r = 0; r < R; ++r) lv[r] = loss_elem<T>(p.loss_kind, A[r] - yv[r], p0);
+      lv = loss_rows_generic<T, R>(p.loss_kind, A, yv, p0);
     }
     if (p.weighted) {
       // padded rows carry w = 0 and a replicated (finite when ok) prediction
@@ -652,11 +677,11 @@ __device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& 
       }
       if constexpr (sizeof(T) == 4 && R % 4 == 0 && VEC == 4) {
         // Float32: a lane's 4 consecutive rows (one 16-byte group: the same rows in every launch
-        // geometry) summed in Float32, (l0 + l1) + (l2 + l3) -- one packed add, one add -- then
-        // widened once: relative error <= 2^-23 for the non-negative distance losses, against the
-        // 1e-6 parity bar; one bit pattern per tree and dataset as before
+        // geometry) summed in Float32, (l0 + l2) + (l1 + l3) -- one packed add of the two register
+        // pairs, one add -- then widened once: relative error <= 2^-23 for the non-negative
+        // distance losses, against the 1e-6 parity bar; one bit pattern per tree and dataset
         UNR for (int r = 0; r < R; r += 4) {
-          const F2 a = {lv[r], lv[r + 2]}, b = {lv[r + 1], lv[r + 3]};
+          const F2 a = {lv[r], lv[r + 1]}, b = {lv[r + 2], lv[r + 3]};
           const F2 q = a + b;
           lacc += (double)(q.x + q.y);
         }
