@@ -167,6 +167,12 @@ template <typename T> DI T dloss_elem(int kind, T d, T p0) {
   }
 }
 
+// (loss, d loss / d output) of the other distance losses, out of line: inline, their math bodies
+// raised the kernel's register count for every loss kind
+template <typename T> __device__ __attribute__((noinline)) typename V2<T>::type loss_dloss_generic(int kind, T d, T p0) {
+  return typename V2<T>::type{loss_elem<T>(kind, d, p0), dloss_elem<T>(kind, d, p0)};
+}
+
 // ---- the dual-number interpreter ----------------------------------------------------------------
 template <typename T> DI T imm_bits(uint64_t b) {
   if constexpr (sizeof(T) == 8) return __builtin_bit_cast(T, b);
@@ -355,8 +361,15 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
         const int rr = tb + 64 * r + lane;
         if (row_base + rr < p.nvalid) {
           const T d = A[r].v - yat(rr);
-          T l = loss_elem<T>(p.loss_kind, d, p0);
-          T dl = dloss_elem<T>(p.loss_kind, d, p0);
+          T l, dl;
+          if (p.loss_kind == SRHIP_LOSS_L2) {
+            l = d * d;
+            dl = T(2) * d;
+          } else {
+            const typename V2<T>::type q = loss_dloss_generic<T>(p.loss_kind, d, p0);
+            l = q[0];
+            dl = q[1];
+          }
           if (p.weighted) {
             const T w = W[row_base + rr];
             l = w * l;
