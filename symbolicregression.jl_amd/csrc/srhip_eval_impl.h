@@ -625,14 +625,14 @@ __device__ __attribute__((always_inline)) inline void precise_hook(const EvalArg
 // The other distance losses, out of line: their bodies call math routines, and inline they made
 // the allocator move the accumulator off the registers the operator bodies use for it.
 template <typename T, int R>
-__device__ __attribute__((noinline)) RV<T, R> loss_rows_generic(int kind, RV<T, R> a, RV<T, R> y, T p0) {
+__device__ __attribute__((noinline)) RV<T, R> loss_rows_generic(RV<T, R> a, RV<T, R> y, int kind, T p0) {
   UNR for (int r = 0; r < R; ++r) a[r] = loss_elem<T>(kind, a[r] - y[r], p0);
   return a;
 }
 
 // Per-tile loss epilogue for a given loss kind (KIND < 0: runtime kind).
 template <typename T, int R>
-__device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& p, const RV<T, R>& A, const T* ybase,
+__device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& p, RV<T, R>& A, const T* ybase,
                                                                 const T* wbase, int lane, int64_t row0,
                                                                 LAccT<T>& lacc) {
   RV<T, R> yv;
@@ -653,9 +653,9 @@ __device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& 
     RV<T, R> wv;
     if (p.weighted) load_rows<T, R>(wbase, lane, wv);
     const T p0 = (T)p.loss_p0;
-    RV<T, R> lv;
+    // (A is dead after the epilogue -- the next tile clears it -- so the residual overwrites it in place)
+    RV<T, R>& lv = A;
     if (p.loss_kind == SRHIP_LOSS_L2) {
-      UNR for (int r = 0; r < R; ++r) lv[r] = A[r];
       bin_rows<T, R, SB_SUB, false>(lv, yv);
       RV<T, R> dv;
       UNR for (int r = 0; r < R; ++r) dv[r] = lv[r];
@@ -663,7 +663,7 @@ __device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& 
     } else if (p.loss_kind == SRHIP_LOSS_L1) {
       UNR for (int r = 0; r < R; ++r) lv[r] = m_abs(A[r] - yv[r]);
     } else {
-      lv = loss_rows_generic<T, R>(p.loss_kind, A, yv, p0);
+      lv = loss_rows_generic<T, R>(A, yv, p.loss_kind, p0);  // (A first: it stays in v0-v15)
     }
     if (p.weighted) {
       // padded rows carry w = 0 and a replicated (finite when ok) prediction
