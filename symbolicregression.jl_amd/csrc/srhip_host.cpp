@@ -21,7 +21,10 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <memory>
 #include <numeric>
 #include <string>
@@ -103,6 +106,12 @@ template <typename T> class TreeCompiler {
   // depth-first left-to-right) in the instruction's operand field.
   TreeCompiler(const srhip_node* nodes, int64_t nn, const srhip_program& prog, int nfeat_hint, bool grad = false)
       : nd_(nodes), nn_(nn), prog_(prog), nfeat_hint_(nfeat_hint), grad_(grad) {}
+  // point a compiler (and its scratch vectors' capacity) at another tree
+  void rebind(const srhip_node* nodes, int64_t nn) {
+    nd_ = nodes;
+    nn_ = nn;
+    dmask_ = 0;
+  }
 
   // returns SRHIP_OK or an error (g_err set); fills info and appends to code
   int compile(TreeInfo& info, std::vector<Ins>& code) {
@@ -491,45 +500,102 @@ template <typename T> class TreeCompiler {
   }
 };
 
-// Derived-column program (srhip_isa.h): count the heavy U(X[f]) nodes reachable in the live trees,
-// keep the pairs used at least DERIVE_MIN_USES times (most used first, at most DERIVE_MAX) and
-// compile every tree again with those nodes as column reads.  SRHIP_NO_DERIVE=1 disables it.
+// Host worker threads for the compiler: created once per process (a fork child makes its own) and
+// parked on a condition variable between jobs, so a population compile pays no thread start-up.
+// One job at a time; a caller that finds the pool busy (concurrent coalescer flushes) runs its items
+// itself.  The pool object is never destroyed: detached workers parked at exit are simply ended.
+class HostPool {
+ public:
+  static HostPool& get() {
+    static std::mutex m;
+    static HostPool* pool = nullptr;
+    std::lock_guard<std::mutex> g(m);
+    if (!pool || pool->pid_ != getpid()) pool = new HostPool();
+    return *pool;
+  }
+  int threads() const { return (int)nthr_ + 1; }
+  // fn(0) .. fn(n - 1) on the pool's threads and the caller; false (nothing run) if busy
+  bool run(int n, const std::function<void(int)>& fn) {
+    std::unique_lock<std::mutex> busy(busy_mu_, std::try_to_lock);
+    if (!busy.owns_lock()) return false;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      fn_ = &fn;
+      n_ = n;
+      next_.store(0);
+      done_ = 0;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_done_.wait(lk, [&] { return done_ == n_; });
+    fn_ = nullptr;
+    return true;
+  }
+
+ private:
+  HostPool() : pid_(getpid()) {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    nthr_ = std::min(7u, hw - 1);
+    for (unsigned i = 0; i < nthr_; ++i) std::thread([this] { loop(); }).detach();
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  void work() {
+    for (;;) {
+      const int i = next_.fetch_add(1);
+      if (i >= n_) return;
+      (*fn_)(i);
+      std::lock_guard<std::mutex> g(mu_);
+      if (++done_ == n_) cv_done_.notify_all();
+    }
+  }
+  const pid_t pid_;
+  unsigned nthr_ = 0;
+  std::mutex busy_mu_, mu_;
+  std::condition_variable cv_, cv_done_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int n_ = 0, done_ = 0;
+  std::atomic<int> next_{0};
+  uint64_t gen_ = 0;
+};
+
+// The population's programs in one pass over the trees: the plain program and, when the population
+// has derived columns (srhip_isa.h), the derived program, compiled tree by tree on the host pool
+// (contiguous tree ranges; per-range code vectors concatenated in tree order: the same bytes as one
+// sequential pass).  Derived columns: the heavy U(X[f]) nodes of the population's trees are counted
+// first, the pairs used at least DERIVE_MIN_USES times kept (most used first, at most DERIVE_MAX).
+// SRHIP_NO_DERIVE=1 disables them.
 template <typename T>
-int compile_derived_t(srhip_program& P) {
+void choose_derived_t(srhip_program& P) {
   P.dspec.clear();
-  P.dmask.assign(P.ntrees, 0);
-  P.dcode.clear();
-  P.dprog_off.assign(P.ntrees, 0);
-  P.dcost.assign(P.ntrees, 0.0);
-  P.dkmax = P.dmax_len = 0;
   const char* env = getenv("SRHIP_NO_DERIVE");
   const bool off = env && *env && *env != '0';
-  if (std::is_same<T, int32_t>::value || off) return SRHIP_OK;
+  if (std::is_same<T, int32_t>::value || off) return;
   std::vector<std::pair<uint32_t, int>> cnt;  // (key, uses)
-  std::vector<int64_t> stack;
-  for (int32_t t = 0; t < P.ntrees; ++t) {
-    if (P.info[t].static_fail) continue;
-    const srhip_node* nd = P.nodes.data() + P.offsets[t];
-    stack.assign(1, 0);
-    while (!stack.empty()) {
-      const int64_t i = stack.back();
-      stack.pop_back();
-      const srhip_node& n = nd[i];
-      if (n.degree == 0) continue;
-      stack.push_back(n.l);
-      if (n.degree == 2) {
-        stack.push_back(n.r);
-        continue;
-      }
-      const srhip_node& c = nd[n.l];
-      if (c.degree != 0 || c.constant) continue;
-      const int u = classify_unop(P.unaops[n.op - 1]);
-      if (!un_derivable(u)) continue;
-      const uint32_t key = ((uint32_t)u << 16) | (uint32_t)(c.feature - 1);
-      auto it = std::find_if(cnt.begin(), cnt.end(), [&](const std::pair<uint32_t, int>& e) { return e.first == key; });
-      if (it == cnt.end()) cnt.emplace_back(key, 1);
-      else ++it->second;
-    }
+  for (int64_t i = 0; i < (int64_t)P.nodes.size(); ++i) {
+    const srhip_node& n = P.nodes[i];
+    if (n.degree != 1) continue;
+    // node tables are per tree with tree-relative child indices: find the child in this tree
+    const int32_t t = (int32_t)(std::upper_bound(P.offsets.begin(), P.offsets.end(), i) - P.offsets.begin()) - 1;
+    const srhip_node& c = P.nodes[P.offsets[t] + n.l];
+    if (c.degree != 0 || c.constant) continue;
+    const int u = classify_unop(P.unaops[n.op - 1]);
+    if (!un_derivable(u)) continue;
+    const uint32_t key = ((uint32_t)u << 16) | (uint32_t)(c.feature - 1);
+    auto it = std::find_if(cnt.begin(), cnt.end(), [&](const std::pair<uint32_t, int>& e) { return e.first == key; });
+    if (it == cnt.end()) cnt.emplace_back(key, 1);
+    else ++it->second;
   }
   std::stable_sort(cnt.begin(), cnt.end(), [](const std::pair<uint32_t, int>& a, const std::pair<uint32_t, int>& b) {
     return a.second > b.second;
@@ -538,94 +604,86 @@ int compile_derived_t(srhip_program& P) {
   const int dmax = dmax_env >= 0 ? std::min(dmax_env, DERIVE_MAX) : DERIVE_MAX;
   for (const auto& e : cnt)
     if (e.second >= DERIVE_MIN_USES && (int)P.dspec.size() < dmax) P.dspec.push_back(e.first);
-  if (P.dspec.empty()) return SRHIP_OK;
-  std::vector<TreeInfo> dinfo(P.ntrees);
-  const int rc = compile_trees<T>(P, P.dcode, dinfo, " (derived program)", [&](int32_t t, TreeCompiler<T>& tc) {
-    if (t >= 0) tc.set_derived(&P.dspec, P.maxfeat);
-    else P.dmask[-1 - t] = tc.dmask();
-  });
-  if (rc) return rc;
-  for (int32_t t = 0; t < P.ntrees; ++t) {
-    const TreeInfo& ti = dinfo[t];
-    P.dprog_off[t] = ti.code_begin;
-    P.dcost[t] = ti.cost;
-    P.dkmax = std::max(P.dkmax, ti.need);
-    P.dmax_len = std::max(P.dmax_len, ti.code_len);
-  }
-  return SRHIP_OK;
-}
-
-// Compile trees [0, P.ntrees) into `code` / `info` (code_begin absolute), `body(t, tc)` configuring
-// each TreeCompiler; large populations are split into contiguous ranges compiled on worker threads
-// (per-thread code vectors concatenated in tree order: the same bytes as one sequential pass).
-template <typename T, typename Setup>
-int compile_trees(srhip_program& P, std::vector<Ins>& code, std::vector<TreeInfo>& info, const char* what, Setup setup) {
-  const int32_t n = P.ntrees;
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const int W = (int)std::min<int64_t>({(int64_t)8, (int64_t)hw, (int64_t)n / 128});
-  auto run = [&](int32_t t0, int32_t t1, std::vector<Ins>& out, std::string& err) -> int {
-    for (int32_t t = t0; t < t1; ++t) {
-      const int64_t b = P.offsets[t], e = P.offsets[t + 1];
-      TreeCompiler<T> tc(P.nodes.data() + b, e - b, P, 0);
-      setup(t, tc);
-      const int rc = tc.compile(info[t], out);
-      if (rc) {
-        err = "tree " + std::to_string(t) + what + ": " + g_err;
-        return rc;
-      }
-      setup(-1 - t, tc);  // after-compile hook (derived masks)
-    }
-    return SRHIP_OK;
-  };
-  if (W <= 1) {
-    std::string err;
-    const int rc = run(0, n, code, err);
-    return rc ? fail(rc, "%s", err.c_str()) : SRHIP_OK;
-  }
-  std::vector<std::vector<Ins>> part(W);
-  std::vector<std::string> errs(W);
-  std::vector<int> rcs(W, SRHIP_OK);
-  std::vector<std::thread> th;
-  for (int w = 0; w < W; ++w)
-    th.emplace_back([&, w] { rcs[w] = run((int32_t)((int64_t)n * w / W), (int32_t)((int64_t)n * (w + 1) / W), part[w], errs[w]); });
-  for (auto& x : th) x.join();
-  for (int w = 0; w < W; ++w)
-    if (rcs[w]) return fail(rcs[w], "%s", errs[w].c_str());
-  for (int w = 0; w < W; ++w) {
-    const int32_t base = (int32_t)code.size();
-    for (int32_t t = (int32_t)((int64_t)n * w / W); t < (int32_t)((int64_t)n * (w + 1) / W); ++t) info[t].code_begin += base;
-    code.insert(code.end(), part[w].begin(), part[w].end());
-  }
-  return SRHIP_OK;
 }
 
 template <typename T>
 int compile_program_t(srhip_program& P) {
+  const int32_t n = P.ntrees;
   P.code.clear();
-  P.prog_off.assign(P.ntrees, 0);
-  P.info.assign(P.ntrees, TreeInfo());
+  P.prog_off.assign(n, 0);
+  P.info.assign(n, TreeInfo());
   P.kmax = 0;
   P.max_ops = 0;
   P.max_len = 0;
   P.total_nodes = 0;
   P.total_ops = 0;
-  const int rc = compile_trees<T>(P, P.code, P.info, "", [](int32_t, TreeCompiler<T>&) {});
-  if (rc) return rc;
-  for (int32_t t = 0; t < P.ntrees; ++t) {
+  P.dmask.assign(n, 0);
+  P.dcode.clear();
+  P.dprog_off.assign(n, 0);
+  P.dcost.assign(n, 0.0);
+  P.dkmax = P.dmax_len = 0;
+  // operator-node count and the largest feature index, from the node tables
+  P.maxfeat = 0;
+  for (const srhip_node& nd : P.nodes) {
+    P.total_ops += nd.degree > 0;
+    if (nd.degree == 0 && !nd.constant) P.maxfeat = std::max<int32_t>(P.maxfeat, nd.feature);
+  }
+  choose_derived_t<T>(P);
+  const bool der = !P.dspec.empty();
+  std::vector<TreeInfo> dinfo(der ? n : 0);
+  HostPool& pool = HostPool::get();
+  const int W = (int)std::max<int64_t>(1, std::min<int64_t>(pool.threads(), (int64_t)n / 64));
+  std::vector<std::vector<Ins>> part(W), dpart(W);
+  std::vector<std::string> errs(W);
+  std::vector<int> rcs(W, SRHIP_OK);
+  const std::function<void(int)> range = [&](int w) {
+    const int32_t t0 = (int32_t)((int64_t)n * w / W), t1 = (int32_t)((int64_t)n * (w + 1) / W);
+    TreeCompiler<T> tc(nullptr, 0, P, 0);
+    for (int32_t t = t0; t < t1 && !rcs[w]; ++t) {
+      const int64_t b = P.offsets[t], e = P.offsets[t + 1];
+      tc.rebind(P.nodes.data() + b, e - b);
+      tc.set_derived(nullptr, 0);
+      int rc = tc.compile(P.info[t], part[w]);
+      if (!rc && der) {
+        tc.set_derived(&P.dspec, P.maxfeat);
+        rc = tc.compile(dinfo[t], dpart[w]);
+        P.dmask[t] = tc.dmask();
+      }
+      if (rc) {
+        errs[w] = "tree " + std::to_string(t) + ": " + g_err;
+        rcs[w] = rc;
+      }
+    }
+  };
+  if (W == 1 || !pool.run(W, range))
+    for (int w = 0; w < W; ++w) range(w);
+  for (int w = 0; w < W; ++w)
+    if (rcs[w]) return fail(rcs[w], "%s", errs[w].c_str());
+  for (int w = 0; w < W; ++w) {
+    const int32_t t0 = (int32_t)((int64_t)n * w / W), t1 = (int32_t)((int64_t)n * (w + 1) / W);
+    const int32_t base = (int32_t)P.code.size(), dbase = (int32_t)P.dcode.size();
+    for (int32_t t = t0; t < t1; ++t) {
+      P.info[t].code_begin += base;
+      if (der) dinfo[t].code_begin += dbase;
+    }
+    P.code.insert(P.code.end(), part[w].begin(), part[w].end());
+    if (der) P.dcode.insert(P.dcode.end(), dpart[w].begin(), dpart[w].end());
+  }
+  for (int32_t t = 0; t < n; ++t) {
     P.prog_off[t] = P.info[t].code_begin;
     P.kmax = std::max(P.kmax, P.info[t].need);
     P.max_ops = std::max(P.max_ops, (int32_t)P.info[t].op_sumcheck.size());
     P.max_len = std::max(P.max_len, P.info[t].code_len);
     P.total_nodes += P.info[t].nnodes;
-  }
-  // operator-node count (degree >= 1), from the node tables
-  P.maxfeat = 0;
-  for (int32_t t = 0; t < P.ntrees; ++t)
-    for (int64_t i = P.offsets[t]; i < P.offsets[t + 1]; ++i) {
-      P.total_ops += P.nodes[i].degree > 0;
-      if (P.nodes[i].degree == 0 && !P.nodes[i].constant) P.maxfeat = std::max<int32_t>(P.maxfeat, P.nodes[i].feature);
+    if (der) {
+      const TreeInfo& ti = dinfo[t];
+      P.dprog_off[t] = ti.code_begin;
+      P.dcost[t] = ti.cost;
+      P.dkmax = std::max(P.dkmax, ti.need);
+      P.dmax_len = std::max(P.dmax_len, ti.code_len);
     }
-  return compile_derived_t<T>(P);
+  }
+  return SRHIP_OK;
 }
 
 template <typename T>
