@@ -633,12 +633,12 @@ __device__ __attribute__((noinline)) RV<T, R> loss_rows_generic(RV<T, R> a, RV<T
 // Per-tile loss epilogue for a given loss kind (KIND < 0: runtime kind).
 template <typename T, int R>
 __device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& p, RV<T, R>& A, const T* ybase,
-                                                                const T* wbase, int lane, int64_t row0,
+                                                                const T* wbase, int lane, int64_t row0, bool full,
                                                                 LAccT<T>& lacc) {
+  // full: every row of the tile is valid (wave-uniform)
   RV<T, R> yv;
   load_rows<T, R>(ybase, lane, yv);
   constexpr int VEC = 16 / sizeof(T);
-  const bool full = row0 + 64 * R <= p.nvalid;  // wave-uniform
   if constexpr (kIsInt<T>) {
     UNR for (int r = 0; r < R; ++r) {
       int32_t l = loss_elem_int(p.loss_kind, IOps::sub(A[r], yv[r]));
@@ -846,6 +846,10 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
   const int lane = threadIdx.x & 63;
   const int64_t row_base = (int64_t)rb * p.rb_rows;
   const int ntiles = p.rb_rows / TILE;
+  // valid rows of this block, block-relative (<= rb_rows): the tile loop's uniform row tests are
+  // 32-bit scalar compares (a 64-bit ordering compare has no scalar form and made them VALU
+  // compares, i.e. a divergent loop)
+  const int nrel = __builtin_amdgcn_readfirstlane((int)min<int64_t>(max<int64_t>(p.nvalid - row_base, 0), (int64_t)p.rb_rows));
 
   // ---- stage this block's rows of X (and y, w) into LDS ----
   const T* xsrc;
@@ -977,8 +981,9 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
     }
     for (int tile = tile0; tile < (failed ? tile0 : tile_end); ++tile) {
       const int64_t row0 = row_base + (int64_t)tile * TILE;
-      if (row0 >= p.nvalid) break;  // whole tile is padding
-      rows_done += (int)min((int64_t)TILE, p.nvalid - row0);
+      const int trel = tile * TILE;
+      if (trel >= nrel) break;  // whole tile is padding
+      rows_done += min(TILE, nrel - trel);
       const T* xt = xsrc + (int64_t)tile * TILE;
       // (cleared per tile: with the registers left undefined or carried over, the allocator moved the
       // accumulator off v0-v15, where the out-of-line operator bodies take and return it)
@@ -1094,10 +1099,11 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
       KDBG("[k]   tile %d done\n", tile);
       KMARK(0, 4);
       if constexpr (MODE == MODE_LOSS) {
-        loss_tile<T, R>(p, A, ysrc + (int64_t)tile * TILE, wsrc + (int64_t)tile * TILE, lane, row0, lacc);
+        loss_tile<T, R>(p, A, ysrc + (int64_t)tile * TILE, wsrc + (int64_t)tile * TILE, lane, row0, trel + TILE <= nrel,
+                        lacc);
         constexpr int CH = sizeof(T) == 8 ? LOSS_CHUNK_8B : LOSS_CHUNK_4B;
         static_assert(CH % TILE == 0, "a loss chunk is whole tiles");
-        const bool flushed = (tile + 1) % (CH / TILE) == 0 || row0 + TILE >= p.nvalid;
+        const bool flushed = (tile + 1) % (CH / TILE) == 0 || trel + TILE >= nrel;
         if (flushed) {  // chunk done (or last valid tile)
           const LAccT<T> s = wave_sum(lacc);
           const int ci = tile / (CH / TILE);
