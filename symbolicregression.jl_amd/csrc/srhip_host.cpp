@@ -957,11 +957,14 @@ int srhip::compile_grad_program(srhip_program& P) {
   if (patched) {  // the device copy differs only in [lo, hi); the snapshot was updated by the patch
     const double t_copy0 = host_now_s();
     HIP_TRY(hipSetDevice(P.ctx->device));
-    if (hi > lo)
-      HIP_TRY(hipMemcpyAsync((Ins*)P.d_gcode.p + lo, P.gcode.data() + lo, (size_t)(hi - lo) * sizeof(Ins),
-                             hipMemcpyHostToDevice, P.ctx->stream));
+    if (hi > lo) {  // through pinned staging: a pageable source makes the runtime stage it synchronously
+      const size_t nb = (size_t)(hi - lo) * sizeof(Ins);
+      HIP_TRY(P.ctx->h_gpatch.ensure(nb));
+      memcpy(P.ctx->h_gpatch.p, P.gcode.data() + lo, nb);
+      HIP_TRY(hipMemcpyAsync((Ins*)P.d_gcode.p + lo, P.ctx->h_gpatch.p, nb, hipMemcpyHostToDevice, P.ctx->stream));
+    }
     // no synchronisation here: the gradient launch follows on the same stream, and eval_grad
-    // synchronises before it returns, so gcode is not touched while this copy is in flight
+    // synchronises before it returns, so the staging is not touched while this copy is in flight
     g_patch_copy_s += host_now_s() - t_copy0;
     P.grad_ready = true;
     return SRHIP_OK;
@@ -1777,6 +1780,8 @@ int srhip_ctx_create(int device, srhip_ctx** out) {
 
 void srhip_ctx_destroy(srhip_ctx* ctx) {
   if (!ctx) return;
+  srhip_ctx_destroy(ctx->aux);
+  ctx->aux = nullptr;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);

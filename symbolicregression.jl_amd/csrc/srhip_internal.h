@@ -123,6 +123,8 @@ struct srhip_ctx {
   srhip::DevBuf slab_loss, slab_chk, slab_prec, order_prec;
   srhip::DevBuf vX, vy, vw, vidx, vstats;  // gathered views (batching idx)
   srhip::DevBuf g_chunks, g_slab, g_red;   // constant-gradient launches
+  srhip::HostBuf h_gchunks[2], h_gred[2];   // their pinned staging, per pass (gradient, value-only)
+  srhip::HostBuf h_gpatch, h_gspec;         // pinned staging of patched / speculative gradient code
   srhip::HostBuf h_loss, h_chk, h_stats, h_prec, h_dbg;
   srhip::DevBuf fail_flag;  // [order slots] int32: launch epoch in which the tree was seen to fail
   int32_t epoch = 0;        // interpreter launches so far (MODE_LOSS with early exit)
@@ -133,6 +135,10 @@ struct srhip_ctx {
   // evaluated node-rows, nominal node-rows (every live tree on every row), evaluated operator-node
   // rows, evaluated tree-rows
   int64_t work[4] = {0, 0, 0, 0};
+  // a second context on the same device (own stream and buffers), created on first use by the
+  // constant optimiser, which runs half of the population on it from a second host thread
+  srhip_ctx* aux = nullptr;
+  std::mutex aux_mu;
 };
 
 struct srhip_dataset {

@@ -18,6 +18,7 @@
 #include <chrono>
 #include <cstdio>
 #include <random>
+#include <thread>
 #include <vector>
 
 #include "srhip_grad.h"
@@ -129,9 +130,12 @@ static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, 
     items.push_back(GradItem{t, t, f + t, g + coff[t], ok ? ok + t : nullptr, value_only && value_only[t]});
   if (extra) items.insert(items.end(), extra->begin(), extra->end());
   auto body = [&]() -> int {
-    if (spec_hi > spec_lo)
-      HIP_TRY(hipMemcpyAsync((Ins*)P->d_gcode.p + spec_lo, P->gcode.data() + spec_lo,
-                             (size_t)(spec_hi - spec_lo) * sizeof(Ins), hipMemcpyHostToDevice, ctx->stream));
+    if (spec_hi > spec_lo) {  // pinned staging (synchronised with the launch in eval_grad_items)
+      const size_t nb = (size_t)(spec_hi - spec_lo) * sizeof(Ins);
+      HIP_TRY(ctx->h_gspec.ensure(nb));
+      memcpy(ctx->h_gspec.p, P->gcode.data() + spec_lo, nb);
+      HIP_TRY(hipMemcpyAsync((Ins*)P->d_gcode.p + spec_lo, ctx->h_gspec.p, nb, hipMemcpyHostToDevice, ctx->stream));
+    }
     return eval_grad_items(ctx, ds, P, loss, v, items);
   };
   rc = body();
@@ -164,7 +168,7 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
   struct Pass {
     int kt;
     std::vector<int32_t> chunks, chunk_item;
-    std::vector<double> red;
+    const double* red = nullptr;  // the reduced records, in the context's pinned staging
     LaunchPlan L;
   } pass[2];
   pass[0].kt = kt;
@@ -205,11 +209,17 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
   HIP_TRY(ctx->g_red.ensure(red_n * sizeof(double)));
   const int K = P->gkmax <= 2 ? 2 : (P->gkmax <= 4 ? 4 : 8);  // stack slots of the kernel variant
   bool first = true;
-  for (Pass& ps : pass) {
+  for (int pi = 0; pi < 2; ++pi) {
+    Pass& ps = pass[pi];
     const int nch = (int)ps.chunks.size() / 2;
     if (nch == 0) continue;
-    // stream order: this copy follows the previous pass's kernel, which has read its chunk list
-    HIP_TRY(hipMemcpyAsync(ctx->g_chunks.p, ps.chunks.data(), ps.chunks.size() * sizeof(int32_t),
+    // pinned staging both ways (a pageable source or destination makes the runtime stage the copy
+    // through its own buffer, synchronously); stream order: this copy follows the previous pass's
+    // kernel, which has read its chunk list
+    HIP_TRY(ctx->h_gchunks[pi].ensure(ps.chunks.size() * sizeof(int32_t)));
+    HIP_TRY(ctx->h_gred[pi].ensure((size_t)nch * (ps.kt + 2) * sizeof(double)));
+    memcpy(ctx->h_gchunks[pi].p, ps.chunks.data(), ps.chunks.size() * sizeof(int32_t));
+    HIP_TRY(hipMemcpyAsync(ctx->g_chunks.p, ctx->h_gchunks[pi].p, ps.chunks.size() * sizeof(int32_t),
                            hipMemcpyHostToDevice, ctx->stream));
     GradArgs a{};
     a.code = (const Ins*)P->d_gcode.p;
@@ -235,9 +245,9 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     HIP_TRY(launch_grad(dtype, K, ps.kt, a, dim3(ps.L.nrb, ps.L.groups), ctx->stream));
     HIP_TRY(launch_grad_reduce(dtype, ps.kt, (const double*)ctx->g_slab.p, ps.L.nrb, nch, (double*)ctx->g_red.p,
                                ctx->stream));
-    ps.red.resize((size_t)nch * (ps.kt + 2));
-    HIP_TRY(hipMemcpyAsync(ps.red.data(), ctx->g_red.p, ps.red.size() * sizeof(double), hipMemcpyDeviceToHost,
-                           ctx->stream));
+    ps.red = (const double*)ctx->h_gred[pi].p;
+    HIP_TRY(hipMemcpyAsync(ctx->h_gred[pi].p, ctx->g_red.p, (size_t)nch * (ps.kt + 2) * sizeof(double),
+                           hipMemcpyDeviceToHost, ctx->stream));
   }
   HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
   ctx->timed = true;
@@ -255,7 +265,7 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     for (int c = 0; c < nch; ++c) {
       const GradItem& it = items[ps.chunk_item[c]];
       const int32_t c0 = ps.chunks[2 * c + 1];
-      const double* r = ps.red.data() + (size_t)c * (ps.kt + 2);
+      const double* r = ps.red + (size_t)c * (ps.kt + 2);
       const int nc = P->info[it.tree].nconst;
       for (int j = 0; j < ps.kt && c0 + j < nc; ++j) it.g[c0 + j] = r[1 + j] / wsum;
       if (c0 == 0) {
@@ -856,6 +866,87 @@ int srhip_eval_grad_predict(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progr
   return SRHIP_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+srhip_ctx* aux_ctx(srhip_ctx* ctx) {
+  std::lock_guard<std::mutex> g(ctx->aux_mu);
+  if (!ctx->aux) {
+    srhip_ctx* a = nullptr;
+    if (srhip_ctx_create(ctx->device, &a) == SRHIP_OK) ctx->aux = a;
+  }
+  return ctx->aux;
+}
+
+// bfgs_pipelined over two halves of the trees at once: the odd-position trees as a program of their
+// own on the context's auxiliary context (own stream and buffers), optimised from a second host
+// thread, the rest on the caller's thread.  Each launch's host turnaround (decisions, constant
+// patches, synchronisation) then overlaps the other half's kernels.  A tree's trajectory does not
+// depend on the trees that share its launches (fixed row blocks, fixed reduction order), so the
+// outcome is the one bfgs_pipelined gives over all trees at once.  SRHIP_OPTIM_SPLIT=0 disables it.
+int optimize_split(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss, const View& v,
+                   const std::vector<int32_t>& trees, const std::vector<int64_t>& coff, int iterations, double g_tol,
+                   const std::vector<std::vector<double>>& starts, std::vector<double>& best_x,
+                   std::vector<double>& best_f, std::vector<int64_t>& fcalls) {
+  const char* se = getenv("SRHIP_OPTIM_SPLIT");
+  const bool split = !(se && *se == '0') && trees.size() >= 64;
+  srhip_ctx* ctx2 = split ? aux_ctx(ctx) : nullptr;
+  if (!ctx2) return bfgs_pipelined(ctx, ds, P, loss, v, trees, coff, iterations, g_tol, starts, best_x, best_f, fcalls);
+  std::vector<int32_t> ta, tb;
+  for (size_t i = 0; i < trees.size(); ++i) (i % 2 ? tb : ta).push_back(trees[i]);
+  std::vector<srhip_node> nodes2;
+  std::vector<int64_t> offs2(1, 0);
+  for (int32_t t : tb) {
+    nodes2.insert(nodes2.end(), P->nodes.begin() + P->offsets[t], P->nodes.begin() + P->offsets[t + 1]);
+    offs2.push_back((int64_t)nodes2.size());
+  }
+  const srhip_operators ops{(int32_t)P->binops.size(), (int32_t)P->unaops.size(), P->binops.data(),
+                            P->unaops.data()};
+  const int32_t n2 = (int32_t)tb.size();
+  srhip_program* P2 = nullptr;
+  int rc = srhip_program_create(ctx2, P->dtype, nodes2.data(), offs2.data(), n2, &ops, &P2);
+  if (rc) return rc;
+  std::unique_ptr<srhip_program, void (*)(srhip_program*)> hold(P2, srhip_program_destroy);
+  const std::vector<int64_t> coff2 = const_offsets(*P2);
+  std::vector<std::vector<double>> starts2(starts.size(), std::vector<double>(coff2.back()));
+  std::vector<double> bx2(coff2.back()), bf2(n2);
+  std::vector<int64_t> fc2(n2);
+  for (int32_t j = 0; j < n2; ++j) {
+    const int32_t t = tb[j];
+    for (int64_t k = 0; k < coff2[j + 1] - coff2[j]; ++k) {
+      for (size_t s = 0; s < starts.size(); ++s) starts2[s][coff2[j] + k] = starts[s][coff[t] + k];
+      bx2[coff2[j] + k] = best_x[coff[t] + k];
+    }
+    bf2[j] = best_f[t];
+    fc2[j] = fcalls[t];
+  }
+  std::vector<int32_t> all2(n2);
+  for (int32_t j = 0; j < n2; ++j) all2[j] = j;
+  int rc2 = SRHIP_OK;
+  std::string err2;
+  std::thread th([&] {
+    (void)hipSetDevice(ctx2->device);
+    rc2 = bfgs_pipelined(ctx2, ds, P2, loss, v, all2, coff2, iterations, g_tol, starts2, bx2, bf2, fc2);
+    if (rc2) err2 = last_error();
+  });
+  rc = bfgs_pipelined(ctx, ds, P, loss, v, ta, coff, iterations, g_tol, starts, best_x, best_f, fcalls);
+  th.join();
+  if (rc) return rc;
+  if (rc2) return fail(rc2, "%s", err2.c_str());
+  for (int32_t j = 0; j < n2; ++j) {
+    const int32_t t = tb[j];
+    for (int64_t k = 0; k < coff2[j + 1] - coff2[j]; ++k) best_x[coff[t] + k] = bx2[coff2[j] + k];
+    best_f[t] = bf2[j];
+    fcalls[t] = fc2[j];
+  }
+  return SRHIP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
                              const int64_t* idx, int64_t nidx, const srhip_optim_options* opt, double* out_loss,
                              uint8_t* out_improved, int64_t* out_fcalls) {
@@ -904,7 +995,7 @@ int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_prog
     for (int64_t& h : g_hist) h = 0;
     g_nonfinite_trials = 0;
     g_spec_launched = g_spec_used = 0;
-    rc = bfgs_pipelined(ctx, ds, P, loss, v, trees, coff, opt->iterations, g_tol, starts, best_x, best_f, fcalls);
+    rc = optimize_split(ctx, ds, P, loss, v, trees, coff, opt->iterations, g_tol, starts, best_x, best_f, fcalls);
     if (g_stats_on)
       fprintf(stderr, "srhip optim: launches by active trees: 1: %lld, 2-4: %lld, 5-16: %lld, 17-64: %lld, >64: %lld; "
               "non-finite trial points %lld; speculative points %lld evaluated, %lld used\n", (long long)g_hist[0],
