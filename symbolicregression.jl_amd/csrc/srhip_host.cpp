@@ -1780,8 +1780,8 @@ int srhip_ctx_create(int device, srhip_ctx** out) {
 
 void srhip_ctx_destroy(srhip_ctx* ctx) {
   if (!ctx) return;
-  srhip_ctx_destroy(ctx->aux);
-  ctx->aux = nullptr;
+  for (srhip_ctx* a : ctx->aux) srhip_ctx_destroy(a);
+  ctx->aux.clear();
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);

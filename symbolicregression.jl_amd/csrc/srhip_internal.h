@@ -137,7 +137,7 @@ struct srhip_ctx {
   int64_t work[4] = {0, 0, 0, 0};
   // a second context on the same device (own stream and buffers), created on first use by the
   // constant optimiser, which runs half of the population on it from a second host thread
-  srhip_ctx* aux = nullptr;
+  std::vector<srhip_ctx*> aux;
   std::mutex aux_mu;
 };
 

@@ -870,75 +870,100 @@ int srhip_eval_grad_predict(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progr
 
 namespace {
 
-srhip_ctx* aux_ctx(srhip_ctx* ctx) {
+// the context's first n auxiliary contexts (created on first use), or fewer if creation fails
+std::vector<srhip_ctx*> aux_ctxs(srhip_ctx* ctx, int n) {
   std::lock_guard<std::mutex> g(ctx->aux_mu);
-  if (!ctx->aux) {
+  while ((int)ctx->aux.size() < n) {
     srhip_ctx* a = nullptr;
-    if (srhip_ctx_create(ctx->device, &a) == SRHIP_OK) ctx->aux = a;
+    if (srhip_ctx_create(ctx->device, &a) != SRHIP_OK) break;
+    ctx->aux.push_back(a);
   }
-  return ctx->aux;
+  return std::vector<srhip_ctx*>(ctx->aux.begin(), ctx->aux.begin() + std::min<size_t>(n, ctx->aux.size()));
 }
 
-// bfgs_pipelined over two halves of the trees at once: the odd-position trees as a program of their
-// own on the context's auxiliary context (own stream and buffers), optimised from a second host
-// thread, the rest on the caller's thread.  Each launch's host turnaround (decisions, constant
-// patches, synchronisation) then overlaps the other half's kernels.  A tree's trajectory does not
-// depend on the trees that share its launches (fixed row blocks, fixed reduction order), so the
-// outcome is the one bfgs_pipelined gives over all trees at once.  SRHIP_OPTIM_SPLIT=0 disables it.
+// bfgs_pipelined over G groups of the trees at once (G = SRHIP_OPTIM_SPLIT, default 2; 1 = off;
+// populations of fewer than 64 trees are not split): tree i goes to group i % G; group 0 runs on the
+// caller's thread and context, group g > 0 as a program of its own on the context's auxiliary
+// context g - 1 (own stream and buffers) from a host thread of its own.  Each launch's host
+// turnaround (decisions, constant patches, synchronisation) then overlaps the other groups' kernels.
+// A tree's trajectory does not depend on the trees that share its launches (fixed row blocks, fixed
+// reduction order), so the outcome is the one bfgs_pipelined gives over all trees at once.
 int optimize_split(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss, const View& v,
                    const std::vector<int32_t>& trees, const std::vector<int64_t>& coff, int iterations, double g_tol,
                    const std::vector<std::vector<double>>& starts, std::vector<double>& best_x,
                    std::vector<double>& best_f, std::vector<int64_t>& fcalls) {
   const char* se = getenv("SRHIP_OPTIM_SPLIT");
-  const bool split = !(se && *se == '0') && trees.size() >= 64;
-  srhip_ctx* ctx2 = split ? aux_ctx(ctx) : nullptr;
-  if (!ctx2) return bfgs_pipelined(ctx, ds, P, loss, v, trees, coff, iterations, g_tol, starts, best_x, best_f, fcalls);
-  std::vector<int32_t> ta, tb;
-  for (size_t i = 0; i < trees.size(); ++i) (i % 2 ? tb : ta).push_back(trees[i]);
-  std::vector<srhip_node> nodes2;
-  std::vector<int64_t> offs2(1, 0);
-  for (int32_t t : tb) {
-    nodes2.insert(nodes2.end(), P->nodes.begin() + P->offsets[t], P->nodes.begin() + P->offsets[t + 1]);
-    offs2.push_back((int64_t)nodes2.size());
-  }
+  int G = se && *se ? std::max(1, std::min(atoi(se), 8)) : 2;
+  if (trees.size() < 64) G = 1;
+  const std::vector<srhip_ctx*> aux = G > 1 ? aux_ctxs(ctx, G - 1) : std::vector<srhip_ctx*>();
+  G = 1 + (int)aux.size();
+  if (G == 1) return bfgs_pipelined(ctx, ds, P, loss, v, trees, coff, iterations, g_tol, starts, best_x, best_f, fcalls);
+  std::vector<std::vector<int32_t>> grp(G);
+  for (size_t i = 0; i < trees.size(); ++i) grp[i % G].push_back(trees[i]);
   const srhip_operators ops{(int32_t)P->binops.size(), (int32_t)P->unaops.size(), P->binops.data(),
                             P->unaops.data()};
-  const int32_t n2 = (int32_t)tb.size();
-  srhip_program* P2 = nullptr;
-  int rc = srhip_program_create(ctx2, P->dtype, nodes2.data(), offs2.data(), n2, &ops, &P2);
-  if (rc) return rc;
-  std::unique_ptr<srhip_program, void (*)(srhip_program*)> hold(P2, srhip_program_destroy);
-  const std::vector<int64_t> coff2 = const_offsets(*P2);
-  std::vector<std::vector<double>> starts2(starts.size(), std::vector<double>(coff2.back()));
-  std::vector<double> bx2(coff2.back()), bf2(n2);
-  std::vector<int64_t> fc2(n2);
-  for (int32_t j = 0; j < n2; ++j) {
-    const int32_t t = tb[j];
-    for (int64_t k = 0; k < coff2[j + 1] - coff2[j]; ++k) {
-      for (size_t s = 0; s < starts.size(); ++s) starts2[s][coff2[j] + k] = starts[s][coff[t] + k];
-      bx2[coff2[j] + k] = best_x[coff[t] + k];
+  struct Part {
+    srhip_program* P = nullptr;
+    std::vector<int64_t> coff;
+    std::vector<std::vector<double>> starts;
+    std::vector<double> bx, bf;
+    std::vector<int64_t> fc;
+    std::vector<int32_t> all;
+    int rc = SRHIP_OK;
+    std::string err;
+    ~Part() { srhip_program_destroy(P); }
+  };
+  std::vector<Part> part(G);
+  for (int gi = 1; gi < G; ++gi) {
+    Part& q = part[gi];
+    const std::vector<int32_t>& tb = grp[gi];
+    std::vector<srhip_node> nodes2;
+    std::vector<int64_t> offs2(1, 0);
+    for (int32_t t : tb) {
+      nodes2.insert(nodes2.end(), P->nodes.begin() + P->offsets[t], P->nodes.begin() + P->offsets[t + 1]);
+      offs2.push_back((int64_t)nodes2.size());
     }
-    bf2[j] = best_f[t];
-    fc2[j] = fcalls[t];
+    const int32_t n2 = (int32_t)tb.size();
+    const int rc = srhip_program_create(aux[gi - 1], P->dtype, nodes2.data(), offs2.data(), n2, &ops, &q.P);
+    if (rc) return rc;
+    q.coff = const_offsets(*q.P);
+    q.starts.assign(starts.size(), std::vector<double>(q.coff.back()));
+    q.bx.resize(q.coff.back());
+    q.bf.resize(n2);
+    q.fc.resize(n2);
+    q.all.resize(n2);
+    for (int32_t j = 0; j < n2; ++j) {
+      const int32_t t = tb[j];
+      for (int64_t k = 0; k < q.coff[j + 1] - q.coff[j]; ++k) {
+        for (size_t s = 0; s < starts.size(); ++s) q.starts[s][q.coff[j] + k] = starts[s][coff[t] + k];
+        q.bx[q.coff[j] + k] = best_x[coff[t] + k];
+      }
+      q.bf[j] = best_f[t];
+      q.fc[j] = fcalls[t];
+      q.all[j] = j;
+    }
   }
-  std::vector<int32_t> all2(n2);
-  for (int32_t j = 0; j < n2; ++j) all2[j] = j;
-  int rc2 = SRHIP_OK;
-  std::string err2;
-  std::thread th([&] {
-    (void)hipSetDevice(ctx2->device);
-    rc2 = bfgs_pipelined(ctx2, ds, P2, loss, v, all2, coff2, iterations, g_tol, starts2, bx2, bf2, fc2);
-    if (rc2) err2 = last_error();
-  });
-  rc = bfgs_pipelined(ctx, ds, P, loss, v, ta, coff, iterations, g_tol, starts, best_x, best_f, fcalls);
-  th.join();
+  std::vector<std::thread> th;
+  for (int gi = 1; gi < G; ++gi)
+    th.emplace_back([&, gi] {
+      Part& q = part[gi];
+      srhip_ctx* c = aux[gi - 1];
+      (void)hipSetDevice(c->device);
+      q.rc = bfgs_pipelined(c, ds, q.P, loss, v, q.all, q.coff, iterations, g_tol, q.starts, q.bx, q.bf, q.fc);
+      if (q.rc) q.err = last_error();
+    });
+  const int rc = bfgs_pipelined(ctx, ds, P, loss, v, grp[0], coff, iterations, g_tol, starts, best_x, best_f, fcalls);
+  for (std::thread& t : th) t.join();
   if (rc) return rc;
-  if (rc2) return fail(rc2, "%s", err2.c_str());
-  for (int32_t j = 0; j < n2; ++j) {
-    const int32_t t = tb[j];
-    for (int64_t k = 0; k < coff2[j + 1] - coff2[j]; ++k) best_x[coff[t] + k] = bx2[coff2[j] + k];
-    best_f[t] = bf2[j];
-    fcalls[t] = fc2[j];
+  for (int gi = 1; gi < G; ++gi) {
+    Part& q = part[gi];
+    if (q.rc) return fail(q.rc, "%s", q.err.c_str());
+    for (int32_t j = 0; j < (int32_t)grp[gi].size(); ++j) {
+      const int32_t t = grp[gi][j];
+      for (int64_t k = 0; k < q.coff[j + 1] - q.coff[j]; ++k) best_x[coff[t] + k] = q.bx[q.coff[j] + k];
+      best_f[t] = q.bf[j];
+      fcalls[t] = q.fc[j];
+    }
   }
   return SRHIP_OK;
 }
