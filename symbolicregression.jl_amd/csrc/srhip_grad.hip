@@ -221,6 +221,8 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   const int rb = blockIdx.x;
   const int64_t row_base = (int64_t)rb * p.rb_rows;
   const int ntiles = p.rb_rows / (64 * R);
+  // valid rows of this block, block-relative: the row tests below are 32-bit (scalar for the tile test)
+  const int nrel = __builtin_amdgcn_readfirstlane((int)min<int64_t>(max<int64_t>(p.nvalid - row_base, 0), (int64_t)p.rb_rows));
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int group_base = blockIdx.y * p.chunks_per_group;
   const int group_n = min(p.chunks_per_group, p.nchunks - group_base);
@@ -265,13 +267,10 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
     T M = T(0);
     for (int tile = 0; tile < ntiles; ++tile) {
       const int tb = tile * 64 * R;  // block-relative first row of the tile
-      if (row_base + tb >= p.nvalid) break;
+      if (tb >= nrel) break;
       // rows up to ld are finite replicas; masked at the loss
       Dual<T, KT> A[R], S[K][R];
-      UNR for (int r = 0; r < R; ++r) {
-        set_feat<GMODE_LOSS>(A[r], T(0), -1);
-        UNR for (int k = 0; k < K; ++k) set_feat<GMODE_LOSS>(S[k][r], T(0), -1);
-      }
+      UNR for (int r = 0; r < R; ++r) set_feat<GMODE_LOSS>(A[r], T(0), -1);
       GIns* prog = code + pc0;
       Ins nxt = prog[0];
       for (int step = 0; step < max_steps; ++step) {
@@ -359,7 +358,7 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
       }
       UNR for (int r = 0; r < R; ++r) {
         const int rr = tb + 64 * r + lane;
-        if (row_base + rr < p.nvalid) {
+        if (rr < nrel) {
           const T d = A[r].v - yat(rr);
           T l, dl;
           if (p.loss_kind == SRHIP_LOSS_L2) {
