@@ -392,3 +392,28 @@ def test_speculative_trials_equal_sequential(ctx, dtype, monkeypatch, capfd):
         assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]), key
         for ca, cb in zip(a[3], b[3]):
             assert np.array_equal(np.asarray(ca).view(np.uint64), np.asarray(cb).view(np.uint64)), key
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_split_optimizer_equals_single_group(ctx, dtype, monkeypatch):
+    """The optimiser splits populations of >= 64 trees into SRHIP_OPTIM_SPLIT groups, each group but
+    the first a program of its own on an auxiliary context driven from its own host thread
+    (srhip_optim.cpp optimize_split).  Losses, improvement flags, evaluation counts and constants are
+    bit-identical to one group (a tree's trajectory does not depend on its launch companions)."""
+    sr = _sr()
+    opts, _, nodes, offs, X, y = _problem(sr, dtype, ntrees=96)
+    ds = sr.DeviceDataset(ctx, X, y)
+    loss = sr.L2DistLoss()
+    res = []
+    for g in ("1", "2", "3"):
+        monkeypatch.setenv("SRHIP_OPTIM_SPLIT", g)
+        prog = sr.Program(ctx, nodes, offs, opts, dtype)
+        out, improved, fcalls = prog.optimize_constants(ds, loss, iterations=8, nrestarts=1, seed=3)
+        res.append((np.asarray(out, np.float64), improved, fcalls, np.concatenate(prog.get_constants())))
+        prog.close()
+    base = res[0]
+    assert base[1].sum() > 10
+    for r in res[1:]:
+        assert np.array_equal(r[0].view(np.uint64), base[0].view(np.uint64))
+        assert np.array_equal(r[1], base[1]) and np.array_equal(r[2], base[2])
+        assert np.array_equal(r[3].view(np.uint64), base[3].view(np.uint64))
