@@ -397,7 +397,10 @@ def pmc_summary(kname, pattern="*pmc_c2*.json"):
     source file).  Nones if no summary for this kernel variant is committed."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    # the round's final summary when committed (file names sort by build, not by date), else the
+    # last by name
+    final = os.path.join(ROOT, "profiles", pattern.replace("*", "r03_", 1).replace("*", "_final"))
+    files = [final] if os.path.exists(final) else sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
     if not files:
         return None, None, None
     try:
