@@ -73,7 +73,9 @@ enum {
   SRHIP_OP_EXP2 = 62, SRHIP_OP_EXPM1 = 63, SRHIP_OP_CBRT = 64
 };
 
-/* ---- loss kinds (LossFunctions.jl 0.10/0.11 distance losses; src/LossFunctions.jl:13-33) - */
+/* ---- loss kinds (LossFunctions.jl 0.10/0.11 supervised losses; src/LossFunctions.jl:13-33,
+ * the list src/Options.jl:209-229 documents).  Distance losses take r = output - target, margin
+ * losses the agreement a = target * output (LossFunctions' MarginLoss convention). */
 enum {
   SRHIP_LOSS_L2 = 0,          /* L2DistLoss (default, src/Options.jl:534-535) */
   SRHIP_LOSS_L1 = 1,          /* L1DistLoss */
@@ -83,7 +85,18 @@ enum {
   SRHIP_LOSS_L2_EPS_INS = 5,  /* L2EpsilonInsLoss(eps): p0 = eps */
   SRHIP_LOSS_LOGIT_DIST = 6,  /* LogitDistLoss */
   SRHIP_LOSS_PERIODIC = 7,    /* PeriodicLoss(c): p0 = c */
-  SRHIP_LOSS_QUANTILE = 8     /* QuantileLoss(tau): p0 = tau */
+  SRHIP_LOSS_QUANTILE = 8,    /* QuantileLoss(tau): p0 = tau */
+  SRHIP_LOSS_ZERO_ONE = 9,            /* ZeroOneLoss */
+  SRHIP_LOSS_PERCEPTRON = 10,         /* PerceptronLoss */
+  SRHIP_LOSS_LOGIT_MARGIN = 11,       /* LogitMarginLoss */
+  SRHIP_LOSS_L1_HINGE = 12,           /* L1HingeLoss (= HingeLoss) */
+  SRHIP_LOSS_L2_HINGE = 13,           /* L2HingeLoss */
+  SRHIP_LOSS_SMOOTHED_L1_HINGE = 14,  /* SmoothedL1HingeLoss(gamma): p0 = gamma */
+  SRHIP_LOSS_MODIFIED_HUBER = 15,     /* ModifiedHuberLoss */
+  SRHIP_LOSS_L2_MARGIN = 16,          /* L2MarginLoss */
+  SRHIP_LOSS_EXP = 17,                /* ExpLoss */
+  SRHIP_LOSS_SIGMOID = 18,            /* SigmoidLoss */
+  SRHIP_LOSS_DWD_MARGIN = 19          /* DWDMarginLoss(q): p0 = q */
 };
 
 /* One Node{T} (DynamicExpressions v0.16 fields: degree, constant, val, feature, op, l, r;

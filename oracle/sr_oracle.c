@@ -111,7 +111,48 @@ static float un_f32(int op, float x) {
     default: return NAN;
   }
 }
-static float loss_f32(int kind, float d, float p0) {
+/* Julia's max (the device's v_maximum: NaN-propagating, +0 above -0) */
+static float fmaxf_nan(float a, float b) {
+  if (a != a || b != b) return NAN;
+  if (a == b) return signbit(a) ? b : a;
+  return a > b ? a : b;
+}
+static double fmax_nan(double a, double b) {
+  if (a != a || b != b) return NAN;
+  if (a == b) return signbit(a) ? b : a;
+  return a > b ? a : b;
+}
+/* LossFunctions.jl 0.11 margin losses of the agreement a = target * output (src/losses/margin.jl;
+ * the package is not in the container: restated from its published definitions, parity unpinned) */
+static float margin_f32(int kind, float a, float p0) {
+  switch (kind) {
+    case SRHIP_LOSS_ZERO_ONE: return a < 0.0f ? 1.0f : 0.0f;
+    case SRHIP_LOSS_PERCEPTRON: return fmaxf_nan(0.0f, -a);
+    case SRHIP_LOSS_LOGIT_MARGIN: return W1(log1p, srm_expf(-a));
+    case SRHIP_LOSS_L1_HINGE: return fmaxf_nan(0.0f, 1.0f - a);
+    case SRHIP_LOSS_L2_HINGE: { const float h = 1.0f - a; return a >= 1.0f ? 0.0f : h * h; }
+    case SRHIP_LOSS_SMOOTHED_L1_HINGE:
+      if (a >= 1.0f - p0) { const float h = fmaxf_nan(0.0f, 1.0f - a); return 0.5f / p0 * (h * h); }
+      return 1.0f - p0 / 2.0f - a;
+    case SRHIP_LOSS_MODIFIED_HUBER:
+      if (a >= -1.0f) { const float h = fmaxf_nan(0.0f, 1.0f - a); return h * h; }
+      return -4.0f * a;
+    case SRHIP_LOSS_L2_MARGIN: { const float h = 1.0f - a; return h * h; }
+    case SRHIP_LOSS_EXP: return srm_expf(-a);
+    case SRHIP_LOSS_SIGMOID: return 1.0f - W1(tanh, a);
+    case SRHIP_LOSS_DWD_MARGIN:
+      if (a <= p0 / (p0 + 1.0f)) return 1.0f - a;
+      return ((float)pow((double)p0, (double)p0) / (float)pow((double)(p0 + 1.0f), (double)(p0 + 1.0f))) /
+             (float)pow((double)a, (double)p0);
+    default: return NAN;
+  }
+}
+static float dist_f32(int kind, float d, float p0);
+/* one row's elementwise loss: distance losses of output - target, margin losses of target * output */
+static float loss_f32(int kind, float out, float y, float p0) {
+  return kind >= SRHIP_LOSS_ZERO_ONE ? margin_f32(kind, y * out, p0) : dist_f32(kind, out - y, p0);
+}
+static float dist_f32(int kind, float d, float p0) {
   switch (kind) {
     case SRHIP_LOSS_L2: return d * d;
     case SRHIP_LOSS_L1: return fabsf(d);
@@ -204,7 +245,33 @@ static double un_f64(int op, double x) {
     default: return NAN;
   }
 }
-static double loss_f64(int kind, double d, double p0) {
+static double margin_f64(int kind, double a, double p0) {
+  switch (kind) {
+    case SRHIP_LOSS_ZERO_ONE: return a < 0.0 ? 1.0 : 0.0;
+    case SRHIP_LOSS_PERCEPTRON: return fmax_nan(0.0, -a);
+    case SRHIP_LOSS_LOGIT_MARGIN: return log1p(srm_exp(-a));
+    case SRHIP_LOSS_L1_HINGE: return fmax_nan(0.0, 1.0 - a);
+    case SRHIP_LOSS_L2_HINGE: { const double h = 1.0 - a; return a >= 1.0 ? 0.0 : h * h; }
+    case SRHIP_LOSS_SMOOTHED_L1_HINGE:
+      if (a >= 1.0 - p0) { const double h = fmax_nan(0.0, 1.0 - a); return 0.5 / p0 * (h * h); }
+      return 1.0 - p0 / 2.0 - a;
+    case SRHIP_LOSS_MODIFIED_HUBER:
+      if (a >= -1.0) { const double h = fmax_nan(0.0, 1.0 - a); return h * h; }
+      return -4.0 * a;
+    case SRHIP_LOSS_L2_MARGIN: { const double h = 1.0 - a; return h * h; }
+    case SRHIP_LOSS_EXP: return srm_exp(-a);
+    case SRHIP_LOSS_SIGMOID: return 1.0 - tanh(a);
+    case SRHIP_LOSS_DWD_MARGIN:
+      if (a <= p0 / (p0 + 1.0)) return 1.0 - a;
+      return (pow(p0, p0) / pow(p0 + 1.0, p0 + 1.0)) / pow(a, p0);
+    default: return NAN;
+  }
+}
+static double dist_f64(int kind, double d, double p0);
+static double loss_f64(int kind, double out, double y, double p0) {
+  return kind >= SRHIP_LOSS_ZERO_ONE ? margin_f64(kind, y * out, p0) : dist_f64(kind, out - y, p0);
+}
+static double dist_f64(int kind, double d, double p0) {
   switch (kind) {
     case SRHIP_LOSS_L2: return d * d;
     case SRHIP_LOSS_L1: return fabs(d);

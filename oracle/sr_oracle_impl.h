@@ -299,7 +299,7 @@ int CAT(oracle_eval_loss_, SFX)(const srhip_node* nodes, const int32_t* binops, 
   long double se = 0.0L, swe = 0.0L;
   T sr = 0, swr = 0;
   for (int64_t j = 0; j < n; ++j) {
-    const T l = CAT(loss_, SFX)(loss_kind, pred[j] - y[j], (T)p0);
+    const T l = CAT(loss_, SFX)(loss_kind, pred[j], y[j], (T)p0);
     if (w) {
       const T wl = w[j] * l;
       se += (long double)wl;
@@ -404,7 +404,7 @@ void CAT(oracle_partials_, SFX)(const srhip_node* nodes, const int64_t* offsets,
       ls += loss_kind == SRHIP_LOSS_L1 ? (d < 0 ? -(long double)d : (long double)d) : (long double)(int32_t)((uint32_t)d * (uint32_t)d);
       ws += 1.0L;
 #else
-      const T l = CAT(loss_, SFX)(loss_kind, pv - y[j], (T)p0);
+      const T l = CAT(loss_, SFX)(loss_kind, pv, y[j], (T)p0);
       if (w) {
         ls += (long double)(w[j] * l);
         ws += (long double)w[j];

@@ -626,7 +626,7 @@ __device__ __attribute__((always_inline)) inline void precise_hook(const EvalArg
 // the allocator move the accumulator off the registers the operator bodies use for it.
 template <typename T, int R>
 __device__ __attribute__((noinline)) RV<T, R> loss_rows_generic(RV<T, R> a, RV<T, R> y, int kind, T p0) {
-  UNR for (int r = 0; r < R; ++r) a[r] = loss_elem<T>(kind, a[r] - y[r], p0);
+  UNR for (int r = 0; r < R; ++r) a[r] = loss_row<T>(kind, a[r], y[r], p0);
   return a;
 }
 

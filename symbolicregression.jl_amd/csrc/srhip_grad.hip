@@ -169,7 +169,33 @@ template <typename T> DI T dloss_elem(int kind, T d, T p0) {
 
 // (loss, d loss / d output) of the other distance losses, out of line: inline, their math bodies
 // raised the kernel's register count for every loss kind
-template <typename T> __device__ __attribute__((noinline)) typename V2<T>::type loss_dloss_generic(int kind, T d, T p0) {
+// d loss / d agreement of the margin losses of srhip_ops.h margin_loss (a = target * output)
+template <typename T> DI T dmargin(int kind, T a, T p0) {
+  switch (kind) {
+    case SRHIP_LOSS_ZERO_ONE: return T(0);
+    case SRHIP_LOSS_PERCEPTRON: return a >= T(0) ? T(0) : T(-1);
+    case SRHIP_LOSS_LOGIT_MARGIN: return T(-1) / (T(1) + m_exp(a));
+    case SRHIP_LOSS_L1_HINGE: return a >= T(1) ? T(0) : T(-1);
+    case SRHIP_LOSS_L2_HINGE: return a >= T(1) ? T(0) : T(2) * (a - T(1));
+    case SRHIP_LOSS_SMOOTHED_L1_HINGE: return a >= T(1) - p0 ? (a >= T(1) ? T(0) : (a - T(1)) / p0) : T(-1);
+    case SRHIP_LOSS_MODIFIED_HUBER: return a >= T(-1) ? (a > T(1) ? T(0) : T(2) * a - T(2)) : T(-4);
+    case SRHIP_LOSS_L2_MARGIN: return T(2) * (a - T(1));
+    case SRHIP_LOSS_EXP: return -m_exp(-a);
+    case SRHIP_LOSS_SIGMOID: { const T t = m_tanh(a); return -(T(1) - t * t); }
+    case SRHIP_LOSS_DWD_MARGIN:
+      return a <= p0 / (p0 + T(1)) ? T(-1) : -m_pow(p0 / (p0 + T(1)), p0 + T(1)) / m_pow(a, p0 + T(1));
+    default: return FP<T>::nan();
+  }
+}
+// (loss, d loss / d output) of one row for the kinds other than L2: distance losses of
+// output - target, margin losses of target * output (chain rule: target * dL/da)
+template <typename T>
+__device__ __attribute__((noinline)) typename V2<T>::type loss_dloss_generic(int kind, T out, T y, T p0) {
+  if (loss_is_margin(kind)) {
+    const T a = y * out;
+    return typename V2<T>::type{margin_loss<T>(kind, a, p0), y * dmargin<T>(kind, a, p0)};
+  }
+  const T d = out - y;
   return typename V2<T>::type{loss_elem<T>(kind, d, p0), dloss_elem<T>(kind, d, p0)};
 }
 
@@ -365,7 +391,7 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
             l = d * d;
             dl = T(2) * d;
           } else {
-            const typename V2<T>::type q = loss_dloss_generic<T>(p.loss_kind, d, p0);
+            const typename V2<T>::type q = loss_dloss_generic<T>(p.loss_kind, A[r].v, yat(rr), p0);
             l = q[0];
             dl = q[1];
           }

@@ -1293,7 +1293,7 @@ int srhip::check_eval_args(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_
     if (!loss) return fail(SRHIP_ERR_INVALID, "null loss");
     if (P->dtype == SRHIP_I32 && loss->kind != SRHIP_LOSS_L2 && loss->kind != SRHIP_LOSS_L1)
       return fail(SRHIP_ERR_UNSUPPORTED, "Int32 datasets support L2/L1 losses only");
-    if (loss->kind < SRHIP_LOSS_L2 || loss->kind > SRHIP_LOSS_QUANTILE)
+    if (loss->kind < SRHIP_LOSS_L2 || loss->kind > SRHIP_LOSS_DWD_MARGIN)
       return fail(SRHIP_ERR_UNSUPPORTED, "loss kind %d", loss->kind);
   }
   return SRHIP_OK;

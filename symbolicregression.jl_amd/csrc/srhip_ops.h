@@ -231,6 +231,42 @@ SRHIP_HD T loss_elem(int kind, T diff, T p0) {
     default: return FP<T>::nan();
   }
 }
+// LossFunctions.jl 0.11 margin losses (src/losses/margin.jl), of the agreement a = target * output.
+// Restated from the published definitions (the package is not in the container; parity with it is
+// unpinned); evaluated in T.
+template <typename T>
+SRHIP_HD T margin_loss(int kind, T a, T p0) {
+  switch (kind) {
+    case SRHIP_LOSS_ZERO_ONE: return a < T(0) ? T(1) : T(0);            // sign(a) < 0
+    case SRHIP_LOSS_PERCEPTRON: return m_max(T(0), -a);
+    case SRHIP_LOSS_LOGIT_MARGIN: return m_log1p(m_exp(-a));
+    case SRHIP_LOSS_L1_HINGE: return m_max(T(0), T(1) - a);
+    case SRHIP_LOSS_L2_HINGE: { const T h = T(1) - a; return a >= T(1) ? T(0) : h * h; }
+    case SRHIP_LOSS_SMOOTHED_L1_HINGE: {                                // gamma = p0
+      if (a >= T(1) - p0) { const T h = m_max(T(0), T(1) - a); return T(0.5) / p0 * (h * h); }
+      return T(1) - p0 / T(2) - a;
+    }
+    case SRHIP_LOSS_MODIFIED_HUBER: {
+      if (a >= T(-1)) { const T h = m_max(T(0), T(1) - a); return h * h; }
+      return -T(4) * a;
+    }
+    case SRHIP_LOSS_L2_MARGIN: { const T h = T(1) - a; return h * h; }
+    case SRHIP_LOSS_EXP: return m_exp(-a);
+    case SRHIP_LOSS_SIGMOID: return T(1) - m_tanh(a);
+    case SRHIP_LOSS_DWD_MARGIN: {                                       // q = p0
+      if (a <= p0 / (p0 + T(1))) return T(1) - a;
+      return (m_pow(p0, p0) / m_pow(p0 + T(1), p0 + T(1))) / m_pow(a, p0);
+    }
+    default: return FP<T>::nan();
+  }
+}
+SRHIP_HD constexpr bool loss_is_margin(int kind) { return kind >= SRHIP_LOSS_ZERO_ONE && kind <= SRHIP_LOSS_DWD_MARGIN; }
+// the elementwise loss of one row: distance losses of output - target, margin losses of
+// target * output (LossFunctions' (loss)(output, target) for the two families)
+template <typename T>
+SRHIP_HD T loss_row(int kind, T output, T target, T p0) {
+  return loss_is_margin(kind) ? margin_loss<T>(kind, target * output, p0) : loss_elem<T>(kind, output - target, p0);
+}
 // Int32 datasets: the elementwise loss is computed in Int32 wrap arithmetic and summed in Int64.
 SRHIP_HD int32_t loss_elem_int(int kind, int32_t diff) {
   switch (kind) {

@@ -32,6 +32,19 @@ from .api import (
 from .dataset import Dataset
 from .device import Coalescer, Context, DeviceDataset, Program, device_count, get_context
 from .losses import (
+    DWDMarginLoss,
+    ExpLoss,
+    HingeLoss,
+    L1HingeLoss,
+    L2HingeLoss,
+    L2MarginLoss,
+    LogitMarginLoss,
+    MarginLoss,
+    ModifiedHuberLoss,
+    PerceptronLoss,
+    SigmoidLoss,
+    SmoothedL1HingeLoss,
+    ZeroOneLoss,
     HuberLoss,
     L1DistLoss,
     L1EpsilonInsLoss,

@@ -31,6 +31,8 @@ OP = dict(
 )
 LOSS = dict(
     L2=0, L1=1, LP=2, HUBER=3, L1_EPS_INS=4, L2_EPS_INS=5, LOGIT_DIST=6, PERIODIC=7, QUANTILE=8,
+    ZERO_ONE=9, PERCEPTRON=10, LOGIT_MARGIN=11, L1_HINGE=12, L2_HINGE=13, SMOOTHED_L1_HINGE=14,
+    MODIFIED_HUBER=15, L2_MARGIN=16, EXP=17, SIGMOID=18, DWD_MARGIN=19,
 )
 
 # struct srhip_node (24 bytes)

@@ -417,3 +417,54 @@ def test_split_optimizer_equals_single_group(ctx, dtype, monkeypatch):
         assert np.array_equal(r[0].view(np.uint64), base[0].view(np.uint64))
         assert np.array_equal(r[1], base[1]) and np.array_equal(r[2], base[2])
         assert np.array_equal(r[3].view(np.uint64), base[3].view(np.uint64))
+
+
+@pytest.mark.parametrize("kind_name,args", [("LogitMarginLoss", ()), ("L2MarginLoss", ()), ("ExpLoss", ()),
+                                            ("SigmoidLoss", ()), ("ModifiedHuberLoss", ()), ("L2HingeLoss", ()),
+                                            ("SmoothedL1HingeLoss", (0.6,)), ("DWDMarginLoss", (1.5,)),
+                                            ("HuberLoss", (0.5,)), ("LogitDistLoss", ())])
+def test_loss_kind_gradients_match_differences(ctx, kind_name, args):
+    """d loss / d c of the dual-number kernel for the other loss kinds (margin losses through the chain
+    rule target * dL/da) vs Richardson central differences of the device's own loss (F64)."""
+    sr = _sr()
+    loss = getattr(sr, kind_name)(*args)
+    opts = sr.Options(binary_operators=("+", "-", "*"), unary_operators=("cos",))
+    trees = sr.random_population(16, opts, 2, np.float64, seed=5, max_size=12)
+    nodes, offs = sr.flatten(trees, opts, np.float64)
+    rng = np.random.default_rng(6)
+    X = rng.standard_normal((2, 800))
+    margin = isinstance(loss, sr.MarginLoss)
+    y = np.where(X[0] + 0.3 * X[1] > 0, 1.0, -1.0) if margin else np.cos(X[0]) + 0.5 * X[1]
+    ds = sr.DeviceDataset(ctx, X, y)
+    prog = sr.Program(ctx, nodes, offs, opts, np.float64)
+    l0, grads, ok = prog.eval_loss_grad(ds, loss)
+    checked = 0
+    for t in np.nonzero(ok)[0]:
+        tn = nodes[offs[t]:offs[t + 1]].copy()
+        cidx = _order(tn)
+        if not cidx or not np.isfinite(l0[t]):
+            continue
+        one = np.array([0, len(tn)], dtype=np.int64)
+
+        def f(nd):
+            p = sr.Program(ctx, nd, one, opts, np.float64)
+            v = p.eval_loss(ds, loss)[0][0]
+            p.close()
+            return v
+
+        for k, i in enumerate(cidx):
+            h = 1e-5 * max(1.0, abs(tn[i]["val"]))
+
+            def fd(hh):
+                fp, fm = tn.copy(), tn.copy()
+                fp[i]["val"] += hh
+                fm[i]["val"] -= hh
+                return (f(fp) - f(fm)) / (2 * hh)
+
+            d1, d2 = fd(h), fd(h / 4)
+            ref = (16 * d2 - d1) / 15
+            if not np.isfinite(ref) or abs(d1 - d2) > 1e-3 * max(1.0, abs(ref)):
+                continue
+            assert abs(grads[t][k] - ref) <= 1e-5 * max(1.0, abs(ref)), (t, k, grads[t][k], ref)
+            checked += 1
+    assert checked >= 6

@@ -540,3 +540,31 @@ def test_loss_in_reference_type_L(ctx, oracle):
         assert isinstance(v, np.float32) and v == np.float32(dl[t])
         s, l2 = sr.score_func(d, trees[t], opts)
         assert isinstance(l2, np.float32) and isinstance(s, np.float32)
+
+
+MARGIN_LOSSES = [("ZeroOneLoss", ()), ("PerceptronLoss", ()), ("LogitMarginLoss", ()), ("L1HingeLoss", ()),
+                 ("L2HingeLoss", ()), ("SmoothedL1HingeLoss", (0.6,)), ("ModifiedHuberLoss", ()),
+                 ("L2MarginLoss", ()), ("ExpLoss", ()), ("SigmoidLoss", ()), ("DWDMarginLoss", (1.5,))]
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("kind_name,args", MARGIN_LOSSES)
+def test_margin_loss_kinds(ctx, oracle, kind_name, args, dtype):
+    """The LossFunctions margin losses the reference lists (src/Options.jl:220-229), of the agreement
+    target * output, fused into the interpreter: device == oracle (same masks; losses within 1e-10
+    for Float64, the Float32 parity bar for Float32).  Targets are +-1 (binary classification)."""
+    sr = _sr()
+    loss = getattr(sr, kind_name)(*args)
+    opts = sr.Options(**OPS_C2)
+    _, nodes, offs = _population(sr, opts, 48, 4, dtype, seed=41, max_size=12)
+    X, _, _ = _data(4, 1500, dtype, seed=42)
+    y = np.where(np.random.default_rng(43).standard_normal(1500) > 0, 1.0, -1.0).astype(dtype)
+    prog = sr.Program(ctx, nodes, offs, opts, dtype)
+    dl, dok = prog.eval_loss(_ds(ctx, X, y), loss)
+    ol, _, ook, _ = oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, X, y, None, loss.kind,
+                                           loss.p0)
+    assert np.array_equal(dok, ook)
+    tol = 1e-10 if dtype == np.float64 else F32_REL
+    for t in np.nonzero(ook)[0]:
+        assert _rel(dl[t], ol[t]) < tol, (t, dl[t], ol[t])
+    assert ook.sum() >= 24
