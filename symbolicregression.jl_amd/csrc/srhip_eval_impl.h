@@ -249,10 +249,49 @@ __device__ __attribute__((noinline)) RV<float, R> trigf_slow(RV<float, R> v) {
   }
   return v;
 }
+// NaN-propagating max (min) |v| over a lane's rows folded into m: one v_maximum3_f32 (v_minimum3_f32)
+// per row pair, the whole chain in ONE asm statement -- the hazard recognizer cannot see into an asm
+// statement and padded every dependent pair of single-instruction statements with an s_nop (one per
+// two rows of every check fold; the chain itself has no hazard)
+#define SRHIP_M3(OP, a, b) OP " %0, %0, |%" #a "|, |%" #b "|\n\t"
+template <int R, bool MAX>
+__device__ __attribute__((always_inline)) inline float abs_fold(float m, const RV<float, R>& v) {
+#define SRHIP_OPC (MAX ? "v_maximum3_f32" : "v_minimum3_f32")
+  if constexpr (R == 16) {
+    if constexpr (MAX)
+      asm(SRHIP_M3("v_maximum3_f32", 1, 2) SRHIP_M3("v_maximum3_f32", 3, 4) SRHIP_M3("v_maximum3_f32", 5, 6)
+          SRHIP_M3("v_maximum3_f32", 7, 8) SRHIP_M3("v_maximum3_f32", 9, 10) SRHIP_M3("v_maximum3_f32", 11, 12)
+          SRHIP_M3("v_maximum3_f32", 13, 14) SRHIP_M3("v_maximum3_f32", 15, 16)
+          : "+v"(m) : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]),
+            "v"(v[8]), "v"(v[9]), "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
+    else
+      asm(SRHIP_M3("v_minimum3_f32", 1, 2) SRHIP_M3("v_minimum3_f32", 3, 4) SRHIP_M3("v_minimum3_f32", 5, 6)
+          SRHIP_M3("v_minimum3_f32", 7, 8) SRHIP_M3("v_minimum3_f32", 9, 10) SRHIP_M3("v_minimum3_f32", 11, 12)
+          SRHIP_M3("v_minimum3_f32", 13, 14) SRHIP_M3("v_minimum3_f32", 15, 16)
+          : "+v"(m) : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]),
+            "v"(v[8]), "v"(v[9]), "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
+  } else if constexpr (R == 8) {
+    if constexpr (MAX)
+      asm(SRHIP_M3("v_maximum3_f32", 1, 2) SRHIP_M3("v_maximum3_f32", 3, 4) SRHIP_M3("v_maximum3_f32", 5, 6)
+          SRHIP_M3("v_maximum3_f32", 7, 8)
+          : "+v"(m) : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]));
+    else
+      asm(SRHIP_M3("v_minimum3_f32", 1, 2) SRHIP_M3("v_minimum3_f32", 3, 4) SRHIP_M3("v_minimum3_f32", 5, 6)
+          SRHIP_M3("v_minimum3_f32", 7, 8)
+          : "+v"(m) : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]));
+  } else {
+    static_assert(R % 2 == 0, "row pairs");
+    UNR for (int r = 0; r < R; r += 2) {
+      if constexpr (MAX) asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(m) : "v"(m), "v"(v[r]), "v"(v[r + 1]));
+      else asm("v_minimum3_f32 %0, %1, |%2|, |%3|" : "=v"(m) : "v"(m), "v"(v[r]), "v"(v[r + 1]));
+    }
+  }
+#undef SRHIP_OPC
+  return m;
+}
+
 template <int R> __device__ __attribute__((always_inline)) inline bool trigf_rows_fast(const RV<float, R>& A) {
-  float mx = 0.0f;
-  UNR for (int r = 0; r < R; r += 2)
-    asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(A[r]), "v"(A[r + 1]));
+  const float mx = abs_fold<R, true>(0.0f, A);
   return __builtin_amdgcn_ballot_w64(!(mx < SRM_PIO2F_BIG_F)) == 0;  // false for NaN
 }
 
@@ -276,9 +315,7 @@ __device__ __attribute__((always_inline)) inline RV<float, R> trigf_rows(RV<floa
     if (big) res = trigf_fix_tan<R>(v, res);
   } else {
     static_assert(R % 2 == 0, "row pairs");
-    float mx = 0.0f;
-    UNR for (int r = 0; r < R; r += 2)
-      asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(v[r]), "v"(v[r + 1]));
+    const float mx = abs_fold<R, true>(0.0f, v);
     UNR for (int r = 0; r < R; ++r) {
       res[r] = sincosf_dev<KIND>((double)v[r]);
       if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
@@ -295,9 +332,7 @@ __device__ __attribute__((noinline)) RV<T, R> heavy_un(RV<T, R> v) {
     return trigf_rows<R, U == UN_COS ? 0 : (U == UN_SIN ? 1 : 2)>(v);
   if constexpr (std::is_same<T, float>::value && U == UN_EXP && R % 2 == 0) {
     // one NaN-propagating max |x| per row pair decides for the whole wave (false for NaN)
-    float mx = 0.0f;
-    UNR for (int r = 0; r < R; r += 2)
-      asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(v[r]), "v"(v[r + 1]));
+    const float mx = abs_fold<R, true>(0.0f, v);
     if (__builtin_amdgcn_ballot_w64(!(mx <= EXPF_FAST_MAX)) == 0) {
       UNR for (int r = 0; r < R; r += 2) {
         const F2 e = expf2_fast((F2){v[r], v[r + 1]});
@@ -392,8 +427,7 @@ template <typename T> struct Chk {
 // Float32: one v_maximum3_f32 per two rows, chained through M (the compiler's reassociation into
 // a pairwise tree costs R/2 + 2 instructions instead of R/2).
 template <int R> __device__ __attribute__((always_inline)) inline void chk_update(float& M, const RV<float, R>& A) {
-  UNR for (int r = 0; r < R; r += 2)
-    asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(M) : "v"(M), "v"(A[r]), "v"(A[r + 1]));
+  M = abs_fold<R, true>(M, A);
 }
 template <int R> __device__ __attribute__((always_inline)) inline void chk_update(double& M, const RV<double, R>& A) {
   UNR for (int r = 0; r < R; ++r) M = __builtin_fma(__builtin_fabs(A[r]), 0x1p-512, M);
@@ -451,18 +485,14 @@ template <int R, bool SWAP, bool CHK, bool CONSTB = false>
 __device__ __attribute__((always_inline)) inline void div_rows(RV<float, R>& A, const RV<float, R>& B, float& M) {
   float mx = 0.0f, mn = __builtin_inff();
   if constexpr (CONSTB) {
-    UNR for (int r = 0; r < R; r += 2) {
-      asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(A[r]), "v"(A[r + 1]));
-      asm("v_minimum3_f32 %0, %1, |%2|, |%3|" : "=v"(mn) : "v"(mn), "v"(A[r]), "v"(A[r + 1]));
-    }
+    mx = abs_fold<R, true>(mx, A);
+    mn = abs_fold<R, false>(mn, A);
     const float c = __builtin_fabsf(B[0]);
     mx = __builtin_elementwise_maximum(mx, c);
     mn = __builtin_elementwise_minimum(mn, c);
   } else {
-    UNR for (int r = 0; r < R; ++r) {
-      asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(A[r]), "v"(B[r]));
-      asm("v_minimum3_f32 %0, %1, |%2|, |%3|" : "=v"(mn) : "v"(mn), "v"(A[r]), "v"(B[r]));
-    }
+    mx = abs_fold<R, true>(abs_fold<R, true>(mx, A), B);
+    mn = abs_fold<R, false>(abs_fold<R, false>(mn, A), B);
   }
   const bool fast = mx <= DIV_FAST_HI && mn >= DIV_FAST_LO;  // false for NaN
   if (__builtin_amdgcn_ballot_w64(!fast) == 0) {
