@@ -911,6 +911,9 @@ int optimize_split(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, co
     std::vector<int32_t> all;
     int rc = SRHIP_OK;
     std::string err;
+    Part() = default;
+    Part(const Part&) = delete;  // owns P
+    Part& operator=(const Part&) = delete;
     ~Part() { srhip_program_destroy(P); }
   };
   std::vector<Part> part(G);
