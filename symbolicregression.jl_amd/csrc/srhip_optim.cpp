@@ -881,7 +881,7 @@ std::vector<srhip_ctx*> aux_ctxs(srhip_ctx* ctx, int n) {
   return std::vector<srhip_ctx*>(ctx->aux.begin(), ctx->aux.begin() + std::min<size_t>(n, ctx->aux.size()));
 }
 
-// bfgs_pipelined over G groups of the trees at once (G = SRHIP_OPTIM_SPLIT, default 2; 1 = off;
+// bfgs_pipelined over G groups of the trees at once (G = SRHIP_OPTIM_SPLIT, default 3; 1 = off;
 // populations of fewer than 64 trees are not split): tree i goes to group i % G; group 0 runs on the
 // caller's thread and context, group g > 0 as a program of its own on the context's auxiliary
 // context g - 1 (own stream and buffers) from a host thread of its own.  Each launch's host
@@ -893,7 +893,7 @@ int optimize_split(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, co
                    const std::vector<std::vector<double>>& starts, std::vector<double>& best_x,
                    std::vector<double>& best_f, std::vector<int64_t>& fcalls) {
   const char* se = getenv("SRHIP_OPTIM_SPLIT");
-  int G = se && *se ? std::max(1, std::min(atoi(se), 8)) : 2;
+  int G = se && *se ? std::max(1, std::min(atoi(se), 8)) : 3;
   if (trees.size() < 64) G = 1;
   const std::vector<srhip_ctx*> aux = G > 1 ? aux_ctxs(ctx, G - 1) : std::vector<srhip_ctx*>();
   G = 1 + (int)aux.size();
