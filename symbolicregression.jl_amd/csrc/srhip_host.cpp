@@ -507,11 +507,15 @@ template <typename T> class TreeCompiler {
 class HostPool {
  public:
   static HostPool& get() {
-    static std::mutex m;
-    static HostPool* pool = nullptr;
-    std::lock_guard<std::mutex> g(m);
-    if (!pool || pool->pid_ != getpid()) pool = new HostPool();
-    return *pool;
+    // lock-free, so that a fork taken while another thread is here cannot leave a held mutex behind;
+    // two threads racing to create it may leave one extra parked pool (never destroyed)
+    static std::atomic<HostPool*> pool{nullptr};
+    HostPool* p = pool.load();
+    if (!p || p->pid_ != getpid()) {
+      HostPool* q = new HostPool();
+      if (pool.compare_exchange_strong(p, q)) p = q;
+    }
+    return *p;
   }
   int threads() const { return (int)nthr_ + 1; }
   // fn(0) .. fn(n - 1) on the pool's threads and the caller; false (nothing run) if busy
