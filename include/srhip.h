@@ -254,6 +254,21 @@ int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_prog
                              const srhip_loss* loss, const int64_t* idx, int64_t nidx,
                              const srhip_optim_options* opt, double* out_loss,
                              uint8_t* out_improved, int64_t* out_fcalls);
+/* The same, with the restarts' starting points exchanged with the caller
+ * (src/ConstantOptimization.jl:53-68: tmptree = copy(tree); val *= T(1) + T(1//2) * randn(T)):
+ *   starts_in  (nullable): [nrestarts][sum nconst] restart points in get_constants order, tree-major,
+ *              used instead of the library's own draws (a Float32 program rounds them to Float32);
+ *   starts_out (nullable): [nrestarts][sum nconst] the restart points actually used.
+ * The library's own draws perturb in the program's type: Float32 programs draw a Float32 normal
+ * and compute val * (1f + 0.5f * r) in Float32.  Start 0 is always the tree's current constants;
+ * its result is kept unless a restart's minimum is strictly smaller (:65-67), and the kept result
+ * replaces the constants only if it beats the baseline (:70-78).  Trees without constants or
+ * failing statically report their current constants. */
+int srhip_optimize_constants_starts(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* prog,
+                                    const srhip_loss* loss, const int64_t* idx, int64_t nidx,
+                                    const srhip_optim_options* opt, const double* starts_in,
+                                    double* starts_out, double* out_loss, uint8_t* out_improved,
+                                    int64_t* out_fcalls);
 
 /* ---- measurement hooks (bench / profiling) --------------------------------------------- */
 /* Device time (ms) of the last main kernel on this context -- the interpreter of srhip_eval_loss /

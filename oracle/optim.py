@@ -374,10 +374,12 @@ def optimize_constants_exact(tree_nodes, binops, unaops, X, y, w=None, iteration
     algorithm = newton_exact if len(x0) == 1 else bfgs_exact
     baseline = f(x0)
     best_x, best_f, calls = x0, np.inf, 0
-    for xs in (starts if starts is not None else [x0]):
+    for s, xs in enumerate(starts if starts is not None else [x0]):
         xr, fr, c = algorithm(f, grad, np.asarray(xs, dtype=np.float64), iterations)
         calls += c
-        if fr < best_f:
+        # the first start is `result` unconditionally (:50); a restart replaces it only when its
+        # minimum is strictly smaller (:65-67)
+        if s == 0 or fr < best_f:
             best_x, best_f = xr, fr
     if best_f < baseline:
         return best_x, best_f, True, calls

@@ -503,17 +503,26 @@ template <typename T> class TreeCompiler {
 // Host worker threads for the compiler: created once per process (a fork child makes its own) and
 // parked on a condition variable between jobs, so a population compile pays no thread start-up.
 // One job at a time; a caller that finds the pool busy (concurrent coalescer flushes) runs its items
-// itself.  The pool object is never destroyed: detached workers parked at exit are simply ended.
+// itself.  The process's pool is never destroyed: detached workers parked at exit are simply ended.
+// Work items are claimed from one 64-bit counter holding (job generation << 32 | next index): a
+// worker snapshots (generation, fn, n) under the mutex when it wakes, and a claim succeeds only by a
+// compare-exchange on its own generation, so a worker delayed past the end of its job can never run
+// an item of the next one (nor count it done).
 class HostPool {
  public:
   static HostPool& get() {
     // lock-free, so that a fork taken while another thread is here cannot leave a held mutex behind;
-    // two threads racing to create it may leave one extra parked pool (never destroyed)
+    // the loser of a creation race shuts its own pool down (joins its threads) and deletes it
     static std::atomic<HostPool*> pool{nullptr};
     HostPool* p = pool.load();
     if (!p || p->pid_ != getpid()) {
       HostPool* q = new HostPool();
-      if (pool.compare_exchange_strong(p, q)) p = q;
+      if (pool.compare_exchange_strong(p, q)) {
+        p = q;
+      } else {
+        q->shutdown();
+        delete q;
+      }
     }
     return *p;
   }
@@ -522,16 +531,17 @@ class HostPool {
   bool run(int n, const std::function<void(int)>& fn) {
     std::unique_lock<std::mutex> busy(busy_mu_, std::try_to_lock);
     if (!busy.owns_lock()) return false;
+    uint32_t g;
     {
-      std::lock_guard<std::mutex> g(mu_);
+      std::lock_guard<std::mutex> lk(mu_);
       fn_ = &fn;
       n_ = n;
-      next_.store(0);
       done_ = 0;
-      ++gen_;
+      g = ++gen_;
+      next_.store((uint64_t)g << 32);
     }
     cv_.notify_all();
-    work();
+    work(g, &fn, n);
     std::unique_lock<std::mutex> lk(mu_);
     cv_done_.wait(lk, [&] { return done_ == n_; });
     fn_ = nullptr;
@@ -542,36 +552,59 @@ class HostPool {
   HostPool() : pid_(getpid()) {
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     nthr_ = std::min(7u, hw - 1);
-    for (unsigned i = 0; i < nthr_; ++i) std::thread([this] { loop(); }).detach();
+    for (unsigned i = 0; i < nthr_; ++i) threads_.emplace_back([this] { loop(); });
+  }
+  ~HostPool() {
+    for (std::thread& t : threads_)
+      if (t.joinable()) t.detach();
+  }
+  void shutdown() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (std::thread& t : threads_)
+      if (t.joinable()) t.join();
   }
   void loop() {
-    uint64_t seen = 0;
+    uint32_t seen = 0;
     for (;;) {
+      uint32_t g;
+      const std::function<void(int)>* fn;
+      int n;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = g = gen_;
+        fn = fn_;
+        n = n_;
       }
-      work();
+      if (fn) work(g, fn, n);
     }
   }
-  void work() {
+  void work(uint32_t g, const std::function<void(int)>* fn, int n) {
     for (;;) {
-      const int i = next_.fetch_add(1);
-      if (i >= n_) return;
-      (*fn_)(i);
-      std::lock_guard<std::mutex> g(mu_);
+      uint64_t v = next_.load();
+      if ((uint32_t)(v >> 32) != g || (int)(uint32_t)v >= n) return;
+      if (!next_.compare_exchange_weak(v, v + 1)) continue;
+      (*fn)((int)(uint32_t)v);
+      std::lock_guard<std::mutex> lk(mu_);
       if (++done_ == n_) cv_done_.notify_all();
     }
   }
   const pid_t pid_;
   unsigned nthr_ = 0;
+  std::vector<std::thread> threads_;
   std::mutex busy_mu_, mu_;
   std::condition_variable cv_, cv_done_;
   const std::function<void(int)>* fn_ = nullptr;
   int n_ = 0, done_ = 0;
-  std::atomic<int> next_{0};
-  uint64_t gen_ = 0;
+  bool stop_ = false;
+  std::atomic<uint64_t> next_{0};
+  uint32_t gen_ = 0;
 };
 
 // The population's programs in one pass over the trees: the plain program and, when the population
@@ -592,8 +625,12 @@ void choose_derived_t(srhip_program& P) {
     if (n.degree != 1) continue;
     // node tables are per tree with tree-relative child indices: find the child in this tree
     const int32_t t = (int32_t)(std::upper_bound(P.offsets.begin(), P.offsets.end(), i) - P.offsets.begin()) - 1;
+    // (this pass runs before the trees are validated: a malformed child or operator index is skipped
+    // here and rejected by the compiler's validation with SRHIP_ERR_INVALID)
+    if (t < 0 || t >= P.ntrees || n.l < 0 || n.l >= P.offsets[t + 1] - P.offsets[t]) continue;
+    if (n.op < 1 || (size_t)n.op > P.unaops.size()) continue;
     const srhip_node& c = P.nodes[P.offsets[t] + n.l];
-    if (c.degree != 0 || c.constant) continue;
+    if (c.degree != 0 || c.constant || c.feature < 1) continue;
     const int u = classify_unop(P.unaops[n.op - 1]);
     if (!un_derivable(u)) continue;
     const uint32_t key = ((uint32_t)u << 16) | (uint32_t)(c.feature - 1);

@@ -436,7 +436,9 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
     phase[t] = INIT;
   };
   auto finish_start = [&](int32_t t) {
-    if (f[t] < best_f[t]) {  // src/ConstantOptimization.jl:62-64
+    // the first start is `result` unconditionally (:50); a restart replaces it only if strictly
+    // better (:65-67)
+    if (start[t] == 0 || f[t] < best_f[t]) {
       best_f[t] = f[t];
       for (int64_t k = coff[t]; k < coff[t + 1]; ++k) best_x[k] = x[k];
     }
@@ -975,9 +977,10 @@ int optimize_split(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, co
 
 extern "C" {
 
-int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
-                             const int64_t* idx, int64_t nidx, const srhip_optim_options* opt, double* out_loss,
-                             uint8_t* out_improved, int64_t* out_fcalls) {
+int srhip_optimize_constants_starts(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P,
+                                    const srhip_loss* loss, const int64_t* idx, int64_t nidx,
+                                    const srhip_optim_options* opt, const double* starts_in, double* starts_out,
+                                    double* out_loss, uint8_t* out_improved, int64_t* out_fcalls) {
   if (!opt || !out_loss || !out_improved) return fail(SRHIP_ERR_INVALID, "null argument");
   if (opt->iterations < 0 || opt->nrestarts < 0) return fail(SRHIP_ERR_INVALID, "negative iterations / restarts");
   int rc = check_eval_args(ctx, ds, P, MODE_LOSS, loss);
@@ -1010,10 +1013,30 @@ int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_prog
   if (!trees.empty()) {
     // the starting points: x0, then nrestarts perturbed copies drawn start-major, then tree, then
     // constant (src/ConstantOptimization.jl:53-60: c * (1 + randn/2))
+    // Float32 trees perturb in T as the reference does (node.val * (T(1) + T(1//2) * randn(T))):
+    // a Float32 normal draw and Float32 arithmetic, the start rounded like the constant it replaces.
+    // Caller-supplied starts (starts_in, [nrestarts][sum nconst]) replace the draws; a Float32
+    // program rounds them to Float32.  Trees without constants or failing statically keep x0.
     std::vector<std::vector<double>> starts(opt->nrestarts + 1, x0);
+    const bool f32 = P->dtype == SRHIP_F32;
+    const int64_t nall = (int64_t)x0.size();
     for (int start = 1; start <= opt->nrestarts; ++start)
       for (int32_t t : trees)
-        for (int64_t k = coff[t]; k < coff[t + 1]; ++k) starts[start][k] = x0[k] * (1.0 + 0.5 * randn(rng));
+        for (int64_t k = coff[t]; k < coff[t + 1]; ++k) {
+          double xs;
+          if (starts_in) {
+            xs = starts_in[(int64_t)(start - 1) * nall + k];
+          } else if (f32) {
+            const float r = (float)randn(rng);
+            xs = (double)((float)x0[k] * (1.0f + 0.5f * r));
+          } else {
+            xs = x0[k] * (1.0 + 0.5 * randn(rng));
+          }
+          starts[start][k] = f32 ? (double)(float)xs : xs;
+        }
+    if (starts_out)
+      for (int start = 1; start <= opt->nrestarts; ++start)
+        std::copy(starts[start].begin(), starts[start].end(), starts_out + (int64_t)(start - 1) * nall);
     const double tb = now_s();
     g_t_compile = g_t_eval = g_t_host = 0.0;
     g_patch_scan_s = g_patch_copy_s = 0.0;
@@ -1041,6 +1064,9 @@ int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_prog
       upload_program(*P);
       return rc;
     }
+  } else if (starts_out) {
+    for (int start = 1; start <= opt->nrestarts; ++start)
+      std::copy(x0.begin(), x0.end(), starts_out + (int64_t)(start - 1) * (int64_t)x0.size());
   }
   // accept where the best minimum beats the baseline (:70-78)
   std::vector<double> final_x = x0;
@@ -1064,6 +1090,13 @@ int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_prog
   if (out_fcalls)
     for (int32_t t = 0; t < nt; ++t) out_fcalls[t] = fcalls[t] + out_improved[t];
   return SRHIP_OK;
+}
+
+int srhip_optimize_constants(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
+                             const int64_t* idx, int64_t nidx, const srhip_optim_options* opt, double* out_loss,
+                             uint8_t* out_improved, int64_t* out_fcalls) {
+  return srhip_optimize_constants_starts(ctx, ds, P, loss, idx, nidx, opt, nullptr, nullptr, out_loss, out_improved,
+                                         out_fcalls);
 }
 
 }  // extern "C"

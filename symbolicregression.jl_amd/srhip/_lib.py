@@ -99,6 +99,8 @@ SIGNATURES = {
     "srhip_eval_grad_predict": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _vp]),
     "srhip_optimize_constants": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(Loss), _vp, _i64,
                                                 ctypes.POINTER(OptimOptions), _vp, _vp, _vp]),
+    "srhip_optimize_constants_starts": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(Loss), _vp, _i64,
+                                                       ctypes.POINTER(OptimOptions), _vp, _vp, _vp, _vp, _vp]),
     "srhip_batcher_create": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(Operators), ctypes.POINTER(Loss), _i32, _i32,
                                             ctypes.POINTER(_vp)]),
     "srhip_batcher_set_clients": (ctypes.c_int, [_vp, _i32]),

@@ -209,19 +209,29 @@ class Program:
                                                   ptr(pred), ptr(grad), ptr(ok)))
         return pred, np.split(grad, np.cumsum(rows)[:-1]), ok.astype(bool)
 
-    def optimize_constants(self, ds: DeviceDataset, loss, iterations=8, nrestarts=2, seed=0, g_tol=1e-8, idx=None):
+    def optimize_constants(self, ds: DeviceDataset, loss, iterations=8, nrestarts=2, seed=0, g_tol=1e-8, idx=None,
+                           starts=None, return_starts=False):
         """Batched optimize_constants; updates this program's constants in place.
 
-        Returns (loss[T] of the returned trees, improved[T], fcalls[T])."""
+        starts: optional [nrestarts, sum nconst] restart points (get_constants order, tree-major)
+        used instead of the library's draws.  Returns (loss[T] of the returned trees, improved[T],
+        fcalls[T]), plus the restart points used ([nrestarts, sum nconst]) if return_starts."""
         opt = _lib.OptimOptions(int(iterations), int(nrestarts), int(seed) & (2**64 - 1), float(g_tol))
         out = np.empty(self.ntrees, dtype=np.float64)
         imp = np.empty(self.ntrees, dtype=np.uint8)
         fc = np.empty(self.ntrees, dtype=np.int64)
         ls = loss.c_struct()
         idxa = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
-        check(_lib.load().srhip_optimize_constants(self.ctx.handle, ds.handle, self.handle, ctypes.byref(ls), ptr(idxa),
-                                                   0 if idxa is None else len(idxa), ctypes.byref(opt), ptr(out),
-                                                   ptr(imp), ptr(fc)))
+        nall = int(self.num_constants().sum())
+        sin = None
+        if starts is not None:
+            sin = np.ascontiguousarray(starts, dtype=np.float64).reshape(int(nrestarts), nall)
+        sout = np.empty((int(nrestarts), nall), dtype=np.float64) if return_starts else None
+        check(_lib.load().srhip_optimize_constants_starts(
+            self.ctx.handle, ds.handle, self.handle, ctypes.byref(ls), ptr(idxa), 0 if idxa is None else len(idxa),
+            ctypes.byref(opt), ptr(sin), ptr(sout), ptr(out), ptr(imp), ptr(fc)))
+        if return_starts:
+            return out, imp.astype(bool), fc, sout
         return out, imp.astype(bool), fc
 
     # ---- row-sharded evaluation (include/srhip.h "row-sharded evaluation") ----------------------

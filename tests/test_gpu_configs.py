@@ -192,11 +192,15 @@ def test_c4_gradient_vs_oracle_differences(ctx, oracle, c4):
 
 
 def test_c4_optimizer_outcome_vs_oracle(ctx, oracle, c4):
-    """C4's 512 trees, BFGS(8) / Newton + 2 restarts (the bench's call): never worse than the
-    baseline on any tree, improves most; and on a 32-tree sample, single start, the device optimum
-    equals the exact-gradient restatement's (oracle/optim.py optimize_constants_exact over the
-    oracle's dual-number gradient, row sums in the device's order) to 1e-12 relative on EVERY
-    sampled tree -- no exclusions."""
+    """C4's 512 trees, BFGS(8) / Newton + 2 restarts -- the bench's call itself (bench.py --config c4:
+    nrestarts=2, seed=7): never worse than the baseline on any tree, improves most; and on a 32-tree
+    sample the outcome equals the exact-gradient restatement's (oracle/optim.py
+    optimize_constants_exact over the oracle's dual-number gradient, row sums in the device's order)
+    run from the SAME three starts the device used (its own constants, then the two perturbed points
+    it reports) with the reference's selection (src/ConstantOptimization.jl:50-78: the first start's
+    result unless a restart is strictly better, accepted only if it beats the baseline): loss to
+    1e-12 relative, the improved flag, and the returned constants (1e-9) on EVERY sampled tree -- no
+    exclusions."""
     import optim
 
     sr = _sr()
@@ -204,25 +208,117 @@ def test_c4_optimizer_outcome_vs_oracle(ctx, oracle, c4):
     prog = sr.Program(ctx, nodes, offs, opts, np.float64)
     ds = sr.DeviceDataset(ctx, X, y)
     base, base_ok = prog.eval_loss(ds, sr.L2DistLoss())
-    out, improved, fcalls = prog.optimize_constants(ds, sr.L2DistLoss(), iterations=8, nrestarts=2, seed=7)
+    nconst = prog.num_constants().astype(np.int64)
+    coff = np.concatenate([[0], np.cumsum(nconst)])
+    out, improved, fcalls, starts = prog.optimize_constants(ds, sr.L2DistLoss(), iterations=8, nrestarts=2, seed=7,
+                                                           return_starts=True)
+    final = prog.get_constants()
     assert np.all(out[base_ok] <= base[base_ok] * (1 + 1e-12))
     assert improved.sum() >= 0.6 * base_ok.sum()
-    sample = [t for t in np.random.default_rng(10).permutation(len(offs) - 1) if base_ok[t]][:32]
-    sub_nodes = np.concatenate([nodes[offs[t]:offs[t + 1]] for t in sample])
-    sub_offs = np.concatenate([[0], np.cumsum([offs[t + 1] - offs[t] for t in sample])]).astype(np.int64)
-    sub = sr.Program(ctx, sub_nodes, sub_offs, opts, np.float64)
-    dl, _, _ = sub.optimize_constants(ds, sr.L2DistLoss(), iterations=8, nrestarts=0, seed=7)
+    sample = [t for t in np.random.default_rng(10).permutation(len(offs) - 1) if base_ok[t] and nconst[t] > 0][:32]
+    assert len(sample) == 32
 
-    def orc(u):
-        tn = sub_nodes[sub_offs[u]:sub_offs[u + 1]].copy()
-        return optim.optimize_constants_exact(tn, opts.binop_codes, opts.unaop_codes, X, y,
-                                               device_order=True)[1]
+    def orc(t):
+        tn = nodes[offs[t]:offs[t + 1]].copy()
+        x0 = np.array([tn[i]["val"] for i in _const_order(tn)], dtype=np.float64)
+        st = [x0] + [starts[r, coff[t]:coff[t + 1]] for r in range(starts.shape[0])]
+        return optim.optimize_constants_exact(tn, opts.binop_codes, opts.unaop_codes, X, y, starts=st,
+                                              device_order=True)
 
     with cf.ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
-        ref = list(ex.map(orc, range(len(sample))))
-    off = [(int(sample[u]), dl[u], ref[u], base[sample[u]]) for u in range(len(sample))
-           if not (dl[u] == ref[u] or abs(dl[u] - ref[u]) <= 1e-12 * max(abs(dl[u]), abs(ref[u])))]
+        ref = list(ex.map(orc, sample))
+    off = []
+    for t, (rx, rl, rimp, _) in zip(sample, ref):
+        t = int(t)
+        same_loss = out[t] == rl or abs(out[t] - rl) <= 1e-12 * max(abs(out[t]), abs(rl))
+        same_x = np.allclose(final[t], rx, rtol=1e-9, atol=0.0)
+        if not (same_loss and bool(improved[t]) == bool(rimp) and same_x):
+            off.append((t, out[t], rl, bool(improved[t]), bool(rimp), final[t], rx))
     assert not off, off
+
+
+def test_c4_restart_points_are_reported_and_replayable(ctx, c4):
+    """The restart points the device draws are x0 * (1 + randn/2) of the tree's own constants, and
+    handing the reported points back as caller-supplied starts reproduces the outcome bit for bit."""
+    sr = _sr()
+    opts, X, y, _, nodes, offs = c4
+    sub = [int(t) for t in range(64)]
+    sn = np.concatenate([nodes[offs[t]:offs[t + 1]] for t in sub])
+    so = np.concatenate([[0], np.cumsum([offs[t + 1] - offs[t] for t in sub])]).astype(np.int64)
+    ds = sr.DeviceDataset(ctx, X, y)
+    a = sr.Program(ctx, sn, so, opts, np.float64)
+    x0 = np.concatenate(a.get_constants())
+    oa, ia, fa, st = a.optimize_constants(ds, sr.L2DistLoss(), nrestarts=2, seed=3, return_starts=True)
+    assert st.shape == (2, len(x0))
+    ratio = st[:, x0 != 0] / x0[x0 != 0]
+    assert np.all(np.isfinite(ratio)) and abs(float(np.mean(ratio)) - 1.0) < 0.2 and 0.3 < float(np.std(ratio)) < 0.7
+    b = sr.Program(ctx, sn, so, opts, np.float64)
+    ob, ib, fb, st2 = b.optimize_constants(ds, sr.L2DistLoss(), nrestarts=2, seed=999, starts=st, return_starts=True)
+    assert np.array_equal(st, st2)
+    assert np.array_equal(oa, ob) and np.array_equal(ia, ib) and np.array_equal(fa, fb)
+    assert all(np.array_equal(u, v) for u, v in zip(a.get_constants(), b.get_constants()))
+
+
+def test_c4_restart_selection_float32(ctx):
+    """Float32 restart path: the library perturbs in Float32 (val * (1f + 0.5f randn), rounded to
+    Float32), and the outcome with nrestarts=2 is the reference's selection over the three single-start
+    runs the device makes from the same points (src/ConstantOptimization.jl:50-78): the first start's
+    result unless a restart's minimum is strictly smaller, kept only if it beats the baseline.  The
+    single-start runs are pinned separately (test_batched_optimizer_equals_per_tree)."""
+    sr = _sr()
+    opts = sr.Options(binary_operators=("+", "-", "*", "/"), unary_operators=("cos", "exp"))
+    rng = np.random.default_rng(21)
+    X = rng.standard_normal((3, 20000)).astype(np.float32)
+    y = (2.1 * np.cos(1.3 * X[0]) + 0.7 * X[1] * X[2] - 0.4).astype(np.float32)
+    trees = sr.random_population(96, opts, 3, np.float32, seed=22, max_size=16)
+    nodes, offs = sr.flatten(trees, opts, np.float32)
+    ds = sr.DeviceDataset(ctx, X, y)
+    loss = sr.L2DistLoss()
+    p = sr.Program(ctx, nodes, offs, opts, np.float32)
+    x0 = [c.copy() for c in p.get_constants()]
+    base, base_ok = p.eval_loss(ds, loss)
+    out, imp, fc, st = p.optimize_constants(ds, loss, nrestarts=2, seed=5, return_starts=True)
+    assert np.array_equal(st, st.astype(np.float32).astype(np.float64))  # Float32 points
+    nconst = np.array([len(c) for c in x0])
+    coff = np.concatenate([[0], np.cumsum(nconst)])
+    res = []  # (minimum, constants) per start, single-start device runs from each point
+    for s in range(3):
+        q = sr.Program(ctx, nodes, offs, opts, np.float32)
+        if s > 0:
+            q.set_constants(st[s - 1])
+        # the minimum of a single start: run without acceptance against the baseline by reading the
+        # optimiser's best point and re-evaluating it
+        ql, qi, _ = q.optimize_constants(ds, loss, nrestarts=0, seed=0)
+        res.append((ql, qi, [c.copy() for c in q.get_constants()]))
+    final = p.get_constants()
+    checked = 0
+    for t in range(len(nconst)):
+        if nconst[t] == 0 or not base_ok[t]:
+            continue
+        # a single-start run from point s keeps its own start unless its minimum beats that start's
+        # loss, so its reported loss is min(start loss, minimum); only trees where every start's run
+        # improved on its own start expose the minimum itself
+        if not all(res[s][1][t] for s in range(3)):
+            continue
+        mins = [res[s][0][t] for s in range(3)]
+        # (the reported minima are the evaluator's re-scores, within 1e-6 of the optimiser's own
+        # objective values for Float32: near-ties are not decidable from outside and are skipped)
+        if any(abs(mins[a] - mins[b]) <= 1e-5 * max(abs(mins[a]), abs(mins[b])) for a in range(3) for b in range(a)):
+            continue
+        if abs(min(mins) - base[t]) <= 1e-5 * abs(base[t]):
+            continue
+        best = 0
+        for s in (1, 2):
+            if mins[s] < mins[best]:
+                best = s
+        if mins[best] < base[t]:
+            assert imp[t], t
+            assert np.array_equal(final[t], res[best][2][t]), (t, best, final[t], res[best][2][t])
+        else:
+            assert not imp[t], t
+            assert np.array_equal(final[t], x0[t])
+        checked += 1
+    assert checked >= 20, checked
 
 
 def test_c5_int32_population_1m_rows_bit_exact(ctx, oracle):

@@ -37,3 +37,51 @@ def test_concurrent_host_compiles_agree():
     assert not errs, errs
     assert len(out) == 12 and all(o == ref for o in out)
     assert ref[4], "the C2 population has derived columns"
+
+
+def test_malformed_node_tables_are_rejected_cleanly():
+    """A bad child index or a bad unary operator index in a node table (C ABI / coalescer clients)
+    is a clean SRHIP_ERR_INVALID, never an out-of-bounds read -- including in the derived-column
+    pass that scans the tables before the trees are validated."""
+    import pytest
+    import srhip as sr
+    from srhip import _lib
+
+    opts = sr.Options(binary_operators=("+", "*"), unary_operators=("cos", "exp"))
+    # cos(x1) + cos(x1) twice over, so cos(x1) is a derived-column candidate
+    good = [sr.Node(1, sr.Node(1, sr.Node(feature=1)), sr.Node(1, sr.Node(feature=1))) for _ in range(3)]
+    nodes, offs = sr.flatten(good, opts, np.float32)
+    sr.Program(None, nodes, offs, opts, np.float32)  # compiles
+    unary = np.nonzero(nodes["degree"] == 1)[0]
+    for field, bad in (("l", 1000), ("l", -3), ("op", 0), ("op", 77)):
+        nd = nodes.copy()
+        nd[unary[0]][field] = bad
+        with pytest.raises(_lib.SrhipError) as e:
+            sr.Program(None, nd, offs, opts, np.float32)
+        assert e.value.code == _lib.ERR_INVALID, (field, bad, e.value)
+
+
+def test_host_pool_back_to_back_jobs_from_many_threads():
+    """Many small compiles from several threads back to back (the host pool's jobs follow each other
+    closely, and callers that find it busy compile themselves): every result is the sequential one."""
+    import srhip as sr
+    from srhip import workloads
+
+    opts, _, _, _, nodes, offs = workloads.c2(0, 256, 4096)
+    ref = _stats(sr, sr.Program(None, nodes, offs, opts, np.float32))
+    out, errs = [], []
+
+    def work():
+        try:
+            for _ in range(40):
+                out.append(_stats(sr, sr.Program(None, nodes, offs, opts, np.float32)))
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work) for _ in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    assert len(out) == 240 and all(o == ref for o in out)
