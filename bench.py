@@ -133,6 +133,8 @@ def main():
         prog.eval_loss(ds, loss)
     from srhip import parallel
 
+    native = _native_comm(ctx, dist)
+
     # islands: every step's evaluation is followed by the migration exchange of its results (the
     # best args.migrate_k trees of every rank reach every rank: one all_gather_into_tensor over
     # RCCL), issued in flight and collected after the next step's evaluation -- the all-gather runs
@@ -150,7 +152,10 @@ def main():
         if dist is not None:
             if pending is not None:
                 pending.wait()
-            pending = parallel.migrate_topk_async(nodes, offs, l, args.migrate_k, 30)
+            if native is not None:  # libsrhip's RCCL communicator (srhip_comm_migrate_start)
+                pending = native.migrate_start(nodes, offs, l, args.migrate_k, 30)
+            else:
+                pending = parallel.migrate_topk_async(nodes, offs, l, args.migrate_k, 30)
     if pending is not None:
         pending.wait()
     barrier()
@@ -216,6 +221,11 @@ def main():
         dt_full, kern_full, fl_full, nr_full = timed_steps(prog)
         del os.environ["SRHIP_NO_EARLY_EXIT"]
 
+    # trees whose did_succeed needs the precise pass (the bound max|v| x rows reaches half the overflow
+    # threshold): srhip_eval_loss runs it for them inside every step
+    psums, pchk = prog.eval_loss_partials(ds, loss)
+    undecided = int(np.sum(prog.finalize(nfeat, psums, pchk)[2] == 2))
+
     # end-to-end per population (host compile of 1024 fresh trees + upload + eval)
     t0 = time.perf_counter()
     p2 = srhip.Program(ctx, nodes, offs, opts, np.float32)
@@ -257,9 +267,11 @@ def main():
             },
             # N > 1: the per-step migration exchange (parallel.migrate_topk), wall time on rank 0
             "collective": None if dist is None else {
-                "op": f"all_gather_into_tensor of each rank's {args.migrate_k} best trees (node tables + losses), "
+                "op": f"all-gather of each rank's {args.migrate_k} best trees (node tables + losses), "
                       f"in flight during the next step's evaluation",
-                "backend": dist.get_backend(), "ranks": world, "calls_per_step": coll_calls / args.steps,
+                "backend": "rccl (libsrhip srhip_comm_migrate_start/wait)" if native is not None
+                           else f"torch.distributed {dist.get_backend()} all_gather_into_tensor",
+                "ranks": world, "calls_per_step": coll_calls / args.steps,
                 "ms_per_step": coll_s * 1e3 / args.steps},
             "roofline": {
                 "bound": "valu",
@@ -284,6 +296,7 @@ def main():
             "cpu_baseline": cpu,
             "extra": {
                 "compile_ms_1024_trees": compile_ms, "end_to_end_ms_per_population": e2e_ms,
+                "undecided_trees_per_step": undecided,
                 # population scoring rate: every live tree's nodes x every row per step / step time (the
                 # rows a failed tree skipped counted as if evaluated)
                 "nominal_value": nominal_value,
@@ -298,9 +311,29 @@ def main():
             },
         }
         print(json.dumps(out))
+    if native is not None:
+        native.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _native_comm(ctx, dist):
+    """libsrhip's own RCCL communicator for the ranks' exchanges (parallel.NativeComm) when the ranks
+    run on distinct GPUs under the nccl backend; None otherwise (single rank, the gloo rehearsals on
+    one GPU -- RCCL cannot place two ranks on one device -- or SRHIP_BENCH_COMM=torch), and the
+    torch.distributed exchange is used."""
+    if dist is None or os.environ.get("SRHIP_BENCH_BACKEND", "nccl") != "nccl":
+        return None
+    if os.environ.get("SRHIP_BENCH_COMM", "native") != "native":
+        return None
+    from srhip import parallel
+
+    try:
+        return parallel.NativeComm.from_process_group(ctx)
+    except Exception as e:  # pragma: no cover - reported, the torch path takes over
+        print(f"[bench] native RCCL communicator unavailable ({e}); using torch.distributed", file=sys.stderr)
+        return None
 
 
 def bench_rowshard(args):
@@ -344,7 +377,11 @@ def bench_rowshard(args):
     st = prog.stats()
     nfeat = X.shape[0]
 
+    native = _native_comm(ctx, dist)
+
     def step():
+        if native is not None:  # srhip_eval_loss_sharded: partials, RCCL all-reduce, decision in the library
+            return native.eval_loss_sharded(prog, ds, loss)
         return parallel.eval_loss_sharded(prog, nfeat, lambda: prog.eval_loss_partials(ds, loss),
                                           precise=lambda tr: prog.eval_precise_partials(ds, tr))
 
@@ -383,9 +420,13 @@ def bench_rowshard(args):
             "nominal_value": st["total_nodes"] * n * args.steps / dt,
             "kernel_ms_max_over_ranks": kern_max,
             "collective": {"op": "all_reduce SUM (per-tree loss sums, feature stats) + all_reduce MAX (check "
-                                 "statistics) on one buffer", "backend": dist.get_backend(), "ranks": world,
+                                 "statistics) on one buffer",
+                           "backend": "rccl (libsrhip srhip_eval_loss_sharded)" if native is not None
+                                      else f"torch.distributed {dist.get_backend()}", "ranks": world,
                            "ms_per_step_max_over_ranks": coll_max * 1e3 / args.steps},
         }))
+    if native is not None:
+        native.close()
     dist.barrier()
     dist.destroy_process_group()
 
@@ -450,13 +491,19 @@ def cpu_baseline(nodes, offs, opts, X, y, target_s):
     t0 = time.perf_counter()
     _, _, _, used = oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, Xs, ys, nthreads=threads)
     dt = time.perf_counter() - t0
+    # the work definition of `value`: node-rows actually evaluated -- the oracle stops a failed tree at
+    # its first failed check (DynamicExpressions' early return) as the device stops it at its failing tile
+    done = oracle.eval_loss_batch.last_node_rows
     return {
-        "value": nodes_total * m2 / dt,
+        "value": done / dt,
         "unit": "node-row evals/s",
         "cores": int(used),
         "kind": "port",
+        "nominal_value": nodes_total * m2 / dt,
+        "evaluated_fraction": done / (nodes_total * m2),
         "sample": f"all {len(offs) - 1} trees x first {m2} of the 1M rows ({dt:.1f} s), oracle/sr_oracle.c "
-                  f"array-at-a-time restatement, OpenMP over trees",
+                  f"array-at-a-time restatement, OpenMP over trees on {int(used)} threads (the job's core "
+                  f"allotment); value counts the node-rows evaluated before each failed tree's early return",
     }
 
 
@@ -680,12 +727,14 @@ def bench_search(args):
 
 
 def _oracle_scorer_factory(worker, dataset, options):
-    """cpu_baseline leg of c1 under --parallelism multiprocessing: each worker scores with the oracle."""
+    """cpu_baseline legs of c1 / c3: each worker process scores with the oracle (bench only)."""
     return _OracleScorer(dataset, options)
 
 
 class _OracleScorer:
-    """score_func through the oracle (bench cpu_baseline only)."""
+    """score_func through the oracle, and optimize_constants through oracle/optim.py's reference
+    procedure (finite-difference BFGS / Newton + BackTracking) -- the search's whole host-side
+    workload on the CPU (bench cpu_baseline only)."""
 
     def __init__(self, d, o):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -704,54 +753,67 @@ class _OracleScorer:
         return srhip.loss_to_score(loss, self.d.use_baseline, self.d.baseline_loss, tree, self.o,
                                    complexity), loss
 
+    def optimize_constants(self, dataset, members, options, rng=None):
+        """api.optimize_constants' contract (src/ConstantOptimization.jl:11-81) with the oracle's
+        finite-difference optimiser: improved members get the new constants, loss, score, birth."""
+        import numpy as np
+
+        import optim
+        import srhip
+        from srhip.node import set_constants
+        from srhip.utils import get_birth_order
+
+        single = not isinstance(members, (list, tuple))
+        ml = [members] if single else list(members)
+        rng = np.random.default_rng() if rng is None else rng
+        ne = 0.0
+        L = dataset.loss_type.type
+        for m in ml:
+            tree = m.tree if hasattr(m, "tree") else m
+            nodes, _ = srhip.flatten([tree], options, dataset.X.dtype)
+            x, f, improved = optim.optimize_constants(nodes, options.binop_codes, options.unaop_codes, dataset.X,
+                                                      dataset.y, iterations=options.optimizer_iterations,
+                                                      nrestarts=options.optimizer_nrestarts, rng=rng)
+            ne += 1.0
+            if not improved:
+                continue
+            set_constants(tree, x)
+            if hasattr(m, "tree"):
+                m.loss = L(f)
+                m.score = srhip.loss_to_score(m.loss, dataset.use_baseline, dataset.baseline_loss, m, options)
+                if hasattr(m, "birth"):
+                    m.birth = get_birth_order()
+        return (ml[0] if single else ml), ne
+
 
 def cpu_search_baseline(args, c1, X, y, opts, iters, gpu_dt, skw=None):
-    """c1: the same search (same options and seed, same island parallelism) with the oracle scorer on
-    the host, over the device run's iterations (threaded islands; 1 iteration with worker processes); c3: the
-    oracle's multithreaded population eval on a row sample."""
+    """The same search (options, seed, populations, iterations) with the whole host workload on the
+    CPU: every island's iteration in a worker process (the reference's :multiprocessing, over all
+    the cores this job may use), scoring with the oracle (oracle/sr_oracle.c) and optimising
+    constants with oracle/optim.py's finite-difference reference procedure.  c1 on its 100 rows;
+    c3 on the first 100k of the 10M rows (a bounded sample: the oracle's array-at-a-time cost per
+    node-row does not depend on the row count).  value = node-rows scored per second (the same
+    definition as the device line's)."""
     import numpy as np
 
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
     import srhip
     from srhip import search as S
 
-    if c1:
-        d = srhip.Dataset(X, y)
-        d.baseline_loss, d.use_baseline = float(np.mean((y - y.mean()) ** 2)), True
-        if skw:
-            # same worker processes, each scoring with the oracle (constant optimisation stays on the device)
-            t0 = time.perf_counter()
-            res = S.equation_search(d, None, opts, niterations=1, scorer_factory=_oracle_scorer_factory, **skw)
-            dt = time.perf_counter() - t0
-            return {"value": res.node_rows / dt, "unit": "node-row evals/s", "cores": skw["procs"], "kind": "port",
-                    "sample": f"1 iteration of the same search in {skw['procs']} worker processes with the oracle "
-                              f"(oracle/sr_oracle.c) as every worker's scorer, {dt:.1f} s"}
-        # the same iterations as the device run: tree sizes grow over a search, and the oracle's cost
-        # per evaluation grows with them while the device's (latency-bound at 100 rows) does not
-        sc = _OracleScorer(d, opts)
-        t0 = time.perf_counter()
-        S.equation_search(d, None, opts, niterations=iters, scorer=sc)
-        dt = time.perf_counter() - t0
-        return {"value": sc.node_rows / dt, "unit": "node-row evals/s", "cores": 1, "kind": "port",
-                "sample": f"{iters} iteration(s) of the same search (20 populations, Python islands) with the "
-                          f"oracle (oracle/sr_oracle.c) as scorer, {dt:.1f} s"}
-    from srhip import workloads
-
-    _, trees, nodes, offs = workloads.c3_population(opts)
-    threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1), os.cpu_count() or 1)
-    m = 100_000
+    cores = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1), os.cpu_count() or 1)
+    m = X.shape[1] if c1 else min(X.shape[1], 100_000)
+    Xs, ys = (X, y) if c1 else (X[:, :m].copy(), y[:m].copy())
+    d = srhip.Dataset(Xs, ys)
+    npops = S.search_option(opts, "populations")
+    procs = max(1, min(npops, cores))
     t0 = time.perf_counter()
-    oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, X[:, :m].copy(), y[:m].copy(),
-                           nthreads=threads)
-    m = int(min(X.shape[1], max(m, m * args.cpu_seconds / max(time.perf_counter() - t0, 1e-6))))
-    t0 = time.perf_counter()
-    _, _, _, used = oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, X[:, :m].copy(),
-                                           y[:m].copy(), nthreads=threads)
+    res = S.equation_search(d, None, opts, niterations=iters, parallelism="multiprocessing", procs=procs,
+                            worker_backend="host", scorer_factory=_oracle_scorer_factory)
     dt = time.perf_counter() - t0
-    return {"value": int(offs[-1]) * m / dt, "unit": "node-row evals/s", "cores": int(used), "kind": "port",
-            "sample": f"oracle population eval: 64 random trees (size <= 20) x first {m} rows ({dt:.1f} s), "
-                      f"OpenMP over trees"}
+    return {"value": res.node_rows / dt, "unit": "node-row evals/s", "cores": procs, "kind": "port",
+            "sample": f"the same search ({npops} populations, {iters} iteration(s), seed) over "
+                      f"{'all 100' if c1 else f'the first {m} of the {X.shape[1]}'} rows in {procs} worker "
+                      f"processes: oracle/sr_oracle.c scores, oracle/optim.py finite-difference constant "
+                      f"optimisation, {dt:.1f} s wall"}
 
 
 if __name__ == "__main__":

@@ -210,6 +210,42 @@ int srhip_precise_finalize(const srhip_program* prog, const int32_t* trees, int3
 int srhip_chk_reduce_op(int dtype);
 int32_t srhip_program_max_ops(const srhip_program* prog);
 
+/* ---- multi-GPU exchanges on RCCL (csrc/srhip_comm.cpp; one process per GPU) ------------------
+ * Replace the reference's head-node copies between worker processes (Distributed over TCP,
+ * src/SearchUtils.jl:108-127): migration (src/Migration.jl:16-38, applied at
+ * src/SymbolicRegression.jl:933-943) becomes one all-gather of hall-of-fame / best_sub_pop node
+ * tables over xGMI, and row shards combine their partials with one all-reduce.
+ * Setup: rank 0 calls srhip_comm_unique_id and broadcasts the SRHIP_COMM_ID_BYTES bytes with the
+ * job's launcher; every rank then calls srhip_comm_create with its context (collective: all ranks
+ * must call it concurrently).  A communicator owns a HIP stream on its context's device; one
+ * exchange at a time (srhip_comm_migrate_start ... srhip_comm_migrate_wait). */
+typedef struct srhip_comm srhip_comm;
+enum { SRHIP_COMM_ID_BYTES = 128 };
+enum { SRHIP_REDUCE_SUM = 0, SRHIP_REDUCE_MAX = 1 };
+int srhip_comm_unique_id(uint8_t* out_id /* [SRHIP_COMM_ID_BYTES] */);
+int srhip_comm_create(srhip_ctx* ctx, const uint8_t* id, int32_t nranks, int32_t rank, srhip_comm** out);
+void srhip_comm_destroy(srhip_comm* comm);
+int srhip_comm_size(const srhip_comm* comm, int32_t* nranks, int32_t* rank);
+/* In-place all-reduce of a host float64 vector (staged through the communicator's device buffer). */
+int srhip_comm_allreduce_f64(srhip_comm* comm, double* buf, int64_t n, int32_t op);
+/* Fixed-size all-gather: recv[r * bytes .. (r + 1) * bytes) = rank r's send. */
+int srhip_comm_allgather(srhip_comm* comm, const void* send, int64_t bytes, void* recv);
+/* Migration: this rank's k best trees of (nodes, offsets[ntrees+1], losses[ntrees]) -- by loss,
+ * non-finite last, ties by index; trees longer than max_nodes skipped -- packed into one fixed-size
+ * payload and all-gathered (issued on the communicator's stream; returns at once).  _wait collects it:
+ * out_counts[nranks] trees per rank, out_offsets[nranks][k+1] node offsets within each rank's
+ * out_nodes[nranks][k * max_nodes] records, out_losses[nranks][k] (any output may be NULL). */
+int srhip_comm_migrate_start(srhip_comm* comm, const srhip_node* nodes, const int64_t* offsets,
+                             int32_t ntrees, const double* losses, int32_t k, int32_t max_nodes);
+int srhip_comm_migrate_wait(srhip_comm* comm, int32_t* out_counts, int64_t* out_offsets,
+                            double* out_losses, srhip_node* out_nodes);
+/* Row-sharded eval_loss: ds holds THIS rank's rows (every rank the same features); runs steps 1-4
+ * above with the all-reduces on RCCL; out_loss / out_ok identical on every rank.  With one rank it
+ * equals srhip_eval_loss bit for bit. */
+int srhip_eval_loss_sharded(srhip_ctx* ctx, srhip_comm* comm, const srhip_dataset* ds,
+                            const srhip_program* prog, const srhip_loss* loss, const int64_t* idx,
+                            int64_t nidx, double* out_loss, uint8_t* out_ok);
+
 /* ---- constant optimisation (src/ConstantOptimization.jl) ------------------------------------ */
 /* Loss and its exact gradient with respect to every tree's constants (forward-mode dual numbers
  * on the device), for every tree of prog: out_loss[T] (+Inf where did_succeed fails; as eval_loss,

@@ -377,8 +377,78 @@ SRM_FN float srm_trigf(int kind, float x) {
   const int n = srm_rem_pio2f(x, &y);
   return srm_trigf_finish(kind, n, y);
 }
+/* ---- Julia's own Float32 sin / cos (SRHIP_JULIA_TRIG builds; DESIGN.md 4 "Float32 trig") --------
+ * Julia Base.Math evaluates sin(x::Float32) / cos(x::Float32) (base/special/trig.jl, rem_pio2.jl) as
+ * FreeBSD msun's s_sinf.c / s_cosf.c do: |x| < Float32(pi)/4 -> the kernel of x itself (sin: x below
+ * sqrt(eps(Float32)); cos: 1 below sqrt(eps(Float32)/2)); otherwise (n, y) = rem_pio2_kernel(x) in
+ * Float64 -- n = +-1..+-4 with y = xd -+ k pi/2 (pi/2, pi, pi*3/2, pi*4/2 as Julia computes them in
+ * Float64) for |x| <= 9pi/4, Cody-Waite with a 33 + 53-bit pi/2 below 2^28 pi/2, Payne-Hanek above --
+ * and the quadrant n & 3 picks __kernel_sindf or __kernel_cosdf (k_sinf.c / k_cosf.c coefficients,
+ * evaluated as written: no contraction), rounded once to Float32.  Restated from those published
+ * sources; Julia cannot run here, so bits against Julia itself stay unpinned. */
+SRM_FN double srm_jsin_kernel(double y) {
+  const double S1 = -0x15555554cbac77.0p-55, S2 = 0x111110896efbb2.0p-59, S3 = -0x1a00f9e2cae774.0p-65,
+               S4 = 0x16cd878c3b46a7.0p-71;
+  const double z = y * y, w = z * z, r = S3 + z * S4, s = z * y;
+  return (y + s * (S1 + z * S2)) + s * w * r;
+}
+SRM_FN double srm_jcos_kernel(double y) {
+  const double C0 = -0x1ffffffd0c5e81.0p-54, C1 = 0x155553e1053a42.0p-57, C2 = -0x16c087e80f1e27.0p-62,
+               C3 = 0x199342e0ee5069.0p-68;
+  const double z = y * y, w = z * z, r = C2 + z * C3;
+  return ((1.0 + z * C0) + w * C1) + (w * z) * r;
+}
+/* rem_pio2_kernel(x::Float32): n, y for |x| >= Float32(pi)/4, x finite */
+SRM_FN int srm_jrem_pio2f(float x, double* y) {
+  const double pi = 3.141592653589793;
+  const double xd = (double)x, ax = __builtin_fabs(xd);
+  if (ax <= pi * 5 / 4) {
+    if (ax <= pi * 3 / 4) { *y = x > 0 ? xd - pi / 2 : xd + pi / 2; return x > 0 ? 1 : -1; }
+    *y = x > 0 ? xd - pi : xd + pi;
+    return x > 0 ? 2 : -2;
+  }
+  if (ax <= pi * 9 / 4) {
+    if (ax <= pi * 7 / 4) { *y = x > 0 ? xd - pi * 3 / 2 : xd + pi * 3 / 2; return x > 0 ? 3 : -3; }
+    *y = x > 0 ? xd - pi * 4 / 2 : xd + pi * 4 / 2;
+    return x > 0 ? 4 : -4;
+  }
+  if (ax < 421657440.0) { /* Float32(pi)/2 * 2f0^28 */
+    const double pio2_1 = 1.57079631090164184570e+00, pio2_1t = 1.58932547735281966916e-08,
+                 inv_pio2 = 6.36619772367581382433e-01;
+    const double fn = srm_rint(xd * inv_pio2);
+    const double r = xd - fn * pio2_1, w = fn * pio2_1t;
+    *y = r - w;
+    return (int)fn;
+  }
+  return srm_rem_pio2f_big(xd, y);
+}
+/* kind 0: cos, 1: sin (Inf / NaN -> NaN: Julia throws a DomainError for Inf, which the
+ * evaluator never reaches -- a non-finite operand fails the tree first) */
+SRM_FN float srm_jtrigf(int kind, float x) {
+  if (!(x - x == 0.0f)) return x - x;
+  const float ax = __builtin_fabsf(x);
+  if (ax < 0.78539819f) { /* Float32(pi)/4 */
+    if (kind == 1) return ax < 3.4526698e-4f ? x : (float)srm_jsin_kernel((double)x); /* sqrt(eps(Float32)) */
+    return ax < 2.44140625e-4f ? 1.0f : (float)srm_jcos_kernel((double)x);             /* sqrt(eps(Float32)/2) */
+  }
+  double y;
+  const int n = srm_jrem_pio2f(x, &y) & 3;
+  const int q = kind == 0 ? n : (n + 3) & 3; /* sin in quadrant n = cos in quadrant n - 1 */
+  if (q == 0) return (float)srm_jcos_kernel(y);
+  if (q == 1) return (float)-srm_jsin_kernel(y);
+  if (q == 2) return (float)-srm_jcos_kernel(y);
+  return (float)srm_jsin_kernel(y);
+}
+#ifndef SRHIP_JULIA_TRIG
+#define SRHIP_JULIA_TRIG 0
+#endif
+#if SRHIP_JULIA_TRIG
+SRM_FN float srm_cosf(float x) { return srm_jtrigf(0, x); }
+SRM_FN float srm_sinf(float x) { return srm_jtrigf(1, x); }
+#else
 SRM_FN float srm_cosf(float x) { return srm_trigf(0, x); }
 SRM_FN float srm_sinf(float x) { return srm_trigf(1, x); }
+#endif
 SRM_FN float srm_tanf(float x) { return srm_trigf(2, x); }
 /* Float32 exp: Julia Base.Math exp_impl(x::Float32, Val(:e)) (base/special/exp.jl, Julia >= 1.7), a
  * Float32 algorithm (unlike Float32 sin / cos, which Julia evaluates in Float64): N = round(x log2 e)

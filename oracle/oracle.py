@@ -95,12 +95,14 @@ def eval_loss_batch(nodes, offsets, binops, unaops, X, y, w=None, kind=0, p0=0.0
     le = np.empty(nt, dtype=np.float64)
     lr = np.empty(nt, dtype=np.float64)
     ok = np.empty(nt, dtype=np.uint8)
-    fn = _setup(getattr(lib, f"oracle_eval_loss_batch_{sfx}"), ctypes.c_int,
+    nr = np.zeros(nt, dtype=np.int64)
+    fn = _setup(getattr(lib, f"oracle_eval_loss_batch_work_{sfx}"), ctypes.c_int,
                 [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double,
-                 ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p])
+                 ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p])
     used = fn(_p(nodes), _p(offsets), nt, _p(b), _p(u), _p(X), _p(y), _p(w), n, int(kind), float(p0),
-              int(nthreads), _p(le), _p(lr), _p(ok))
+              int(nthreads), _p(le), _p(lr), _p(ok), _p(nr))
+    eval_loss_batch.last_node_rows = int(nr.sum())  # node-rows evaluated (the early return stops a failed tree)
     return le, lr, ok.astype(bool), used
 
 
@@ -160,7 +162,7 @@ def scalar_un(op, x, dtype):
     return np.dtype(dtype).type(fn(int(op), ct(x)))
 
 
-_SRM = {"exp": 0, "log": 1, "sin": 2, "cos": 3, "tan": 4}
+_SRM = {"exp": 0, "log": 1, "sin": 2, "cos": 3, "tan": 4, "jsin": 5, "jcos": 6}  # j*: Julia's Float32 sin / cos restated (srm_jtrigf)
 
 
 def srm(name, x):

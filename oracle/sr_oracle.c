@@ -335,6 +335,8 @@ void oracle_srm_f32(int which, const float* x, float* y, int64_t n) {
       case 1: y[i] = srm_logf(x[i]); break;
       case 2: y[i] = srm_sinf(x[i]); break;
       case 3: y[i] = srm_cosf(x[i]); break;
+      case 5: y[i] = srm_jtrigf(1, x[i]); break; /* Julia's Float32 sin (SRHIP_JULIA_TRIG restatement) */
+      case 6: y[i] = srm_jtrigf(0, x[i]); break; /* Julia's Float32 cos */
       default: y[i] = srm_tanf(x[i]); break;
     }
   }

@@ -24,7 +24,18 @@ typedef struct {
   const int32_t* unaops;
   const T* X; /* [nfeat][n] */
   int64_t n;
+  int64_t* done; /* nodes whose rows this evaluation produced (the early return stops it), or NULL */
 } CAT(Ctx, SFX);
+
+/* count `k` nodes evaluated over every row (cpu_baseline's work count: the reference's early
+ * return skips the nodes after the first failed check) */
+#define DONE(c, k) do { if ((c)->done) *(c)->done += (k); } while (0)
+static int64_t CAT(subtree_size_, SFX)(const srhip_node* nd, int64_t i) {
+  const srhip_node* n = &nd[i];
+  if (n->degree == 0) return 1;
+  if (n->degree == 1) return 1 + CAT(subtree_size_, SFX)(nd, n->l);
+  return 1 + CAT(subtree_size_, SFX)(nd, n->l) + CAT(subtree_size_, SFX)(nd, n->r);
+}
 
 typedef struct {
   T* x;
@@ -101,6 +112,7 @@ static CAT(Res, SFX) CAT(deg0_, SFX)(const CAT(Ctx, SFX) * c, const srhip_node* 
   CAT(Res, SFX) r;
   r.x = CAT(alloc_, SFX)(c->n);
   r.ok = 1;
+  DONE(c, 1);
   if (n->constant) {
     const T v = CAT(leaf_val_, SFX)(n);
     for (int64_t j = 0; j < c->n; ++j) r.x[j] = v;
@@ -141,6 +153,7 @@ static CAT(Res, SFX) CAT(dispatch_deg1_, SFX)(const CAT(Ctx, SFX) * c, int64_t i
       const T xl = CAT(bin_, SFX)(op_l, CAT(leafrow_, SFX)(c, ll, j), CAT(leafrow_, SFX)(c, lr, j));
       r.x[j] = NONFINITE(xl) ? INF_T : CAT(un_, SFX)(op, xl);
     }
+    DONE(c, 4);
     return r;
   }
   if (l->degree == 1 && c->nd[l->l].degree == 0) {
@@ -155,6 +168,7 @@ static CAT(Res, SFX) CAT(dispatch_deg1_, SFX)(const CAT(Ctx, SFX) * c, int64_t i
       const T xl = CAT(un_, SFX)(op_l, CAT(leafrow_, SFX)(c, ll, j));
       r.x[j] = NONFINITE(xl) ? INF_T : CAT(un_, SFX)(op, xl);
     }
+    DONE(c, 3);
     return r;
   }
   /* op(x) for any x */
@@ -165,6 +179,7 @@ static CAT(Res, SFX) CAT(dispatch_deg1_, SFX)(const CAT(Ctx, SFX) * c, int64_t i
     return r;
   }
   for (int64_t j = 0; j < c->n; ++j) r.x[j] = CAT(un_, SFX)(op, r.x[j]);
+  DONE(c, 1);
   return r;
 }
 
@@ -182,6 +197,7 @@ static CAT(Res, SFX) CAT(dispatch_deg2_, SFX)(const CAT(Ctx, SFX) * c, int64_t i
     r.ok = 1;
     for (int64_t j = 0; j < c->n; ++j)
       r.x[j] = CAT(bin_, SFX)(op, CAT(leafrow_, SFX)(c, l, j), CAT(leafrow_, SFX)(c, rr, j));
+    DONE(c, 3);
     return r;
   }
   if (rr->degree == 0) {
@@ -197,6 +213,7 @@ static CAT(Res, SFX) CAT(dispatch_deg2_, SFX)(const CAT(Ctx, SFX) * c, int64_t i
       return L;
     }
     for (int64_t j = 0; j < c->n; ++j) L.x[j] = CAT(bin_, SFX)(op, L.x[j], CAT(leafrow_, SFX)(c, rr, j));
+    DONE(c, 2);
     return L;
   }
   if (l->degree == 0) {
@@ -212,6 +229,7 @@ static CAT(Res, SFX) CAT(dispatch_deg2_, SFX)(const CAT(Ctx, SFX) * c, int64_t i
       return R;
     }
     for (int64_t j = 0; j < c->n; ++j) R.x[j] = CAT(bin_, SFX)(op, CAT(leafrow_, SFX)(c, l, j), R.x[j]);
+    DONE(c, 2);
     return R;
   }
   CAT(Res, SFX) L = CAT(eval_, SFX)(c, n->l);
@@ -232,6 +250,7 @@ static CAT(Res, SFX) CAT(dispatch_deg2_, SFX)(const CAT(Ctx, SFX) * c, int64_t i
   }
   for (int64_t j = 0; j < c->n; ++j) L.x[j] = CAT(bin_, SFX)(op, L.x[j], R.x[j]);
   free(R.x);
+  DONE(c, 1);
   return L;
 }
 
@@ -246,26 +265,33 @@ static CAT(Res, SFX) CAT(eval_, SFX)(const CAT(Ctx, SFX) * c, int64_t i) {
     r.x = CAT(alloc_, SFX)(c->n);
     r.ok = 1;
     for (int64_t j = 0; j < c->n; ++j) r.x[j] = v;
+    DONE(c, CAT(subtree_size_, SFX)(c->nd, i));
     return r;
   }
   if (n->degree == 1) return CAT(dispatch_deg1_, SFX)(c, i);
   return CAT(dispatch_deg2_, SFX)(c, i);
 }
 
-/* eval_tree_array(tree, X, operators) -> (out, ok); X is [nfeat][n] (SoA). out may be NULL. */
-int CAT(oracle_eval_tree_, SFX)(const srhip_node* nodes, const int32_t* binops, const int32_t* unaops, const T* X,
-                                int64_t n, T* out) {
+/* eval_tree_array(tree, X, operators) -> (out, ok); X is [nfeat][n] (SoA). out may be NULL.
+ * *done (nullable) += the nodes evaluated over all rows before the result or the early return. */
+static int CAT(eval_tree_work_, SFX)(const srhip_node* nodes, const int32_t* binops, const int32_t* unaops,
+                                     const T* X, int64_t n, T* out, int64_t* done) {
   CAT(Ctx, SFX) c;
   c.nd = nodes;
   c.binops = binops;
   c.unaops = unaops;
   c.X = X;
   c.n = n;
+  c.done = done;
   CAT(Res, SFX) r = CAT(eval_, SFX)(&c, 0);
   int ok = r.ok && CAT(array_ok_, SFX)(r.x, n);
   if (out) memcpy(out, r.x, (size_t)n * sizeof(T));
   free(r.x);
   return ok;
+}
+int CAT(oracle_eval_tree_, SFX)(const srhip_node* nodes, const int32_t* binops, const int32_t* unaops, const T* X,
+                                int64_t n, T* out) {
+  return CAT(eval_tree_work_, SFX)(nodes, binops, unaops, X, n, out, NULL);
 }
 
 /* _eval_loss(tree, dataset, options; regularization=false):
@@ -273,11 +299,11 @@ int CAT(oracle_eval_tree_, SFX)(const srhip_node* nodes, const int32_t* binops, 
  *   loss_ref   = the reference's own order: sequential fold in T of l_i (mean), or
  *                sum(w .* l) / sum(w) with both sums folded sequentially in T
  * returns ok (did_succeed); losses are +Inf when !ok. */
-int CAT(oracle_eval_loss_, SFX)(const srhip_node* nodes, const int32_t* binops, const int32_t* unaops, const T* X,
-                                const T* y, const T* w, int64_t n, int loss_kind, double p0, double* loss_exact,
-                                double* loss_ref) {
+static int CAT(eval_loss_work_, SFX)(const srhip_node* nodes, const int32_t* binops, const int32_t* unaops,
+                                     const T* X, const T* y, const T* w, int64_t n, int loss_kind, double p0,
+                                     double* loss_exact, double* loss_ref, int64_t* done) {
   T* pred = CAT(alloc_, SFX)(n);
-  int ok = CAT(oracle_eval_tree_, SFX)(nodes, binops, unaops, X, n, pred);
+  int ok = CAT(eval_tree_work_, SFX)(nodes, binops, unaops, X, n, pred, done);
   if (!ok) {
     free(pred);
     if (loss_exact) *loss_exact = INFINITY;
@@ -317,13 +343,18 @@ int CAT(oracle_eval_loss_, SFX)(const srhip_node* nodes, const int32_t* binops, 
   free(pred);
   return 1;
 }
+int CAT(oracle_eval_loss_, SFX)(const srhip_node* nodes, const int32_t* binops, const int32_t* unaops, const T* X,
+                                const T* y, const T* w, int64_t n, int loss_kind, double p0, double* loss_exact,
+                                double* loss_ref) {
+  return CAT(eval_loss_work_, SFX)(nodes, binops, unaops, X, y, w, n, loss_kind, p0, loss_exact, loss_ref, NULL);
+}
 
 /* Batched: every tree of a population (threads across trees, as the reference's
  * :multithreading runs one task per population).  Returns the number of threads used. */
-int CAT(oracle_eval_loss_batch_, SFX)(const srhip_node* nodes, const int64_t* offsets, int32_t ntrees,
-                                      const int32_t* binops, const int32_t* unaops, const T* X, const T* y,
-                                      const T* w, int64_t n, int loss_kind, double p0, int nthreads,
-                                      double* loss_exact, double* loss_ref, uint8_t* ok) {
+int CAT(oracle_eval_loss_batch_work_, SFX)(const srhip_node* nodes, const int64_t* offsets, int32_t ntrees,
+                                           const int32_t* binops, const int32_t* unaops, const T* X, const T* y,
+                                           const T* w, int64_t n, int loss_kind, double p0, int nthreads,
+                                           double* loss_exact, double* loss_ref, uint8_t* ok, int64_t* node_rows) {
   int used = 1;
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -334,7 +365,9 @@ int CAT(oracle_eval_loss_batch_, SFX)(const srhip_node* nodes, const int64_t* of
 #pragma omp for schedule(dynamic, 1)
     for (int32_t t = 0; t < ntrees; ++t) {
       double le, lr;
-      ok[t] = (uint8_t)CAT(oracle_eval_loss_, SFX)(nodes + offsets[t], binops, unaops, X, y, w, n, loss_kind, p0, &le, &lr);
+      int64_t done = 0;
+      ok[t] = (uint8_t)CAT(eval_loss_work_, SFX)(nodes + offsets[t], binops, unaops, X, y, w, n, loss_kind, p0, &le, &lr, &done);
+      if (node_rows) node_rows[t] = done * n;
       loss_exact[t] = le;
       if (loss_ref) loss_ref[t] = lr;
     }
@@ -343,7 +376,9 @@ int CAT(oracle_eval_loss_batch_, SFX)(const srhip_node* nodes, const int64_t* of
   (void)nthreads;
   for (int32_t t = 0; t < ntrees; ++t) {
     double le, lr;
-    ok[t] = (uint8_t)CAT(oracle_eval_loss_, SFX)(nodes + offsets[t], binops, unaops, X, y, w, n, loss_kind, p0, &le, &lr);
+    int64_t done = 0;
+    ok[t] = (uint8_t)CAT(eval_loss_work_, SFX)(nodes + offsets[t], binops, unaops, X, y, w, n, loss_kind, p0, &le, &lr, &done);
+    if (node_rows) node_rows[t] = done * n;
     loss_exact[t] = le;
     if (loss_ref) loss_ref[t] = lr;
   }
@@ -351,8 +386,17 @@ int CAT(oracle_eval_loss_batch_, SFX)(const srhip_node* nodes, const int64_t* of
   return used;
 }
 
+int CAT(oracle_eval_loss_batch_, SFX)(const srhip_node* nodes, const int64_t* offsets, int32_t ntrees,
+                                      const int32_t* binops, const int32_t* unaops, const T* X, const T* y,
+                                      const T* w, int64_t n, int loss_kind, double p0, int nthreads,
+                                      double* loss_exact, double* loss_ref, uint8_t* ok) {
+  return CAT(oracle_eval_loss_batch_work_, SFX)(nodes, offsets, ntrees, binops, unaops, X, y, w, n, loss_kind, p0,
+                                                nthreads, loss_exact, loss_ref, ok, NULL);
+}
+
 #undef INF_T
 #undef NONFINITE
+#undef DONE
 
 /* ---- row-shard partials (test infrastructure for the multi-GPU protocol, include/srhip.h) ----
  * Row-wise restatement of what one shard contributes: per tree {sum (w*)loss, sum w (or rows)},
@@ -394,6 +438,7 @@ void CAT(oracle_partials_, SFX)(const srhip_node* nodes, const int64_t* offsets,
     c.unaops = unaops;
     c.X = X;
     c.n = n;
+    c.done = NULL;
     long double ls = 0.0L, ws = 0.0L;
     double ck = 0.0;
     int ck_nan = 0;

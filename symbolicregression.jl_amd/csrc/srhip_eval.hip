@@ -16,21 +16,42 @@ __global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab
                                                      const CT* __restrict__ slab_chk, int nrb, int nslots,
                                                      const int32_t* __restrict__ order, LT* __restrict__ out_loss,
                                                      CT* __restrict__ out_chk, const int32_t* __restrict__ slab_rows,
-                                                     int64_t* __restrict__ out_rows) {
+                                                     int64_t* __restrict__ out_rows, UndecidedList ul) {
   const int lane = threadIdx.x & 63;
   const int slot = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (slot >= nslots) return;
   LT s = 0;
   CT m = 0;
   long long rows = 0;
+  // The same sequential per-lane order as a plain strided loop (lane l adds chunks l, l + 64, ...:
+  // the bits every launch form reproduces), with RB_BATCH independent loads issued before their adds:
+  // a strided loop waited out one memory latency per iteration (16 per lane for C2's 977 chunks).
+  constexpr int RB_BATCH = 8;
   if (slab_loss)
-    for (int c = lane; c < nch; c += 64) s += slab_loss[((int64_t)(c / cpb) * nslots + slot) * cpb + c % cpb];
-  for (int i = lane; i < nrb; i += 64) {
-    if (slab_chk) {
-      const CT v = slab_chk[(int64_t)i * nslots + slot];
-      if constexpr (CHK_MAX) m = __builtin_elementwise_maximum(m, v); else m += v;
+    for (int c0 = lane; c0 < nch; c0 += 64 * RB_BATCH) {
+      LT v[RB_BATCH];
+      UNR for (int j = 0; j < RB_BATCH; ++j) {
+        const int c = c0 + 64 * j;
+        v[j] = c < nch ? slab_loss[((int64_t)(c / cpb) * nslots + slot) * cpb + c % cpb] : LT(0);
+      }
+      UNR for (int j = 0; j < RB_BATCH; ++j)
+        if (c0 + 64 * j < nch) s += v[j];
     }
-    if (slab_rows) rows += slab_rows[(int64_t)i * nslots + slot];
+  for (int i0 = lane; i0 < nrb; i0 += 64 * RB_BATCH) {
+    CT cv[RB_BATCH];
+    int32_t rv[RB_BATCH];
+    UNR for (int j = 0; j < RB_BATCH; ++j) {
+      const int i = i0 + 64 * j;
+      cv[j] = slab_chk && i < nrb ? slab_chk[(int64_t)i * nslots + slot] : CT(0);
+      rv[j] = slab_rows && i < nrb ? slab_rows[(int64_t)i * nslots + slot] : 0;
+    }
+    UNR for (int j = 0; j < RB_BATCH; ++j) {
+      if (i0 + 64 * j >= nrb) break;
+      if (slab_chk) {
+        if constexpr (CHK_MAX) m = __builtin_elementwise_maximum(m, cv[j]); else m += cv[j];
+      }
+      if (slab_rows) rows += rv[j];
+    }
   }
   UNR for (int o = 32; o > 0; o >>= 1) {
     if (slab_loss) s += __shfl_xor(s, o);
@@ -43,6 +64,46 @@ __global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab
     if (out_loss) out_loss[tree] = s;
     if (out_chk) out_chk[tree] = m;
     if (out_rows) out_rows[tree] = rows;
+    if (ul.ulist && out_chk) {
+      bool und;
+      if constexpr (CHK_MAX) {
+        // exact comparison of chk x rows with 2^127 - 2^102 (the host's long double test)
+        const double c = (double)m, p = c * ul.rows, e = __builtin_fma(c, ul.rows, -p), h = 0x1.ffffffp126;
+        und = __builtin_isfinite(c) && (p > h || (p == h && e >= 0.0));
+      } else {
+        und = __builtin_isfinite((double)m) && (double)m >= 0x1p511;
+      }
+      if (und) {
+        const int u = atomicAdd(ul.ulist, 1);
+        if (u < ul.umax) ul.ulist[1 + u] = tree;
+      }
+    }
+  }
+}
+
+// one workgroup: the listed trees' per-operator precise sums over the row blocks, in row-block
+// order with a compensated (TwoSum) accumulator, into coherent host memory; then the list is reset
+// for the next launch on the stream
+__global__ __launch_bounds__(256) void precise_reduce_kernel(const double* __restrict__ slab, int nrb, int stride,
+                                                             int32_t* __restrict__ ulist, int umax,
+                                                             int32_t* __restrict__ out_list, double* __restrict__ out) {
+  const int cnt = __hip_atomic_load(ulist, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int nu = min(cnt, umax);
+  for (int i = threadIdx.x; i < nu * stride; i += blockDim.x) {
+    const double* src = slab + (int64_t)i * nrb;
+    double s = 0.0, c = 0.0;
+    for (int b = 0; b < nrb; ++b) {
+      const double x = src[b], t = s + x, bp = t - s;
+      c += (s - (t - bp)) + (x - bp);
+      s = t;
+    }
+    out[i] = s + c;
+  }
+  for (int i = threadIdx.x; i < nu; i += blockDim.x) out_list[1 + i] = ulist[1 + i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out_list[0] = cnt;
+    __hip_atomic_store(ulist, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -144,25 +205,31 @@ hipError_t launch_eval(int dtype, const EvalArgs& a, int R, int K, int mode, boo
   }
 }
 
+hipError_t launch_precise_reduce(const double* slab, int nrb, int stride, int32_t* ulist, int umax,
+                                 int32_t* out_list, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(precise_reduce_kernel, dim3(1), dim3(256), 0, s, slab, nrb, stride, ulist, umax, out_list, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, int cpb, const void* slab_chk, int nrb, int nslots,
                          const int32_t* order, void* out_loss, void* out_chk, hipStream_t s, const int32_t* slab_rows,
-                         int64_t* out_rows) {
+                         int64_t* out_rows, const UndecidedList& ul) {
   dim3 grid((nslots + 3) / 4), block(256);
   switch (dtype) {
     case SRHIP_F32:
       hipLaunchKernelGGL((reduce_kernel<double, float, true>), grid, block, 0, s, (const double*)slab_loss, nch, cpb,
                          (const float*)slab_chk, nrb, nslots, order, (double*)out_loss, (float*)out_chk, slab_rows,
-                         out_rows);
+                         out_rows, ul);
       break;
     case SRHIP_F64:
       hipLaunchKernelGGL((reduce_kernel<double, double, false>), grid, block, 0, s, (const double*)slab_loss, nch, cpb,
                          (const double*)slab_chk, nrb, nslots, order, (double*)out_loss, (double*)out_chk, slab_rows,
-                         out_rows);
+                         out_rows, ul);
       break;
     case SRHIP_I32:
       hipLaunchKernelGGL((reduce_kernel<long long, float, true>), grid, block, 0, s, (const long long*)slab_loss, nch,
                          cpb, (const float*)nullptr, nrb, nslots, order, (long long*)out_loss, (float*)nullptr,
-                         slab_rows, out_rows);
+                         slab_rows, out_rows, UndecidedList());
       break;
     default: return hipErrorInvalidValue;
   }

@@ -52,6 +52,63 @@
 #ifndef SRHIP_TRIG_ROWS
 #define SRHIP_TRIG_ROWS 1  // Float32 cos/sin/tan batched over the rows (trigf_rows)
 #endif
+// Hot handlers (SRHIP_HOT_CASES): the switch's binary search is built weighted by case likelihood,
+// so the commonest handlers -- loads, pushes, + - * / in every operand form, the common unary
+// operators -- sit near the root of the compare-and-branch tree
+#ifndef SRHIP_HOT_CASES
+#define SRHIP_HOT_CASES 0
+#endif
+#if SRHIP_HOT_CASES
+#define SRHIP_LK [[likely]]
+#else
+#define SRHIP_LK
+#endif
+#define SRHIP_HOTB_ADD SRHIP_LK
+#define SRHIP_HOTB_SUB SRHIP_LK
+#define SRHIP_HOTB_MUL SRHIP_LK
+#define SRHIP_HOTB_DIV SRHIP_LK
+#define SRHIP_HOTB_GREATER
+#define SRHIP_HOTB_COND
+#define SRHIP_HOTB_LOGICAL_OR
+#define SRHIP_HOTB_LOGICAL_AND
+#define SRHIP_HOTB_MAX
+#define SRHIP_HOTB_MIN
+#define SRHIP_HOTU_NEG SRHIP_LK
+#define SRHIP_HOTU_SQUARE SRHIP_LK
+#define SRHIP_HOTU_CUBE SRHIP_LK
+#define SRHIP_HOTU_ABS SRHIP_LK
+#define SRHIP_HOTU_RELU
+#define SRHIP_HOTU_COS SRHIP_LK
+#define SRHIP_HOTU_SIN SRHIP_LK
+#define SRHIP_HOTU_TAN
+#define SRHIP_HOTU_EXP SRHIP_LK
+#define SRHIP_HOTU_LOG SRHIP_LK
+#define SRHIP_HOTU_LOG2
+#define SRHIP_HOTU_LOG10
+#define SRHIP_HOTU_LOG1P
+#define SRHIP_HOTU_SQRT
+#define SRHIP_HOTU_ACOSH
+#define SRHIP_HOTU_ATANH_CLIP
+#define SRHIP_HOTU_SINH
+#define SRHIP_HOTU_COSH
+#define SRHIP_HOTU_TANH
+#define SRHIP_HOTU_ASIN
+#define SRHIP_HOTU_ACOS
+#define SRHIP_HOTU_ATAN
+#define SRHIP_HOTU_ASINH
+#define SRHIP_HOTU_ERF
+#define SRHIP_HOTU_ERFC
+#define SRHIP_HOTU_GAMMA
+#define SRHIP_HOTU_ROUND
+#define SRHIP_HOTU_FLOOR
+#define SRHIP_HOTU_CEIL
+#define SRHIP_HOTU_SIGN
+#define SRHIP_HOTU_EXP2
+#define SRHIP_HOTU_EXPM1
+#define SRHIP_HOTU_CBRT
+#ifndef SRHIP_ASM_DEF
+#define SRHIP_ASM_DEF 0
+#endif
 #ifndef SRHIP_ROW_FENCE
 #define SRHIP_ROW_FENCE() __builtin_amdgcn_sched_barrier(0)
 #endif
@@ -946,7 +1003,10 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
 
   // tree group of this workgroup: uniform, or the host's tail-shaped sizes (group_off)
   const int group_base = __builtin_amdgcn_readfirstlane(snap_base);
-  const int group_n = __builtin_amdgcn_readfirstlane(snap_n);
+  int group_n = __builtin_amdgcn_readfirstlane(snap_n);
+  if constexpr (MODE == MODE_PRECISE) {
+    if (p.dev_count) group_n = min(group_n, __builtin_amdgcn_readfirstlane(*p.dev_count));
+  }
 
   // the group's trees are in descending estimated cost (host make_order): wave w starts with tree w,
   // then each wave claims the next unclaimed tree from an LDS counter as it finishes one — longest
@@ -975,6 +1035,12 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
     KMARK(1, tree);
     if (p.debug_stop == 3) break;  // (diagnostic) skip the trees; a continue would not claim the next one
 
+    if constexpr (MODE == MODE_PRECISE) {
+      // device-listed trees: this wave owns the (tree, row block) entries, zeroed before accumulating
+      if (p.dev_count && lane == WAVE_LAST)
+        for (int k = 0; k < p.prec_stride; ++k)
+          reinterpret_cast<double*>(p.slab_prec)[((int64_t)ti * p.prec_stride + k) * p.nrb + rb] = 0.0;
+    }
     LAccT<T> lacc = 0;
     CT M = 0;
     // another row block already saw this tree fail in this launch: nothing here can change its
@@ -1018,8 +1084,15 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
       // (cleared per tile: with the registers left undefined or carried over, the allocator moved the
       // accumulator off v0-v15, where the out-of-line operator bodies take and return it)
       RV<T, R> A, S[K];
+#if SRHIP_ASM_DEF
+      // defined by an empty asm statement: a def the allocator sees at this point, no instruction
+      // (every program writes A before reading it and pushes before it pops)
+      asm volatile("" : "=v"(A));
+      UNR for (int k = 0; k < K; ++k) asm volatile("" : "=v"(S[k]));
+#else
       UNR for (int r = 0; r < R; ++r) A[r] = T(0);
       UNR for (int k = 0; k < K; ++k) UNR for (int r = 0; r < R; ++r) S[k][r] = T(0);
+#endif
       // The program is read through the constant address space with a wave-uniform pc, so every
       // instruction is one s_load_dwordx4 (scalar cache), prefetched one instruction ahead.
       const CIns* prog = code + pc0;
@@ -1031,8 +1104,8 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
         KDBG("[k]   tile=%d step=%d h=%u a=%u\n", tile, step, ins.h, ins.a);
         if (ins.h == H_END) break;
         switch (ins.h) {
-          case H_LOADF: load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A); break;
-          case H_LOADC: { const T c = imm_as<T>(ins.imm); UNR for (int r = 0; r < R; ++r) A[r] = c; break; }
+          SRHIP_LK case H_LOADF: load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A); break;
+          SRHIP_LK case H_LOADC: { const T c = imm_as<T>(ins.imm); UNR for (int r = 0; r < R; ++r) A[r] = c; break; }
 #define SRHIP_K_CASES(BASE, ...)                                                            \
   case BASE + 0: if constexpr (0 < K) { constexpr int k = 0; __VA_ARGS__ } break;                 \
   case BASE + 1: if constexpr (1 < K) { constexpr int k = 1; __VA_ARGS__ } break;                 \
@@ -1042,12 +1115,30 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
   case BASE + 5: if constexpr (5 < K) { constexpr int k = 5; __VA_ARGS__ } break;                 \
   case BASE + 6: if constexpr (6 < K) { constexpr int k = 6; __VA_ARGS__ } break;                 \
   case BASE + 7: if constexpr (7 < K) { constexpr int k = 7; __VA_ARGS__ } break;
-          SRHIP_K_CASES(H_PUSH0, { UNR for (int r = 0; r < R; ++r) S[k][r] = A[r]; })
+#define SRHIP_K_CASES_H(HOT, BASE, ...)                                                     \
+  HOT case BASE + 0: if constexpr (0 < K) { constexpr int k = 0; __VA_ARGS__ } break;             \
+  HOT case BASE + 1: if constexpr (1 < K) { constexpr int k = 1; __VA_ARGS__ } break;             \
+  case BASE + 2: if constexpr (2 < K) { constexpr int k = 2; __VA_ARGS__ } break;                 \
+  case BASE + 3: if constexpr (3 < K) { constexpr int k = 3; __VA_ARGS__ } break;                 \
+  case BASE + 4: if constexpr (4 < K) { constexpr int k = 4; __VA_ARGS__ } break;                 \
+  case BASE + 5: if constexpr (5 < K) { constexpr int k = 5; __VA_ARGS__ } break;                 \
+  case BASE + 6: if constexpr (6 < K) { constexpr int k = 6; __VA_ARGS__ } break;                 \
+  case BASE + 7: if constexpr (7 < K) { constexpr int k = 7; __VA_ARGS__ } break;
+          SRHIP_K_CASES_H(SRHIP_LK, H_PUSH0, { UNR for (int r = 0; r < R; ++r) S[k][r] = A[r]; })
+          SRHIP_K_CASES_H(SRHIP_LK, H_PUSHLF0, {
+            UNR for (int r = 0; r < R; ++r) S[k][r] = A[r];
+            load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A);
+          })
+          SRHIP_K_CASES_H(SRHIP_LK, H_PUSHLC0, {
+            UNR for (int r = 0; r < R; ++r) S[k][r] = A[r];
+            const T c = imm_as<T>(ins.imm);
+            UNR for (int r = 0; r < R; ++r) A[r] = c;
+          })
           SRHIP_K_CASES(H_SLOADF0, { load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, S[k]); })
           SRHIP_K_CASES(H_SLOADC0, { const T c = imm_as<T>(ins.imm); UNR for (int r = 0; r < R; ++r) S[k][r] = c; })
 
 #define SRHIP_SPEC_CASE(NAME, FN)                                                                  \
-  case h_spec(SB_##NAME, SPEC_AF):                                                                 \
+  SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_AF):                                                \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       RV<T, R> xv;                                                                                     \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
@@ -1055,7 +1146,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
-  case h_spec(SB_##NAME, SPEC_FA):                                                                 \
+  SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_FA):                                                \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       RV<T, R> xv;                                                                                     \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
@@ -1063,23 +1154,46 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
-  case h_spec(SB_##NAME, SPEC_AC):                                                                 \
+  SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_AC):                                                \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       bin_rows_c_chk<T, R, SB_##NAME, false>(A, imm_as<T>(ins.imm), M);                            \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
-  case h_spec(SB_##NAME, SPEC_CA):                                                                 \
+  SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_CA):                                                \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       bin_rows_c_chk<T, R, SB_##NAME, true>(A, imm_as<T>(ins.imm), M);                             \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
-    SRHIP_K_CASES(h_spec(SB_##NAME, SPEC_SA0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
+  SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_FF):                                              \
+    if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
+      RV<T, R> xv;                                                                                 \
+      load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A);                          \
+      load_rows<T, R>(xt + (int64_t)(ins.imm & 0xffff) * xstride, lane, xv);                       \
+      bin_rows_chk<T, R, SB_##NAME, false>(A, xv, M);                                              \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);     \
+    }                                                                                              \
+    break;                                                                                         \
+  SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_FC):                                              \
+    if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
+      load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A);                          \
+      bin_rows_c_chk<T, R, SB_##NAME, false>(A, imm_as<T>(ins.imm), M);                            \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);     \
+    }                                                                                              \
+    break;                                                                                         \
+  SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_CF):                                              \
+    if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
+      load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A);                          \
+      bin_rows_c_chk<T, R, SB_##NAME, true>(A, imm_as<T>(ins.imm), M);                             \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);     \
+    }                                                                                              \
+    break;                                                                                         \
+    SRHIP_K_CASES_H(SRHIP_HOTB_##NAME, h_spec(SB_##NAME, SPEC_SA0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
       bin_rows_chk<T, R, SB_##NAME, true>(A, S[k], M);                                             \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     })                                                                                             \
-    SRHIP_K_CASES(h_spec(SB_##NAME, SPEC_AS0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
+    SRHIP_K_CASES_H(SRHIP_HOTB_##NAME, h_spec(SB_##NAME, SPEC_AS0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
       bin_rows_chk<T, R, SB_##NAME, false>(A, S[k], M);                                            \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
     })
@@ -1101,7 +1215,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
 #undef SRHIP_HEAVY_CASE
 
 #define SRHIP_UN_CASE(NAME, FN)                                                  \
-  case h_un(UN_##NAME):                                                          \
+  SRHIP_HOTU_##NAME case h_un(UN_##NAME):                                        \
     if constexpr (un_ok<T>(UN_##NAME) && (K == K_MAX || !un_wide(UN_##NAME))) {  \
       apply_un<T, R, UN_##NAME>(A);                                              \
       chk_update<R>(M, A);                                                       \
@@ -1110,13 +1224,13 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
     break;
           SRHIP_UNOPS(SRHIP_UN_CASE)
 #undef SRHIP_UN_CASE
-          case H_COS_NC:
+          SRHIP_LK case H_COS_NC:
             if constexpr (un_ok<T>(UN_COS)) {
               apply_un<T, R, UN_COS>(A);
               if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);
             }
             break;
-          case H_SIN_NC:
+          SRHIP_LK case H_SIN_NC:
             if constexpr (un_ok<T>(UN_SIN)) {
               apply_un<T, R, UN_SIN>(A);
               if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);
@@ -1238,6 +1352,20 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
   // Grid launches run their one (blockIdx.x, blockIdx.y) item.  One call site: the interpreter
   // body is inlined once.
   __shared__ int claimed;
+  if (p.tile_claims && !p.persistent) {
+    // the probe's combining entries start from zero (eval_block's first barrier orders these stores
+    // before any wave's atomics); no memset launches before the probe
+    if (p.zero_ctr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+      __hip_atomic_store(p.zero_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int gs = p.grid_interleave ? (int)blockIdx.y : 0, gst = p.grid_interleave ? (int)gridDim.y : 1;
+    const int nz = p.grid_interleave ? (p.ntrees - gs + gst - 1) / gst : 0;
+    for (int i = threadIdx.x; i < nz; i += blockDim.x) {
+      const int64_t at = (int64_t)blockIdx.x * p.ntrees + gs + (int64_t)i * gst;
+      if (p.slab_chk) __hip_atomic_store(reinterpret_cast<uint32_t*>(p.slab_chk) + at, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (p.slab_rows) __hip_atomic_store(p.slab_rows + at, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __threadfence();
+  }
   const int nfull = p.nrb - p.block0 - p.tail_blocks;
   const int nitems = nfull + p.tail_blocks * p.tail_slices;
   for (int it = 0;; ++it) {

@@ -146,6 +146,7 @@ template <typename T> class TreeCompiler {
       code_ = &code;
       info_ = &info;
       emit(0, 0, -1);
+      if (super_) fuse_push_loads(code, info.code_begin);
       Ins end{H_END, 0, 0};
       code.push_back(end);
       for (int64_t i = info.code_begin; i < (int64_t)code.size(); ++i) info.cost += op_cost(code[i].h);
@@ -428,6 +429,26 @@ template <typename T> class TreeCompiler {
   }
   bool leaf_is_feature(int64_t i) const { return nd_[i].degree == 0 && !nd_[i].constant; }
 
+  // Superinstructions (evaluation programs; SRHIP_NO_SUPER=1 turns them off): the leaf-leaf operand
+  // forms (emit) and a push fused with the leaf load that follows it: one dispatch instead of two.
+  const bool super_ = !grad_ && ![] { const char* e = getenv("SRHIP_NO_SUPER"); return e && *e && *e != '0'; }();
+  static void fuse_push_loads(std::vector<Ins>& code, int32_t begin) {
+    size_t w = (size_t)begin;
+    for (size_t r = (size_t)begin; r < code.size(); ++r) {
+      const Ins& a = code[r];
+      if (a.h >= H_PUSH0 && a.h < H_PUSH0 + K_MAX && r + 1 < code.size() &&
+          (code[r + 1].h == H_LOADF || code[r + 1].h == H_LOADC)) {
+        const Ins& b = code[r + 1];
+        const uint32_t k = a.h - H_PUSH0;
+        code[w++] = Ins{(b.h == H_LOADF ? H_PUSHLF0 : H_PUSHLC0) + k, b.a, b.imm};
+        ++r;
+        continue;
+      }
+      code[w++] = a;
+    }
+    code.resize(w);
+  }
+
   void emit_leaf(int64_t i) {
     const int col = leaf_col(i);
     if (col >= 0) push_ins(H_LOADF, (uint32_t)col, 0);
@@ -454,6 +475,14 @@ template <typename T> class TreeCompiler {
     const int64_t L = n.l, Rr = n.r;
     const bool ll = leafish(L), rl = leafish(Rr);
     if (sb >= 0) {
+      if (ll && rl && super_) {
+        // deg2_l0_r0: both operands leaves (feature, derived column or constant) in one instruction
+        const int cl = leaf_col(L), cr = leaf_col(Rr);
+        if (cl >= 0 && cr >= 0) push_op(h_spec(sb, SPEC_FF), cl, (uint64_t)cr, i, parent);
+        else if (cl >= 0) push_op(h_spec(sb, SPEC_FC), cl, leaf_imm(Rr), i, parent);
+        else push_op(h_spec(sb, SPEC_CF), cr, leaf_imm(L), i, parent);
+        return;
+      }
       if (rl) {
         emit(L, base, i);
         if (leaf_col(Rr) >= 0) push_op(h_spec(sb, SPEC_AF), leaf_col(Rr), 0, i, parent);
@@ -722,6 +751,24 @@ int compile_program_t(srhip_program& P) {
       P.dcost[t] = ti.cost;
       P.dkmax = std::max(P.dkmax, ti.need);
       P.dmax_len = std::max(P.dmax_len, ti.code_len);
+    }
+  }
+  // (diagnostic) SRHIP_DUMP_CODE=path: the derived (or plain) program's instructions as (h, a) pairs
+  // with a -1 separator per tree, for instruction-mix studies (scripts/code_stats.py)
+  if (const char* dump = getenv("SRHIP_DUMP_CODE")) {
+    if (FILE* f = fopen(dump, "wb")) {
+      const std::vector<Ins>& code = der ? P.dcode : P.code;
+      for (int32_t t = 0; t < n; ++t) {
+        const TreeInfo& ti = der ? dinfo[t] : P.info[t];
+        for (int32_t i = 0; i < ti.code_len; ++i) {
+          const Ins& ins = code[(size_t)ti.code_begin + i];
+          const int32_t rec[2] = {(int32_t)ins.h, (int32_t)ins.a};
+          fwrite(rec, sizeof rec, 1, f);
+        }
+        const int32_t sep[2] = {-1, ti.static_fail ? 1 : 0};
+        fwrite(sep, sizeof sep, 1, f);
+      }
+      fclose(f);
     }
   }
   return SRHIP_OK;
@@ -1349,10 +1396,24 @@ static int env_int(const char* name, int dflt) {
   return e && *e ? atoi(e) : dflt;
 }
 
+// run_eval's device-decided precise pass: the reduction lists the trees whose overflow bound needs
+// the precise pass, and the precise launch + its reduction follow on the stream before the one host
+// synchronisation (no host round trip between the main launch and the precise pass)
+constexpr int32_t DEV_PRECISE_MAX = 64;
+struct DevPrecise {
+  bool used = false;
+  int32_t count = 0;             // trees the device listed (may exceed DEV_PRECISE_MAX)
+  int stride = 1;
+  std::vector<int32_t> list;     // the first min(count, DEV_PRECISE_MAX) of them
+  std::vector<double> opsums;    // [list.size()][stride]
+};
+
 // Device stage: one interpreter launch over the view + the per-tree reduction.  Fills the partials
-// (sums layout above; chk[T]) and, in MODE_PRED, out_pred.
+// (sums layout above; chk[T]) and, in MODE_PRED, out_pred.  dp (nullable): also the device-decided
+// precise pass (multi-block launches; single-block launches finish inside the interpreter and leave
+// the precise pass to the caller).
 static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
-                         const View& v, void* out_pred, double* sums, double* chk) {
+                         const View& v, void* out_pred, double* sums, double* chk, DevPrecise* dp = nullptr) {
   const int dtype = P->dtype;
   const int32_t nt = P->ntrees;
   const int64_t nf = ds->nfeat;
@@ -1563,6 +1624,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   if (persistent) HIP_TRY(ctx->block_ctr.ensure(sizeof(int32_t)));
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
   if (persistent) {
+    bool ctr_zeroed = false;
     if (probe_blocks > 0) {
       // leading row blocks, one tree per wave (uniform groups of consecutive slots), with the plain
       // program: a probe workgroup serves 16 trees, too few to pay for deriving columns (the values,
@@ -1576,11 +1638,13 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       q.grid_interleave = 1;
       // one (tree, tile) per claim: the costliest tree's two tiles run on two waves at once (the
       // probe's duration is that tree's); chk / rows of the probe blocks combine by atomics from 0
+      // (the probe's workgroups zero their own combining entries and the persistent launch's block
+      // counter: no memset launches on the stream)
       const bool no_tile_claims = env_flag("SRHIP_PROBE_TREE_CLAIMS");
       if (!no_tile_claims) {
         q.tile_claims = 1;
-        HIP_TRY(hipMemsetAsync(ctx->slab_chk.p, 0, (size_t)probe_blocks * nl * sizeof(float), ctx->stream));
-        HIP_TRY(hipMemsetAsync(ctx->slab_rows.p, 0, (size_t)probe_blocks * nl * sizeof(int32_t), ctx->stream));
+        q.zero_ctr = (int32_t*)ctx->block_ctr.p;
+        ctr_zeroed = true;
       }
       q.code = P->code_dev;
       q.prog_off = P->off_dev;
@@ -1592,7 +1656,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       const dim3 pgrid(probe_blocks, (unsigned)((nl + q.trees_per_group - 1) / q.trees_per_group));
       HIP_TRY(launch_eval(dtype, q, R, K, mode, true, pgrid, qlds, ctx->stream));
     }
-    HIP_TRY(hipMemsetAsync(ctx->block_ctr.p, 0, sizeof(int32_t), ctx->stream));
+    if (!ctr_zeroed) HIP_TRY(hipMemsetAsync(ctx->block_ctr.p, 0, sizeof(int32_t), ctx->stream));
     a.persistent = 1;
     a.block0 = probe_blocks;
     a.block_ctr = (int32_t*)ctx->block_ctr.p;
@@ -1637,14 +1701,66 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       }
     }
   }
+  const bool devp = dp && !a.fused && dtype != SRHIP_I32 && !env_flag("SRHIP_NO_DEVICE_PRECISE");
+  UndecidedList ul;
+  if (devp) {
+    if (!ctx->d_ulist.p) {
+      HIP_TRY(ctx->d_ulist.ensure((1 + DEV_PRECISE_MAX) * sizeof(int32_t)));
+      HIP_TRY(hipMemsetAsync(ctx->d_ulist.p, 0, ctx->d_ulist.bytes, ctx->stream));
+    }
+    ul.ulist = (int32_t*)ctx->d_ulist.p;
+    ul.umax = DEV_PRECISE_MAX;
+    ul.rows = (double)v.m;
+  }
   if (!a.fused)
     HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, nch, cpb,
                           dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p, L.nrb, nl, (const int32_t*)d_order,
                           mode == MODE_LOSS ? ctx->h_loss.p : nullptr, dtype == SRHIP_I32 ? nullptr : ctx->h_chk.p,
-                          ctx->stream, a.slab_rows, (int64_t*)ctx->h_rows.p));
+                          ctx->stream, a.slab_rows, (int64_t*)ctx->h_rows.p, ul));
+  if (devp) {
+    // the precise pass over the device's list (capped; its launch reads the count): the plain program,
+    // K_MAX, global reads -- eval_precise's launch with the list as the tree order
+    const int stride = std::max(1, P->max_ops);
+    const int Rp = pick_rows_per_lane(dtype, K_MAX, MODE_PRECISE, v.m);
+    LaunchPlan Lp = plan_launch(ctx, dtype, ds->nfeat, false, false, v.m, DEV_PRECISE_MAX, 64 * Rp);
+    HIP_TRY(ctx->slab_prec.ensure((size_t)DEV_PRECISE_MAX * stride * Lp.nrb * sizeof(double)));
+    HIP_TRY(ctx->h_pout.ensure((size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t) +
+                               (size_t)DEV_PRECISE_MAX * stride * sizeof(double), hipHostMallocCoherent));
+    EvalArgs q{};
+    q.code = P->code_dev;
+    q.prog_off = P->off_dev;
+    q.order = ul.ulist + 1;
+    q.X = v.X;
+    q.ld = v.ld;
+    q.nvalid = v.m;
+    q.ntrees = DEV_PRECISE_MAX;
+    q.nfeat = (int32_t)ds->nfeat;
+    q.rb_rows = Lp.rb_rows;
+    q.nrb = Lp.nrb;
+    q.trees_per_group = DEV_PRECISE_MAX;
+    q.slab_prec = ctx->slab_prec.p;
+    q.prec_stride = stride;
+    q.max_steps = P->max_len;
+    q.dev_count = ul.ulist;
+    HIP_TRY(launch_eval(dtype, q, Rp, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, 1), 16, ctx->stream));
+    int32_t* hl = (int32_t*)ctx->h_pout.p;
+    double* hs = (double*)((uint8_t*)ctx->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
+    HIP_TRY(launch_precise_reduce((const double*)ctx->slab_prec.p, Lp.nrb, stride, ul.ulist, DEV_PRECISE_MAX, hl, hs,
+                                  ctx->stream));
+    dp->used = true;
+    dp->stride = stride;
+  }
   if (mode == MODE_PRED)
     HIP_TRY(hipMemcpyAsync(out_pred, pred.p, (size_t)nt * v.m * es, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if (devp) {
+    const int32_t* hl = (const int32_t*)ctx->h_pout.p;
+    const double* hs = (const double*)((const uint8_t*)ctx->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
+    dp->count = hl[0];
+    const int nu = std::min(dp->count, DEV_PRECISE_MAX);
+    dp->list.assign(hl + 1, hl + 1 + nu);
+    dp->opsums.assign(hs, hs + (size_t)nu * dp->stride);
+  }
   for (int32_t t : live) {
     if (mode == MODE_LOSS)
       sums[2 * (size_t)t] = dtype == SRHIP_I32 ? (double)((long long*)ctx->h_loss.p)[t] : ((double*)ctx->h_loss.p)[t];
@@ -1746,7 +1862,8 @@ int srhip::run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program
   const int32_t nt = P->ntrees;
   if (nt == 0) return SRHIP_OK;
   std::vector<double> sums(sums_len(nt, ds->nfeat)), chk(nt);
-  rc = eval_partials(ctx, ds, P, mode, loss, v, out_pred, sums.data(), chk.data());
+  DevPrecise dp;
+  rc = eval_partials(ctx, ds, P, mode, loss, v, out_pred, sums.data(), chk.data(), &dp);
   if (rc) return rc;
   std::vector<uint8_t> status(nt), ok(nt);
   std::vector<double> lossv(nt);
@@ -1754,10 +1871,87 @@ int srhip::run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program
   std::vector<int32_t> unc;
   for (int32_t t = 0; t < nt; ++t)
     if (status[t] == 2) unc.push_back(t);
+  if (dp.used && !unc.empty()) {
+    // undecided trees the device's precise pass already covered (every undecided tree is listed by
+    // the device: its test is the host's minus the host-only checks, so the list is a superset)
+    std::vector<int32_t> rest;
+    for (int32_t t : unc) {
+      const auto it = std::find(dp.list.begin(), dp.list.end(), t);
+      if (it == dp.list.end()) {
+        rest.push_back(t);
+        continue;
+      }
+      const size_t u = (size_t)(it - dp.list.begin());
+      uint8_t uok = 0;
+      finalize_precise(*P, &t, 1, dp.opsums.data() + u * dp.stride, &uok);
+      ok[t] = uok;
+      lossv[t] = uok ? sums[2 * (size_t)t] / sums[2 * (size_t)t + 1] : INFINITY;
+    }
+    unc.swap(rest);
+  }
   if (!unc.empty()) {
     const int stride = std::max(1, P->max_ops);
     std::vector<double> opsums(unc.size() * stride);
     rc = eval_precise(ctx, ds, P, v, unc.data(), (int32_t)unc.size(), opsums.data());
+    if (rc) return rc;
+    std::vector<uint8_t> uok(unc.size());
+    finalize_precise(*P, unc.data(), (int32_t)unc.size(), opsums.data(), uok.data());
+    for (size_t u = 0; u < unc.size(); ++u) {
+      const int32_t t = unc[u];
+      ok[t] = uok[u];
+      lossv[t] = uok[u] ? sums[2 * (size_t)t] / sums[2 * (size_t)t + 1] : INFINITY;
+    }
+  }
+  for (int32_t t = 0; t < nt; ++t) {
+    if (out_ok) out_ok[t] = ok[t];
+    if (out_loss) out_loss[t] = lossv[t];
+  }
+  return SRHIP_OK;
+}
+
+// Row-sharded evaluation (srhip_eval_loss_sharded): this shard's partials, ONE all-reduce of
+// [sums | chk] (sums by SUM, chk by MAX for Float32 / SUM otherwise; a non-finite statistic travels
+// as +Inf), the decision every rank takes identically, and for the undecided trees a precise pass
+// over this shard with a SUM all-reduce of its per-operator sums.  The reductions are the caller's
+// (srhip_comm.cpp: RCCL on the device); nfeat_total is the dataset's feature count on every rank.
+int srhip::run_eval_sharded(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const srhip_loss* loss,
+                            const int64_t* idx, int64_t nidx, const ShardReduce& reduce, double* out_loss,
+                            uint8_t* out_ok) {
+  int rc = check_eval_args(ctx, ds, P, MODE_LOSS, loss);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(ctx->device));
+  View v;
+  rc = make_view(ctx, ds, idx, nidx, true, v);
+  if (rc) return rc;
+  if (idx && ds->weighted) {
+    rc = gathered_weight_sum(ctx, ds, nidx, v);
+    if (rc) return rc;
+  }
+  const int32_t nt = P->ntrees;
+  const size_t ns = sums_len(nt, ds->nfeat);
+  // [sums | chk] in one buffer: the all-reduce sees one message
+  std::vector<double> buf(ns + (size_t)nt, 0.0);
+  double* sums = buf.data();
+  double* chk = buf.data() + ns;
+  rc = eval_partials(ctx, ds, P, MODE_LOSS, loss, v, nullptr, sums, chk);
+  if (rc) return rc;
+  for (int32_t t = 0; t < nt; ++t)
+    if (!std::isfinite(chk[t])) chk[t] = INFINITY;
+  rc = reduce(buf.data(), ns, (size_t)nt, P->dtype == SRHIP_F32);
+  if (rc) return rc;
+  std::vector<uint8_t> status(nt), ok(nt);
+  std::vector<double> lossv(nt);
+  finalize(*P, ds->nfeat, sums, chk, lossv.data(), ok.data(), status.data());
+  std::vector<int32_t> unc;
+  for (int32_t t = 0; t < nt; ++t)
+    if (status[t] == 2) unc.push_back(t);
+  // every rank took the same decision from the same reduced partials: the undecided set agrees
+  if (!unc.empty()) {
+    const int stride = std::max(1, P->max_ops);
+    std::vector<double> opsums(unc.size() * stride);
+    rc = eval_precise(ctx, ds, P, v, unc.data(), (int32_t)unc.size(), opsums.data());
+    if (rc) return rc;
+    rc = reduce(opsums.data(), opsums.size(), 0, false);
     if (rc) return rc;
     std::vector<uint8_t> uok(unc.size());
     finalize_precise(*P, unc.data(), (int32_t)unc.size(), opsums.data(), uok.data());

@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -131,6 +132,8 @@ struct srhip_ctx {
   srhip::DevBuf block_ctr;  // persistent launches: the row-block counter (one int32, zeroed per launch)
   srhip::DevBuf slab_rows;  // [row block][order slot] valid rows evaluated
   srhip::HostBuf h_rows;    // [program trees] int64 rows evaluated per tree (coherent pinned)
+  srhip::DevBuf d_ulist;    // the device's undecided-tree list ([0] = count; reset by its consumer)
+  srhip::HostBuf h_pout;    // the device precise pass's results (coherent pinned)
   // work of the last srhip_eval_loss / srhip_eval_predict on this context (srhip_last_work):
   // evaluated node-rows, nominal node-rows (every live tree on every row), evaluated operator-node
   // rows, evaluated tree-rows
@@ -271,5 +274,12 @@ int run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, in
 // evaluation program or (grad = true) on the gradient program: out_ok[u] for trees[u].
 int precise_decide(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const View& v,
                    const int32_t* trees, int32_t nu, bool grad, uint8_t* out_ok);
+
+// Row-sharded evaluation with caller-supplied reductions: reduce(buf, nsum, nchk, chk_max) combines
+// buf[0, nsum) by SUM and buf[nsum, nsum + nchk) by MAX (chk_max) or SUM across the shards, in place;
+// returns an SRHIP status.
+using ShardReduce = std::function<int(double* buf, size_t nsum, size_t nchk, bool chk_max)>;
+int run_eval_sharded(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const srhip_loss* loss,
+                     const int64_t* idx, int64_t nidx, const ShardReduce& reduce, double* out_loss, uint8_t* out_ok);
 
 }  // namespace srhip

@@ -75,10 +75,17 @@ enum : uint32_t {
   H_SLOADF0 = 3,                      // S[k] = X[a]   (operand of a heavy binary op)
   H_SLOADC0 = H_SLOADF0 + K_MAX,      // S[k] = imm
   H_PUSH0 = H_SLOADC0 + K_MAX,        // S[k] = A
-  H_BIN0 = H_PUSH0 + K_MAX,           // specialised binary ops, SPEC_STRIDE handlers each
+  // superinstructions (evaluation programs only; the gradient program keeps the plain forms):
+  H_PUSHLF0 = H_PUSH0 + K_MAX,        // S[k] = A; A = X[a]     (a push followed by a feature leaf)
+  H_PUSHLC0 = H_PUSHLF0 + K_MAX,      // S[k] = A; A = imm      (a push followed by a constant leaf)
+  H_BIN0 = H_PUSHLC0 + K_MAX,         // specialised binary ops, SPEC_STRIDE handlers each
 };
+// operand forms of a specialised binary op: A op X[a], X[a] op A, A op imm, imm op A, S[k] op A,
+// A op S[k], and the leaf-leaf forms of DynamicExpressions' deg2_l0_r0 (one instruction instead of a
+// load and an op): X[a] op X[imm], X[a] op imm, imm op X[a]
 constexpr uint32_t SPEC_AF = 0, SPEC_FA = 1, SPEC_AC = 2, SPEC_CA = 3, SPEC_SA0 = 4,
-                   SPEC_AS0 = 4 + K_MAX, SPEC_STRIDE = 4 + 2 * K_MAX;
+                   SPEC_AS0 = 4 + K_MAX, SPEC_FF = 4 + 2 * K_MAX, SPEC_FC = SPEC_FF + 1, SPEC_CF = SPEC_FF + 2,
+                   SPEC_STRIDE = SPEC_FF + 3;
 // heavy binary ops take their second operand from a stack slot: A = S[k] op A, or A = A op S[k]
 constexpr uint32_t HEAVY_SA0 = 0, HEAVY_AS0 = K_MAX, HEAVY_STRIDE = 2 * K_MAX;
 constexpr uint32_t H_HEAVY0 = H_BIN0 + NUM_SPEC_BIN * SPEC_STRIDE;

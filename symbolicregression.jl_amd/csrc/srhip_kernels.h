@@ -99,6 +99,14 @@ struct EvalArgs {
   int32_t grid_interleave;  // grid launches: workgroup (x, y) takes order slots y, y + grid.y, ... (group_off unused)
   int32_t tile_claims;      // a wave claims one (tree, tile) at a time (R = 16 probe; slab_chk / slab_rows zeroed first)
   int32_t* block_ctr;
+  // probe launches (tile_claims): zero_ctr, if set, is the persistent launch's block counter, zeroed
+  // by workgroup (0, 0) -- the persistent launch follows on the same stream; and every workgroup zeroes
+  // its own (row block, slot) entries of slab_chk / slab_rows before its waves combine into them
+  int32_t* zero_ctr;
+  // MODE_PRECISE launches over a device-built list of undecided trees (order = the list): the number
+  // of listed trees is read here (*dev_count, capped at trees_per_group); each wave zeroes its
+  // (tree, row block) slab entries before accumulating into them
+  const int32_t* dev_count;
   int32_t* slab_rows;       // [nrb][ntrees] valid rows each (row block, order slot) evaluated, or nullptr
   int64_t* fused_rows;      // fused launches: [program trees] rows evaluated (coherent pinned host), or nullptr
 };
@@ -111,9 +119,23 @@ hipError_t launch_eval(int dtype, const EvalArgs& a, int R, int K, int mode, boo
 // per-tree reduction of eval_kernel's slabs: nslots order slots, cpb loss chunks per row block, results
 // at out[order[slot]]
 // slab_rows (optional): [nrb][nslots] rows evaluated, summed per tree into out_rows (int64)
+// The device's share of the did_succeed decision: a tree whose check statistic is finite
+// but whose overflow bound reaches half the threshold (Float32: chk x rows >= 2^127 - 2^102 exactly;
+// Float64: chk >= 2^511) is appended to ulist (ulist[0] = count, trees from ulist[1], at most umax;
+// the count keeps growing past umax) for the precise pass that follows on the stream.
+struct UndecidedList {
+  int32_t* ulist = nullptr;  // nullptr: no device list (the host decides after the launch)
+  int32_t umax = 0;
+  double rows = 0.0;
+};
 hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, int cpb, const void* slab_chk, int nrb, int nslots,
                          const int32_t* order, void* out_loss, void* out_chk, hipStream_t s,
-                         const int32_t* slab_rows = nullptr, int64_t* out_rows = nullptr);
+                         const int32_t* slab_rows = nullptr, int64_t* out_rows = nullptr,
+                         const UndecidedList& ul = UndecidedList());
+// The precise pass's per-(listed tree, operator) sums over the row blocks (fixed order, compensated),
+// written to out (coherent host memory: out_count, then [umax][stride] doubles); resets ulist[0].
+hipError_t launch_precise_reduce(const double* slab, int nrb, int stride, int32_t* ulist, int umax,
+                                 int32_t* out_list, double* out, hipStream_t s);
 hipError_t launch_gather(int dtype, const void* X, const void* y, const void* w, int64_t ld_src, int nfeat,
                          const int64_t* idx, int64_t m, int64_t ld_dst, void* Xd, void* yd, void* wd, hipStream_t s);
 hipError_t launch_feature_stats(int dtype, const void* X, int64_t ld, int64_t m, int nfeat, FeatStat* out,

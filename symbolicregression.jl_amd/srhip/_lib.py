@@ -19,6 +19,8 @@ LIB_PATH = os.environ.get(
 
 # ---- constants mirrored from include/srhip.h (tests/test_abi.py checks them against the header)
 OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_DEVICE, ERR_NOMEM = 0, 1, 2, 3, 4
+COMM_ID_BYTES = 128
+REDUCE_SUM, REDUCE_MAX = 0, 1
 F32, F64, I32 = 0, 1, 2
 
 OP = dict(
@@ -111,6 +113,15 @@ SIGNATURES = {
     "srhip_batcher_stats": (ctypes.c_int, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
     "srhip_batcher_timing": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "srhip_batcher_destroy": (None, [_vp]),
+    "srhip_comm_unique_id": (ctypes.c_int, [_vp]),
+    "srhip_comm_create": (ctypes.c_int, [_vp, _vp, _i32, _i32, ctypes.POINTER(_vp)]),
+    "srhip_comm_destroy": (None, [_vp]),
+    "srhip_comm_size": (ctypes.c_int, [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+    "srhip_comm_allreduce_f64": (ctypes.c_int, [_vp, _vp, _i64, _i32]),
+    "srhip_comm_allgather": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
+    "srhip_comm_migrate_start": (ctypes.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _i32]),
+    "srhip_comm_migrate_wait": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "srhip_eval_loss_sharded": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.POINTER(Loss), _vp, _i64, _vp, _vp]),
     "srhip_last_kernel_ms": (_dbl, [_vp]),
     "srhip_last_work": (ctypes.c_int, [_vp, ctypes.POINTER(_i64)]),
     "srhip_program_stats": (ctypes.c_int, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64),

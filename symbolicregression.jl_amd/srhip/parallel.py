@@ -12,6 +12,11 @@ on MI355X; "gloo" for the CPU tests).  SURVEY.md 8(e) names two partitions, both
   statistic by MAX for Float32) and every rank takes the did_succeed decision identically
   (include/srhip.h "row-sharded evaluation").  One fused all-reduce per population, plus one
   more only when a tree's overflow check is undecided.
+
+Both exchanges exist twice: natively in libsrhip on RCCL (:class:`NativeComm`, the C ABI's
+srhip_comm_* -- what a Julia caller binds), used whenever the ranks run on
+distinct GPUs under the nccl backend; and as torch.distributed calls below (the gloo CPU tests and
+the one-GPU multi-rank rehearsals, where RCCL cannot place two ranks on one device).
 """
 from __future__ import annotations
 
@@ -322,3 +327,150 @@ def migrate_topk(nodes: np.ndarray, offsets: np.ndarray, losses: np.ndarray, k: 
     round (src/Migration.jl:16-38: every population's best members reach every other).  Trees
     longer than max_nodes are skipped.  Returns [(nodes, offsets, losses)] by rank."""
     return migrate_topk_async(nodes, offsets, losses, k, max_nodes, group).wait()
+
+
+# ---- the native exchanges: libsrhip's RCCL communicator (include/srhip.h srhip_comm_*) -----------
+
+class _NativePending:
+    """An in-flight NativeComm.migrate_start: wait() -> [(nodes, offsets, losses)] by rank."""
+
+    def __init__(self, comm, k, max_nodes, t_issue):
+        self.comm, self.k, self.max_nodes, self.t_issue = comm, k, max_nodes, t_issue
+
+    def wait(self):
+        import ctypes
+        import time
+
+        from . import _lib
+
+        t0 = time.perf_counter()
+        ws, k, mx = self.comm.nranks, self.k, self.max_nodes
+        counts = np.zeros(ws, dtype=np.int32)
+        offs = np.zeros((ws, k + 1), dtype=np.int64)
+        losses = np.zeros((ws, k), dtype=np.float64)
+        nodes = np.zeros(ws * k * mx, dtype=NODE_DTYPE)
+        _lib.check(_lib.load().srhip_comm_migrate_wait(self.comm.handle, _lib.ptr(counts), _lib.ptr(offs),
+                                                        _lib.ptr(losses), ctypes.c_void_p(nodes.ctypes.data)))
+        out = []
+        for r in range(ws):
+            c = int(counts[r])
+            of = offs[r, :c + 1].copy()
+            nd = nodes[r * k * mx: r * k * mx + int(of[-1])].copy()
+            out.append((nd, of, losses[r, :c].copy()))
+        timer.seconds += time.perf_counter() - t0
+        timer.calls += 1
+        return out
+
+
+class NativeComm:
+    """libsrhip's RCCL communicator for one rank (one process per GPU): the migration all-gather and
+    the row-shard all-reduces run inside the library on device buffers (csrc/srhip_comm.cpp), with no
+    torch tensors on the data path.  ``from_process_group`` creates it collectively: rank 0 draws the
+    communicator id and the torch.distributed group broadcasts its 128 bytes."""
+
+    def __init__(self, ctx, nranks: int, rank: int, uid: bytes):
+        import ctypes
+
+        from . import _lib
+
+        if len(uid) != _lib.COMM_ID_BYTES:
+            raise ValueError("communicator id must be 128 bytes")
+        self.ctx, self.nranks, self.rank = ctx, int(nranks), int(rank)
+        self._uid = (ctypes.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(uid)
+        h = ctypes.c_void_p()
+        _lib.check(_lib.load().srhip_comm_create(ctx.handle, ctypes.cast(self._uid, ctypes.c_void_p), self.nranks,
+                                                 self.rank, ctypes.byref(h)))
+        self.handle = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes
+
+        from . import _lib
+
+        buf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+        _lib.check(_lib.load().srhip_comm_unique_id(ctypes.cast(buf, ctypes.c_void_p)))
+        return bytes(buf)
+
+    @classmethod
+    def from_process_group(cls, ctx, group=None):
+        import torch
+
+        dist = _dist()
+        rank, ws = dist.get_rank(group), dist.get_world_size(group)
+        uid = cls.unique_id() if rank == 0 else bytes(128)
+        t = torch.tensor(list(uid), dtype=torch.uint8, device=_device(group))
+        dist.broadcast(t, 0, group=group)
+        return cls(ctx, ws, rank, bytes(t.cpu().numpy().tobytes()))
+
+    def migrate_start(self, nodes, offsets, losses, k: int, max_nodes: int) -> _NativePending:
+        """Issue the migration all-gather of this rank's k best trees (by loss) and return at once."""
+        import ctypes
+        import time
+
+        from . import _lib
+
+        t0 = time.perf_counter()
+        nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        losses = np.ascontiguousarray(losses, dtype=np.float64)
+        _lib.check(_lib.load().srhip_comm_migrate_start(self.handle, ctypes.c_void_p(nodes.ctypes.data),
+                                                         _lib.ptr(offsets), len(offsets) - 1, _lib.ptr(losses),
+                                                         int(k), int(max_nodes)))
+        timer.seconds += time.perf_counter() - t0
+        return _NativePending(self, int(k), int(max_nodes), t0)
+
+    def migrate_topk(self, nodes, offsets, losses, k: int, max_nodes: int):
+        return self.migrate_start(nodes, offsets, losses, k, max_nodes).wait()
+
+    def allreduce_f64(self, a, op: str = "sum") -> np.ndarray:
+        from . import _lib
+
+        b = np.ascontiguousarray(a, dtype=np.float64).copy()
+        _lib.check(_lib.load().srhip_comm_allreduce_f64(self.handle, _lib.ptr(b), b.size,
+                                                         _lib.REDUCE_MAX if op == "max" else _lib.REDUCE_SUM))
+        return b
+
+    def allgather(self, data: bytes) -> list:
+        import ctypes
+
+        from . import _lib
+
+        src = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+        dst = np.zeros(len(src) * self.nranks, dtype=np.uint8)
+        _lib.check(_lib.load().srhip_comm_allgather(self.handle, ctypes.c_void_p(src.ctypes.data), len(src),
+                                                     ctypes.c_void_p(dst.ctypes.data)))
+        return [dst[r * len(src):(r + 1) * len(src)].tobytes() for r in range(self.nranks)]
+
+    def eval_loss_sharded(self, prog, ds, loss, idx=None):
+        """Row-sharded eval_loss over this rank's rows (srhip_eval_loss_sharded): (loss[T], ok[T]),
+        identical on every rank."""
+        import ctypes
+        import time
+
+        from . import _lib
+
+        t0 = time.perf_counter()
+        out = np.empty(prog.ntrees, dtype=np.float64)
+        ok = np.empty(prog.ntrees, dtype=np.uint8)
+        ls = loss.c_struct()
+        idxa = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        _lib.check(_lib.load().srhip_eval_loss_sharded(self.ctx.handle, self.handle, ds.handle, prog.handle,
+                                                        ctypes.byref(ls), _lib.ptr(idxa),
+                                                        0 if idxa is None else len(idxa), _lib.ptr(out), _lib.ptr(ok)))
+        timer.seconds += time.perf_counter() - t0
+        timer.calls += 1
+        return out, ok.astype(bool)
+
+    def close(self):
+        from . import _lib
+
+        if getattr(self, "handle", None):
+            _lib.load().srhip_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -538,7 +538,7 @@ class Island:
                 tree = gen_random_tree_fixed_size(size, o, self.nfeatures, self.dtype, rng)
             elif choice == "optimize":
                 cur = PopMember(tree, before_score, before_loss, parent=member.ref)
-                cur, ne = optimize_constants(self.dataset, cur, o, rng=rng)
+                cur, ne = self._optimizer()(self.dataset, cur, o, rng=rng)
                 self.num_evals += ne
                 return cur, True
             elif choice == "do_nothing":
@@ -660,9 +660,14 @@ class Island:
         if search_option(o, "should_optimize_constants"):
             chosen = [m for m, d in zip(pop, do_opt) if d and count_constants(m.tree) > 0]
             if chosen:
-                _, ne = optimize_constants(self.dataset, chosen, o, rng=rng)
+                _, ne = self._optimizer()(self.dataset, chosen, o, rng=rng)
                 self.num_evals += ne
         return pop
+
+    def _optimizer(self):
+        """optimize_constants, or the scorer's own (testing / CPU-baseline hook: a scorer object may
+        carry ``optimize_constants(dataset, members, options, rng=...)`` with the same contract)."""
+        return getattr(self.scorer, "optimize_constants", None) or optimize_constants
 
     def run_iteration(self, pop, curmaxsize, stats):
         """_dispatch_s_r_cycle (src/SymbolicRegression.jl:1088-1129)."""

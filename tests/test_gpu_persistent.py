@@ -58,3 +58,34 @@ def test_persistent_launch_equals_grid_launch_bitwise(c2_small, oracle, monkeypa
     live = np.nonzero(ook)[0]
     rel = np.abs(l0[live] - ol[live]) / np.maximum(np.abs(ol[live]), 1e-300)
     assert np.all((l0[live] == ol[live]) | (rel <= 1e-6)), live[rel > 1e-6]
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_superinstructions_equal_plain_programs_bitwise(c2_small, monkeypatch, dtype):
+    """The leaf-leaf operand forms and the fused push + leaf load (SRHIP_NO_SUPER=1 compiles without
+    them): the same losses, masks and predictions bit for bit, in the persistent launch, the grid
+    launch and the prediction mode; and the programs really are shorter."""
+    opts, X, y, nodes, offs = c2_small
+    ctx = srhip.Context(0)
+    X, y = X.astype(dtype), y.astype(dtype)
+    ds = srhip.DeviceDataset(ctx, X, y)
+    out = {}
+    for sup in ("0", "1"):
+        monkeypatch.setenv("SRHIP_NO_SUPER", sup)
+        monkeypatch.setenv("SRHIP_DUMP_CODE", f"/tmp/srhip_super_{sup}.bin")
+        prog = srhip.Program(ctx, nodes, offs, opts, dtype)
+        monkeypatch.delenv("SRHIP_DUMP_CODE")
+        res = [prog.eval_loss(ds, srhip.L2DistLoss())]
+        monkeypatch.setenv("SRHIP_NO_PERSISTENT", "1")
+        res.append(prog.eval_loss(ds, srhip.L2DistLoss()))
+        monkeypatch.delenv("SRHIP_NO_PERSISTENT")
+        pred, pok = prog.eval_predict(ds, idx=np.arange(0, X.shape[1], 7))
+        res.append((pred, pok))
+        out[sup] = res
+        prog.close()
+    for (a, b) in zip(out["0"], out["1"]):
+        assert np.array_equal(a[1], b[1])
+        assert np.array_equal(np.asarray(a[0]).view(np.uint8), np.asarray(b[0]).view(np.uint8))
+    n_sup = (np.fromfile("/tmp/srhip_super_0.bin", dtype=np.int32).reshape(-1, 2)[:, 0] >= 0).sum()
+    n_plain = (np.fromfile("/tmp/srhip_super_1.bin", dtype=np.int32).reshape(-1, 2)[:, 0] >= 0).sum()
+    assert n_sup < 0.9 * n_plain, (n_sup, n_plain)

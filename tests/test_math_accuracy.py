@@ -195,3 +195,27 @@ def test_float32_sine_kernel_error():
         exact = mpmath.sin(mpmath.mpf(float(y))) / mpmath.mpf(float(y))
         worst = max(worst, abs(float((p - exact) / exact)))
     assert worst < 2.0 ** -35, worst
+
+
+@pytest.mark.parametrize("name", ["sin", "cos"])
+def test_julia_float32_trig_restatement(oracle, name):
+    """srm_jtrigf (include/srhip_math.h): Julia's own Float32 sin / cos -- FreeBSD __kernel_sindf /
+    __kernel_cosdf per quadrant after Julia's rem_pio2_kernel(::Float32) -- restated from the
+    published sources (bits against Julia unpinned: Julia cannot run here).  It is within 1 ULP of the
+    correctly rounded value (mpmath), differs from it on < 1 % of arguments, and the default
+    minimax kernel (srm_trigf) agrees with it on all but a small share of arguments: the rows where
+    the two kernels' errors straddle a Float32 rounding boundary."""
+    mpmath.mp.prec = 200
+    x = F32_CASES[name](3000).astype(np.float32)
+    # the reduction branches: |x| < pi/4, the +-k pi/2 special cases up to 9pi/4, Cody-Waite, Payne-Hanek
+    x = np.concatenate([x, np.float32([0.0, -0.0, 1e-5, -3e-4, 0.7853981, 0.7853982, 2.356194, 3.926990,
+                                       5.497787, 7.0685835, -7.0685835, 1e9, -3e20, 3.4e38])])
+    got = oracle.srm("j" + name, x)
+    fn = getattr(mpmath, name)
+    cr = np.array([float(fn(mpmath.mpf(float(v)))) for v in x]).astype(np.float32)
+    u = _ulps32(got, cr)
+    assert u.max() <= 1, (name, x[np.argmax(u)])
+    assert np.mean(u > 0) < 0.01, np.mean(u > 0)
+    y = F32_CASES[name](400_000).astype(np.float32)
+    diff = np.mean(oracle.srm("j" + name, y) != oracle.srm(name, y))
+    assert diff < 0.005, diff
