@@ -13,7 +13,7 @@ from srhip import workloads  # noqa: E402
 
 opts, X, y, trees, nodes, offs = workloads.c2(0, 1024, 4096)
 sr.Program(None, nodes, offs, opts, np.float32)
-rec = np.fromfile("/tmp/srhip_code.bin", dtype=np.int32).reshape(-1, 2)
+rec = np.fromfile("/tmp/srhip_code.bin", dtype=np.int32).reshape(-1, 4)[:, :2]
 
 # handler names (srhip_isa.h layout)
 K_MAX = 8

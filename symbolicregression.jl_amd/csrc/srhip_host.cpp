@@ -26,10 +26,12 @@
 #include <condition_variable>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <numeric>
 #include <string>
 #include <thread>
 #include <type_traits>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/srhip.h"
@@ -114,48 +116,41 @@ template <typename T> class TreeCompiler {
   }
 
   // returns SRHIP_OK or an error (g_err set); fills info and appends to code
-  int compile(TreeInfo& info, std::vector<Ins>& code) {
+  int compile(TreeInfo& info, std::vector<Ins>& code) { return compile_pair(info, code, nullptr, nullptr); }
+  // The program of the tree (derived columns as set by set_derived) and, when dinfo is given, its
+  // derived program too (derived columns dspec at dbase, set_derived's meaning) from the same
+  // analysis: validation, counts, constant numbering and the host-decided checks do not depend on the
+  // derived columns, so they run once.  Only code_begin / code_len / need / cost / static_fail of
+  // *dinfo are filled (what a population's derived program keeps).
+  int compile_pair(TreeInfo& info, std::vector<Ins>& code, TreeInfo* dinfo, std::vector<Ins>* dcode,
+                   const std::vector<uint32_t>* dspec = nullptr, int dbase = 0) {
     info = TreeInfo();
     if (nn_ <= 0) return fail(SRHIP_ERR_INVALID, "empty tree");
     memo_const_.assign(nn_, -1);
-    memo_need_.assign(nn_, -1);
     state_.assign(nn_, 0);
     int rc = validate(0, 0);
     if (rc) return rc;
-    info.nnodes = count_nodes(0);
-    info.nops = count_opnodes(0);
-    info.nconst = count_constants(0);
     cidx_.assign(nn_, -1);
-    dcolv_.assign(dspec_ && !grad_ ? nn_ : 0, -1);
-    for (int64_t i = 0; i < (int64_t)dcolv_.size(); ++i) {
-      const srhip_node& n = nd_[i];
-      if (n.degree != 1 || !leaf_is_feature(n.l)) continue;
-      const uint32_t key = ((uint32_t)classify_unop(unaop(i)) << 16) | (uint32_t)(nd_[n.l].feature - 1);
-      for (size_t d = 0; d < dspec_->size(); ++d)
-        if ((*dspec_)[d] == key) dcolv_[i] = (int32_t)d;
-    }
-    int32_t nc = 0;
-    number_constants(0, nc);
+    tally(0, info);
     // host-decided checks (reference semantics, see header comment)
     static_checks(0, -1, info);
-    info.code_begin = (int32_t)code.size();
-    if (!info.static_fail) {
-      info.need = need(0);
-      if (info.need > K_MAX)
-        return fail(SRHIP_ERR_UNSUPPORTED, "tree needs %d stack slots (> %d)", info.need, K_MAX);
-      code_ = &code;
-      info_ = &info;
-      emit(0, 0, -1);
-      if (super_) fuse_push_loads(code, info.code_begin);
-      Ins end{H_END, 0, 0};
-      code.push_back(end);
-      for (int64_t i = info.code_begin; i < (int64_t)code.size(); ++i) info.cost += op_cost(code[i].h);
-    } else {
-      Ins end{H_END, 0, 0};
-      code.push_back(end);
-    }
-    info.code_len = (int32_t)code.size() - info.code_begin;
-    return SRHIP_OK;
+    rc = emit_program(info, code);
+    if (rc || !dinfo) return rc;
+    const std::vector<uint32_t>* ds0 = dspec_;
+    const int db0 = dbase_;
+    set_derived(dspec, dbase);
+    scratch_.op_sumcheck.clear();
+    scratch_.static_fail = info.static_fail;
+    scratch_.need = 0;
+    scratch_.cost = 0.0;
+    rc = emit_program(scratch_, *dcode);
+    set_derived(ds0, db0);
+    dinfo->static_fail = scratch_.static_fail;
+    dinfo->need = scratch_.need;
+    dinfo->cost = scratch_.cost;
+    dinfo->code_begin = scratch_.code_begin;
+    dinfo->code_len = scratch_.code_len;
+    return rc;
   }
 
  private:
@@ -191,6 +186,53 @@ template <typename T> class TreeCompiler {
   }
 
  private:
+  TreeInfo scratch_;  // compile_pair's derived-program info (its op_sumcheck's capacity reused)
+
+  // code for the analysed tree (validate, tally and static_checks done) under the current derived
+  // columns, appended to code; fills info's need, cost, code_begin and code_len
+  int emit_program(TreeInfo& info, std::vector<Ins>& code) {
+    dcolv_.assign(dspec_ && !grad_ ? nn_ : 0, -1);
+    for (int64_t i = 0; i < (int64_t)dcolv_.size(); ++i) {
+      const srhip_node& n = nd_[i];
+      if (n.degree != 1 || !leaf_is_feature(n.l)) continue;
+      const uint32_t key = ((uint32_t)classify_unop(unaop(i)) << 16) | (uint32_t)(nd_[n.l].feature - 1);
+      for (size_t d = 0; d < dspec_->size(); ++d)
+        if ((*dspec_)[d] == key) dcolv_[i] = (int32_t)d;
+    }
+    memo_need_.assign(nn_, -1);
+    info.code_begin = (int32_t)code.size();
+    if (!info.static_fail) {
+      info.need = need(0);
+      if (info.need > K_MAX)
+        return fail(SRHIP_ERR_UNSUPPORTED, "tree needs %d stack slots (> %d)", info.need, K_MAX);
+      code_ = &code;
+      info_ = &info;
+      emit(0, 0, -1);
+      if (super_) fuse_push_loads(code, info.code_begin);
+      Ins end{H_END, 0, 0};
+      code.push_back(end);
+      for (int64_t i = info.code_begin; i < (int64_t)code.size(); ++i) info.cost += op_cost(code[i].h);
+    } else {
+      Ins end{H_END, 0, 0};
+      code.push_back(end);
+    }
+    info.code_len = (int32_t)code.size() - info.code_begin;
+    return SRHIP_OK;
+  }
+
+  // one depth-first pass: node, operator-node and constant counts (count_nodes walks, shared
+  // subtrees counted per use) and the get_constants numbering of the constant leaves
+  void tally(int64_t i, TreeInfo& info) {
+    const srhip_node& n = nd_[i];
+    ++info.nnodes;
+    if (n.degree == 0) {
+      if (n.constant) cidx_[i] = info.nconst++;
+      return;
+    }
+    ++info.nops;
+    tally(n.l, info);
+    if (n.degree == 2) tally(n.r, info);
+  }
 
   int validate(int64_t i, int depth) {
     if (i < 0 || i >= nn_) return fail(SRHIP_ERR_INVALID, "child index %lld out of range", (long long)i);
@@ -228,24 +270,6 @@ template <typename T> class TreeCompiler {
     return rc;
   }
 
-  int32_t count_opnodes(int64_t i) const {  // operator nodes (degree >= 1), as count_nodes walks them
-    const srhip_node& n = nd_[i];
-    if (n.degree == 0) return 0;
-    if (n.degree == 1) return 1 + count_opnodes(n.l);
-    return 1 + count_opnodes(n.l) + count_opnodes(n.r);
-  }
-  int32_t count_nodes(int64_t i) const {
-    const srhip_node& n = nd_[i];
-    if (n.degree == 0) return 1;
-    if (n.degree == 1) return 1 + count_nodes(n.l);
-    return 1 + count_nodes(n.l) + count_nodes(n.r);
-  }
-  int32_t count_constants(int64_t i) const {
-    const srhip_node& n = nd_[i];
-    if (n.degree == 0) return n.constant ? 1 : 0;
-    if (n.degree == 1) return count_constants(n.l);
-    return count_constants(n.l) + count_constants(n.r);
-  }
   bool is_const(int64_t i) {
     if (memo_const_[i] >= 0) return memo_const_[i];
     const srhip_node& n = nd_[i];
@@ -267,15 +291,6 @@ template <typename T> class TreeCompiler {
     if (d < 0) return -1;
     dmask_ |= 1ull << d;
     return dbase_ + d;
-  }
-  void number_constants(int64_t i, int32_t& k) {
-    const srhip_node& n = nd_[i];
-    if (n.degree == 0) {
-      if (n.constant) cidx_[i] = k++;
-      return;
-    }
-    number_constants(n.l, k);
-    if (n.degree == 2) number_constants(n.r, k);
   }
   // operand field of an instruction that consumes constant leaf i (gradient program only)
   uint32_t cop(int64_t i) const { return grad_ && cidx_[i] >= 0 ? (uint32_t)cidx_[i] : 0u; }
@@ -431,7 +446,15 @@ template <typename T> class TreeCompiler {
 
   // Superinstructions (evaluation programs; SRHIP_NO_SUPER=1 turns them off): the leaf-leaf operand
   // forms (emit) and a push fused with the leaf load that follows it: one dispatch instead of two.
-  const bool super_ = !grad_ && ![] { const char* e = getenv("SRHIP_NO_SUPER"); return e && *e && *e != '0'; }();
+  const bool super_ = !grad_ && super_env();
+
+ public:
+  static bool super_env() {
+    const char* e = getenv("SRHIP_NO_SUPER");
+    return !(e && *e && *e != '0');
+  }
+
+ private:
   static void fuse_push_loads(std::vector<Ins>& code, int32_t begin) {
     size_t w = (size_t)begin;
     for (size_t r = (size_t)begin; r < code.size(); ++r) {
@@ -636,6 +659,143 @@ class HostPool {
   uint32_t gen_ = 0;
 };
 
+// Per-tree code cache: a tree's compiled code and metadata depend only on its node table (constant
+// values included: folded constants are immediates), the operator tables and the element type, and
+// its derived-program code also on which derived column each of its U(X[f]) nodes reads and where the
+// derived columns start (the population's feature count).  Entries are keyed by a hash of the node
+// bytes and operator tables and confirmed by comparing them in full, so a hit returns exactly the
+// bytes a compile would produce.  Sharded by hash; a shard that grows past its share of
+// CODE_CACHE_ENTRIES is emptied (the cache holds recent trees: the search's survivors, migrants and
+// re-scored members).  SRHIP_NO_CODE_CACHE=1 bypasses it (read per compile).
+constexpr int CODE_CACHE_SHARDS = 64;
+constexpr size_t CODE_CACHE_ENTRIES = 1 << 15;
+
+inline uint64_t mix64(uint64_t h) {
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ull;
+  return h ^ (h >> 33);
+}
+inline uint64_t hash_words(const void* p, size_t bytes, uint64_t h) {
+  const unsigned char* c = (const unsigned char*)p;
+  size_t i = 0;
+  for (; i + 8 <= bytes; i += 8) {
+    uint64_t w;
+    memcpy(&w, c + i, 8);
+    h = mix64(h ^ w) + 0x9e3779b97f4a7c15ull;
+  }
+  for (; i < bytes; ++i) h = mix64(h ^ c[i]);
+  return h;
+}
+inline uint64_t ops_hash(const srhip_program& P) {
+  uint64_t h = hash_words(P.binops.data(), P.binops.size() * 4, 0x5eed ^ P.binops.size());
+  return hash_words(P.unaops.data(), P.unaops.size() * 4, h ^ (P.unaops.size() << 20));
+}
+
+template <typename T> class CodeCache {
+ public:
+  struct Derived {
+    int32_t dbase = -1;
+    std::vector<int32_t> dsig;  // derived column of each U(X[f]) node, in node order (-1: none)
+    std::vector<Ins> code;
+    TreeInfo info;              // need, cost, code_len, static_fail
+    uint64_t dmask = 0;
+  };
+  static CodeCache& get() {
+    static CodeCache* c = new CodeCache();  // never destroyed (worker threads may outlive statics)
+    return *c;
+  }
+  static bool enabled() {
+    const char* e = getenv("SRHIP_NO_CODE_CACHE");
+    return !(e && *e && *e != '0');
+  }
+  // derived column per U(X[f]) node of a valid tree (as TreeCompiler::emit_program assigns them)
+  static void derived_sig(const srhip_node* nd, int64_t nn, const srhip_program& P, std::vector<int32_t>& sig) {
+    sig.clear();
+    for (int64_t i = 0; i < nn; ++i) {
+      const srhip_node& n = nd[i];
+      if (n.degree != 1 || nd[n.l].degree != 0 || nd[n.l].constant) continue;
+      const uint32_t key = ((uint32_t)classify_unop(P.unaops[n.op - 1]) << 16) | (uint32_t)(nd[n.l].feature - 1);
+      int32_t d = -1;
+      for (size_t k = 0; k < P.dspec.size(); ++k)
+        if (P.dspec[k] == key) d = (int32_t)k;
+      sig.push_back(d);
+    }
+  }
+  // On a hit, appends the plain code to code (and, with dcode, the derived code to dcode) exactly as
+  // TreeCompiler::compile / compile_pair would, fills info / *dinfo / *dmask and returns true.
+  bool lookup(uint64_t h, const srhip_node* nd, int64_t nn, const srhip_program& P, bool sup, TreeInfo& info,
+              std::vector<Ins>& code, TreeInfo* dinfo, std::vector<Ins>* dcode, uint64_t* dmask,
+              std::vector<int32_t>& sig) {
+    Shard& s = shards_[h % CODE_CACHE_SHARDS];
+    std::lock_guard<std::mutex> lk(s.mu);
+    auto it = s.map.find(h);
+    if (it == s.map.end()) return false;
+    const Entry& e = it->second;
+    if (!same(e, nd, nn, P, sup)) return false;
+    if (dinfo) {
+      derived_sig(nd, nn, P, sig);
+      if (!e.d || e.d->dbase != P.maxfeat || e.d->dsig != sig) return false;
+      dinfo->static_fail = e.d->info.static_fail;
+      dinfo->need = e.d->info.need;
+      dinfo->cost = e.d->info.cost;
+      dinfo->code_len = e.d->info.code_len;
+      dinfo->code_begin = (int32_t)dcode->size();
+      dcode->insert(dcode->end(), e.d->code.begin(), e.d->code.end());
+      *dmask = e.d->dmask;
+    }
+    info = e.info;
+    info.code_begin = (int32_t)code.size();
+    code.insert(code.end(), e.code.begin(), e.code.end());
+    return true;
+  }
+  void insert(uint64_t h, const srhip_node* nd, int64_t nn, const srhip_program& P, bool sup, const TreeInfo& info,
+              const Ins* code, const TreeInfo* dinfo, const Ins* dcode, uint64_t dmask) {
+    Entry e;
+    e.nodes.assign(nd, nd + nn);
+    e.binops = P.binops;
+    e.unaops = P.unaops;
+    e.super = sup;
+    e.info = info;
+    e.code.assign(code, code + info.code_len);
+    if (dinfo) {
+      e.d.reset(new Derived());
+      e.d->dbase = P.maxfeat;
+      derived_sig(nd, nn, P, e.d->dsig);
+      e.d->info.static_fail = dinfo->static_fail;
+      e.d->info.need = dinfo->need;
+      e.d->info.cost = dinfo->cost;
+      e.d->info.code_len = dinfo->code_len;
+      e.d->code.assign(dcode, dcode + dinfo->code_len);
+      e.d->dmask = dmask;
+    }
+    Shard& s = shards_[h % CODE_CACHE_SHARDS];
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (s.map.size() >= CODE_CACHE_ENTRIES / CODE_CACHE_SHARDS) s.map.clear();
+    s.map[h] = std::move(e);
+  }
+
+ private:
+  struct Entry {
+    std::vector<srhip_node> nodes;
+    std::vector<int32_t> binops, unaops;
+    bool super = true;  // compiled with superinstructions (SRHIP_NO_SUPER unset)
+    TreeInfo info;
+    std::vector<Ins> code;
+    std::unique_ptr<Derived> d;
+  };
+  struct Shard {
+    std::mutex mu;
+    std::unordered_map<uint64_t, Entry> map;
+  };
+  static bool same(const Entry& e, const srhip_node* nd, int64_t nn, const srhip_program& P, bool sup) {
+    return e.super == sup && (int64_t)e.nodes.size() == nn && memcmp(e.nodes.data(), nd, (size_t)nn * sizeof(srhip_node)) == 0 &&
+           e.binops == P.binops && e.unaops == P.unaops;
+  }
+  Shard shards_[CODE_CACHE_SHARDS];
+};
+
 // The population's programs in one pass over the trees: the plain program and, when the population
 // has derived columns (srhip_isa.h), the derived program, compiled tree by tree on the host pool
 // (contiguous tree ranges; per-range code vectors concatenated in tree order: the same bytes as one
@@ -648,24 +808,39 @@ void choose_derived_t(srhip_program& P) {
   const char* env = getenv("SRHIP_NO_DERIVE");
   const bool off = env && *env && *env != '0';
   if (std::is_same<T, int32_t>::value || off) return;
-  std::vector<std::pair<uint32_t, int>> cnt;  // (key, uses)
-  for (int64_t i = 0; i < (int64_t)P.nodes.size(); ++i) {
-    const srhip_node& n = P.nodes[i];
-    if (n.degree != 1) continue;
-    // node tables are per tree with tree-relative child indices: find the child in this tree
-    const int32_t t = (int32_t)(std::upper_bound(P.offsets.begin(), P.offsets.end(), i) - P.offsets.begin()) - 1;
-    // (this pass runs before the trees are validated: a malformed child or operator index is skipped
-    // here and rejected by the compiler's validation with SRHIP_ERR_INVALID)
-    if (t < 0 || t >= P.ntrees || n.l < 0 || n.l >= P.offsets[t + 1] - P.offsets[t]) continue;
-    if (n.op < 1 || (size_t)n.op > P.unaops.size()) continue;
-    const srhip_node& c = P.nodes[P.offsets[t] + n.l];
-    if (c.degree != 0 || c.constant || c.feature < 1) continue;
-    const int u = classify_unop(P.unaops[n.op - 1]);
-    if (!un_derivable(u)) continue;
-    const uint32_t key = ((uint32_t)u << 16) | (uint32_t)(c.feature - 1);
-    auto it = std::find_if(cnt.begin(), cnt.end(), [&](const std::pair<uint32_t, int>& e) { return e.first == key; });
-    if (it == cnt.end()) cnt.emplace_back(key, 1);
-    else ++it->second;
+  std::vector<std::pair<uint32_t, int>> cnt;  // (key, uses), in order of first use
+  // uses counted in a dense (unary class, feature) table when it is small, else by search in cnt
+  const int64_t nf = std::max<int32_t>(P.maxfeat, 1);
+  const bool dense = (int64_t)NUM_UNOP * nf <= (1 << 16);
+  std::vector<int32_t> slot(dense ? (size_t)(NUM_UNOP * nf) : 0, -1);  // index into cnt
+  for (int32_t t = 0; t < P.ntrees; ++t) {
+    // node tables are per tree with tree-relative child indices
+    const int64_t b = P.offsets[t], e = P.offsets[t + 1];
+    for (int64_t i = b; i < e; ++i) {
+      const srhip_node& n = P.nodes[i];
+      if (n.degree != 1) continue;
+      // (this pass runs before the trees are validated: a malformed child or operator index is
+      // skipped here and rejected by the compiler's validation with SRHIP_ERR_INVALID)
+      if (n.l < 0 || n.l >= e - b) continue;
+      if (n.op < 1 || (size_t)n.op > P.unaops.size()) continue;
+      const srhip_node& c = P.nodes[b + n.l];
+      if (c.degree != 0 || c.constant || c.feature < 1) continue;
+      const int u = classify_unop(P.unaops[n.op - 1]);
+      if (!un_derivable(u)) continue;
+      const uint32_t key = ((uint32_t)u << 16) | (uint32_t)(c.feature - 1);
+      int32_t* sl = dense && c.feature <= nf ? &slot[(size_t)u * nf + (c.feature - 1)] : nullptr;
+      int32_t k = sl ? *sl : -1;
+      if (!sl) {
+        auto it = std::find_if(cnt.begin(), cnt.end(), [&](const std::pair<uint32_t, int>& q) { return q.first == key; });
+        if (it != cnt.end()) k = (int32_t)(it - cnt.begin());
+      }
+      if (k < 0) {
+        k = (int32_t)cnt.size();
+        cnt.emplace_back(key, 0);
+        if (sl) *sl = k;
+      }
+      ++cnt[k].second;
+    }
   }
   std::stable_sort(cnt.begin(), cnt.end(), [](const std::pair<uint32_t, int>& a, const std::pair<uint32_t, int>& b) {
     return a.second > b.second;
@@ -706,19 +881,30 @@ int compile_program_t(srhip_program& P) {
   std::vector<std::vector<Ins>> part(W), dpart(W);
   std::vector<std::string> errs(W);
   std::vector<int> rcs(W, SRHIP_OK);
+  CodeCache<T>* cache = CodeCache<T>::enabled() ? &CodeCache<T>::get() : nullptr;
+  const bool sup = TreeCompiler<T>::super_env();
+  const uint64_t oph = cache ? ops_hash(P) ^ (sup ? 0x5u : 0u) : 0;
   const std::function<void(int)> range = [&](int w) {
     const int32_t t0 = (int32_t)((int64_t)n * w / W), t1 = (int32_t)((int64_t)n * (w + 1) / W);
     TreeCompiler<T> tc(nullptr, 0, P, 0);
+    std::vector<int32_t> sig;
     for (int32_t t = t0; t < t1 && !rcs[w]; ++t) {
       const int64_t b = P.offsets[t], e = P.offsets[t + 1];
-      tc.rebind(P.nodes.data() + b, e - b);
-      tc.set_derived(nullptr, 0);
-      int rc = tc.compile(P.info[t], part[w]);
-      if (!rc && der) {
-        tc.set_derived(&P.dspec, P.maxfeat);
-        rc = tc.compile(dinfo[t], dpart[w]);
-        P.dmask[t] = tc.dmask();
+      const srhip_node* tn = P.nodes.data() + b;
+      uint64_t h = 0;
+      if (cache) {
+        h = hash_words(tn, (size_t)(e - b) * sizeof(srhip_node), oph ^ (uint64_t)(e - b));
+        if (cache->lookup(h, tn, e - b, P, sup, P.info[t], part[w], der ? &dinfo[t] : nullptr, der ? &dpart[w] : nullptr,
+                          &P.dmask[t], sig))
+          continue;
       }
+      tc.rebind(tn, e - b);
+      const int rc = der ? tc.compile_pair(P.info[t], part[w], &dinfo[t], &dpart[w], &P.dspec, P.maxfeat)
+                         : tc.compile(P.info[t], part[w]);
+      if (!rc && der) P.dmask[t] = tc.dmask();
+      if (!rc && cache)
+        cache->insert(h, tn, e - b, P, sup, P.info[t], part[w].data() + P.info[t].code_begin, der ? &dinfo[t] : nullptr,
+                      der ? dpart[w].data() + dinfo[t].code_begin : nullptr, P.dmask[t]);
       if (rc) {
         errs[w] = "tree " + std::to_string(t) + ": " + g_err;
         rcs[w] = rc;
@@ -753,19 +939,25 @@ int compile_program_t(srhip_program& P) {
       P.dmax_len = std::max(P.dmax_len, ti.code_len);
     }
   }
-  // (diagnostic) SRHIP_DUMP_CODE=path: the derived (or plain) program's instructions as (h, a) pairs
-  // with a -1 separator per tree, for instruction-mix studies (scripts/code_stats.py)
+  // (diagnostic) SRHIP_DUMP_CODE=path: the derived (or plain) program's instructions as int32 (h, a,
+  // imm low, imm high) records with a (-1, static_fail, need, cost) separator per tree, for
+  // instruction-mix studies (scripts/code_stats.py) and the code-cache test; with derived columns the
+  // plain program's go to path.plain
   if (const char* dump = getenv("SRHIP_DUMP_CODE")) {
-    if (FILE* f = fopen(dump, "wb")) {
-      const std::vector<Ins>& code = der ? P.dcode : P.code;
+    for (int pass = 0; pass < (der ? 2 : 1); ++pass) {
+      const bool dd = der && pass == 0;
+      FILE* f = fopen(pass ? (std::string(dump) + ".plain").c_str() : dump, "wb");
+      if (!f) break;
+      const std::vector<Ins>& code = dd ? P.dcode : P.code;
       for (int32_t t = 0; t < n; ++t) {
-        const TreeInfo& ti = der ? dinfo[t] : P.info[t];
+        const TreeInfo& ti = dd ? dinfo[t] : P.info[t];
         for (int32_t i = 0; i < ti.code_len; ++i) {
           const Ins& ins = code[(size_t)ti.code_begin + i];
-          const int32_t rec[2] = {(int32_t)ins.h, (int32_t)ins.a};
+          const int32_t rec[4] = {(int32_t)ins.h, (int32_t)ins.a, (int32_t)(uint32_t)ins.imm,
+                                  (int32_t)(uint32_t)(ins.imm >> 32)};
           fwrite(rec, sizeof rec, 1, f);
         }
-        const int32_t sep[2] = {-1, ti.static_fail ? 1 : 0};
+        const int32_t sep[4] = {-1, ti.static_fail ? 1 : 0, ti.need, (int32_t)ti.cost};
         fwrite(sep, sizeof sep, 1, f);
       }
       fclose(f);
@@ -1467,6 +1659,9 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   const int probe_env = env_int("SRHIP_PROBE_BLOCKS", -1);
   bool persistent = false;
   int probe_blocks = 0;
+  // SRHIP_XWIDE=1: the persistent main launch runs the extra-wide variant (R = 32, 2 waves per SIMD);
+  // the probe keeps R = 16 (a probe tile is one loss chunk)
+  const bool xwide = env_flag("SRHIP_XWIDE");
   {
     const int Kp = kvariant(P->kmax);
     persistent = !no_persistent && mode == MODE_LOSS && debug_stop() == 0 && dtype == SRHIP_F32 &&
@@ -1478,6 +1673,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       const int tile = 64 * R;
       int rb = prb_env >= tile && prb_env <= ROW_ALIGN && (prb_env & (prb_env - 1)) == 0 ? prb_env : 2048;
       rb = std::max(rb, std::max(tile, loss_chunk(dtype)));
+      if (xwide) rb = std::max(rb, 64 * R_F32_XWIDE);
       const size_t es = dtype_size(dtype);
       const int base_cols = P->maxfeat + 1 + (weighted ? 1 : 0);
       use_d = nd > 0 && (size_t)(base_cols + nd) * rb * es <= lds_budget(R, K, true);
@@ -1671,7 +1867,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     const int slices = std::max(1, std::min(slices_env, 64));
     a.tail_slices = slices;
     a.tail_blocks = slices > 1 && nmain > wgs && nl >= 16 * slices ? nmain % wgs : 0;
-    HIP_TRY(launch_eval(dtype, a, R, K, mode, true, dim3(wgs, 1), L.lds, ctx->stream));
+    HIP_TRY(launch_eval(dtype, a, xwide ? R_F32_XWIDE : R, K, mode, true, dim3(wgs, 1), L.lds, ctx->stream));
   } else {
     HIP_TRY(launch_eval(dtype, a, R, K, mode, L.xlds, grid, L.lds, ctx->stream));
   }

@@ -85,3 +85,37 @@ def test_host_pool_back_to_back_jobs_from_many_threads():
         t.join()
     assert not errs, errs
     assert len(out) == 240 and all(o == ref for o in out)
+
+
+def test_code_cache_hits_equal_fresh_compiles(tmp_path, monkeypatch):
+    """The per-tree code cache (csrc/srhip_host.cpp CodeCache): a population compiled from cached
+    entries (second compile of the same trees, and a population mixing cached and new trees) has
+    exactly the instructions (handler, operand, immediate), stack needs and costs of a compile with the
+    cache off -- plain and derived programs -- and the superinstruction switch is part of the key."""
+    import srhip as sr
+    from srhip import workloads
+
+    opts, _, _, _, nodes, offs = workloads.c2(0, 512, 4096)
+    _, _, _, _, nodes2, offs2 = workloads.c2(1, 512, 4096)
+    # a population of half old trees (cache hits) and half new ones
+    half = int(offs[256])
+    mixed = np.concatenate([nodes[:half], nodes2[: int(offs2[256])]])
+    moffs = np.concatenate([offs[:257], half + offs2[1:257]])
+
+    def dump(nd, of, tag, cache, nosuper=False):
+        path = str(tmp_path / f"{tag}.bin")
+        monkeypatch.setenv("SRHIP_DUMP_CODE", path)
+        monkeypatch.setenv("SRHIP_NO_CODE_CACHE", "0" if cache else "1")
+        monkeypatch.setenv("SRHIP_NO_SUPER", "1" if nosuper else "0")
+        p = sr.Program(None, nd, of, opts, np.float32)
+        st = _stats(sr, p)
+        monkeypatch.delenv("SRHIP_DUMP_CODE")
+        return open(path, "rb").read(), open(path + ".plain", "rb").read(), st
+
+    for nosuper in (False, True):
+        fresh = dump(nodes, offs, f"fresh{nosuper}", False, nosuper)
+        first = dump(nodes, offs, f"first{nosuper}", True, nosuper)
+        again = dump(nodes, offs, f"again{nosuper}", True, nosuper)
+        assert first == fresh and again == fresh
+    assert dump(nodes, offs, "s", True)[0] != dump(nodes, offs, "n", True, True)[0]
+    assert dump(mixed, moffs, "mixc", True) == dump(mixed, moffs, "mixf", False)
