@@ -185,6 +185,10 @@ int pick_rows_per_lane(int dtype, int K, int mode, int64_t m) {
 
 hipError_t launch_eval(int dtype, const EvalArgs& a, int R, int K, int mode, bool xlds, dim3 grid, size_t lds,
                        hipStream_t s) {
+  if (R == R_F32_XWIDE) {  // the extra-wide Float32 persistent loss launch (K = 2, LDS-staged)
+    if (dtype != SRHIP_F32 || K > 2 || mode != MODE_LOSS || !xlds || !a.persistent) return hipErrorInvalidValue;
+    return launch_eval_f32x(a, grid, lds, s);
+  }
   if (R != pick_rows_per_lane(dtype, K, mode, a.nvalid)) return hipErrorInvalidValue;
   if (R == R_F32_WIDE && R != R_F32) {  // Float32, K = 2, loss or prediction
     if (mode != MODE_LOSS && mode != MODE_PRED) return hipErrorInvalidValue;

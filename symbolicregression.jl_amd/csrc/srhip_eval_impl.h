@@ -327,6 +327,11 @@ __device__ __attribute__((always_inline)) inline float abs_fold(float m, const R
           SRHIP_M3("v_minimum3_f32", 13, 14) SRHIP_M3("v_minimum3_f32", 15, 16)
           : "+v"(m) : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]),
             "v"(v[8]), "v"(v[9]), "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
+  } else if constexpr (R == 32) {
+    RV<float, 16> lo, hi;
+    UNR for (int r = 0; r < 16; ++r) { lo[r] = v[r]; hi[r] = v[16 + r]; }
+    m = abs_fold<16, MAX>(m, lo);
+    m = abs_fold<16, MAX>(m, hi);
   } else if constexpr (R == 8) {
     if constexpr (MAX)
       asm(SRHIP_M3("v_maximum3_f32", 1, 2) SRHIP_M3("v_maximum3_f32", 3, 4) SRHIP_M3("v_maximum3_f32", 5, 6)
@@ -721,7 +726,11 @@ __device__ __attribute__((noinline)) RV<T, R> loss_rows_generic(RV<T, R> a, RV<T
 template <typename T, int R>
 __device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& p, RV<T, R>& A, const T* ybase,
                                                                 const T* wbase, int lane, int64_t row0, bool full,
-                                                                LAccT<T>& lacc) {
+                                                                LAccT<T>* lacc) {
+  // lacc[CPT]: this lane's sum per loss chunk of the tile (a tile longer than a chunk, R = 32, covers
+  // two: register r of a lane belongs to chunk r / (R / CPT))
+  constexpr int CHK = sizeof(T) == 8 ? LOSS_CHUNK_8B : LOSS_CHUNK_4B;
+  constexpr int CPT = 64 * R > CHK ? 64 * R / CHK : 1, RPC = R / CPT;
   // full: every row of the tile is valid (wave-uniform)
   RV<T, R> yv;
   load_rows<T, R>(ybase, lane, yv);
@@ -734,7 +743,7 @@ __device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& 
         const int64_t row = row0 + (r / VEC) * 64 * VEC + lane * VEC + (r % VEC);
         c = row < p.nvalid ? c : 0;
       }
-      lacc += c;
+      lacc[r / RPC] += c;
     }
   } else {
     RV<T, R> wv;
@@ -754,7 +763,7 @@ __device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& 
     }
     if (p.weighted) {
       // padded rows carry w = 0 and a replicated (finite when ok) prediction
-      UNR for (int r = 0; r < R; ++r) lacc += (double)(wv[r] * lv[r]);
+      UNR for (int r = 0; r < R; ++r) lacc[r / RPC] += (double)(wv[r] * lv[r]);
     } else {
       if (!full) {
         UNR for (int r = 0; r < R; ++r) {
@@ -770,10 +779,10 @@ __device__ __attribute__((always_inline)) inline void loss_tile(const EvalArgs& 
         UNR for (int r = 0; r < R; r += 4) {
           const F2 a = {lv[r], lv[r + 1]}, b = {lv[r + 2], lv[r + 3]};
           const F2 q = a + b;
-          lacc += (double)(q.x + q.y);
+          lacc[r / RPC] += (double)(q.x + q.y);
         }
       } else {
-        UNR for (int r = 0; r < R; ++r) lacc += (double)lv[r];
+        UNR for (int r = 0; r < R; ++r) lacc[r / RPC] += (double)lv[r];
       }
     }
   }
@@ -1020,7 +1029,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
   // at a time, so the two tiles of a row block's costliest tree run on two waves at once; the check
   // statistic and the row count then combine by atomics (max of non-negative float bits; NaN bits
   // order above every finite and infinite value), each loss chunk is still written by one wave
-  const bool tile_claims = p.tile_claims != 0 && TILE % (sizeof(T) == 8 ? LOSS_CHUNK_8B : LOSS_CHUNK_4B) == 0;
+  const bool tile_claims = p.tile_claims != 0 && TILE == (sizeof(T) == 8 ? LOSS_CHUNK_8B : LOSS_CHUNK_4B);
   const int nclaims = tile_claims ? group_n * ntiles : group_n;
   for (int cl = wave; cl < nclaims;) {
     const int ti = tile_claims ? cl / ntiles : cl;
@@ -1041,7 +1050,12 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
         for (int k = 0; k < p.prec_stride; ++k)
           reinterpret_cast<double*>(p.slab_prec)[((int64_t)ti * p.prec_stride + k) * p.nrb + rb] = 0.0;
     }
-    LAccT<T> lacc = 0;
+    // loss chunks per tile (CPT > 1: R = 32 tiles span two chunks) / tiles per loss chunk
+    constexpr int CHS = sizeof(T) == 8 ? LOSS_CHUNK_8B : LOSS_CHUNK_4B;
+    constexpr int CPT = TILE > CHS ? TILE / CHS : 1, TPC = TILE > CHS ? 1 : CHS / TILE;
+    static_assert(TILE > CHS ? TILE % CHS == 0 : CHS % TILE == 0, "tiles and loss chunks nest");
+    LAccT<T> lacc[CPT];
+    UNR for (int c = 0; c < CPT; ++c) lacc[c] = 0;
     CT M = 0;
     // another row block already saw this tree fail in this launch: nothing here can change its
     // result (did_succeed = false, loss L(Inf)); NaN partials and check statistic stand in
@@ -1245,18 +1259,18 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
       if constexpr (MODE == MODE_LOSS) {
         loss_tile<T, R>(p, A, ysrc + (int64_t)tile * TILE, wsrc + (int64_t)tile * TILE, lane, row0, trel + TILE <= nrel,
                         lacc);
-        constexpr int CH = sizeof(T) == 8 ? LOSS_CHUNK_8B : LOSS_CHUNK_4B;
-        static_assert(CH % TILE == 0, "a loss chunk is whole tiles");
-        const bool flushed = (tile + 1) % (CH / TILE) == 0 || trel + TILE >= nrel;
-        if (flushed) {  // chunk done (or last valid tile)
-          const LAccT<T> s = wave_sum(lacc);
-          const int ci = tile / (CH / TILE);
-          if (lane == WAVE_LAST) lslab[ci] = s;
-          if (p.fused) {  // reduce_kernel's lane-strided accumulation: lane c % 64 adds chunk c
-            const LAccT<T> sb = __shfl(s, WAVE_LAST);
-            if (lane == ci % 64) csum += sb;
+        const bool flushed = (tile + 1) % TPC == 0 || trel + TILE >= nrel;
+        const int ci0 = tile * CPT / TPC;  // the tile's (first) loss chunk
+        if (flushed) {  // chunk(s) done (or last valid tile)
+          UNR for (int c = 0; c < CPT; ++c) {
+            const LAccT<T> s = wave_sum(lacc[c]);
+            if (lane == WAVE_LAST) lslab[ci0 + c] = s;
+            if (p.fused) {  // reduce_kernel's lane-strided accumulation: lane c % 64 adds chunk c
+              const LAccT<T> sb = __shfl(s, WAVE_LAST);
+              if (lane == (ci0 + c) % 64) csum += sb;
+            }
+            lacc[c] = 0;
           }
-          lacc = 0;
         }
         if constexpr (!kIsInt<T>) {
           // Early return (DynamicExpressions returns at the first bad array): a non-finite check
@@ -1267,7 +1281,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
           if (p.early_exit && __builtin_amdgcn_ballot_w64(!(M < (CT)INFINITY)) != 0) {
             csum = (LAccT<T>)NAN;
             if (lane == WAVE_LAST) {
-              for (int c = tile / (CH / TILE) + (flushed ? 1 : 0); c < (tile_claims ? tile_end : p.cpb); ++c)
+              for (int c = ci0 + (flushed ? CPT : 0); c < (tile_claims ? tile_end : p.cpb); ++c)
                 lslab[c] = (LAccT<T>)NAN;
               __hip_atomic_store(p.fail_flag + slot, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }

@@ -429,12 +429,22 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(const double* __restri
   const int lane = threadIdx.x & 63;
   const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (chunk >= nchunks) return;
+  // (each lane folds its row blocks b = lane, lane + 64, ... in order -- the loads of a batch issued
+  // before its adds: a strided loop waited out one memory latency per block and element)
+  constexpr int BB = 8;
   for (int e = 0; e < KT + 2; ++e) {
     const bool is_max = CHK_MAX && e == KT + 1;
     double s = 0.0;
-    for (int b = lane; b < nrb; b += 64) {
-      const double v = slab[((int64_t)chunk * nrb + b) * (KT + 2) + e];
-      s = is_max ? __builtin_elementwise_maximum(s, v) : s + v;
+    for (int b0 = lane; b0 < nrb; b0 += 64 * BB) {
+      double v[BB];
+      UNR for (int j = 0; j < BB; ++j) {
+        const int b = b0 + 64 * j;
+        v[j] = b < nrb ? slab[((int64_t)chunk * nrb + b) * (KT + 2) + e] : 0.0;
+      }
+      UNR for (int j = 0; j < BB; ++j) {
+        if (b0 + 64 * j >= nrb) break;
+        s = is_max ? __builtin_elementwise_maximum(s, v[j]) : s + v[j];
+      }
     }
     UNR for (int o = 32; o > 0; o >>= 1) {
       const double t = __shfl_xor(s, o);

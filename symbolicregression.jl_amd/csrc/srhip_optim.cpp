@@ -217,7 +217,7 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     // through its own buffer, synchronously); stream order: this copy follows the previous pass's
     // kernel, which has read its chunk list
     HIP_TRY(ctx->h_gchunks[pi].ensure(ps.chunks.size() * sizeof(int32_t)));
-    HIP_TRY(ctx->h_gred[pi].ensure((size_t)nch * (ps.kt + 2) * sizeof(double)));
+    HIP_TRY(ctx->h_gred[pi].ensure((size_t)nch * (ps.kt + 2) * sizeof(double), hipHostMallocCoherent));
     memcpy(ctx->h_gchunks[pi].p, ps.chunks.data(), ps.chunks.size() * sizeof(int32_t));
     HIP_TRY(hipMemcpyAsync(ctx->g_chunks.p, ctx->h_gchunks[pi].p, ps.chunks.size() * sizeof(int32_t),
                            hipMemcpyHostToDevice, ctx->stream));
@@ -243,11 +243,10 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     if (first) HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));  // srhip_last_kernel_ms: the gradient kernels
     first = false;
     HIP_TRY(launch_grad(dtype, K, ps.kt, a, dim3(ps.L.nrb, ps.L.groups), ctx->stream));
-    HIP_TRY(launch_grad_reduce(dtype, ps.kt, (const double*)ctx->g_slab.p, ps.L.nrb, nch, (double*)ctx->g_red.p,
+    // the reduction writes the records straight into coherent pinned host memory (no copy on the stream)
+    HIP_TRY(launch_grad_reduce(dtype, ps.kt, (const double*)ctx->g_slab.p, ps.L.nrb, nch, (double*)ctx->h_gred[pi].p,
                                ctx->stream));
     ps.red = (const double*)ctx->h_gred[pi].p;
-    HIP_TRY(hipMemcpyAsync(ctx->h_gred[pi].p, ctx->g_red.p, (size_t)nch * (ps.kt + 2) * sizeof(double),
-                           hipMemcpyDeviceToHost, ctx->stream));
   }
   HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
   ctx->timed = true;

@@ -144,7 +144,12 @@ def load() -> ctypes.CDLL:
                                          "(or __graft_entry__.build()); there is no CPU fallback")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
+            try:
+                fn = getattr(lib, name)
+            except AttributeError:
+                # an older library build (same-box A/B of builds via SRHIP_LIB): the call raises when used;
+                # tests/test_abi.py requires every symbol of the in-tree build
+                continue
             fn.restype = res
             fn.argtypes = args
         _lib = lib
