@@ -20,8 +20,10 @@ K_MAX = 8
 SB = ["ADD", "SUB", "MUL", "DIV", "GT", "COND", "OR", "AND", "MAX", "MIN"]
 UN = ["NEG", "SQUARE", "CUBE", "ABS", "RELU", "COS", "SIN", "TAN", "EXP", "LOG"]
 H_SLOADF0, H_SLOADC0, H_PUSH0 = 3, 3 + K_MAX, 3 + 2 * K_MAX
-H_BIN0 = H_PUSH0 + K_MAX
-SPEC_STRIDE = 4 + 2 * K_MAX
+H_PUSHLF0, H_PUSHLC0 = H_PUSH0 + K_MAX, H_PUSH0 + 2 * K_MAX
+H_BIN0 = H_PUSHLC0 + K_MAX
+SPEC_STRIDE = 4 + 2 * K_MAX + 3
+FORMS = ["AF", "FA", "AC", "CA"] + [f"SA{k}" for k in range(K_MAX)] + [f"AS{k}" for k in range(K_MAX)] + ["FF", "FC", "CF"]
 H_HEAVY0 = H_BIN0 + 10 * SPEC_STRIDE
 H_UN0 = H_HEAVY0 + 3 * 2 * K_MAX
 NUN = 33
@@ -33,10 +35,12 @@ def name(h):
     if h == 2: return "LOADC"
     if h < H_SLOADC0: return f"SLOADF{h - H_SLOADF0}"
     if h < H_PUSH0: return f"SLOADC{h - H_SLOADC0}"
-    if h < H_BIN0: return f"PUSH{h - H_PUSH0}"
+    if h < H_PUSHLF0: return f"PUSH{h - H_PUSH0}"
+    if h < H_PUSHLC0: return f"PUSHLF{h - H_PUSHLF0}"
+    if h < H_BIN0: return f"PUSHLC{h - H_PUSHLC0}"
     if h < H_HEAVY0:
         sb, f = divmod(h - H_BIN0, SPEC_STRIDE)
-        form = ["AF", "FA", "AC", "CA"][f] if f < 4 else (f"SA{f - 4}" if f < 4 + K_MAX else f"AS{f - 4 - K_MAX}")
+        form = FORMS[f]
         return f"{SB[sb]}_{form}"
     if h < H_UN0: return f"HEAVY{h - H_HEAVY0}"
     if h < H_UN0 + NUN:

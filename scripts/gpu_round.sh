@@ -15,4 +15,14 @@ if [ -n "${ROWSHARD:-}" ]; then
   rc=$?; echo "rowshard rc=$rc"; tail -1 gpurun_out/rowshard_n1.log | cut -c1-600
   [ $rc -eq 0 ] || exit $rc
 fi
-if [ -n "${BUILDS:-}" ]; then bash scripts/ab2.sh; fi
+if [ -n "${BUILDS:-}" ]; then bash scripts/ab2.sh || exit $?; fi
+# BENCHES="c4:--config c4 --no-cpu;c2:": extra bench lines, name:args separated by ';'
+if [ -n "${BENCHES:-}" ]; then
+  IFS=';' read -ra items <<< "$BENCHES"
+  for it in "${items[@]}"; do
+    nm=${it%%:*}; args=${it#*:}
+    timeout -k 10 400 python -u bench.py $args > gpurun_out/bench_$nm.json 2> gpurun_out/bench_$nm.err
+    rc=$?; echo "bench $nm rc=$rc"; tail -1 gpurun_out/bench_$nm.json | cut -c1-400
+    [ $rc -eq 0 ] || exit $rc
+  done
+fi

@@ -89,13 +89,21 @@ __global__ __launch_bounds__(256) void precise_reduce_kernel(const double* __res
                                                              int32_t* __restrict__ out_list, double* __restrict__ out) {
   const int cnt = __hip_atomic_load(ulist, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int nu = min(cnt, umax);
+  // the row blocks in order, PB independent loads issued before their (dependent) TwoSum steps: one
+  // memory latency per PB blocks instead of per block
+  constexpr int PB = 16;
   for (int i = threadIdx.x; i < nu * stride; i += blockDim.x) {
     const double* src = slab + (int64_t)i * nrb;
     double s = 0.0, c = 0.0;
-    for (int b = 0; b < nrb; ++b) {
-      const double x = src[b], t = s + x, bp = t - s;
-      c += (s - (t - bp)) + (x - bp);
-      s = t;
+    for (int b0 = 0; b0 < nrb; b0 += PB) {
+      double xv[PB];
+      UNR for (int j = 0; j < PB; ++j) xv[j] = b0 + j < nrb ? src[b0 + j] : 0.0;
+      UNR for (int j = 0; j < PB; ++j) {
+        if (b0 + j >= nrb) break;
+        const double x = xv[j], t = s + x, bp = t - s;
+        c += (s - (t - bp)) + (x - bp);
+        s = t;
+      }
     }
     out[i] = s + c;
   }
@@ -185,10 +193,6 @@ int pick_rows_per_lane(int dtype, int K, int mode, int64_t m) {
 
 hipError_t launch_eval(int dtype, const EvalArgs& a, int R, int K, int mode, bool xlds, dim3 grid, size_t lds,
                        hipStream_t s) {
-  if (R == R_F32_XWIDE) {  // the extra-wide Float32 persistent loss launch (K = 2, LDS-staged)
-    if (dtype != SRHIP_F32 || K > 2 || mode != MODE_LOSS || !xlds || !a.persistent) return hipErrorInvalidValue;
-    return launch_eval_f32x(a, grid, lds, s);
-  }
   if (R != pick_rows_per_lane(dtype, K, mode, a.nvalid)) return hipErrorInvalidValue;
   if (R == R_F32_WIDE && R != R_F32) {  // Float32, K = 2, loss or prediction
     if (mode != MODE_LOSS && mode != MODE_PRED) return hipErrorInvalidValue;

@@ -106,8 +106,11 @@
 #define SRHIP_HOTU_EXP2
 #define SRHIP_HOTU_EXPM1
 #define SRHIP_HOTU_CBRT
+// SRHIP_ASM_DEF=1 (default): the tile's accumulator and stack registers are defined by empty asm
+// statements instead of 16 x (K + 1) clears per (tree, tile) (C2, one MI355X: 1.12-1.15 ->
+// 1.085-1.095 ms; -DSRHIP_ASM_DEF=0 restores the clears)
 #ifndef SRHIP_ASM_DEF
-#define SRHIP_ASM_DEF 0
+#define SRHIP_ASM_DEF 1
 #endif
 #ifndef SRHIP_ROW_FENCE
 #define SRHIP_ROW_FENCE() __builtin_amdgcn_sched_barrier(0)
@@ -1014,7 +1017,8 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
   const int group_base = __builtin_amdgcn_readfirstlane(snap_base);
   int group_n = __builtin_amdgcn_readfirstlane(snap_n);
   if constexpr (MODE == MODE_PRECISE) {
-    if (p.dev_count) group_n = min(group_n, __builtin_amdgcn_readfirstlane(*p.dev_count));
+    // device-listed trees: this group's slots that the list filled
+    if (p.dev_count) group_n = max(0, min(group_n, __builtin_amdgcn_readfirstlane(*p.dev_count) - group_base));
   }
 
   // the group's trees are in descending estimated cost (host make_order): wave w starts with tree w,

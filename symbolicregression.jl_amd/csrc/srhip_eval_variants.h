@@ -9,8 +9,6 @@ hipError_t launch_eval_f32_pred(const EvalArgs& a, int K, bool xlds, dim3 grid, 
 hipError_t launch_eval_f32_precise(const EvalArgs& a, dim3 grid, size_t lds, hipStream_t s);
 // Float32, R = R_F32_WIDE, K = 2: MODE_LOSS or MODE_PRED
 hipError_t launch_eval_f32w(const EvalArgs& a, int mode, bool xlds, dim3 grid, size_t lds, hipStream_t s);
-// Float32, R = R_F32_XWIDE, K = 2: the persistent MODE_LOSS launch over LDS-staged row blocks
-hipError_t launch_eval_f32x(const EvalArgs& a, dim3 grid, size_t lds, hipStream_t s);
 hipError_t launch_eval_f64_loss(const EvalArgs& a, int K, bool xlds, dim3 grid, size_t lds, hipStream_t s);
 hipError_t launch_eval_f64_pred(const EvalArgs& a, int K, bool xlds, dim3 grid, size_t lds, hipStream_t s);
 hipError_t launch_eval_f64_precise(const EvalArgs& a, dim3 grid, size_t lds, hipStream_t s);

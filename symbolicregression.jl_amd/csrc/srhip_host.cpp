@@ -1659,9 +1659,6 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   const int probe_env = env_int("SRHIP_PROBE_BLOCKS", -1);
   bool persistent = false;
   int probe_blocks = 0;
-  // SRHIP_XWIDE=1: the persistent main launch runs the extra-wide variant (R = 32, 2 waves per SIMD);
-  // the probe keeps R = 16 (a probe tile is one loss chunk)
-  const bool xwide = env_flag("SRHIP_XWIDE");
   {
     const int Kp = kvariant(P->kmax);
     persistent = !no_persistent && mode == MODE_LOSS && debug_stop() == 0 && dtype == SRHIP_F32 &&
@@ -1673,7 +1670,6 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       const int tile = 64 * R;
       int rb = prb_env >= tile && prb_env <= ROW_ALIGN && (prb_env & (prb_env - 1)) == 0 ? prb_env : 2048;
       rb = std::max(rb, std::max(tile, loss_chunk(dtype)));
-      if (xwide) rb = std::max(rb, 64 * R_F32_XWIDE);
       const size_t es = dtype_size(dtype);
       const int base_cols = P->maxfeat + 1 + (weighted ? 1 : 0);
       use_d = nd > 0 && (size_t)(base_cols + nd) * rb * es <= lds_budget(R, K, true);
@@ -1867,7 +1863,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     const int slices = std::max(1, std::min(slices_env, 64));
     a.tail_slices = slices;
     a.tail_blocks = slices > 1 && nmain > wgs && nl >= 16 * slices ? nmain % wgs : 0;
-    HIP_TRY(launch_eval(dtype, a, xwide ? R_F32_XWIDE : R, K, mode, true, dim3(wgs, 1), L.lds, ctx->stream));
+    HIP_TRY(launch_eval(dtype, a, R, K, mode, true, dim3(wgs, 1), L.lds, ctx->stream));
   } else {
     HIP_TRY(launch_eval(dtype, a, R, K, mode, L.xlds, grid, L.lds, ctx->stream));
   }
@@ -1905,7 +1901,9 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       HIP_TRY(hipMemsetAsync(ctx->d_ulist.p, 0, ctx->d_ulist.bytes, ctx->stream));
     }
     ul.ulist = (int32_t*)ctx->d_ulist.p;
-    ul.umax = DEV_PRECISE_MAX;
+    // list capacity: twice the trees the program's last launch listed (8 .. DEV_PRECISE_MAX); trees
+    // past it are decided by the host-launched pass
+    ul.umax = std::min(DEV_PRECISE_MAX, std::max(8, 2 * P->und_hint));
     ul.rows = (double)v.m;
   }
   if (!a.fused)
@@ -1918,8 +1916,9 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     // K_MAX, global reads -- eval_precise's launch with the list as the tree order
     const int stride = std::max(1, P->max_ops);
     const int Rp = pick_rows_per_lane(dtype, K_MAX, MODE_PRECISE, v.m);
-    LaunchPlan Lp = plan_launch(ctx, dtype, ds->nfeat, false, false, v.m, DEV_PRECISE_MAX, 64 * Rp);
-    HIP_TRY(ctx->slab_prec.ensure((size_t)DEV_PRECISE_MAX * stride * Lp.nrb * sizeof(double)));
+    const int G = ul.umax;  // one tree group per list entry: the listed trees run side by side
+    LaunchPlan Lp = plan_launch(ctx, dtype, ds->nfeat, false, false, v.m, G, 64 * Rp);
+    HIP_TRY(ctx->slab_prec.ensure((size_t)G * stride * Lp.nrb * sizeof(double)));
     HIP_TRY(ctx->h_pout.ensure((size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t) +
                                (size_t)DEV_PRECISE_MAX * stride * sizeof(double), hipHostMallocCoherent));
     EvalArgs q{};
@@ -1929,19 +1928,19 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     q.X = v.X;
     q.ld = v.ld;
     q.nvalid = v.m;
-    q.ntrees = DEV_PRECISE_MAX;
+    q.ntrees = G;
     q.nfeat = (int32_t)ds->nfeat;
     q.rb_rows = Lp.rb_rows;
     q.nrb = Lp.nrb;
-    q.trees_per_group = DEV_PRECISE_MAX;
+    q.trees_per_group = 1;
     q.slab_prec = ctx->slab_prec.p;
     q.prec_stride = stride;
     q.max_steps = P->max_len;
     q.dev_count = ul.ulist;
-    HIP_TRY(launch_eval(dtype, q, Rp, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, 1), 16, ctx->stream));
+    HIP_TRY(launch_eval(dtype, q, Rp, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, G), 16, ctx->stream));
     int32_t* hl = (int32_t*)ctx->h_pout.p;
     double* hs = (double*)((uint8_t*)ctx->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
-    HIP_TRY(launch_precise_reduce((const double*)ctx->slab_prec.p, Lp.nrb, stride, ul.ulist, DEV_PRECISE_MAX, hl, hs,
+    HIP_TRY(launch_precise_reduce((const double*)ctx->slab_prec.p, Lp.nrb, stride, ul.ulist, G, hl, hs,
                                   ctx->stream));
     dp->used = true;
     dp->stride = stride;
@@ -1953,7 +1952,8 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     const int32_t* hl = (const int32_t*)ctx->h_pout.p;
     const double* hs = (const double*)((const uint8_t*)ctx->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
     dp->count = hl[0];
-    const int nu = std::min(dp->count, DEV_PRECISE_MAX);
+    P->und_hint = dp->count;
+    const int nu = std::min(dp->count, ul.umax);
     dp->list.assign(hl + 1, hl + 1 + nu);
     dp->opsums.assign(hs, hs + (size_t)nu * dp->stride);
   }

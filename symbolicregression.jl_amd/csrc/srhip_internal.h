@@ -176,6 +176,7 @@ struct srhip_program {
   mutable srhip::DevBuf d_prog;
   mutable std::vector<uint8_t> blob;  // its host image (alive until the next upload)
   mutable bool upload_pending = false;
+  mutable int32_t und_hint = 0;  // trees the last device-listed precise pass saw (list capacity hint)
   mutable size_t blob_off[6] = {0, 0, 0, 0, 0, 0};  // section offsets: off, dcode, doff, dspec, dmask, end
   mutable const srhip::Ins* code_dev = nullptr;
   mutable const int32_t* off_dev = nullptr;

@@ -17,10 +17,6 @@ constexpr int EVAL_WAVES = SRHIP_EVAL_WAVES;  // wavefronts per workgroup of the
 // 1.47 -> 1.34 ms)
 constexpr int EVAL_WAVES_WIDE = 16;
 constexpr int eval_waves(int R, int K) { return (R == 16 && K <= 2) ? EVAL_WAVES_WIDE : EVAL_WAVES; }
-// ... and the extra-wide Float32 variant (R = 32, K = 2; SRHIP_XWIDE=1, the persistent main launch):
-// 8-wave workgroups, one per CU, two waves per SIMD with up to 256 VGPRs each: half the dispatches
-// per row of the wide variant, a tile of 2048 rows = two loss chunks
-constexpr int R_F32_XWIDE = 32;
 constexpr int EVAL_WAVES_MAX = EVAL_WAVES_WIDE > EVAL_WAVES ? EVAL_WAVES_WIDE : EVAL_WAVES;
 #ifndef SRHIP_R_F32
 #define SRHIP_R_F32 8
