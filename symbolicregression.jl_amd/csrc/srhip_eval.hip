@@ -81,37 +81,55 @@ __global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab
   }
 }
 
-// one workgroup: the listed trees' per-operator precise sums over the row blocks, in row-block
-// order with a compensated (TwoSum) accumulator, into coherent host memory; then the list is reset
-// for the next launch on the stream
+// The listed trees' per-operator precise sums over the row blocks, one wave per (tree, operator)
+// item: lane l adds row blocks l, l + 64, ... with a compensated (TwoSum) accumulator -- every load
+// of the item in flight at once -- and the 64 (sum, compensation) pairs are combined by a fixed xor
+// butterfly of double-double additions; results to coherent host memory.  The grid is sized for the
+// list's capacity (the count is read on the device); the last workgroup to finish resets the list
+// for the next launch on the stream (ulist[1 + PRECISE_DONE_SLOT] counts finished workgroups).
+__device__ __forceinline__ void two_sum_acc(double& s, double& c, double x) {
+  const double t = s + x, bp = t - s;
+  c += (s - (t - bp)) + (x - bp);
+  s = t;
+}
 __global__ __launch_bounds__(256) void precise_reduce_kernel(const double* __restrict__ slab, int nrb, int stride,
-                                                             int32_t* __restrict__ ulist, int umax,
+                                                             int32_t* __restrict__ ulist, int umax, int done_slot,
                                                              int32_t* __restrict__ out_list, double* __restrict__ out) {
   const int cnt = __hip_atomic_load(ulist, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int nu = min(cnt, umax);
-  // the row blocks in order, PB independent loads issued before their (dependent) TwoSum steps: one
-  // memory latency per PB blocks instead of per block
-  constexpr int PB = 16;
-  for (int i = threadIdx.x; i < nu * stride; i += blockDim.x) {
-    const double* src = slab + (int64_t)i * nrb;
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (item < nu * stride) {
+    const double* src = slab + (int64_t)item * nrb;
     double s = 0.0, c = 0.0;
-    for (int b0 = 0; b0 < nrb; b0 += PB) {
+    constexpr int PB = 8;
+    for (int b0 = lane; b0 < nrb; b0 += 64 * PB) {
       double xv[PB];
-      UNR for (int j = 0; j < PB; ++j) xv[j] = b0 + j < nrb ? src[b0 + j] : 0.0;
-      UNR for (int j = 0; j < PB; ++j) {
-        if (b0 + j >= nrb) break;
-        const double x = xv[j], t = s + x, bp = t - s;
-        c += (s - (t - bp)) + (x - bp);
-        s = t;
-      }
+      UNR for (int j = 0; j < PB; ++j) xv[j] = b0 + 64 * j < nrb ? src[b0 + 64 * j] : 0.0;
+      UNR for (int j = 0; j < PB; ++j)
+        if (b0 + 64 * j < nrb) two_sum_acc(s, c, xv[j]);
     }
-    out[i] = s + c;
+    UNR for (int o = 1; o < 64; o <<= 1) {
+      const double s2 = __shfl_xor(s, o), c2 = __shfl_xor(c, o);
+      // (s, c) + (s2, c2) in an order that does not depend on which lane computes it
+      const double a = lane & o ? s2 : s, b = lane & o ? s : s2;
+      const double t = a + b, bp = t - a, e = (a - (t - bp)) + (b - bp);
+      c = (lane & o ? c2 + c : c + c2) + e;
+      s = t;
+    }
+    if (lane == 0) out[item] = s + c;
   }
-  for (int i = threadIdx.x; i < nu; i += blockDim.x) out_list[1 + i] = ulist[1 + i];
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < nu; i += blockDim.x) out_list[1 + i] = ulist[1 + i];
+  if (blockIdx.x == 0 && threadIdx.x == 0) out_list[0] = cnt;
   __syncthreads();
+  // (every wave's read of the count completed before its value was used, so no fence: the last
+  // workgroup's reset cannot overtake another workgroup's read)
   if (threadIdx.x == 0) {
-    out_list[0] = cnt;
-    __hip_atomic_store(ulist, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (atomicAdd(ulist + 1 + done_slot, 1) == (int)gridDim.x - 1) {
+      __hip_atomic_store(ulist + 1 + done_slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ulist, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -213,9 +231,11 @@ hipError_t launch_eval(int dtype, const EvalArgs& a, int R, int K, int mode, boo
   }
 }
 
-hipError_t launch_precise_reduce(const double* slab, int nrb, int stride, int32_t* ulist, int umax,
+hipError_t launch_precise_reduce(const double* slab, int nrb, int stride, int32_t* ulist, int umax, int done_slot,
                                  int32_t* out_list, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(precise_reduce_kernel, dim3(1), dim3(256), 0, s, slab, nrb, stride, ulist, umax, out_list, out);
+  const int items = std::max(1, umax * stride);
+  hipLaunchKernelGGL(precise_reduce_kernel, dim3((items + 3) / 4), dim3(256), 0, s, slab, nrb, stride, ulist, umax,
+                     done_slot, out_list, out);
   return hipGetLastError();
 }
 

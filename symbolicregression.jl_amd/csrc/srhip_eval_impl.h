@@ -984,7 +984,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
   }
   KDBG("[k] staged, ntiles=%d rb_rows=%d nvalid=%ld max_steps=%d\n", ntiles, p.rb_rows, (long)p.nvalid, p.max_steps);
   __shared__ int next_tree;  // the group's next unclaimed tree (waves claim trees dynamically)
-  if (threadIdx.x == 0) next_tree = WAVES;
+  if (threadIdx.x == 0) next_tree = blockDim.x >> 6;  // the waves present (a launch may run fewer than WAVES)
   // failed-tree marks of the group's first FLAG_SNAP trees as this workgroup starts (one coherent
   // load per thread, in parallel, instead of a memory round trip per wave and tree): workgroups that
   // start after another row block saw a tree fail skip it.  A stale snapshot only skips less.
@@ -1372,7 +1372,9 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
   __shared__ int claimed;
   if (p.tile_claims && !p.persistent) {
     // the probe's combining entries start from zero (eval_block's first barrier orders these stores
-    // before any wave's atomics); no memset launches before the probe
+    // before any wave's atomics); no memset launches before the probe.  Only this workgroup's waves
+    // combine into its entries, and the later readers are later launches: a workgroup-scope release
+    // suffices (an agent-scope fence is an L2 write-back on every workgroup: probe 39 -> 98 us)
     if (p.zero_ctr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
       __hip_atomic_store(p.zero_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int gs = p.grid_interleave ? (int)blockIdx.y : 0, gst = p.grid_interleave ? (int)gridDim.y : 1;
@@ -1382,7 +1384,7 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
       if (p.slab_chk) __hip_atomic_store(reinterpret_cast<uint32_t*>(p.slab_chk) + at, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (p.slab_rows) __hip_atomic_store(p.slab_rows + at, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __threadfence();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   }
   const int nfull = p.nrb - p.block0 - p.tail_blocks;
   const int nitems = nfull + p.tail_blocks * p.tail_slices;
@@ -1422,7 +1424,8 @@ inline hipError_t launch_eval_t(const EvalArgs& a, dim3 grid, size_t lds, hipStr
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(kern, grid, dim3(64 * eval_waves(R, K)), lds, s, a);
+  const int waves = a.wg_waves > 0 ? std::min(a.wg_waves, eval_waves(R, K)) : eval_waves(R, K);
+  hipLaunchKernelGGL(kern, grid, dim3(64 * waves), lds, s, a);
   return hipGetLastError();
 }
 

@@ -58,6 +58,31 @@ int srhip::fail(int code, const char* fmt, ...) {
 }
 const char* srhip::last_error() { return g_err.c_str(); }
 
+// Environment switches read per call (tests and the bench toggle them inside one process) through a
+// per-thread cache: a getenv scans the whole environment (~1 us each, ~10 per evaluation); the cache
+// is dropped whenever the environment's entry pointers change (every setenv / putenv / unsetenv
+// replaces, adds or removes one), which a walk over those pointers detects in ~50 ns.
+extern "C" char** environ;
+static const char* env_get(const char* name) {
+  struct Ent {
+    const char* name;
+    const char* val;
+  };
+  static thread_local uint64_t sig = 0;
+  static thread_local std::vector<Ent> cache;
+  uint64_t h = 1469598103934665603ull ^ (uint64_t)(uintptr_t)environ;
+  for (char** e = environ; e && *e; ++e) h = (h ^ (uint64_t)(uintptr_t)*e) * 1099511628211ull;
+  if (h != sig) {
+    cache.clear();
+    sig = h;
+  }
+  for (const Ent& c : cache)
+    if (c.name == name || strcmp(c.name, name) == 0) return c.val;
+  const char* v = getenv(name);
+  cache.push_back(Ent{name, v});
+  return v;
+}
+
 // ---------------------------------------------------------------------------------------------
 // tree compiler
 // ---------------------------------------------------------------------------------------------
@@ -450,7 +475,7 @@ template <typename T> class TreeCompiler {
 
  public:
   static bool super_env() {
-    const char* e = getenv("SRHIP_NO_SUPER");
+    const char* e = env_get("SRHIP_NO_SUPER");
     return !(e && *e && *e != '0');
   }
 
@@ -707,7 +732,7 @@ template <typename T> class CodeCache {
     return *c;
   }
   static bool enabled() {
-    const char* e = getenv("SRHIP_NO_CODE_CACHE");
+    const char* e = env_get("SRHIP_NO_CODE_CACHE");
     return !(e && *e && *e != '0');
   }
   // derived column per U(X[f]) node of a valid tree (as TreeCompiler::emit_program assigns them)
@@ -805,7 +830,7 @@ template <typename T> class CodeCache {
 template <typename T>
 void choose_derived_t(srhip_program& P) {
   P.dspec.clear();
-  const char* env = getenv("SRHIP_NO_DERIVE");
+  const char* env = env_get("SRHIP_NO_DERIVE");
   const bool off = env && *env && *env != '0';
   if (std::is_same<T, int32_t>::value || off) return;
   std::vector<std::pair<uint32_t, int>> cnt;  // (key, uses), in order of first use
@@ -943,7 +968,7 @@ int compile_program_t(srhip_program& P) {
   // imm low, imm high) records with a (-1, static_fail, need, cost) separator per tree, for
   // instruction-mix studies (scripts/code_stats.py) and the code-cache test; with derived columns the
   // plain program's go to path.plain
-  if (const char* dump = getenv("SRHIP_DUMP_CODE")) {
+  if (const char* dump = env_get("SRHIP_DUMP_CODE")) {
     for (int pass = 0; pass < (der ? 2 : 1); ++pass) {
       const bool dd = der && pass == 0;
       FILE* f = fopen(pass ? (std::string(dump) + ".plain").c_str() : dump, "wb");
@@ -1580,11 +1605,11 @@ int srhip::check_eval_args(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_
 }
 
 static bool env_flag(const char* name) {
-  const char* e = getenv(name);
+  const char* e = env_get(name);
   return e && *e && *e != '0';
 }
 static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
+  const char* e = env_get(name);
   return e && *e ? atoi(e) : dflt;
 }
 
@@ -1700,7 +1725,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     // (C2, one MI355X, warm, separate processes: 10 columns at 2048-row blocks 1.29 ms vs the plain
     // program at 4096 rows 1.27 ms with 16-wave workgroups; 1.56 vs 1.41 ms at 1024 / 2048 rows with
     // 8-wave workgroups)
-    const char* always = getenv("SRHIP_DERIVE_ALWAYS");  // (tests: the derived program whatever the blocks)
+    const char* always = env_get("SRHIP_DERIVE_ALWAYS");  // (tests: the derived program whatever the blocks)
     if (use_d && !(always && *always && *always != '0')) {
       const int Kp = kvariant(P->kmax), Rp = pick_rows_per_lane(dtype, Kp, mode, v.m);
       const LaunchPlan Lp = plan_launch(ctx, dtype, P->maxfeat, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(),
@@ -1787,7 +1812,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   a.debug_stop = debug_stop();
   // one row block: the waves finish the per-tree reduction themselves (SRHIP_NO_FUSED_REDUCE=1: the
   // reduce kernel instead; read per launch)
-  const char* nofuse = getenv("SRHIP_NO_FUSED_REDUCE");
+  const char* nofuse = env_get("SRHIP_NO_FUSED_REDUCE");
   if (L.nrb == 1 && !(nofuse && *nofuse && *nofuse != '0')) {
     a.fused = 1;
     a.fused_loss = mode == MODE_LOSS ? ctx->h_loss.p : nullptr;
@@ -1897,7 +1922,8 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   UndecidedList ul;
   if (devp) {
     if (!ctx->d_ulist.p) {
-      HIP_TRY(ctx->d_ulist.ensure((1 + DEV_PRECISE_MAX) * sizeof(int32_t)));
+      // [count, DEV_PRECISE_MAX trees, the precise reduction's finished-workgroup counter]
+      HIP_TRY(ctx->d_ulist.ensure((2 + DEV_PRECISE_MAX) * sizeof(int32_t)));
       HIP_TRY(hipMemsetAsync(ctx->d_ulist.p, 0, ctx->d_ulist.bytes, ctx->stream));
     }
     ul.ulist = (int32_t*)ctx->d_ulist.p;
@@ -1916,8 +1942,12 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     // K_MAX, global reads -- eval_precise's launch with the list as the tree order
     const int stride = std::max(1, P->max_ops);
     const int Rp = pick_rows_per_lane(dtype, K_MAX, MODE_PRECISE, v.m);
-    const int G = ul.umax;  // one tree group per list entry: the listed trees run side by side
+    // one tree group per list entry (the listed trees side by side), one-tile row blocks and one-wave
+    // workgroups: every (tree, tile) of the few listed trees on a wave of its own
+    const int G = ul.umax;
     LaunchPlan Lp = plan_launch(ctx, dtype, ds->nfeat, false, false, v.m, G, 64 * Rp);
+    Lp.rb_rows = 64 * Rp;
+    Lp.nrb = (int)((v.m + Lp.rb_rows - 1) / Lp.rb_rows);
     HIP_TRY(ctx->slab_prec.ensure((size_t)G * stride * Lp.nrb * sizeof(double)));
     HIP_TRY(ctx->h_pout.ensure((size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t) +
                                (size_t)DEV_PRECISE_MAX * stride * sizeof(double), hipHostMallocCoherent));
@@ -1937,17 +1967,21 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     q.prec_stride = stride;
     q.max_steps = P->max_len;
     q.dev_count = ul.ulist;
+    q.wg_waves = 1;
     HIP_TRY(launch_eval(dtype, q, Rp, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, G), 16, ctx->stream));
     int32_t* hl = (int32_t*)ctx->h_pout.p;
     double* hs = (double*)((uint8_t*)ctx->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
-    HIP_TRY(launch_precise_reduce((const double*)ctx->slab_prec.p, Lp.nrb, stride, ul.ulist, G, hl, hs,
+    HIP_TRY(launch_precise_reduce((const double*)ctx->slab_prec.p, Lp.nrb, stride, ul.ulist, G, DEV_PRECISE_MAX, hl, hs,
                                   ctx->stream));
     dp->used = true;
     dp->stride = stride;
   }
   if (mode == MODE_PRED)
     HIP_TRY(hipMemcpyAsync(out_pred, pred.p, (size_t)nt * v.m * es, hipMemcpyDeviceToHost, ctx->stream));
-  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  {
+    const int rc = stream_wait(ctx);
+    if (rc) return rc;
+  }
   if (devp) {
     const int32_t* hl = (const int32_t*)ctx->h_pout.p;
     const double* hs = (const double*)((const uint8_t*)ctx->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
@@ -2042,9 +2076,53 @@ int srhip::gathered_weight_sum(srhip_ctx* ctx, const srhip_dataset* ds, int64_t 
   return SRHIP_OK;
 }
 
+// (diagnostic) SRHIP_HOST_TIMING=1: run_eval's host time before the wait (argument checks, view,
+// schedule, launches), in the wait, and after it (decisions), averaged over every 50 calls on stderr
+static thread_local std::chrono::steady_clock::time_point g_wait_begin, g_wait_done;
+int srhip::stream_wait(srhip_ctx* ctx) {
+  g_wait_begin = std::chrono::steady_clock::now();
+  static const bool block = env_flag("SRHIP_SYNC_BLOCK");
+  if (block || !ctx->ev_sync) {
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    g_wait_done = std::chrono::steady_clock::now();
+    return SRHIP_OK;
+  }
+  HIP_TRY(hipEventRecord(ctx->ev_sync, ctx->stream));
+  for (;;) {
+    const hipError_t q = hipEventQuery(ctx->ev_sync);
+    if (q == hipSuccess) {
+      g_wait_done = std::chrono::steady_clock::now();
+      return SRHIP_OK;
+    }
+    if (q != hipErrorNotReady) HIP_TRY(q);
+    __builtin_ia32_pause();
+  }
+}
+
 // Single-device evaluation: partials -> decision -> precise pass for undecided trees.
 int srhip::run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
                     const int64_t* idx, int64_t nidx, double* out_loss, void* out_pred, uint8_t* out_ok) {
+  static const bool timing = env_flag("SRHIP_HOST_TIMING");
+  const auto t_entry = std::chrono::steady_clock::now();
+  struct Report {  // on every return path
+    bool on;
+    std::chrono::steady_clock::time_point t0;
+    ~Report() {
+      if (!on) return;
+      static thread_local double acc[3];
+      static thread_local int cnt;
+      const auto t3 = std::chrono::steady_clock::now();
+      acc[0] += std::chrono::duration<double>(g_wait_begin - t0).count();
+      acc[1] += std::chrono::duration<double>(g_wait_done - g_wait_begin).count();
+      acc[2] += std::chrono::duration<double>(t3 - g_wait_done).count();
+      if (++cnt % 50 == 0) {
+        fprintf(stderr, "[srhip host] run_eval: before wait %.1f us, wait %.1f us, after %.1f us (mean of %d)\n",
+                acc[0] / cnt * 1e6, acc[1] / cnt * 1e6, acc[2] / cnt * 1e6, cnt);
+        acc[0] = acc[1] = acc[2] = 0.0;
+        cnt = 0;
+      }
+    }
+  } report{timing, t_entry};
   int rc = check_eval_args(ctx, ds, P, mode, loss);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
@@ -2205,6 +2283,7 @@ int srhip_ctx_create(int device, srhip_ctx** out) {
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
+  HIP_TRY(hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
   *out = c.release();
   return SRHIP_OK;
 }
@@ -2217,6 +2296,7 @@ void srhip_ctx_destroy(srhip_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->ev_sync) (void)hipEventDestroy(ctx->ev_sync);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   (void)hipGetLastError();

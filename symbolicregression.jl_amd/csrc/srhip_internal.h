@@ -118,6 +118,7 @@ struct srhip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev_sync = nullptr;  // stream_wait's completion marker (no timing)
   bool timed = false;
   int num_cu = 256;
   int lds_max = 160 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerBlock of the device
@@ -280,6 +281,10 @@ int precise_decide(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program*
 // buf[0, nsum) by SUM and buf[nsum, nsum + nchk) by MAX (chk_max) or SUM across the shards, in place;
 // returns an SRHIP status.
 using ShardReduce = std::function<int(double* buf, size_t nsum, size_t nchk, bool chk_max)>;
+// Wait for the context's stream by polling a completion event (a spin: the host thread resumes
+// within ~1 us of the last kernel, where a blocking hipStreamSynchronize wakes on an interrupt);
+// SRHIP_SYNC_BLOCK=1 uses hipStreamSynchronize.
+int stream_wait(srhip_ctx* ctx);
 int run_eval_sharded(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const srhip_loss* loss,
                      const int64_t* idx, int64_t nidx, const ShardReduce& reduce, double* out_loss, uint8_t* out_ok);
 

@@ -107,6 +107,7 @@ struct EvalArgs {
   // of listed trees is read here (*dev_count, capped at trees_per_group); each wave zeroes its
   // (tree, row block) slab entries before accumulating into them
   const int32_t* dev_count;
+  int32_t wg_waves;         // waves per workgroup (0: the variant's eval_waves; fewer claim the same trees)
   int32_t* slab_rows;       // [nrb][ntrees] valid rows each (row block, order slot) evaluated, or nullptr
   int64_t* fused_rows;      // fused launches: [program trees] rows evaluated (coherent pinned host), or nullptr
 };
@@ -133,8 +134,9 @@ hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, int cpb, con
                          const int32_t* slab_rows = nullptr, int64_t* out_rows = nullptr,
                          const UndecidedList& ul = UndecidedList());
 // The precise pass's per-(listed tree, operator) sums over the row blocks (fixed order, compensated),
-// written to out (coherent host memory: out_count, then [umax][stride] doubles); resets ulist[0].
-hipError_t launch_precise_reduce(const double* slab, int nrb, int stride, int32_t* ulist, int umax,
+// written to out (coherent host memory: out_count, then [umax][stride] doubles); the last workgroup
+// resets ulist[0] (ulist[1 + done_slot]: its finished-workgroup counter, zero between launches).
+hipError_t launch_precise_reduce(const double* slab, int nrb, int stride, int32_t* ulist, int umax, int done_slot,
                                  int32_t* out_list, double* out, hipStream_t s);
 hipError_t launch_gather(int dtype, const void* X, const void* y, const void* w, int64_t ld_src, int nfeat,
                          const int64_t* idx, int64_t m, int64_t ld_dst, void* Xd, void* yd, void* wd, hipStream_t s);
