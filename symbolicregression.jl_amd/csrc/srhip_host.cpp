@@ -62,6 +62,8 @@ const char* srhip::last_error() { return g_err.c_str(); }
 // per-thread cache: a getenv scans the whole environment (~1 us each, ~10 per evaluation); the cache
 // is dropped whenever the environment's entry pointers change (every setenv / putenv / unsetenv
 // replaces, adds or removes one), which a walk over those pointers detects in ~50 ns.
+// (diagnostic) SRHIP_HOST_TIMING=1 timestamps: run_eval's wait and the end of eval_partials' tail
+static thread_local std::chrono::steady_clock::time_point g_wait_begin, g_wait_done, g_tail_done;
 extern "C" char** environ;
 static const char* env_get(const char* name) {
   struct Ent {
@@ -1523,13 +1525,13 @@ static int decide_info(const TreeInfo& I, int dtype, int32_t T, int64_t nfeat, c
   for (int f : I.feat_checks) {
     const double fsum = sums[2 * (size_t)T + 2 * (size_t)f], fbad = sums[2 * (size_t)T + 2 * (size_t)f + 1];
     if (fbad > 0) return 1;
-    const long double sum = dtype == SRHIP_F64 ? ldexpl((long double)fsum, 64) : (long double)fsum;
+    const long double sum = dtype == SRHIP_F64 ? (long double)fsum * 0x1p64L : (long double)fsum;
     if (!isfinite(fsum) || fabsl(sum) >= ovf) return 1;
   }
   if (I.op_sumcheck.empty()) return 0;
   if (!isfinite(chk)) return 1;  // a NaN / Inf operator output
   long double bound;
-  if (dtype == SRHIP_F64) bound = ldexpl((long double)chk, 512);  // sum |v|
+  if (dtype == SRHIP_F64) bound = (long double)chk * 0x1p512L;  // sum |v|
   else bound = (long double)chk * m;                              // m * max |v|
   if (bound * 2.0L >= ovf) return 2;
   return 0;
@@ -1557,7 +1559,7 @@ static void finalize_precise(const srhip_program& P, const int32_t* trees, int32
       const double s = opsums[(size_t)u * stride + k];
       if (!isfinite(s)) st = 1;
       else if (I.op_sumcheck[k]) {
-        const long double S = P.dtype == SRHIP_F64 ? ldexpl((long double)s, 64) : (long double)s;
+        const long double S = P.dtype == SRHIP_F64 ? (long double)s * 0x1p64L : (long double)s;
         if (fabsl(S) >= ovf) st = 1;
       }
     }
@@ -1991,21 +1993,31 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     dp->list.assign(hl + 1, hl + 1 + nu);
     dp->opsums.assign(hs, hs + (size_t)nu * dp->stride);
   }
+  // the reduction's records, read from the device-written (coherent) host buffers in bulk copies:
+  // line-sized reads, not one uncached access per tree
+  static thread_local std::vector<uint64_t> r_loss, r_chk, r_rows;
+  r_loss.resize(nt);
+  r_chk.resize(nt);
+  r_rows.resize(nt);
+  if (mode == MODE_LOSS) memcpy(r_loss.data(), ctx->h_loss.p, (size_t)nt * 8);
+  if (dtype != SRHIP_I32) memcpy(r_chk.data(), ctx->h_chk.p, (size_t)nt * (dtype == SRHIP_F32 ? 4 : 8));
+  memcpy(r_rows.data(), ctx->h_rows.p, (size_t)nt * 8);
   for (int32_t t : live) {
     if (mode == MODE_LOSS)
-      sums[2 * (size_t)t] = dtype == SRHIP_I32 ? (double)((long long*)ctx->h_loss.p)[t] : ((double*)ctx->h_loss.p)[t];
-    if (dtype == SRHIP_F32) chk[t] = ((float*)ctx->h_chk.p)[t];
-    else if (dtype == SRHIP_F64) chk[t] = ((double*)ctx->h_chk.p)[t];
+      sums[2 * (size_t)t] = dtype == SRHIP_I32 ? (double)((const long long*)r_loss.data())[t] : ((const double*)r_loss.data())[t];
+    if (dtype == SRHIP_F32) chk[t] = ((const float*)r_chk.data())[t];
+    else if (dtype == SRHIP_F64) chk[t] = ((const double*)r_chk.data())[t];
   }
   // the launch's work, counted on the device (rows each tree was evaluated on)
   for (int i = 0; i < 4; ++i) ctx->work[i] = 0;
   for (int32_t t : live) {
-    const int64_t rows = ((const int64_t*)ctx->h_rows.p)[t];
+    const int64_t rows = ((const int64_t*)r_rows.data())[t];
     ctx->work[0] += rows * P->info[t].nnodes;
     ctx->work[1] += v.m * P->info[t].nnodes;
     ctx->work[2] += rows * P->info[t].nops;
     ctx->work[3] += rows;
   }
+  g_tail_done = std::chrono::steady_clock::now();
   return SRHIP_OK;
 }
 
@@ -2078,7 +2090,6 @@ int srhip::gathered_weight_sum(srhip_ctx* ctx, const srhip_dataset* ds, int64_t 
 
 // (diagnostic) SRHIP_HOST_TIMING=1: run_eval's host time before the wait (argument checks, view,
 // schedule, launches), in the wait, and after it (decisions), averaged over every 50 calls on stderr
-static thread_local std::chrono::steady_clock::time_point g_wait_begin, g_wait_done;
 int srhip::stream_wait(srhip_ctx* ctx) {
   g_wait_begin = std::chrono::steady_clock::now();
   static const bool block = env_flag("SRHIP_SYNC_BLOCK");
@@ -2109,16 +2120,17 @@ int srhip::run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program
     std::chrono::steady_clock::time_point t0;
     ~Report() {
       if (!on) return;
-      static thread_local double acc[3];
+      static thread_local double acc[4];
       static thread_local int cnt;
       const auto t3 = std::chrono::steady_clock::now();
       acc[0] += std::chrono::duration<double>(g_wait_begin - t0).count();
       acc[1] += std::chrono::duration<double>(g_wait_done - g_wait_begin).count();
-      acc[2] += std::chrono::duration<double>(t3 - g_wait_done).count();
+      acc[2] += std::chrono::duration<double>(g_tail_done - g_wait_done).count();
+      acc[3] += std::chrono::duration<double>(t3 - g_tail_done).count();
       if (++cnt % 50 == 0) {
-        fprintf(stderr, "[srhip host] run_eval: before wait %.1f us, wait %.1f us, after %.1f us (mean of %d)\n",
-                acc[0] / cnt * 1e6, acc[1] / cnt * 1e6, acc[2] / cnt * 1e6, cnt);
-        acc[0] = acc[1] = acc[2] = 0.0;
+        fprintf(stderr, "[srhip host] run_eval: before wait %.1f us, wait %.1f us, records %.1f us, decisions %.1f us "
+                "(mean of %d)\n", acc[0] / cnt * 1e6, acc[1] / cnt * 1e6, acc[2] / cnt * 1e6, acc[3] / cnt * 1e6, cnt);
+        acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
         cnt = 0;
       }
     }
