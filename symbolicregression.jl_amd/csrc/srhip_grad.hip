@@ -258,6 +258,12 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char grad_lds[];
   T* xs = reinterpret_cast<T*>(grad_lds);
   const int rbr = p.rb_rows;
+  // chunks are claimed dynamically from an LDS counter (wave w starts with chunk w): the host orders
+  // each group's chunks by descending cost, so the waves of a workgroup finish within about one cheap
+  // chunk of each other (a static round-robin left the cost spread idle at every workgroup's end);
+  // every (chunk, row block) record is computed by one wave as before, so the bits do not change
+  __shared__ int next_chunk;
+  if (threadIdx.x == 0) next_chunk = GRAD_WAVES;
   if constexpr (XLDS) {
     const int nf = p.nfeat;
     const bool has_y = GM == GMODE_LOSS && Yg != nullptr;
@@ -268,8 +274,8 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
       if (row < p.ld) v = f < nf ? Xg[(int64_t)f * p.ld + row] : (has_y ? Yg[row] : T(0));
       xs[i] = v;
     }
-    __syncthreads();
   }
+  __syncthreads();
   // feature f / target at block-relative row rr of this row block
   auto xat = [&](int f, int rr) -> T {
     if constexpr (XLDS) return xs[f * rbr + rr];
@@ -282,7 +288,12 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   GIns* code = (GIns*)(uintptr_t)p.code;
   const T p0 = (T)p.loss_p0;
   const int max_steps = __builtin_amdgcn_readfirstlane(p.max_steps);
-  for (int ci = wave; ci < group_n; ci += GRAD_WAVES) {
+  auto claim = [&]() {
+    int c = 0;
+    if (lane == 0) c = atomicAdd(&next_chunk, 1);
+    return __builtin_amdgcn_readfirstlane(c);
+  };
+  for (int ci = wave; ci < group_n; ci = claim()) {
     const int chunk = group_base + ci;
     const int tree = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk]);
     const int c0 = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk + 1]);

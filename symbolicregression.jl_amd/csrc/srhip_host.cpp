@@ -65,7 +65,7 @@ const char* srhip::last_error() { return g_err.c_str(); }
 // (diagnostic) SRHIP_HOST_TIMING=1 timestamps: run_eval's wait and the end of eval_partials' tail
 static thread_local std::chrono::steady_clock::time_point g_wait_begin, g_wait_done, g_tail_done;
 extern "C" char** environ;
-static const char* env_get(const char* name) {
+const char* srhip::env_get(const char* name) {
   struct Ent {
     const char* name;
     const char* val;
@@ -1570,9 +1570,10 @@ static void finalize_precise(const srhip_program& P, const int32_t* trees, int32
 }  // namespace
 
 int srhip::next_fail_epoch(srhip_ctx* ctx, int64_t n, int32_t** flags, int32_t* epoch) {
-  const void* before = ctx->fail_flag.p;
-  HIP_TRY(ctx->fail_flag.ensure((size_t)std::max<int64_t>(n, 1) * sizeof(int32_t)));
-  if (ctx->fail_flag.p != before || ctx->epoch == INT32_MAX) {  // fresh buffer (or wrap): no stale epochs
+  const size_t need = (size_t)std::max<int64_t>(n, 1) * sizeof(int32_t);
+  const bool fresh = !ctx->fail_flag.p || ctx->fail_flag.bytes < need;  // (a new buffer may reuse an address)
+  HIP_TRY(ctx->fail_flag.ensure(need));
+  if (fresh || ctx->epoch == INT32_MAX) {  // fresh buffer (or wrap): no stale epochs
     HIP_TRY(hipMemsetAsync(ctx->fail_flag.p, 0, ctx->fail_flag.bytes, ctx->stream));
     ctx->epoch = 0;
   }

@@ -283,6 +283,8 @@ int precise_decide(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program*
 // buf[0, nsum) by SUM and buf[nsum, nsum + nchk) by MAX (chk_max) or SUM across the shards, in place;
 // returns an SRHIP status.
 using ShardReduce = std::function<int(double* buf, size_t nsum, size_t nchk, bool chk_max)>;
+// getenv through a per-thread cache that is dropped whenever the environment changes (srhip_host.cpp)
+const char* env_get(const char* name);
 // Wait for the context's stream by polling a completion event (a spin: the host thread resumes
 // within ~1 us of the last kernel, where a blocking hipStreamSynchronize wakes on an interrupt);
 // SRHIP_SYNC_BLOCK=1 uses hipStreamSynchronize.

@@ -15,6 +15,7 @@
 //   finite differences, and Newton's Hessian as a central difference of those exact gradients instead
 //   of a second difference of losses -- parity is on the optimised loss, SURVEY.md 8(a) A13.
 #include <algorithm>
+#include <numeric>
 #include <chrono>
 #include <cstdio>
 #include <random>
@@ -97,6 +98,9 @@ static thread_local int64_t g_n_launch = 0;
 static thread_local bool g_stats_on = false;
 static thread_local int64_t g_hist[5] = {0, 0, 0, 0, 0}, g_nonfinite_trials = 0;
 static thread_local int64_t g_spec_launched = 0, g_spec_used = 0;  // speculative trial points
+// (SRHIP_OPTIM_TIMING=2) evaluated items by pass (0 gradient, 1 value-only) and launch size (items
+// <= 64 / > 64): [pass][big][all, non-finite f]
+static thread_local int64_t g_items[2][2][2] = {};
 static double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -161,7 +165,7 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     cost4 += (int64_t)((nc + 3) / 4) * (3 + 4);
     cost8 += (int64_t)((nc + GRAD_KT - 1) / GRAD_KT) * (3 + GRAD_KT);
   }
-  const char* kte = getenv("SRHIP_GRAD_KT");  // tuning / tests: force 4 or 8
+  const char* kte = env_get("SRHIP_GRAD_KT");  // tuning / tests: force 4 or 8
   int kt = cost4 < cost8 ? 4 : GRAD_KT;
   if (kte && (atoi(kte) == 4 || atoi(kte) == GRAD_KT)) kt = atoi(kte);
   // two passes on the stream (gradient chunks, then value-only chunks), one synchronisation
@@ -200,6 +204,29 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     const int nch = (int)ps.chunks.size() / 2;
     if (nch == 0) continue;
     ps.L = grad_plan(ctx, v.m, nch);
+    // launch order: descending estimated cost, dealt round-robin over the tree groups (each group's
+    // range stays contiguous), so every group gets the same cost mix and its waves -- which claim
+    // chunks dynamically -- start with the longest ones.  Records are read back by position.
+    if (nch > 1) {
+      std::vector<int32_t> by(nch);
+      std::iota(by.begin(), by.end(), 0);
+      std::stable_sort(by.begin(), by.end(), [&](int32_t x, int32_t y) {
+        return P->ginfo[ps.chunks[2 * x]].cost > P->ginfo[ps.chunks[2 * y]].cost;
+      });
+      const int G = ps.L.groups, tpg = ps.L.tpg;
+      std::vector<int32_t> fill(G, 0), chunks2(ps.chunks.size()), item2(nch);
+      int g = 0;
+      for (int32_t k : by) {
+        while (fill[g] >= std::min(tpg, nch - g * tpg)) g = (g + 1) % G;
+        const int pos = g * tpg + fill[g]++;
+        chunks2[2 * pos] = ps.chunks[2 * k];
+        chunks2[2 * pos + 1] = ps.chunks[2 * k + 1];
+        item2[pos] = ps.chunk_item[k];
+        g = (g + 1) % G;
+      }
+      ps.chunks.swap(chunks2);
+      ps.chunk_item.swap(item2);
+    }
     slab_n = std::max(slab_n, (size_t)nch * ps.L.nrb * (ps.kt + 2));
     red_n = std::max(red_n, (size_t)nch * (ps.kt + 2));
     chunk_n = std::max(chunk_n, ps.chunks.size());
@@ -278,6 +305,12 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
       }
     }
   }
+  if (g_stats_on)
+    for (const GradItem& it : items) {
+      int64_t* c = g_items[it.value_only ? 1 : 0][items.size() > 64 ? 1 : 0];
+      c[0] += 1;
+      c[1] += !std::isfinite(*it.f);
+    }
   // near-overflow sums: the exact per-operator-node pass on the gradient program decides, so the
   // objective is eval_loss's (L(Inf) exactly where did_succeed fails)
   if (!undecided.empty()) {
@@ -1045,12 +1078,19 @@ int srhip_optimize_constants_starts(srhip_ctx* ctx, const srhip_dataset* ds, srh
     for (int64_t& h : g_hist) h = 0;
     g_nonfinite_trials = 0;
     g_spec_launched = g_spec_used = 0;
+    for (auto& a : g_items)
+      for (auto& b : a) b[0] = b[1] = 0;
     rc = optimize_split(ctx, ds, P, loss, v, trees, coff, opt->iterations, g_tol, starts, best_x, best_f, fcalls);
     if (g_stats_on)
       fprintf(stderr, "srhip optim: launches by active trees: 1: %lld, 2-4: %lld, 5-16: %lld, 17-64: %lld, >64: %lld; "
               "non-finite trial points %lld; speculative points %lld evaluated, %lld used\n", (long long)g_hist[0],
               (long long)g_hist[1], (long long)g_hist[2], (long long)g_hist[3], (long long)g_hist[4],
               (long long)g_nonfinite_trials, (long long)g_spec_launched, (long long)g_spec_used);
+    if (g_stats_on)
+      fprintf(stderr, "srhip optim: items (all / non-finite f): gradient small %lld/%lld big %lld/%lld; value-only "
+              "small %lld/%lld big %lld/%lld\n", (long long)g_items[0][0][0], (long long)g_items[0][0][1],
+              (long long)g_items[0][1][0], (long long)g_items[0][1][1], (long long)g_items[1][0][0],
+              (long long)g_items[1][0][1], (long long)g_items[1][1][0], (long long)g_items[1][1][1]);
     if (te && (*te == '1' || *te == '2'))
       fprintf(stderr,
               "srhip optim: %.1f ms total, %lld launches, eval_grad %.1f ms (compile/patch %.1f ms: scan+recompile %.1f, "
