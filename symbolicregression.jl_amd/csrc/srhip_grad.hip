@@ -240,6 +240,31 @@ DI void chk_fold(double& M, double v) { M = __builtin_fma(__builtin_fabs(v), 0x1
 // R rows per lane: a tile is 64 R rows (row tile_base + 64 r + lane), one bytecode dispatch per tile.
 // Every lane still folds its rows in ascending row order (tile-major, r inner), so losses and
 // gradients are bit-identical for any R.
+// The value of lane (lane ^ O) for the xor butterflies of the per-(chunk, row block) sums: DPP for
+// O <= 8 (quad permutes; half-row / row mirrors composed with them), ds_swizzle for 16, ds_bpermute
+// for 32 -- the partner's exact bits, so every sum is the one __shfl_xor gave, with four of the six
+// levels off the LDS crossbar's latency.
+template <int O> DI uint32_t xor_lane_u32(uint32_t v, int lane) {
+  if constexpr (O == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad [1,0,3,2]
+  else if constexpr (O == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad [2,3,0,1]
+  else if constexpr (O == 4)  // half-row mirror (i ^ 7), then quad mirror (^ 3)
+    return (uint32_t)__builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false), 0x1B, 0xF, 0xF, false);
+  else if constexpr (O == 8)  // row mirror (i ^ 15), then half-row mirror (^ 7)
+    return (uint32_t)__builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false), 0x141, 0xF, 0xF, false);
+  else if constexpr (O == 16)  // bitmask swizzle within 32 lanes: and 0x1f, or 0, xor 0x10
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);
+  else
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((lane ^ O) << 2, (int)v);
+}
+template <int O> DI double xor_lane(double x, int lane) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, x);
+  const uint64_t r = (uint64_t)xor_lane_u32<O>((uint32_t)b, lane) | ((uint64_t)xor_lane_u32<O>((uint32_t)(b >> 32), lane) << 32);
+  return __builtin_bit_cast(double, r);
+}
+template <int O> DI float xor_lane(float x, int lane) {
+  return __builtin_bit_cast(float, xor_lane_u32<O>(__builtin_bit_cast(uint32_t, x), lane));
+}
+
 template <typename T, int KT, int K, int GM, bool XLDS, int R>
 __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   constexpr int CW = GM == GMODE_LOSS ? 2 : 4;  // ints per chunk record
@@ -418,12 +443,19 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
     }
     if constexpr (GM != GMODE_LOSS) continue;
     // wave reductions, one slab entry per (chunk, row block)
-    UNR for (int o = 32; o > 0; o >>= 1) {
-      lacc += __shfl_xor(lacc, o);
-      UNR for (int j = 0; j < KT; ++j) gacc[j] += __shfl_xor(gacc[j], o);
-      if constexpr (sizeof(T) == 4) M = __builtin_elementwise_maximum(M, __shfl_xor(M, o));
-      else M += __shfl_xor(M, o);
-    }
+    auto level = [&](auto oc) {
+      constexpr int O = decltype(oc)::value;
+      lacc += xor_lane<O>(lacc, lane);
+      UNR for (int j = 0; j < KT; ++j) gacc[j] += xor_lane<O>(gacc[j], lane);
+      if constexpr (sizeof(T) == 4) M = __builtin_elementwise_maximum(M, xor_lane<O>(M, lane));
+      else M += xor_lane<O>(M, lane);
+    };
+    level(std::integral_constant<int, 32>());
+    level(std::integral_constant<int, 16>());
+    level(std::integral_constant<int, 8>());
+    level(std::integral_constant<int, 4>());
+    level(std::integral_constant<int, 2>());
+    level(std::integral_constant<int, 1>());
     if (lane == 0) {
       double* out = p.slab + ((int64_t)chunk * p.nrb + rb) * (KT + 2);
       out[0] = lacc;
