@@ -232,6 +232,7 @@ def main():
     p2.eval_loss(ds, loss)
     e2e_ms = (time.perf_counter() - t0) * 1e3
     p2.close()
+    pipeline = None if args.headline_only else population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -296,6 +297,7 @@ def main():
             "cpu_baseline": cpu,
             "extra": {
                 "compile_ms_1024_trees": compile_ms, "end_to_end_ms_per_population": e2e_ms,
+                "population_pipeline": pipeline,
                 "undecided_trees_per_step": undecided,
                 # population scoring rate: every live tree's nodes x every row per step / step time (the
                 # rows a failed tree skipped counted as if evaluated)
@@ -316,6 +318,63 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=6):
+    """Fresh populations through the whole boundary (SURVEY.md section 8 row f1's producer side): host
+    compile (no code-cache hits: every population is new trees), upload and fused-loss evaluation of
+    `npop` C2-shaped populations, (a) one after another and (b) pipelined -- population i + 1
+    compiled on a host thread while population i evaluates (both calls release the interpreter
+    lock) -- plus the compile of a population seen before (per-tree code-cache hits)."""
+    import concurrent.futures as cf
+    pops = []
+    for i in range(npop + 1):
+        _, _, _, _, nd, of = workloads.c2(rank + 1000 + i, args.ntrees, 4096)
+        pops.append((nd, of))
+
+    def make(i):
+        return srhip.Program(ctx, pops[i][0], pops[i][1], opts, np.float32)
+
+    p = make(npop)  # warm-up (thread pool, allocations) on a population the timed ones do not share
+    p.eval_loss(ds, loss)
+    p.close()
+    comp = []
+    for i in range(npop // 2):
+        t0 = time.perf_counter()
+        p = make(i)
+        comp.append(time.perf_counter() - t0)
+        p.close()
+    t0 = time.perf_counter()
+    p = make(0)  # the same trees again: code-cache hits
+    warm = time.perf_counter() - t0
+    p.close()
+    seq = []
+    for i in range(npop // 2, npop):
+        t0 = time.perf_counter()
+        p = make(i)
+        p.eval_loss(ds, loss)
+        seq.append(time.perf_counter() - t0)
+        p.close()
+    # pipelined over fresh populations (new seeds: no cache hits)
+    for i in range(npop + 1):
+        _, _, _, _, nd, of = workloads.c2(rank + 2000 + i, args.ntrees, 4096)
+        pops[i] = (nd, of)
+    with cf.ThreadPoolExecutor(1) as ex:
+        fut = ex.submit(make, 0)
+        t0 = time.perf_counter()
+        for i in range(npop):
+            p = fut.result()
+            if i + 1 < npop:
+                fut = ex.submit(make, i + 1)
+            p.eval_loss(ds, loss)
+            p.close()
+        pipe = (time.perf_counter() - t0) / npop
+    return {"populations": npop, "trees_each": args.ntrees,
+            "compile_ms_fresh": 1e3 * float(np.median(comp)), "compile_ms_cached": 1e3 * warm,
+            "sequential_ms_per_population": 1e3 * float(np.mean(seq)),
+            "pipelined_ms_per_population": 1e3 * pipe,
+            "note": "compile + upload + srhip_eval_loss per fresh 1024-tree population; pipelined: the next "
+                    "population compiled on a host thread during the current evaluation"}
 
 
 def _native_comm(ctx, dist):

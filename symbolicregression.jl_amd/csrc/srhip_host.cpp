@@ -629,8 +629,10 @@ class HostPool {
 
  private:
   HostPool() : pid_(getpid()) {
+    // up to 15 workers + the caller: the CPU share a GPU process gets on the MI355X boxes (16);
+    // hardware_concurrency there reports the whole machine
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    nthr_ = std::min(7u, hw - 1);
+    nthr_ = std::min(15u, hw - 1);
     for (unsigned i = 0; i < nthr_; ++i) threads_.emplace_back([this] { loop(); });
   }
   ~HostPool() {
