@@ -327,6 +327,8 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
     compiled on a host thread while population i evaluates (both calls release the interpreter
     lock) -- plus the compile of a population seen before (per-tree code-cache hits)."""
     import concurrent.futures as cf
+
+    import numpy as np
     pops = []
     for i in range(npop + 1):
         _, _, _, _, nd, of = workloads.c2(rank + 1000 + i, args.ntrees, 4096)
