@@ -1326,7 +1326,7 @@ static void set_prog_pointers(const srhip_program& P) {
   P.dmask_dev = der ? (const uint64_t*)(d + P.blob_off[4]) : nullptr;
 }
 
-int srhip::upload_program(srhip_program& P, bool sync, bool defer) {
+int srhip::upload_program(srhip_program& P, bool sync, bool defer, hipStream_t stream) {
   HIP_TRY(hipSetDevice(P.ctx->device));
   // one host image and one copy (each hipMemcpyAsync costs a few us of API time and a blit on the
   // stream: the coalescer uploads a small program per flush)
@@ -1353,9 +1353,10 @@ int srhip::upload_program(srhip_program& P, bool sync, bool defer) {
   }
   P.upload_pending = false;
   HIP_TRY(P.d_prog.ensure(total));
-  HIP_TRY(hipMemcpyAsync(P.d_prog.p, h, total, hipMemcpyHostToDevice, P.ctx->stream));
+  hipStream_t st = stream ? stream : P.ctx->stream;
+  HIP_TRY(hipMemcpyAsync(P.d_prog.p, h, total, hipMemcpyHostToDevice, st));
   set_prog_pointers(P);
-  if (sync) HIP_TRY(hipStreamSynchronize(P.ctx->stream));
+  if (sync) HIP_TRY(hipStreamSynchronize(st));
   return SRHIP_OK;
 }
 
@@ -2095,8 +2096,8 @@ int srhip::gathered_weight_sum(srhip_ctx* ctx, const srhip_dataset* ds, int64_t 
 // schedule, launches), in the wait, and after it (decisions), averaged over every 50 calls on stderr
 int srhip::stream_wait(srhip_ctx* ctx) {
   g_wait_begin = std::chrono::steady_clock::now();
-  static const bool block = env_flag("SRHIP_SYNC_BLOCK");
-  if (block || !ctx->ev_sync) {
+  static const bool spin = env_flag("SRHIP_SYNC_SPIN");
+  if (!spin || !ctx->ev_sync) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     g_wait_done = std::chrono::steady_clock::now();
     return SRHIP_OK;
@@ -2299,6 +2300,7 @@ int srhip_ctx_create(int device, srhip_ctx** out) {
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
+  HIP_TRY(hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking));
   *out = c.release();
   return SRHIP_OK;
 }
@@ -2313,6 +2315,7 @@ void srhip_ctx_destroy(srhip_ctx* ctx) {
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->ev_sync) (void)hipEventDestroy(ctx->ev_sync);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->up_stream) (void)hipStreamDestroy(ctx->up_stream);
   delete ctx;
   (void)hipGetLastError();
 }
@@ -2422,7 +2425,7 @@ int srhip_program_create(srhip_ctx* ctx, int dtype, const srhip_node* nodes, con
   int rc = compile_program(*P);
   if (rc) return rc;
   if (ctx) {  // ctx == NULL: host-only program (compile + did_succeed metadata, e.g. for finalize)
-    rc = upload_program(*P);
+    rc = upload_program(*P, true, false, ctx->up_stream);
     if (rc) return rc;
   }
   *out = P.release();

@@ -121,6 +121,7 @@ struct srhip_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t ev_sync = nullptr;  // stream_wait's completion marker (no timing)
+  hipStream_t up_stream = nullptr;  // new programs' uploads (srhip_program_create)
   bool timed = false;
   int num_cu = 256;
   int lds_max = 160 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerBlock of the device
@@ -259,7 +260,9 @@ bool spec_instantiate(srhip_program& P, int32_t slot, int32_t t, const double* c
                       int64_t& hi);
 // sync = false: the copies stay queued on the context's stream (the caller's next evaluation, which
 // synchronises before returning, must follow before P's host code changes again)
-int upload_program(srhip_program& P, bool sync = true, bool defer = false);
+// stream: the copy's stream (nullptr: the context's; srhip_program_create uses the context's upload
+// stream, so a program built on one host thread does not wait for evaluations queued on another)
+int upload_program(srhip_program& P, bool sync = true, bool defer = false, hipStream_t stream = nullptr);
 int make_view(srhip_ctx* ctx, const srhip_dataset* ds, const int64_t* idx, int64_t nidx, bool need_y, View& v);
 int gathered_weight_sum(srhip_ctx* ctx, const srhip_dataset* ds, int64_t nidx, View& v);
 // ncols: feature (+ derived) columns staged; lds_budget: bytes of LDS a workgroup may use
@@ -285,9 +288,10 @@ int precise_decide(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program*
 using ShardReduce = std::function<int(double* buf, size_t nsum, size_t nchk, bool chk_max)>;
 // getenv through a per-thread cache that is dropped whenever the environment changes (srhip_host.cpp)
 const char* env_get(const char* name);
-// Wait for the context's stream by polling a completion event (a spin: the host thread resumes
-// within ~1 us of the last kernel, where a blocking hipStreamSynchronize wakes on an interrupt);
-// SRHIP_SYNC_BLOCK=1 uses hipStreamSynchronize.
+// Wait for the context's stream: hipStreamSynchronize, or with SRHIP_SYNC_SPIN=1 a spin on a
+// completion event.  The spin measured the same C2 step time and slowed a host thread compiling the
+// next population beside the evaluation (fresh compile 0.59 -> 0.80 ms, pipelined population
+// 1.63 -> 1.95 ms), so blocking is the default.
 int stream_wait(srhip_ctx* ctx);
 int run_eval_sharded(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const srhip_loss* loss,
                      const int64_t* idx, int64_t nidx, const ShardReduce& reduce, double* out_loss, uint8_t* out_ok);
