@@ -501,7 +501,7 @@ def pmc_summary(kname, pattern="*pmc_c2*.json"):
 
     # the round's final summary when committed (file names sort by build, not by date), else the
     # last by name
-    final = os.path.join(ROOT, "profiles", pattern.replace("*", "r03_", 1).replace("*", "_final"))
+    final = os.path.join(ROOT, "profiles", pattern.replace("*", "r04_", 1).replace("*", "_final"))
     files = [final] if os.path.exists(final) else sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
     if not files:
         return None, None, None

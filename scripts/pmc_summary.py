@@ -2,7 +2,10 @@
 
     python scripts/pmc_summary.py [root] [kernel-substring] [--json out.json]
 
-Counters are averaged per dispatch.  HBM bytes follow MI355X_MICROARCH.md "HBM [CDNA4]": FETCH_SIZE
+Counters are averaged per dispatch class: when one kernel symbol has dispatches of very different
+durations (the C2 probe and persistent launches share a symbol, grid size and static LDS), the
+dispatches above the geometric mean of the shortest and longest keep the plain kernel name and the
+others are summarised apart as "<name> [short]".  HBM bytes follow MI355X_MICROARCH.md "HBM [CDNA4]": FETCH_SIZE
 and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read, so
 fetch bytes = 2 x 1024 x FETCH_SIZE and write bytes = 1024 x WRITE_SIZE.
 """
@@ -20,13 +23,20 @@ root = args[0] if len(args) > 0 else "gpurun_out/pmc"
 match = args[1] if len(args) > 1 else "eval_kernel"
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 cnt = collections.defaultdict(lambda: collections.defaultdict(int))
+rows = collections.defaultdict(list)  # kernel -> [(pass file, dispatch id, counter, value, duration)]
 for f in sorted(glob.glob(f"{root}/p*/p*_counter_collection.csv")):
     for row in csv.DictReader(open(f)):
-        k = row["Kernel_Name"]
-        if match not in k:
+        if match not in row["Kernel_Name"]:
             continue
-        agg[k][row["Counter_Name"]] += float(row["Counter_Value"])
-        cnt[k][row["Counter_Name"]] += 1
+        rows[row["Kernel_Name"]].append((f, row["Dispatch_Id"], row["Counter_Name"], float(row["Counter_Value"]),
+                                         int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
+for k, rs in rows.items():
+    lo, hi = min(r[4] for r in rs), max(r[4] for r in rs)
+    cut = (lo * hi) ** 0.5 if hi > 3 * lo else -1
+    for f, did, name, val, d in rs:
+        key = k if d >= cut else f"{k} [short]"
+        agg[key][name] += val
+        cnt[key][name] += 1
 summary = {}
 for k, v in agg.items():
     c = {name: x / cnt[k][name] for name, x in v.items()}
