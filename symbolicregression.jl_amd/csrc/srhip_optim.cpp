@@ -1082,7 +1082,8 @@ int srhip_optimize_constants_starts(srhip_ctx* ctx, const srhip_dataset* ds, srh
       for (auto& b : a) b[0] = b[1] = 0;
     rc = optimize_split(ctx, ds, P, loss, v, trees, coff, opt->iterations, g_tol, starts, best_x, best_f, fcalls);
     if (g_stats_on)
-      fprintf(stderr, "srhip optim: launches by active trees: 1: %lld, 2-4: %lld, 5-16: %lld, 17-64: %lld, >64: %lld; "
+      fprintf(stderr, "srhip optim (the caller's group: 1 of SRHIP_OPTIM_SPLIT groups): launches by active trees: "
+              "1: %lld, 2-4: %lld, 5-16: %lld, 17-64: %lld, >64: %lld; "
               "non-finite trial points %lld; speculative points %lld evaluated, %lld used\n", (long long)g_hist[0],
               (long long)g_hist[1], (long long)g_hist[2], (long long)g_hist[3], (long long)g_hist[4],
               (long long)g_nonfinite_trials, (long long)g_spec_launched, (long long)g_spec_used);
@@ -1093,7 +1094,8 @@ int srhip_optimize_constants_starts(srhip_ctx* ctx, const srhip_dataset* ds, srh
               (long long)g_items[1][0][1], (long long)g_items[1][1][0], (long long)g_items[1][1][1]);
     if (te && (*te == '1' || *te == '2'))
       fprintf(stderr,
-              "srhip optim: %.1f ms total, %lld launches, eval_grad %.1f ms (compile/patch %.1f ms: scan+recompile %.1f, "
+              "srhip optim: %.1f ms total (all groups), caller's group: %lld launches, eval_grad %.1f ms (compile/patch "
+              "%.1f ms: scan+recompile %.1f, "
               "snapshot+upload %.1f), set_consts %.1f ms\n",
               1e3 * (now_s() - tb), (long long)g_n_launch, 1e3 * g_t_eval, 1e3 * g_t_compile, 1e3 * g_patch_scan_s,
               1e3 * g_patch_copy_s, 1e3 * g_t_host);

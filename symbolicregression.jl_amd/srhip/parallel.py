@@ -90,13 +90,15 @@ timer = CollectiveTimer()
 _bufs = {}
 
 
-def _staging(n: int, dtype, dev):
+def _staging(n: int, dtype, dev, role: str):
     """Reused (pinned host, device) buffer pair of n elements for a collective's copies: no allocation
-    and no pageable-memory copy per call.  One exchange of a given size in flight at a time (an
-    async migration is collected before the next is issued)."""
+    and no pageable-memory copy per call.  Keyed by role ("partials", "migrate_in", "migrate_out"), so
+    a collective's input and output never share a buffer (at world size 1 they have the same size).
+    One exchange per role in flight at a time (an async migration is collected before the next is
+    issued)."""
     import torch
 
-    key = (n, dtype, str(dev))
+    key = (role, n, dtype, str(dev))
     if key not in _bufs:
         host = torch.empty(n, dtype=dtype, pin_memory=dev.type == "cuda")
         _bufs[key] = (host, host if dev.type != "cuda" else torch.empty(n, dtype=dtype, device=dev))
@@ -117,7 +119,7 @@ def allreduce_partials(sums: np.ndarray, chk: np.ndarray, chk_op: str, group=Non
     t0 = time.perf_counter()
     ns, nc = len(sums), len(chk)
     dev = _device(group)
-    host, buf = _staging(ns + nc, torch.float64, dev)
+    host, buf = _staging(ns + nc, torch.float64, dev, "partials")
     hv = host.numpy()
     hv[:ns] = sums
     hv[ns:] = np.where(np.isfinite(chk), chk, np.inf)
@@ -284,11 +286,11 @@ def migrate_topk_async(nodes: np.ndarray, offsets: np.ndarray, losses: np.ndarra
     ws = dist.get_world_size(group)
     payload, head = _pack_topk(nodes, offsets, losses, k, max_nodes)
     dev = _device(group)
-    host_in, src = _staging(len(payload), torch.uint8, dev)
+    host_in, src = _staging(len(payload), torch.uint8, dev, "migrate_in")
     host_in.numpy()[:] = payload
     if src is not host_in:
         src.copy_(host_in, non_blocking=True)
-    host_out, dst = _staging(ws * len(payload), torch.uint8, dev)
+    host_out, dst = _staging(ws * len(payload), torch.uint8, dev, "migrate_out")
     work = dist.all_gather_into_tensor(dst, src, group=group, async_op=True)
     timer.seconds += time.perf_counter() - t0
     return _Pending(work, dst, host_out, ws, head, k, len(payload), t0)
