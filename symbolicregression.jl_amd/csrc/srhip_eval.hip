@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab
   // The same sequential per-lane order as a plain strided loop (lane l adds chunks l, l + 64, ...:
   // the bits every launch form reproduces), with RB_BATCH independent loads issued before their adds:
   // a strided loop waited out one memory latency per iteration (16 per lane for C2's 977 chunks).
-  constexpr int RB_BATCH = 8;
+  constexpr int RB_BATCH = 16;
   if (slab_loss)
     for (int c0 = lane; c0 < nch; c0 += 64 * RB_BATCH) {
       LT v[RB_BATCH];

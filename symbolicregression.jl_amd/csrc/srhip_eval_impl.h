@@ -698,7 +698,7 @@ __device__ __attribute__((always_inline)) inline int32_t wave_chk(int32_t v) { r
 // One wave owns a (tree, row block), so plain read-modify-write of its slab entry is race-free.
 template <typename T, int R>
 __device__ __attribute__((always_inline)) inline void precise_hook(const EvalArgs& p, uint32_t a, const RV<T, R>& A,
-                                                                   int ti, int rb, int lane, int64_t row0) {
+                                                                   int slot, int rb, int lane, int64_t row0) {
   if constexpr (!kIsInt<T>) {
     const uint32_t opidx = a >> 16;
     if (opidx == 0) return;
@@ -711,8 +711,10 @@ __device__ __attribute__((always_inline)) inline void precise_hook(const EvalArg
     }
     s = wave_sum_d(s);
     if (lane == WAVE_LAST) {
-      double* slot = reinterpret_cast<double*>(p.slab_prec) + ((int64_t)ti * p.prec_stride + (opidx - 1)) * p.nrb + rb;
-      *slot += s;
+      // the launch's order slot (a listed tree's index in the device list), not its index inside the
+      // workgroup's group: a device-listed launch runs one tree per group
+      double* e = reinterpret_cast<double*>(p.slab_prec) + ((int64_t)slot * p.prec_stride + (opidx - 1)) * p.nrb + rb;
+      *e += s;
     }
   }
 }
@@ -1052,7 +1054,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
       // device-listed trees: this wave owns the (tree, row block) entries, zeroed before accumulating
       if (p.dev_count && lane == WAVE_LAST)
         for (int k = 0; k < p.prec_stride; ++k)
-          reinterpret_cast<double*>(p.slab_prec)[((int64_t)ti * p.prec_stride + k) * p.nrb + rb] = 0.0;
+          reinterpret_cast<double*>(p.slab_prec)[((int64_t)slot * p.prec_stride + k) * p.nrb + rb] = 0.0;
     }
     // loss chunks per tile (CPT > 1: R = 32 tiles span two chunks) / tiles per loss chunk
     constexpr int CHS = sizeof(T) == 8 ? LOSS_CHUNK_8B : LOSS_CHUNK_4B;
@@ -1161,7 +1163,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
       RV<T, R> xv;                                                                                     \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
       bin_rows_chk<T, R, SB_##NAME, false>(A, xv, M);                                              \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
   SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_FA):                                                \
@@ -1169,19 +1171,19 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
       RV<T, R> xv;                                                                                     \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
       bin_rows_chk<T, R, SB_##NAME, true>(A, xv, M);                                               \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
   SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_AC):                                                \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       bin_rows_c_chk<T, R, SB_##NAME, false>(A, imm_as<T>(ins.imm), M);                            \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
   SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_CA):                                                \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       bin_rows_c_chk<T, R, SB_##NAME, true>(A, imm_as<T>(ins.imm), M);                             \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
   SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_FF):                                              \
@@ -1190,30 +1192,30 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A);                          \
       load_rows<T, R>(xt + (int64_t)(ins.imm & 0xffff) * xstride, lane, xv);                       \
       bin_rows_chk<T, R, SB_##NAME, false>(A, xv, M);                                              \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);     \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);     \
     }                                                                                              \
     break;                                                                                         \
   SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_FC):                                              \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A);                          \
       bin_rows_c_chk<T, R, SB_##NAME, false>(A, imm_as<T>(ins.imm), M);                            \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);     \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);     \
     }                                                                                              \
     break;                                                                                         \
   SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_CF):                                              \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A);                          \
       bin_rows_c_chk<T, R, SB_##NAME, true>(A, imm_as<T>(ins.imm), M);                             \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);     \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);     \
     }                                                                                              \
     break;                                                                                         \
     SRHIP_K_CASES_H(SRHIP_HOTB_##NAME, h_spec(SB_##NAME, SPEC_SA0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
       bin_rows_chk<T, R, SB_##NAME, true>(A, S[k], M);                                             \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);         \
     })                                                                                             \
     SRHIP_K_CASES_H(SRHIP_HOTB_##NAME, h_spec(SB_##NAME, SPEC_AS0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
       bin_rows_chk<T, R, SB_##NAME, false>(A, S[k], M);                                            \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);         \
     })
           SRHIP_SPEC_BINOPS(SRHIP_SPEC_CASE)
 #undef SRHIP_SPEC_CASE
@@ -1222,12 +1224,12 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
     SRHIP_K_CASES(h_heavy(HB_##NAME, HEAVY_SA0), if constexpr (hb_ok<T>(HB_##NAME)) {           \
       apply_heavy<T, R, HB_##NAME>(A, S[k], A);                                                 \
       chk_update<R>(M, A);                                                                      \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);  \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);  \
     })                                                                                          \
     SRHIP_K_CASES(h_heavy(HB_##NAME, HEAVY_AS0), if constexpr (hb_ok<T>(HB_##NAME)) {           \
       apply_heavy<T, R, HB_##NAME>(A, A, S[k]);                                                 \
       chk_update<R>(M, A);                                                                      \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);  \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);  \
     })
           SRHIP_HEAVY_BINOPS(SRHIP_HEAVY_CASE)
 #undef SRHIP_HEAVY_CASE
@@ -1237,7 +1239,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
     if constexpr (un_ok<T>(UN_##NAME) && (K == K_MAX || !un_wide(UN_##NAME))) {  \
       apply_un<T, R, UN_##NAME>(A);                                              \
       chk_update<R>(M, A);                                                       \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0); \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0); \
     }                                                                            \
     break;
           SRHIP_UNOPS(SRHIP_UN_CASE)
@@ -1245,13 +1247,13 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
           SRHIP_LK case H_COS_NC:
             if constexpr (un_ok<T>(UN_COS)) {
               apply_un<T, R, UN_COS>(A);
-              if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);
+              if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);
             }
             break;
           SRHIP_LK case H_SIN_NC:
             if constexpr (un_ok<T>(UN_SIN)) {
               apply_un<T, R, UN_SIN>(A);
-              if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, ti, rb, lane, row0);
+              if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);
             }
             break;
 #undef SRHIP_K_CASES

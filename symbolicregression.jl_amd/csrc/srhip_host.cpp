@@ -1933,9 +1933,10 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       HIP_TRY(hipMemsetAsync(ctx->d_ulist.p, 0, ctx->d_ulist.bytes, ctx->stream));
     }
     ul.ulist = (int32_t*)ctx->d_ulist.p;
-    // list capacity: twice the trees the program's last launch listed (8 .. DEV_PRECISE_MAX); trees
-    // past it are decided by the host-launched pass
-    ul.umax = std::min(DEV_PRECISE_MAX, std::max(8, 2 * P->und_hint));
+    // list capacity: the trees the program's last launch listed plus two (4 .. DEV_PRECISE_MAX): the
+    // precise launch has one tree group per entry, and empty groups still cost their workgroups'
+    // dispatch; trees past it are decided by the host-launched pass
+    ul.umax = std::min(DEV_PRECISE_MAX, std::max(4, P->und_hint + 2));
     ul.rows = (double)v.m;
   }
   if (!a.fused)
