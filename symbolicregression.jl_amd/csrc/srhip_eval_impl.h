@@ -714,7 +714,8 @@ __device__ __attribute__((always_inline)) inline void precise_hook(const EvalArg
       // the launch's order slot (a listed tree's index in the device list), not its index inside the
       // workgroup's group: a device-listed launch runs one tree per group
       double* e = reinterpret_cast<double*>(p.slab_prec) + ((int64_t)slot * p.prec_stride + (opidx - 1)) * p.nrb + rb;
-      *e += s;
+      if (p.prec_assign) *e = s;  // the block's only tile: no read-modify-write round trip per operator
+      else *e += s;
     }
   }
 }

@@ -1975,6 +1975,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     q.max_steps = P->max_len;
     q.dev_count = ul.ulist;
     q.wg_waves = 1;
+    q.prec_assign = 1;  // one-tile row blocks
     HIP_TRY(launch_eval(dtype, q, Rp, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, G), 16, ctx->stream));
     int32_t* hl = (int32_t*)ctx->h_pout.p;
     double* hs = (double*)((uint8_t*)ctx->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));

@@ -108,6 +108,8 @@ struct EvalArgs {
   // (tree, row block) slab entries before accumulating into them
   const int32_t* dev_count;
   int32_t wg_waves;         // waves per workgroup (0: the variant's eval_waves; fewer claim the same trees)
+  int32_t prec_assign;      // MODE_PRECISE with one tile per (tree, row block): store the per-operator
+                            // sums instead of adding to them (no dependent load per operator)
   int32_t* slab_rows;       // [nrb][ntrees] valid rows each (row block, order slot) evaluated, or nullptr
   int64_t* fused_rows;      // fused launches: [program trees] rows evaluated (coherent pinned host), or nullptr
 };
