@@ -227,9 +227,14 @@ class Program:
         if starts is not None:
             sin = np.ascontiguousarray(starts, dtype=np.float64).reshape(int(nrestarts), nall)
         sout = np.empty((int(nrestarts), nall), dtype=np.float64) if return_starts else None
-        check(_lib.load().srhip_optimize_constants_starts(
-            self.ctx.handle, ds.handle, self.handle, ctypes.byref(ls), ptr(idxa), 0 if idxa is None else len(idxa),
-            ctypes.byref(opt), ptr(sin), ptr(sout), ptr(out), ptr(imp), ptr(fc)))
+        if sin is None and sout is None:  # the library's own draws, not reported: the plain entry point
+            check(_lib.load().srhip_optimize_constants(
+                self.ctx.handle, ds.handle, self.handle, ctypes.byref(ls), ptr(idxa), 0 if idxa is None else len(idxa),
+                ctypes.byref(opt), ptr(out), ptr(imp), ptr(fc)))
+        else:
+            check(_lib.load().srhip_optimize_constants_starts(
+                self.ctx.handle, ds.handle, self.handle, ctypes.byref(ls), ptr(idxa), 0 if idxa is None else len(idxa),
+                ctypes.byref(opt), ptr(sin), ptr(sout), ptr(out), ptr(imp), ptr(fc)))
         if return_starts:
             return out, imp.astype(bool), fc, sout
         return out, imp.astype(bool), fc
