@@ -3,14 +3,14 @@
 # --pmc pass per counter group under its own hard timeout; stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/pmcg
+D=${PMCG_DIR:-gpurun_out/pmcg}; mkdir -p $D
 export TMPDIR=/tmp
 i=0
 while read -r counters; do
   [ -z "$counters" ] && continue
   i=$((i+1))
   echo "pass $i: $counters"
-  timeout -s KILL 120 rocprofv3 --pmc $counters -d gpurun_out/pmcg/p$i -o p$i --output-format csv -- python3 scripts/grad_bench.py 5 > gpurun_out/pmcg/p$i.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $counters -d $D/p$i -o p$i --output-format csv -- python3 scripts/grad_bench.py 5 > $D/p$i.log 2>&1
   rc=$?
   echo "  rc=$rc"
   [ $rc -eq 0 ] || exit $rc

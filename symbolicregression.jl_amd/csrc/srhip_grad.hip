@@ -43,40 +43,44 @@ template <int U> constexpr bool dun_inline() {
          U == UN_ROUND || U == UN_FLOOR || U == UN_CEIL;
 }
 
-// f(x) and f'(x) for a heavy unary operator U (one out-of-line body per (T, U))
-template <typename T, int U> __device__ __attribute__((noinline)) typename V2<T>::type dual_un_heavy(T x) {
+// f(x) and f'(x) for a heavy unary operator U (one out-of-line body per (T, U, D)); D = false: the
+// value alone (value-only passes: the derivative of cos is a sin, of log a division -- out of line the
+// compiler cannot drop them), the same f
+template <typename T, int U, bool D> __device__ __attribute__((noinline)) typename V2<T>::type dual_un_heavy(T x) {
   using O = FOps<T>;
   T f = T(0), df = T(0);
   switch (U) {
-    case UN_COS: f = O::cos(x); df = -O::sin(x); break;
-    case UN_SIN: f = O::sin(x); df = O::cos(x); break;
-    case UN_TAN: f = O::tan(x); df = T(1) + f * f; break;
-    case UN_EXP: f = O::exp(x); df = f; break;
-    case UN_LOG: f = O::log(x); df = T(1) / x; break;
-    case UN_LOG2: f = O::log2(x); df = T(1) / (x * T(0.69314718055994530942)); break;
-    case UN_LOG10: f = O::log10(x); df = T(1) / (x * T(2.30258509299404568402)); break;
-    case UN_LOG1P: f = O::log1p(x); df = T(1) / (T(1) + x); break;
-    case UN_SQRT: f = O::sqrt(x); df = T(0.5) / f; break;
-    case UN_ACOSH: f = O::acosh(x); df = T(1) / m_sqrt(x * x - T(1)); break;
+    case UN_COS: f = O::cos(x); if constexpr (D) df = -O::sin(x); break;
+    case UN_SIN: f = O::sin(x); if constexpr (D) df = O::cos(x); break;
+    case UN_TAN: f = O::tan(x); if constexpr (D) df = T(1) + f * f; break;
+    case UN_EXP: f = O::exp(x); if constexpr (D) df = f; break;
+    case UN_LOG: f = O::log(x); if constexpr (D) df = T(1) / x; break;
+    case UN_LOG2: f = O::log2(x); if constexpr (D) df = T(1) / (x * T(0.69314718055994530942)); break;
+    case UN_LOG10: f = O::log10(x); if constexpr (D) df = T(1) / (x * T(2.30258509299404568402)); break;
+    case UN_LOG1P: f = O::log1p(x); if constexpr (D) df = T(1) / (T(1) + x); break;
+    case UN_SQRT: f = O::sqrt(x); if constexpr (D) df = T(0.5) / f; break;
+    case UN_ACOSH: f = O::acosh(x); if constexpr (D) df = T(1) / m_sqrt(x * x - T(1)); break;
     case UN_ATANH_CLIP: {
       f = O::atanh_clip(x);
-      const T u = O::mod(x + T(1), T(2)) - T(1);
-      df = T(1) / (T(1) - u * u);
+      if constexpr (D) {
+        const T u = O::mod(x + T(1), T(2)) - T(1);
+        df = T(1) / (T(1) - u * u);
+      }
       break;
     }
-    case UN_SINH: f = O::sinh(x); df = O::cosh(x); break;
-    case UN_COSH: f = O::cosh(x); df = O::sinh(x); break;
-    case UN_TANH: f = O::tanh(x); df = T(1) - f * f; break;
-    case UN_ASIN: f = O::asin(x); df = T(1) / m_sqrt(T(1) - x * x); break;
-    case UN_ACOS: f = O::acos(x); df = -T(1) / m_sqrt(T(1) - x * x); break;
-    case UN_ATAN: f = O::atan(x); df = T(1) / (T(1) + x * x); break;
-    case UN_ASINH: f = O::asinh(x); df = T(1) / m_sqrt(x * x + T(1)); break;
-    case UN_ERF: f = O::erf(x); df = T(1.12837916709551257390) * O::exp(-x * x); break;
-    case UN_ERFC: f = O::erfc(x); df = -T(1.12837916709551257390) * O::exp(-x * x); break;
-    case UN_GAMMA: f = O::gamma(x); df = FP<T>::nan(); break;  // no digamma: no gradient (optimizer keeps c)
-    case UN_EXP2: f = O::exp2(x); df = f * T(0.69314718055994530942); break;
-    case UN_EXPM1: f = O::expm1(x); df = f + T(1); break;
-    case UN_CBRT: f = O::cbrt(x); df = T(1) / (T(3) * f * f); break;
+    case UN_SINH: f = O::sinh(x); if constexpr (D) df = O::cosh(x); break;
+    case UN_COSH: f = O::cosh(x); if constexpr (D) df = O::sinh(x); break;
+    case UN_TANH: f = O::tanh(x); if constexpr (D) df = T(1) - f * f; break;
+    case UN_ASIN: f = O::asin(x); if constexpr (D) df = T(1) / m_sqrt(T(1) - x * x); break;
+    case UN_ACOS: f = O::acos(x); if constexpr (D) df = -T(1) / m_sqrt(T(1) - x * x); break;
+    case UN_ATAN: f = O::atan(x); if constexpr (D) df = T(1) / (T(1) + x * x); break;
+    case UN_ASINH: f = O::asinh(x); if constexpr (D) df = T(1) / m_sqrt(x * x + T(1)); break;
+    case UN_ERF: f = O::erf(x); if constexpr (D) df = T(1.12837916709551257390) * O::exp(-x * x); break;
+    case UN_ERFC: f = O::erfc(x); if constexpr (D) df = -T(1.12837916709551257390) * O::exp(-x * x); break;
+    case UN_GAMMA: f = O::gamma(x); if constexpr (D) df = FP<T>::nan(); break;  // no digamma: no gradient (optimizer keeps c)
+    case UN_EXP2: f = O::exp2(x); if constexpr (D) df = f * T(0.69314718055994530942); break;
+    case UN_EXPM1: f = O::expm1(x); if constexpr (D) df = f + T(1); break;
+    case UN_CBRT: f = O::cbrt(x); if constexpr (D) df = T(1) / (T(3) * f * f); break;
     default: f = FP<T>::nan(); df = FP<T>::nan(); break;
   }
   typename V2<T>::type r;
@@ -85,7 +89,7 @@ template <typename T, int U> __device__ __attribute__((noinline)) typename V2<T>
   return r;
 }
 
-template <typename T, int U> DI void dual_un(T x, T& f, T& df) {
+template <typename T, int U, bool D = true> DI void dual_un(T x, T& f, T& df) {
   using O = FOps<T>;
   if constexpr (dun_inline<U>()) {
     switch (U) {
@@ -101,7 +105,7 @@ template <typename T, int U> DI void dual_un(T x, T& f, T& df) {
       default: break;
     }
   } else {
-    const typename V2<T>::type r = dual_un_heavy<T, U>(x);
+    const typename V2<T>::type r = dual_un_heavy<T, U, D>(x);
     f = r[0];
     df = r[1];
   }
@@ -126,17 +130,23 @@ template <typename T, int SB> DI void dual_spec(T a, T b, T& f, T& fa, T& fb) {
 }
 
 // heavy binary (pow, mod, atan2): out of line; returns (f, df/da, df/db, -)
-template <typename T, int HB> __device__ __attribute__((noinline)) typename V4<T>::type dual_heavy(T a, T b) {
+template <typename T, int HB, bool D> __device__ __attribute__((noinline)) typename V4<T>::type dual_heavy(T a, T b) {
   using O = FOps<T>;
-  T f, fa, fb;
+  T f, fa = T(0), fb = T(0);
   switch (HB) {
     case HB_POW:
       f = O::pow(a, b);
-      fa = b * O::pow(a, b - T(1));
-      fb = a > T(0) ? f * m_log(a) : T(0);
+      if constexpr (D) {
+        fa = b * O::pow(a, b - T(1));
+        fb = a > T(0) ? f * m_log(a) : T(0);
+      }
       break;
-    case HB_MOD: f = O::mod(a, b); fa = T(1); fb = -m_floor(a / b); break;
-    case HB_ATAN2: { f = O::atan2(a, b); const T r = T(1) / (a * a + b * b); fa = b * r; fb = -a * r; break; }
+    case HB_MOD: f = O::mod(a, b); if constexpr (D) { fa = T(1); fb = -m_floor(a / b); } break;
+    case HB_ATAN2: {
+      f = O::atan2(a, b);
+      if constexpr (D) { const T r = T(1) / (a * a + b * b); fa = b * r; fb = -a * r; }
+      break;
+    }
     default: f = FP<T>::nan(); fa = f; fb = f; break;
   }
   typename V4<T>::type r;
@@ -384,16 +394,16 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
 #undef GK_SPEC
 #define GK_HEAVY(NAME, FN)                                                                         \
   GK_CASES(h_heavy(HB_##NAME, HEAVY_SA0), {                                                        \
-    RR(const typename V4<T>::type q = dual_heavy<T, HB_##NAME>(S[k][r].v, A[r].v);                 \
+    RR(const typename V4<T>::type q = dual_heavy<T, HB_##NAME, (KT > 0)>(S[k][r].v, A[r].v);                 \
        combine(A[r], S[k][r], A[r], q[0], q[1], q[2]); chk_fold(M, A[r].v);) })                    \
   GK_CASES(h_heavy(HB_##NAME, HEAVY_AS0), {                                                        \
-    RR(const typename V4<T>::type q = dual_heavy<T, HB_##NAME>(A[r].v, S[k][r].v);                 \
+    RR(const typename V4<T>::type q = dual_heavy<T, HB_##NAME, (KT > 0)>(A[r].v, S[k][r].v);                 \
        combine(A[r], A[r], S[k][r], q[0], q[1], q[2]); chk_fold(M, A[r].v);) })
           SRHIP_HEAVY_BINOPS(GK_HEAVY)
 #undef GK_HEAVY
 #define GK_UN(NAME, FN)                                                                            \
   case h_un(UN_##NAME): {                                                                          \
-    RR(T f, df; dual_un<T, UN_##NAME>(A[r].v, f, df);                                              \
+    RR(T f, df; dual_un<T, UN_##NAME, (KT > 0)>(A[r].v, f, df);                                              \
        A[r].v = f;                                                                                 \
        UNR for (int j = 0; j < KT; ++j) A[r].d[j] = df * A[r].d[j];                                \
        chk_fold(M, A[r].v);) break; }

@@ -798,7 +798,13 @@ int srhip_eval_loss_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program*
   const std::vector<int64_t> coff = const_offsets(*P);
   std::vector<int32_t> all(P->ntrees);
   for (int32_t t = 0; t < P->ntrees; ++t) all[t] = t;
-  rc = eval_grad(ctx, ds, P, loss, v, all, coff, out_loss, out_grad, out_ok);
+  // (diagnostic, scripts/grad_bench.py: SRHIP_GRAD_VALUE_ONLY=1 runs the line search's value-only pass
+  // over every tree -- losses only, the gradients are left zero)
+  const char* vo = env_get("SRHIP_GRAD_VALUE_ONLY");
+  std::vector<uint8_t> value_only;
+  if (vo && atoi(vo) == 1) value_only.assign(P->ntrees, 1);
+  rc = eval_grad(ctx, ds, P, loss, v, all, coff, out_loss, out_grad, out_ok, nullptr, 0, -1,
+                 value_only.empty() ? nullptr : value_only.data());
   if (rc) return rc;
   return SRHIP_OK;
 }
