@@ -272,6 +272,23 @@ SRM_FN double srm_sin(double x) {
     default: return -c;
   }
 }
+/* sin and cos over one shared reduction: the same two values srm_sin and srm_cos return (the
+ * constant-gradient kernels need both for a cos or sin node) */
+SRM_FN void srm_sincos(double x, double* sn, double* cs) {
+  if (!(x - x == 0.0)) {
+    *sn = *cs = srm_nan();
+    return;
+  }
+  double y0, y1;
+  const int n = srm_rem_pio2(x, &y0, &y1);
+  const double c = srm_kcos(y0, y1), s = srm_ksin(y0, y1);
+  switch (n & 3) {
+    case 0: *sn = s; *cs = c; break;
+    case 1: *sn = c; *cs = -s; break;
+    case 2: *sn = -s; *cs = -c; break;
+    default: *sn = -c; *cs = s; break;
+  }
+}
 /* tan = sin/cos over one shared reduction (<= ~1.5 ULP; fdlibm's k_tan is not restated) */
 SRM_FN double srm_tan(double x) {
   if (!(x - x == 0.0)) return srm_nan();

@@ -50,8 +50,28 @@ template <typename T, int U, bool D> __device__ __attribute__((noinline)) typena
   using O = FOps<T>;
   T f = T(0), df = T(0);
   switch (U) {
-    case UN_COS: f = O::cos(x); if constexpr (D) df = -O::sin(x); break;
-    case UN_SIN: f = O::sin(x); if constexpr (D) df = O::cos(x); break;
+    case UN_COS:
+      if constexpr (D && sizeof(T) == 8) {  // one Float64 reduction for both (srm_sincos: the same bits)
+        double sn, cs;
+        srm_sincos(x, &sn, &cs);
+        f = cs;
+        df = -sn;
+      } else {
+        f = O::cos(x);
+        if constexpr (D) df = -O::sin(x);
+      }
+      break;
+    case UN_SIN:
+      if constexpr (D && sizeof(T) == 8) {
+        double sn, cs;
+        srm_sincos(x, &sn, &cs);
+        f = sn;
+        df = cs;
+      } else {
+        f = O::sin(x);
+        if constexpr (D) df = O::cos(x);
+      }
+      break;
     case UN_TAN: f = O::tan(x); if constexpr (D) df = T(1) + f * f; break;
     case UN_EXP: f = O::exp(x); if constexpr (D) df = f; break;
     case UN_LOG: f = O::log(x); if constexpr (D) df = T(1) / x; break;
