@@ -45,6 +45,8 @@ for c in clients:
     if out.returncode != 0:
         print(out.stderr, file=sys.stderr)
         sys.exit(out.returncode)
+    if os.environ.get("SRHIP_HOST_TIMING"):
+        print(out.stderr, file=sys.stderr)
     line = json.loads(out.stdout.strip().splitlines()[-1])
     line["shape"] = shape
     print(json.dumps(line), flush=True)

@@ -1356,7 +1356,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
 // The interpreter kernel.
 //   grid.x = row blocks (RB rows each), grid.y = tree groups; block = WAVES wavefronts.
 //   Persistent launches (p.persistent, one tree group): grid.x workgroups, each claims row blocks
-//   block0, block0 + 1, ... from the counter p.block_ctr (zeroed before the launch) and interprets
+//   block0, block0 + 1, ... from the counter p.block_ctr (zero at the launch) and interprets
 //   the whole population over each, until the blocks run out -- every workgroup leaves the loop on
 //   the same claimed index, so the grid always drains.
 //   MODE_LOSS: fused loss partial + check partial per (tree, row block) -> slabs
@@ -1397,7 +1397,13 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
       if (threadIdx.x == 0) claimed = atomicAdd(p.block_ctr, 1);
       __syncthreads();
       const int item = __builtin_amdgcn_readfirstlane(claimed);
-      if (item >= nitems) break;
+      if (item >= nitems) {
+        // every workgroup ends on one failing claim; the last of them (nitems + grid - 1) leaves the
+        // counter at zero for the context's next persistent launch (no memset launch before it)
+        if (threadIdx.x == 0 && item == nitems + (int)gridDim.x - 1)
+          __hip_atomic_store(p.block_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
       const int q = item - nfull;
       const bool whole = item < nfull;
       rb = p.block0 + (whole ? item : nfull + q / p.tail_slices);

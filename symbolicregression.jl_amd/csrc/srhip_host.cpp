@@ -1844,10 +1844,13 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     a.out_pred = pred.p;
   }
   dim3 grid(L.nrb, (unsigned)goff.size() - 1);
-  if (persistent) HIP_TRY(ctx->block_ctr.ensure(sizeof(int32_t)));
+  if (persistent && !ctx->block_ctr.p) {
+    // zeroed once: every persistent launch leaves it at zero (its last claim resets it)
+    HIP_TRY(ctx->block_ctr.ensure(sizeof(int32_t)));
+    HIP_TRY(hipMemsetAsync(ctx->block_ctr.p, 0, sizeof(int32_t), ctx->stream));
+  }
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
   if (persistent) {
-    bool ctr_zeroed = false;
     if (probe_blocks > 0) {
       // leading row blocks, one tree per wave (uniform groups of consecutive slots), with the plain
       // program: a probe workgroup serves 16 trees, too few to pay for deriving columns (the values,
@@ -1867,7 +1870,6 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       if (!no_tile_claims) {
         q.tile_claims = 1;
         q.zero_ctr = (int32_t*)ctx->block_ctr.p;
-        ctr_zeroed = true;
       }
       q.code = P->code_dev;
       q.prog_off = P->off_dev;
@@ -1879,7 +1881,6 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       const dim3 pgrid(probe_blocks, (unsigned)((nl + q.trees_per_group - 1) / q.trees_per_group));
       HIP_TRY(launch_eval(dtype, q, R, K, mode, true, pgrid, qlds, ctx->stream));
     }
-    if (!ctr_zeroed) HIP_TRY(hipMemsetAsync(ctx->block_ctr.p, 0, sizeof(int32_t), ctx->stream));
     a.persistent = 1;
     a.block0 = probe_blocks;
     a.block_ctr = (int32_t*)ctx->block_ctr.p;
