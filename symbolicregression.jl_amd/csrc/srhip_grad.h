@@ -40,7 +40,11 @@ struct GradArgs {
   // per-row modes: out_der[row + j][nvalid] for the components c0 + j < end (the values come from the
   // evaluator, which also decides did_succeed)
   void* out_der;
+  // GMODE_LOSS launches of at most GRAD_INLINE chunks pass their (tree, c0) list here, in the kernel
+  // arguments (chunks = nullptr): no host-to-device copy on the stream before the launch
+  int32_t inl[2 * 96];
 };
+constexpr int GRAD_INLINE = 96;
 
 // kt = tangent components per chunk: 4 or GRAD_KT (the slab / reduced layout stride is kt + 2)
 hipError_t launch_grad(int dtype, int K, int kt, const GradArgs& a, dim3 grid, hipStream_t s);

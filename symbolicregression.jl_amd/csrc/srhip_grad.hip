@@ -350,8 +350,14 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   };
   for (int ci = wave; ci < group_n; ci = claim()) {
     const int chunk = group_base + ci;
-    const int tree = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk]);
-    const int c0 = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk + 1]);
+    int tree, c0;
+    if (GM == GMODE_LOSS && !p.chunks) {  // the list in the kernel arguments
+      tree = __builtin_amdgcn_readfirstlane(p.inl[2 * chunk]);
+      c0 = __builtin_amdgcn_readfirstlane(p.inl[2 * chunk + 1]);
+    } else {
+      tree = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk]);
+      c0 = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk + 1]);
+    }
     const int pc0 = __builtin_amdgcn_readfirstlane(p.prog_off[tree]);
     double lacc = 0.0;
     double gacc[KT > 0 ? KT : 1];

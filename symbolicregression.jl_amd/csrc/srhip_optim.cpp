@@ -243,15 +243,21 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     // pinned staging both ways (a pageable source or destination makes the runtime stage the copy
     // through its own buffer, synchronously); stream order: this copy follows the previous pass's
     // kernel, which has read its chunk list
-    HIP_TRY(ctx->h_gchunks[pi].ensure(ps.chunks.size() * sizeof(int32_t)));
     HIP_TRY(ctx->h_gred[pi].ensure((size_t)nch * (ps.kt + 2) * sizeof(double), hipHostMallocCoherent));
-    memcpy(ctx->h_gchunks[pi].p, ps.chunks.data(), ps.chunks.size() * sizeof(int32_t));
-    HIP_TRY(hipMemcpyAsync(ctx->g_chunks.p, ctx->h_gchunks[pi].p, ps.chunks.size() * sizeof(int32_t),
-                           hipMemcpyHostToDevice, ctx->stream));
     GradArgs a{};
+    static const bool no_inline = [] { const char* e = getenv("SRHIP_GRAD_NO_INLINE"); return e && *e && *e != '0'; }();
+    const bool inl = nch <= GRAD_INLINE && !no_inline;
+    if (inl) {  // in the kernel arguments
+      memcpy(a.inl, ps.chunks.data(), ps.chunks.size() * sizeof(int32_t));
+    } else {
+      HIP_TRY(ctx->h_gchunks[pi].ensure(ps.chunks.size() * sizeof(int32_t)));
+      memcpy(ctx->h_gchunks[pi].p, ps.chunks.data(), ps.chunks.size() * sizeof(int32_t));
+      HIP_TRY(hipMemcpyAsync(ctx->g_chunks.p, ctx->h_gchunks[pi].p, ps.chunks.size() * sizeof(int32_t),
+                             hipMemcpyHostToDevice, ctx->stream));
+    }
     a.code = (const Ins*)P->d_gcode.p;
     a.prog_off = (const int32_t*)P->d_goff.p;
-    a.chunks = (const int32_t*)ctx->g_chunks.p;
+    a.chunks = inl ? nullptr : (const int32_t*)ctx->g_chunks.p;
     a.X = v.X;
     a.y = v.y;
     a.w = weighted ? v.w : nullptr;
