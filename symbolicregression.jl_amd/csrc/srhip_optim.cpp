@@ -245,8 +245,11 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     // kernel, which has read its chunk list
     HIP_TRY(ctx->h_gred[pi].ensure((size_t)nch * (ps.kt + 2) * sizeof(double), hipHostMallocCoherent));
     GradArgs a{};
-    static const bool no_inline = [] { const char* e = getenv("SRHIP_GRAD_NO_INLINE"); return e && *e && *e != '0'; }();
-    const bool inl = nch <= GRAD_INLINE && !no_inline;
+    static const int inline_max = [] {
+      const char* e = getenv("SRHIP_GRAD_INLINE_MAX");  // 0: always copy the list
+      return e ? std::max(0, std::min(atoi(e), GRAD_INLINE)) : GRAD_INLINE;
+    }();
+    const bool inl = nch <= inline_max;
     if (inl) {  // in the kernel arguments
       memcpy(a.inl, ps.chunks.data(), ps.chunks.size() * sizeof(int32_t));
     } else {
