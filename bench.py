@@ -31,9 +31,15 @@ PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector (= FP32 MFMA) peak, MI355X_MICROA
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 vector peak
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: WORLD_SIZE when launched by torch.distributed.run, else 1). "
+                         "Without WORLD_SIZE and N > 1 the bench starts the N ranks itself (torch.distributed.run "
+                         "child, before any GPU call) and exits with the worst rank's status")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="(tests) every rank prints its rank / world / device assignment as JSON and exits before "
+                         "touching the GPU")
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default: c2 20, c4 10)")
     ap.add_argument("--warmup", type=int, default=None,
                     help="untimed steps first (default: c2 30 -- the GPU reaches its steady clocks over the "
@@ -63,7 +69,7 @@ def parse():
                     help="c1/c3: islands as threads of one process, or in worker processes (:multiprocessing)")
     ap.add_argument("--procs", type=int, default=0, help="c1/c3 multiprocessing: worker processes "
                     "(default min(populations per GPU, 16))")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     if args.steps is None:
         args.steps = 20 if args.config == "c2" else 10
     if args.warmup is None:
@@ -71,9 +77,60 @@ def parse():
     return args
 
 
+def rank_plan(gpus, env):
+    """How this process runs `--gpus gpus` given its environment: ("launch", N) when it must start N ranks
+    itself (no WORLD_SIZE, N > 1), ("run", N) when it is one of N ranks (or the only one).  A WORLD_SIZE
+    that disagrees with an explicit --gpus is an error: the line would report a rank count it did not
+    run."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        n = 1 if gpus is None else int(gpus)
+        if n < 1:
+            raise SystemExit(f"bench.py: --gpus {n} < 1")
+        return ("launch", n) if n > 1 else ("run", 1)
+    ws = int(ws)
+    if gpus is not None and int(gpus) != ws:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws} (launched with a different rank count)")
+    return "run", ws
+
+
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(n, argv, port):
+    """The child command that runs this bench as n ranks on one node (the driver's own form)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n, argv):
+    """Start the n ranks as ONE child process (torch.distributed.run) -- this process has made no GPU or
+    torch call, so nothing is inherited or exec'd over an initialised runtime -- and return the child's
+    status (torch.distributed.run fails when any rank fails).  Rank 0 prints the JSON line."""
+    import subprocess
+
+    return subprocess.call(launch_cmd(n, argv, free_port()))
+
+
 def main():
     args = parse()
+    plan, n = rank_plan(args.gpus, os.environ)
+    if plan == "launch":  # (an explicit --gpus N > 1 is in argv: every rank re-reads it)
+        sys.exit(launch_ranks(n, sys.argv[1:]))
+    args.gpus = n
+    if args.launch_check:
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": n,
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
+        return
     if args.config == "c4":
+        if n > 1:
+            raise SystemExit("bench.py: --config c4 is a one-GPU configuration (BASELINE.json C4)")
         return bench_c4(args)
     if args.config in ("c1", "c3"):
         return bench_search(args)
@@ -451,6 +508,7 @@ def bench_rowshard(args):
     ctx.synchronize()
     dist.barrier()
     parallel.timer.reset()
+    n0 = native.stats()[1] if native is not None else 0.0
     t0 = time.perf_counter()
     kms, done = [], 0.0
     for _ in range(args.steps):
@@ -460,7 +518,9 @@ def bench_rowshard(args):
     ctx.synchronize()
     dist.barrier()
     dt = time.perf_counter() - t0
-    coll_s = parallel.timer.seconds
+    # the exchanges alone: the library's own clock around its RCCL group (issue -> completion seen), or
+    # the torch path's timer around its all-reduces
+    coll_s = (native.stats()[1] - n0) * 1e-3 if native is not None else parallel.timer.seconds
     red = torch.device("cuda", local_rank) if backend == "nccl" else torch.device("cpu")
     tt = torch.tensor([dt, coll_s, float(np.mean(kms))], dtype=torch.float64, device=red)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)

@@ -226,9 +226,16 @@ int srhip_comm_unique_id(uint8_t* out_id /* [SRHIP_COMM_ID_BYTES] */);
 int srhip_comm_create(srhip_ctx* ctx, const uint8_t* id, int32_t nranks, int32_t rank, srhip_comm** out);
 void srhip_comm_destroy(srhip_comm* comm);
 int srhip_comm_size(const srhip_comm* comm, int32_t* nranks, int32_t* rank);
-/* In-place all-reduce of a host float64 vector (staged through the communicator's device buffer). */
+/* Host wall time of the communicator's exchanges (issue -> completion seen; a migration counts from
+ * srhip_comm_migrate_start to its _wait): the last one, the total, and how many (any may be NULL). */
+int srhip_comm_stats(const srhip_comm* comm, double* ms_last, double* ms_total, int64_t* calls);
+/* In-place all-reduce of a float64 vector: on device memory (complete before the call) in place, no
+ * host staging; a host vector is staged through the communicator's device buffer.  Every exchange
+ * waits at most SRHIP_COMM_TIMEOUT_S seconds (default 300) -- past that, or on an asynchronous RCCL
+ * error, the communicator is aborted and this and every later call on it fail. */
 int srhip_comm_allreduce_f64(srhip_comm* comm, double* buf, int64_t n, int32_t op);
-/* Fixed-size all-gather: recv[r * bytes .. (r + 1) * bytes) = rank r's send. */
+/* Fixed-size all-gather: recv[r * bytes .. (r + 1) * bytes) = rank r's send (both device pointers: no
+ * staging). */
 int srhip_comm_allgather(srhip_comm* comm, const void* send, int64_t bytes, void* recv);
 /* Migration: this rank's k best trees of (nodes, offsets[ntrees+1], losses[ntrees]) -- by loss,
  * non-finite last, ties by index; trees longer than max_nodes skipped -- packed into one fixed-size
@@ -240,8 +247,10 @@ int srhip_comm_migrate_start(srhip_comm* comm, const srhip_node* nodes, const in
 int srhip_comm_migrate_wait(srhip_comm* comm, int32_t* out_counts, int64_t* out_offsets,
                             double* out_losses, srhip_node* out_nodes);
 /* Row-sharded eval_loss: ds holds THIS rank's rows (every rank the same features); runs steps 1-4
- * above with the all-reduces on RCCL; out_loss / out_ok identical on every rank.  With one rank it
- * equals srhip_eval_loss bit for bit. */
+ * above with the all-reduces on RCCL -- the per-tree partials are written by the reduction straight
+ * into the communicator's device buffer and all-reduced there (one group: loss sums, check statistics,
+ * the shard's weight / feature / row totals), then copied to the host once; out_loss / out_ok
+ * identical on every rank.  With one rank it equals srhip_eval_loss bit for bit. */
 int srhip_eval_loss_sharded(srhip_ctx* ctx, srhip_comm* comm, const srhip_dataset* ds,
                             const srhip_program* prog, const srhip_loss* loss, const int64_t* idx,
                             int64_t nidx, double* out_loss, uint8_t* out_ok);

@@ -439,6 +439,31 @@ SRM_FN int srm_jrem_pio2f(float x, double* y) {
   }
   return srm_rem_pio2f_big(xd, y);
 }
+/* The same function in the branch-free pieces the device runs per wave (srhip_eval_impl.h
+ * jtrigf_rows), each proven equal to srm_jtrigf on every float it may see by tools/check_trigf.c:
+ *   tier A, |x| < Float32(pi)/4 (SRM_JPIO4F): no reduction, ONE kernel of xd (sin: the sign of x
+ *     copied onto the result -- the kernel returns |x| itself below sqrt(eps(Float32)), and +0 for -0);
+ *   tier B, |x| <= pi*9/4 (SRM_J9PIO4F, the largest float below it): fn = rint(xd 2/pi) is Julia's
+ *     region index n (0 below Float32(pi)/4, +-1..+-4 above), and fn * (pi/2) rounds to exactly the
+ *     constant Julia subtracts (pi/2, pi, pi*3/2, pi*4/2: scaling by 2 commutes with the rounding),
+ *     so y = xd - fn (pi/2) is Julia's y; both kernels, the quadrant selects (srm_jtrigf_q);
+ *   tier C, |x| < 2^28 pi/2: per row Julia's own choice between that y and its Cody-Waite reduction.
+ * sin(-0) is the only row tier B / C would get wrong (y = +0): the caller keeps x where x == 0. */
+#define SRM_JPIO4F 0.78539819f
+#define SRM_J9PIO4F 7.068583f
+#define SRM_JINV_PIO2 6.36619772367581382433e-01
+#define SRM_JPIO2 1.5707963267948966
+#define SRM_JPIO2_1 1.57079631090164184570e+00  /* first 25 bits of pi/2: fn * pio2_1 is exact */
+#define SRM_JPIO2_1T 1.58932547735281966916e-08
+SRM_FN double srm_jfn(double xd) { return srm_rint(xd * SRM_JINV_PIO2); }
+SRM_FN double srm_jred_near(double xd, double fn) { return xd - fn * SRM_JPIO2; }
+SRM_FN double srm_jred_cw(double xd, double fn) { return (xd - fn * SRM_JPIO2_1) - fn * SRM_JPIO2_1T; }
+/* kind 0: cos, 1: sin of the reduced argument y in quadrant n: both kernels, one select and the sign */
+SRM_FN float srm_jtrigf_q(int kind, int n, double y) {
+  const float fs = (float)srm_jsin_kernel(y), fc = (float)srm_jcos_kernel(y);
+  const float r = ((n & 1) ^ kind) ? fs : fc;
+  return (((n + 1 - kind) >> 1) & 1) ? -r : r;
+}
 /* kind 0: cos, 1: sin (Inf / NaN -> NaN: Julia throws a DomainError for Inf, which the
  * evaluator never reaches -- a non-finite operand fails the tree first) */
 SRM_FN float srm_jtrigf(int kind, float x) {
@@ -456,8 +481,10 @@ SRM_FN float srm_jtrigf(int kind, float x) {
   if (q == 2) return (float)-srm_jcos_kernel(y);
   return (float)srm_jsin_kernel(y);
 }
+/* Julia's kernels are the default (round 5: the minimax moved C2 losses by up to 1.6e-6 relative
+ * against them, oracle/libm_sensitivity.py); -DSRHIP_JULIA_TRIG=0 builds the minimax form */
 #ifndef SRHIP_JULIA_TRIG
-#define SRHIP_JULIA_TRIG 0
+#define SRHIP_JULIA_TRIG 1
 #endif
 #if SRHIP_JULIA_TRIG
 SRM_FN float srm_cosf(float x) { return srm_jtrigf(0, x); }

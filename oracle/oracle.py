@@ -33,6 +33,20 @@ def load():
     return _lib
 
 
+def use_variant(name=None) -> None:
+    """Switch this process's oracle to a libm-sensitivity build (oracle/Makefile `variants`):
+    "jtrig" (Julia's Float32 sin / cos kernels), "glibc64" (glibc Float64 exp / log / sin / cos), or
+    None for the default checker.  oracle/libm_sensitivity.py only -- the parity tests use the default."""
+    global _lib
+    if name is None:
+        _lib = None
+        return
+    path = os.path.join(HERE, "build", f"liboracle_{name}.so")
+    if not os.path.exists(path):
+        subprocess.run(["make", "-C", HERE, "variants"], check=True, capture_output=True)
+    _lib = ctypes.CDLL(path)
+
+
 def _p(a):
     return None if a is None else ctypes.c_void_p(a.ctypes.data)
 

@@ -167,7 +167,21 @@ static float dist_f32(int kind, float d, float p0) {
   }
 }
 
-/* ---------------- Float64 ---------------- */
+/* ---------------- Float64 ----------------
+ * ORACLE_LIBM_GLIBC (the liboracle_glibc64.so variant, oracle/libm_sensitivity.py only): Float64
+ * exp / log / sin / cos from glibc instead of the shared header -- a second near-correctly-rounded
+ * libm, to measure how far a loss moves when only the transcendental algorithm changes. */
+#if ORACLE_LIBM_GLIBC
+#define ORC_EXP64(x) exp(x)
+#define ORC_LOG64(x) log(x)
+#define ORC_SIN64(x) sin(x)
+#define ORC_COS64(x) cos(x)
+#else
+#define ORC_EXP64(x) srm_exp(x)
+#define ORC_LOG64(x) srm_log(x)
+#define ORC_SIN64(x) srm_sin(x)
+#define ORC_COS64(x) srm_cos(x)
+#endif
 static double julia_modf64(double x, double y) {
   const double r = fmod(x, y);
   if (r == 0.0) return copysign(r, y);
@@ -214,11 +228,11 @@ static double un_f64(int op, double x) {
     case SRHIP_OP_CUBE: return x * x * x;
     case SRHIP_OP_ABS: return fabs(x);
     case SRHIP_OP_RELU: return x > 0.0 ? x : copysign(0.0, x);
-    case SRHIP_OP_COS: return srm_cos(x);
-    case SRHIP_OP_SIN: return srm_sin(x);
+    case SRHIP_OP_COS: return ORC_COS64(x);
+    case SRHIP_OP_SIN: return ORC_SIN64(x);
     case SRHIP_OP_TAN: return srm_tan(x);
-    case SRHIP_OP_EXP: return srm_exp(x);
-    case SRHIP_OP_LOG: return x <= 0.0 ? NAN : srm_log(x);
+    case SRHIP_OP_EXP: return ORC_EXP64(x);
+    case SRHIP_OP_LOG: return x <= 0.0 ? NAN : ORC_LOG64(x);
     case SRHIP_OP_LOG2: return x <= 0.0 ? NAN : log2(x);
     case SRHIP_OP_LOG10: return x <= 0.0 ? NAN : log10(x);
     case SRHIP_OP_LOG1P: return x <= -1.0 ? NAN : log1p(x);

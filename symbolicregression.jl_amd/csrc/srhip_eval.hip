@@ -16,7 +16,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab
                                                      const CT* __restrict__ slab_chk, int nrb, int nslots,
                                                      const int32_t* __restrict__ order, LT* __restrict__ out_loss,
                                                      CT* __restrict__ out_chk, const int32_t* __restrict__ slab_rows,
-                                                     int64_t* __restrict__ out_rows, UndecidedList ul) {
+                                                     int64_t* __restrict__ out_rows, UndecidedList ul, int chk_inf) {
   const int lane = threadIdx.x & 63;
   const int slot = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (slot >= nslots) return;
@@ -62,7 +62,9 @@ __global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab
   if (lane == 0) {
     const int tree = order[slot];
     if (out_loss) out_loss[tree] = s;
-    if (out_chk) out_chk[tree] = m;
+    // chk_inf (row shards): a non-finite statistic is stored as +Inf, which RCCL's MAX / SUM across the
+    // shards keep (a max that drops NaN operands would lose a failed shard)
+    if (out_chk) out_chk[tree] = chk_inf && !__builtin_isfinite((double)m) ? CT(INFINITY) : m;
     if (out_rows) out_rows[tree] = rows;
     if (ul.ulist && out_chk) {
       bool und;
@@ -241,23 +243,23 @@ hipError_t launch_precise_reduce(const double* slab, int nrb, int stride, int32_
 
 hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, int cpb, const void* slab_chk, int nrb, int nslots,
                          const int32_t* order, void* out_loss, void* out_chk, hipStream_t s, const int32_t* slab_rows,
-                         int64_t* out_rows, const UndecidedList& ul) {
+                         int64_t* out_rows, const UndecidedList& ul, bool chk_inf) {
   dim3 grid((nslots + 3) / 4), block(256);
   switch (dtype) {
     case SRHIP_F32:
       hipLaunchKernelGGL((reduce_kernel<double, float, true>), grid, block, 0, s, (const double*)slab_loss, nch, cpb,
                          (const float*)slab_chk, nrb, nslots, order, (double*)out_loss, (float*)out_chk, slab_rows,
-                         out_rows, ul);
+                         out_rows, ul, (int)chk_inf);
       break;
     case SRHIP_F64:
       hipLaunchKernelGGL((reduce_kernel<double, double, false>), grid, block, 0, s, (const double*)slab_loss, nch, cpb,
                          (const double*)slab_chk, nrb, nslots, order, (double*)out_loss, (double*)out_chk, slab_rows,
-                         out_rows, ul);
+                         out_rows, ul, (int)chk_inf);
       break;
     case SRHIP_I32:
       hipLaunchKernelGGL((reduce_kernel<long long, float, true>), grid, block, 0, s, (const long long*)slab_loss, nch,
                          cpb, (const float*)nullptr, nrb, nslots, order, (long long*)out_loss, (float*)nullptr,
-                         slab_rows, out_rows, UndecidedList());
+                         slab_rows, out_rows, UndecidedList(), 0);
       break;
     default: return hipErrorInvalidValue;
   }

@@ -360,6 +360,78 @@ template <int R> __device__ __attribute__((always_inline)) inline bool trigf_row
   return __builtin_amdgcn_ballot_w64(!(mx < SRM_PIO2F_BIG_F)) == 0;  // false for NaN
 }
 
+// ---- Julia's own Float32 cos / sin (the default: SRHIP_JULIA_TRIG, include/srhip_math.h) -----------
+// Julia evaluates sin(x::Float32) / cos(x::Float32) by quadrant with two different Float64 kernels
+// (FreeBSD __kernel_sindf / __kernel_cosdf) after its rem_pio2_kernel, whose reduction itself changes
+// with |x|.  Per row that is a case analysis a SIMD lane would pay in full, so the handler classifies
+// the WAVE by its largest |x| (one NaN-propagating max per row pair and up to three ballots) and runs
+// one of four branch-free leaf bodies, each proven equal to srm_jtrigf on every float it may see
+// (tools/check_trigf.c, all 2^32 inputs):
+//   A  every |x| < Float32(pi)/4: no reduction, ONE kernel (sin: the sign of x copied onto it);
+//   B  every |x| <= pi*9/4: fn = rint(xd 2/pi), y = xd - fn (pi/2) (Julia's +-k pi/2 cases, one
+//      rounding), both kernels, the quadrant picks one and its sign;
+//   C  every |x| < 2^28 pi/2: per row Julia's choice between that y and its Cody-Waite reduction;
+//   slow  any larger / Inf / NaN row: C for the rest, the scalar srm_jtrigf (Payne-Hanek) for those.
+// C2's cos-of-operator tiles fall 11 % / 47 % / 36 % / 6 % into A / B / C / slow
+// (scripts/trig_arg_tiers.py).
+template <int KIND>
+__device__ __attribute__((always_inline)) inline float jtrigf_q_dev(double fn, double y) {
+  const int n = cvt_i32_sat(fn);
+  const float fs = (float)srm_jsin_kernel(y), fc = (float)srm_jcos_kernel(y);
+  const float r = ((n & 1) ^ KIND) ? fs : fc;
+  // the sign: bit 1 of n + 1 - KIND (cos: quadrants 1, 2; sin: 2, 3), added into bit 31 (the xor)
+  uint32_t o;
+  asm("v_lshl_add_u32 %0, %1, 31, %2" : "=v"(o) : "v"((n + 1 - KIND) >> 1), "v"(__builtin_bit_cast(uint32_t, r)));
+  return __builtin_bit_cast(float, o);
+}
+template <int R, int KIND>
+__device__ __attribute__((noinline)) RV<float, R> jtrigf_a(RV<float, R> v) {
+  UNR for (int r = 0; r < R; ++r) {
+    const float x = v[r];
+    if constexpr (KIND == 0) {
+      v[r] = (float)srm_jcos_kernel((double)x);
+    } else {
+      v[r] = __builtin_copysignf((float)srm_jsin_kernel((double)x), x);
+    }
+    if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
+  }
+  return v;
+}
+template <int KIND, bool CW>
+__device__ __attribute__((always_inline)) inline float jtrigf_row(float x) {
+  const double xd = (double)x, fn = srm_jfn(xd);
+  double y = srm_jred_near(xd, fn);
+  if constexpr (CW) y = __builtin_fabsf(x) <= SRM_J9PIO4F ? y : srm_jred_cw(xd, fn);
+  const float r = jtrigf_q_dev<KIND>(fn, y);
+  return (KIND == 1 && x == 0.0f) ? x : r;  // sin(-0) = -0 (the reduction gives +0)
+}
+template <int R, int KIND, bool CW>
+__device__ __attribute__((noinline)) RV<float, R> jtrigf_bc(RV<float, R> v) {
+  UNR for (int r = 0; r < R; ++r) {
+    v[r] = jtrigf_row<KIND, CW>(v[r]);
+    if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
+  }
+  return v;
+}
+template <int R, int KIND>
+__device__ __attribute__((noinline)) RV<float, R> jtrigf_slow(RV<float, R> v) {
+  UNR for (int r = 0; r < R; ++r) {
+    const float x = v[r];
+    v[r] = __builtin_fabsf(x) < SRM_PIO2F_BIG_F ? jtrigf_row<KIND, true>(x) : srm_jtrigf(KIND, x);
+  }
+  return v;
+}
+template <int R, int KIND>
+__device__ __attribute__((always_inline)) inline RV<float, R> jtrigf_rows(const RV<float, R>& A) {
+  RV<float, R> v;
+  UNR for (int r = 0; r < R; ++r) v[r] = A[r];
+  const float mx = abs_fold<R, true>(0.0f, A);  // NaN-propagating: a NaN row fails every test below
+  if (__builtin_amdgcn_ballot_w64(!(mx < SRM_JPIO4F)) == 0) return jtrigf_a<R, KIND>(v);
+  if (__builtin_amdgcn_ballot_w64(!(mx <= SRM_J9PIO4F)) == 0) return jtrigf_bc<R, KIND, false>(v);
+  if (__builtin_amdgcn_ballot_w64(!(mx < SRM_PIO2F_BIG_F)) == 0) return jtrigf_bc<R, KIND, true>(v);
+  return jtrigf_slow<R, KIND>(v);
+}
+
 template <int R, int KIND>
 __device__ __attribute__((always_inline)) inline RV<float, R> trigf_rows(RV<float, R> v) {
   RV<float, R> res;
@@ -378,6 +450,8 @@ __device__ __attribute__((always_inline)) inline RV<float, R> trigf_rows(RV<floa
       if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
     }
     if (big) res = trigf_fix_tan<R>(v, res);
+  } else if constexpr (SRHIP_JULIA_TRIG) {
+    res = jtrigf_rows<R, KIND>(v);
   } else {
     static_assert(R % 2 == 0, "row pairs");
     const float mx = abs_fold<R, true>(0.0f, v);
@@ -456,8 +530,12 @@ __device__ __attribute__((always_inline)) inline void apply_un(RV<T, R>& A) {
   if constexpr (SRHIP_TRIG_ROWS && std::is_same<T, float>::value && (U == UN_COS || U == UN_SIN) && R % 2 == 0) {
     constexpr int KIND = U == UN_COS ? 0 : 1;
     RV<T, R> v;
-    UNR for (int r = 0; r < R; ++r) v[r] = A[r];
-    v = trigf_rows_fast<R>(A) ? trigf_fast<R, KIND>(v) : trigf_slow<R, KIND>(v);
+    if constexpr (SRHIP_JULIA_TRIG) {
+      v = jtrigf_rows<R, KIND>(A);
+    } else {
+      UNR for (int r = 0; r < R; ++r) v[r] = A[r];
+      v = trigf_rows_fast<R>(A) ? trigf_fast<R, KIND>(v) : trigf_slow<R, KIND>(v);
+    }
     UNR for (int r = 0; r < R; ++r) A[r] = v[r];
   } else if constexpr (un_inline<U>()) {
     using O = OpsT<T>;

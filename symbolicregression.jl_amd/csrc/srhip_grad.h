@@ -45,6 +45,8 @@ struct GradArgs {
   int32_t inl[2 * 96];
 };
 constexpr int GRAD_INLINE = 96;  // (448 measured the same on C4)
+// a chunk is a (tree, c0) pair: the inline list holds GRAD_INLINE of them
+static_assert(2 * GRAD_INLINE == sizeof(GradArgs::inl) / sizeof(int32_t), "inline chunk list size");
 static_assert(sizeof(GradArgs) <= 4096, "kernel arguments are limited to 4 KB");
 
 // kt = tangent components per chunk: 4 or GRAD_KT (the slab / reduced layout stride is kt + 2)

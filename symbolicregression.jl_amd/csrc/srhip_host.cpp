@@ -1635,8 +1635,20 @@ struct DevPrecise {
 // (sums layout above; chk[T]) and, in MODE_PRED, out_pred.  dp (nullable): also the device-decided
 // precise pass (multi-block launches; single-block launches finish inside the interpreter and leave
 // the precise pass to the caller).
+// Row shards (run_eval_sharded): the reduction writes each tree's loss sum and check statistic into the
+// exchange's device buffer instead of host memory (sums[2t] / chk stay to be filled from the all-reduced
+// buffer); the rows each tree was evaluated on come back for the caller's lost-block check.
+struct ShardDev {
+  void* d_loss = nullptr;
+  void* d_chk = nullptr;
+  size_t zero_bytes = 0;  // [loss | chk] cleared before the launch (static-fail trees are never written)
+  std::vector<int64_t> rows;
+  bool persistent = false;
+};
+
 static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
-                         const View& v, void* out_pred, double* sums, double* chk, DevPrecise* dp = nullptr) {
+                         const View& v, void* out_pred, double* sums, double* chk, DevPrecise* dp = nullptr,
+                         ShardDev* sd = nullptr) {
   const int dtype = P->dtype;
   const int32_t nt = P->ntrees;
   const int64_t nf = ds->nfeat;
@@ -1819,7 +1831,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   // one row block: the waves finish the per-tree reduction themselves (SRHIP_NO_FUSED_REDUCE=1: the
   // reduce kernel instead; read per launch)
   const char* nofuse = env_get("SRHIP_NO_FUSED_REDUCE");
-  if (L.nrb == 1 && !(nofuse && *nofuse && *nofuse != '0')) {
+  if (L.nrb == 1 && !sd && !(nofuse && *nofuse && *nofuse != '0')) {
     a.fused = 1;
     a.fused_loss = mode == MODE_LOSS ? ctx->h_loss.p : nullptr;
     a.fused_chk = dtype == SRHIP_I32 ? nullptr : ctx->h_chk.p;
@@ -1844,11 +1856,16 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     a.out_pred = pred.p;
   }
   dim3 grid(L.nrb, (unsigned)goff.size() - 1);
-  if (persistent && !ctx->block_ctr.p) {
-    // zeroed once: every persistent launch leaves it at zero (its last claim resets it)
+  if (persistent && (!ctx->block_ctr.p || ctx->block_ctr_dirty)) {
+    // zeroed once: every persistent launch that drains its claims leaves it at zero (its last claim
+    // resets it); again after a launch that was never seen to complete (an error return between the
+    // launch and its synchronisation, or a lost row block below)
     HIP_TRY(ctx->block_ctr.ensure(sizeof(int32_t)));
     HIP_TRY(hipMemsetAsync(ctx->block_ctr.p, 0, sizeof(int32_t), ctx->stream));
+    ctx->block_ctr_dirty = false;
   }
+  if (persistent) ctx->block_ctr_dirty = true;  // until the launch is seen to have drained
+  if (sd) HIP_TRY(hipMemsetAsync(sd->d_loss, 0, sd->zero_bytes, ctx->stream));
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
   if (persistent) {
     if (probe_blocks > 0) {
@@ -1943,8 +1960,9 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   if (!a.fused)
     HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, nch, cpb,
                           dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p, L.nrb, nl, (const int32_t*)d_order,
-                          mode == MODE_LOSS ? ctx->h_loss.p : nullptr, dtype == SRHIP_I32 ? nullptr : ctx->h_chk.p,
-                          ctx->stream, a.slab_rows, (int64_t*)ctx->h_rows.p, ul));
+                          mode == MODE_LOSS ? (sd ? sd->d_loss : ctx->h_loss.p) : nullptr,
+                          dtype == SRHIP_I32 ? nullptr : (sd ? sd->d_chk : ctx->h_chk.p), ctx->stream, a.slab_rows,
+                          (int64_t*)ctx->h_rows.p, ul, sd != nullptr));
   if (devp) {
     // the precise pass over the device's list (capped; its launch reads the count): the plain program,
     // K_MAX, global reads -- eval_precise's launch with the list as the tree order
@@ -2009,11 +2027,28 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   if (mode == MODE_LOSS) memcpy(r_loss.data(), ctx->h_loss.p, (size_t)nt * 8);
   if (dtype != SRHIP_I32) memcpy(r_chk.data(), ctx->h_chk.p, (size_t)nt * (dtype == SRHIP_F32 ? 4 : 8));
   memcpy(r_rows.data(), ctx->h_rows.p, (size_t)nt * 8);
+  if (sd) {
+    sd->rows.assign(nt, 0);
+    for (int32_t t : live) sd->rows[t] = ((const int64_t*)r_rows.data())[t];
+    sd->persistent = persistent;
+  }
   for (int32_t t : live) {
+    if (sd) break;  // the shard's loss sums and statistics are in the exchange's device buffer
     if (mode == MODE_LOSS)
       sums[2 * (size_t)t] = dtype == SRHIP_I32 ? (double)((const long long*)r_loss.data())[t] : ((const double*)r_loss.data())[t];
     if (dtype == SRHIP_F32) chk[t] = ((const float*)r_chk.data())[t];
     else if (dtype == SRHIP_F64) chk[t] = ((const double*)r_chk.data())[t];
+  }
+  if (persistent && !sd) {  // (row shards: checked by the caller against the all-reduced statistic)
+    // every row block was claimed exactly once: a tree that did not fail was evaluated on every row
+    // (a counter left non-zero by an earlier launch would make this launch skip blocks silently)
+    for (int32_t t : live) {
+      const int64_t rows = ((const int64_t*)r_rows.data())[t];
+      if (rows != v.m && std::isfinite(chk[t]))
+        return fail(SRHIP_ERR_DEVICE, "persistent launch evaluated tree %d on %lld of %lld rows (row-block counter "
+                    "not at zero); the counter is reset for the next launch", t, (long long)rows, (long long)v.m);
+    }
+    ctx->block_ctr_dirty = false;
   }
   // the launch's work, counted on the device (rows each tree was evaluated on)
   for (int i = 0; i < 4; ++i) ctx->work[i] = 0;
@@ -2202,14 +2237,15 @@ int srhip::run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program
   return SRHIP_OK;
 }
 
-// Row-sharded evaluation (srhip_eval_loss_sharded): this shard's partials, ONE all-reduce of
-// [sums | chk] (sums by SUM, chk by MAX for Float32 / SUM otherwise; a non-finite statistic travels
-// as +Inf), the decision every rank takes identically, and for the undecided trees a precise pass
-// over this shard with a SUM all-reduce of its per-operator sums.  The reductions are the caller's
-// (srhip_comm.cpp: RCCL on the device); nfeat_total is the dataset's feature count on every rank.
+// Row-sharded evaluation (srhip_eval_loss_sharded): this shard's partials written by the reduction
+// into the exchange's device buffer [loss | chk | aux], ONE all-reduce group of it in place (loss sums
+// SUM, chk MAX for Float32 / SUM otherwise -- a non-finite statistic stored as +Inf -- and the aux
+// entries SUM: the weight sum, the feature statistics, the row count), one copy to the host, and the
+// decision every rank takes identically from the same reduced values; for undecided trees a precise pass
+// over this shard with a SUM all-reduce of its per-operator sums.  The exchanges are the caller's
+// (srhip_comm.cpp: RCCL on the device); nfeat is the dataset's feature count on every rank.
 int srhip::run_eval_sharded(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const srhip_loss* loss,
-                            const int64_t* idx, int64_t nidx, const ShardReduce& reduce, double* out_loss,
-                            uint8_t* out_ok) {
+                            const int64_t* idx, int64_t nidx, const ShardIO& io, double* out_loss, uint8_t* out_ok) {
   int rc = check_eval_args(ctx, ds, P, MODE_LOSS, loss);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
@@ -2221,30 +2257,63 @@ int srhip::run_eval_sharded(srhip_ctx* ctx, const srhip_dataset* ds, const srhip
     if (rc) return rc;
   }
   const int32_t nt = P->ntrees;
-  const size_t ns = sums_len(nt, ds->nfeat);
-  // [sums | chk] in one buffer: the all-reduce sees one message
-  std::vector<double> buf(ns + (size_t)nt, 0.0);
-  double* sums = buf.data();
-  double* chk = buf.data() + ns;
-  rc = eval_partials(ctx, ds, P, MODE_LOSS, loss, v, nullptr, sums, chk);
+  if (nt == 0) return SRHIP_OK;
+  const int64_t nf = ds->nfeat;
+  const size_t ns = sums_len(nt, nf);
+  ShardLayout SL;
+  SL.dtype = P->dtype;
+  SL.nt = (size_t)nt;
+  SL.naux = 2 + 2 * (size_t)nf;  // [weight sum | feature stats (2F) | rows]
+  void* dbuf = nullptr;
+  rc = io.buffer(SL.bytes(), &dbuf);
   if (rc) return rc;
-  for (int32_t t = 0; t < nt; ++t)
-    if (!std::isfinite(chk[t])) chk[t] = INFINITY;
-  rc = reduce(buf.data(), ns, (size_t)nt, P->dtype == SRHIP_F32);
+  ShardDev sd;
+  sd.d_loss = dbuf;
+  sd.d_chk = (uint8_t*)dbuf + SL.chk_off();
+  sd.zero_bytes = SL.chk_off() + SL.nt * SL.chk_size();
+  std::vector<double> sums(ns, 0.0), chk(nt, 0.0);
+  rc = eval_partials(ctx, ds, P, MODE_LOSS, loss, v, nullptr, sums.data(), chk.data(), nullptr, &sd);
   if (rc) return rc;
+  // the host-known entries (the same for every tree): weight sum, feature statistics, rows
+  std::vector<double> aux(SL.naux);
+  aux[0] = sums[1];
+  for (size_t i = 0; i < 2 * (size_t)nf + 1; ++i) aux[1 + i] = sums[2 * (size_t)nt + i];
+  const void* red = nullptr;
+  rc = io.reduce(SL, aux.data(), &red);
+  if (rc) return rc;
+  const uint8_t* rb = (const uint8_t*)red;
+  const double* raux = (const double*)(rb + SL.aux_off());
+  for (int32_t t = 0; t < nt; ++t) {
+    sums[2 * (size_t)t] = P->dtype == SRHIP_I32 ? (double)((const long long*)rb)[t] : ((const double*)rb)[t];
+    sums[2 * (size_t)t + 1] = raux[0];
+    if (P->dtype == SRHIP_F32) chk[t] = ((const float*)(rb + SL.chk_off()))[t];
+    else if (P->dtype == SRHIP_F64) chk[t] = ((const double*)(rb + SL.chk_off()))[t];
+  }
+  for (size_t i = 0; i < 2 * (size_t)nf + 1; ++i) sums[2 * (size_t)nt + i] = raux[1 + i];
+  if (sd.persistent) {
+    // this shard's persistent launch claimed every row block: a tree no shard failed was evaluated on all
+    // of this shard's rows
+    for (int32_t t = 0; t < nt; ++t)
+      if (!P->info[t].static_fail && sd.rows[t] != v.m && std::isfinite(chk[t]))
+        return fail(SRHIP_ERR_DEVICE, "persistent launch evaluated tree %d on %lld of %lld rows (row-block counter "
+                    "not at zero); the counter is reset for the next launch", t, (long long)sd.rows[t], (long long)v.m);
+    ctx->block_ctr_dirty = false;
+  }
   std::vector<uint8_t> status(nt), ok(nt);
   std::vector<double> lossv(nt);
-  finalize(*P, ds->nfeat, sums, chk, lossv.data(), ok.data(), status.data());
+  finalize(*P, nf, sums.data(), chk.data(), lossv.data(), ok.data(), status.data());
   std::vector<int32_t> unc;
   for (int32_t t = 0; t < nt; ++t)
     if (status[t] == 2) unc.push_back(t);
-  // every rank took the same decision from the same reduced partials: the undecided set agrees
+  // every rank took the same decision from the same reduced partials: the undecided set agrees, and so
+  // does whether the second exchange happens.  (The single-device path lists undecided trees on the
+  // device; here the list depends on the all-reduced statistic, which the host already holds.)
   if (!unc.empty()) {
     const int stride = std::max(1, P->max_ops);
     std::vector<double> opsums(unc.size() * stride);
     rc = eval_precise(ctx, ds, P, v, unc.data(), (int32_t)unc.size(), opsums.data());
     if (rc) return rc;
-    rc = reduce(opsums.data(), opsums.size(), 0, false);
+    rc = io.reduce_host(opsums.data(), opsums.size());
     if (rc) return rc;
     std::vector<uint8_t> uok(unc.size());
     finalize_precise(*P, unc.data(), (int32_t)unc.size(), opsums.data(), uok.data());

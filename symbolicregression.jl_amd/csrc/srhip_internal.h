@@ -133,7 +133,11 @@ struct srhip_ctx {
   srhip::HostBuf h_loss, h_chk, h_stats, h_prec, h_dbg;
   srhip::DevBuf fail_flag;  // [order slots] int32: launch epoch in which the tree was seen to fail
   int32_t epoch = 0;        // interpreter launches so far (MODE_LOSS with early exit)
-  srhip::DevBuf block_ctr;  // persistent launches: the row-block counter (one int32, zeroed per launch)
+  // persistent launches: the row-block counter (one int32).  Zeroed once; every launch that drains its
+  // claims leaves it at zero (the last claim stores 0).  block_ctr_dirty: a launch was issued and not
+  // yet seen to drain (error return in between, or lost blocks) -- the next launch zeroes it first
+  srhip::DevBuf block_ctr;
+  bool block_ctr_dirty = false;
   srhip::DevBuf slab_rows;  // [row block][order slot] valid rows evaluated
   srhip::HostBuf h_rows;    // [program trees] int64 rows evaluated per tree (coherent pinned)
   srhip::DevBuf d_ulist;    // the device's undecided-tree list ([0] = count; reset by its consumer)
@@ -282,10 +286,28 @@ int run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, in
 int precise_decide(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const View& v,
                    const int32_t* trees, int32_t nu, bool grad, uint8_t* out_ok);
 
-// Row-sharded evaluation with caller-supplied reductions: reduce(buf, nsum, nchk, chk_max) combines
-// buf[0, nsum) by SUM and buf[nsum, nsum + nchk) by MAX (chk_max) or SUM across the shards, in place;
-// returns an SRHIP status.
-using ShardReduce = std::function<int(double* buf, size_t nsum, size_t nchk, bool chk_max)>;
+// Row-sharded evaluation with caller-supplied exchanges (srhip_comm.cpp: RCCL).  The per-tree partials
+// stay in device memory: the evaluation's reduction kernel writes them into the exchange's own device
+// buffer, laid out [loss | chk | aux] (ShardLayout), which is all-reduced in place and copied to the
+// host once.  Every callback returns an SRHIP status.
+struct ShardLayout {
+  int dtype = 0;
+  size_t nt = 0, naux = 0;
+  size_t loss_bytes() const { return nt * 8; }  // f64 sums (Int32 data: int64 sums), SUM
+  size_t chk_size() const { return dtype == SRHIP_F64 ? 8 : (dtype == SRHIP_F32 ? 4 : 0); }  // f32 MAX / f64 SUM
+  size_t chk_off() const { return loss_bytes(); }
+  size_t aux_off() const { return (chk_off() + nt * chk_size() + 7) & ~(size_t)7; }  // f64, SUM
+  size_t bytes() const { return aux_off() + naux * 8; }
+};
+struct ShardIO {
+  // the device buffer (>= bytes) the reduction writes [loss | chk] into
+  std::function<int(size_t bytes, void** dptr)> buffer;
+  // after the evaluation completed: aux (host) copied behind [loss | chk], the three segments all-reduced
+  // in place as one group, the whole buffer copied into host memory; *out points at that copy
+  std::function<int(const ShardLayout& L, const double* aux, const void** out)> reduce;
+  // plain f64 SUM of a host array in place (the precise pass's per-operator sums of undecided trees)
+  std::function<int(double* buf, size_t n)> reduce_host;
+};
 // getenv through a per-thread cache that is dropped whenever the environment changes (srhip_host.cpp)
 const char* env_get(const char* name);
 // Wait for the context's stream: hipStreamSynchronize, or with SRHIP_SYNC_SPIN=1 a spin on a
@@ -294,6 +316,6 @@ const char* env_get(const char* name);
 // 1.63 -> 1.95 ms), so blocking is the default.
 int stream_wait(srhip_ctx* ctx);
 int run_eval_sharded(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const srhip_loss* loss,
-                     const int64_t* idx, int64_t nidx, const ShardReduce& reduce, double* out_loss, uint8_t* out_ok);
+                     const int64_t* idx, int64_t nidx, const ShardIO& io, double* out_loss, uint8_t* out_ok);
 
 }  // namespace srhip

@@ -245,10 +245,10 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     // kernel, which has read its chunk list
     HIP_TRY(ctx->h_gred[pi].ensure((size_t)nch * (ps.kt + 2) * sizeof(double), hipHostMallocCoherent));
     GradArgs a{};
-    static const int inline_max = [] {
-      const char* e = getenv("SRHIP_GRAD_INLINE_MAX");  // 0: always copy the list
-      return e ? std::max(0, std::min(atoi(e), GRAD_INLINE)) : GRAD_INLINE;
-    }();
+    // SRHIP_GRAD_INLINE_MAX (0: always copy the list), read per pass through the environment cache
+    // so a test can compare both forms in one process
+    const char* ie = env_get("SRHIP_GRAD_INLINE_MAX");
+    const int inline_max = ie && *ie ? std::max(0, std::min(atoi(ie), GRAD_INLINE)) : GRAD_INLINE;
     const bool inl = nch <= inline_max;
     if (inl) {  // in the kernel arguments
       memcpy(a.inl, ps.chunks.data(), ps.chunks.size() * sizeof(int32_t));

@@ -117,6 +117,8 @@ SIGNATURES = {
     "srhip_comm_create": (ctypes.c_int, [_vp, _vp, _i32, _i32, ctypes.POINTER(_vp)]),
     "srhip_comm_destroy": (None, [_vp]),
     "srhip_comm_size": (ctypes.c_int, [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+    "srhip_comm_stats": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_int64)]),
     "srhip_comm_allreduce_f64": (ctypes.c_int, [_vp, _vp, _i64, _i32]),
     "srhip_comm_allgather": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
     "srhip_comm_migrate_start": (ctypes.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _i32]),

@@ -235,6 +235,123 @@ def exchange_members(trees, scores, losses, options, dtype, group=None):
     return out
 
 
+class IterationExchange:
+    """The island search's whole per-iteration exchange as ONE fixed-size all-gather (src/Migration.jl:16-38
+    fed from every rank as the reference's head node sees every population's best_sub_pop and the hall of
+    fame, src/SymbolicRegression.jl:910-943; the adaptive-parsimony size counts of
+    src/SearchUtils.jl RunningSearchStatistics ride along).  Each rank sends one payload
+
+        [nsub, nmembers | offsets (cap + 1) | scores (cap) | losses (cap) | counts (nbin) | node pool]
+
+    of a size every rank computes from the options alone (cap = the most best_sub_pops members a rank
+    can hold + one frontier member per complexity; the node pool cap x (maxsize + 1) records), so no
+    size round precedes it.  On the nccl backend with ranks on distinct GPUs it travels through
+    libsrhip's RCCL communicator (NativeComm.allgather: device buffers, no torch tensors); otherwise
+    through one torch.distributed all_gather_into_tensor (gloo CPU tests, one-GPU rehearsals); with
+    neither (world size 1, no process group) it is the identity."""
+
+    def __init__(self, cap: int, pool_nodes: int, nbin: int, comm=None, group=None, world: int = 1):
+        self.cap, self.pool, self.nbin = int(cap), int(pool_nodes), int(nbin)
+        self.comm, self.group, self.world = comm, group, int(world)
+        self.head = 8 * (2 + (self.cap + 1) + 2 * self.cap + self.nbin)
+        self.size = self.head + self.pool * NODE_DTYPE.itemsize
+
+    @classmethod
+    def for_search(cls, options, npops: int, world: int, topn: int, nbin: int, make_ctx=None, group=None,
+                   native: bool = True):
+        """The search's exchange: its capacity from the options; NativeComm (on make_ctx()'s device) when
+        native and the process group is nccl -- or no process group exists: world 1 through the library
+        -- torch otherwise (SRHIP_SEARCH_COMM=torch forces it)."""
+        import os
+        import sys
+
+        per_rank = -(-int(npops) // max(1, int(world)))
+        maxsize = int(options.maxsize)
+        cap = per_rank * int(topn) + maxsize
+        comm = None
+        use_native = native and make_ctx is not None and os.environ.get("SRHIP_SEARCH_COMM", "native") == "native"
+        initialised = "torch" in sys.modules and _dist().is_available() and _dist().is_initialized()
+        if use_native and (not initialised or _dist().get_backend(group) == "nccl"):
+            ctx = make_ctx()
+            comm = NativeComm.from_process_group(ctx, group) if initialised else \
+                NativeComm(ctx, 1, 0, NativeComm.unique_id())
+        return cls(cap, cap * (maxsize + 1), nbin, comm, group, world)
+
+    def pack(self, trees, scores, losses, nsub: int, counts, options, dtype) -> np.ndarray:
+        from .node import flatten
+
+        n = len(trees)
+        if n > self.cap:
+            raise ValueError(f"{n} members exceed the exchange's capacity {self.cap}")
+        nodes, offs = flatten(trees, options, dtype) if n else (np.zeros(0, NODE_DTYPE), np.zeros(1, np.int64))
+        if len(nodes) > self.pool:
+            raise ValueError(f"{len(nodes)} nodes exceed the exchange's node pool {self.pool}")
+        buf = np.zeros(self.size, dtype=np.uint8)
+        h = buf[:self.head].view(np.float64)
+        hi = buf[:self.head].view(np.int64)
+        c = self.cap
+        hi[0], hi[1] = int(nsub), n
+        hi[2:2 + n + 1] = offs
+        h[3 + c:3 + c + n] = np.asarray(scores, dtype=np.float64)
+        h[3 + 2 * c:3 + 2 * c + n] = np.asarray(losses, dtype=np.float64)
+        h[3 + 3 * c:3 + 3 * c + self.nbin] = np.asarray(counts, dtype=np.float64)
+        buf[self.head:self.head + len(nodes) * NODE_DTYPE.itemsize] = np.ascontiguousarray(nodes).view(np.uint8)
+        return buf
+
+    def unpack(self, buf, options):
+        """-> (nsub, [(tree, score, loss)], counts)"""
+        from .node import unflatten
+
+        buf = np.asarray(buf, dtype=np.uint8)
+        h = buf[:self.head].view(np.float64)
+        hi = buf[:self.head].view(np.int64)
+        c = self.cap
+        nsub, n = int(hi[0]), int(hi[1])
+        offs = hi[2:2 + n + 1].copy()
+        scores, losses = h[3 + c:3 + c + n], h[3 + 2 * c:3 + 2 * c + n]
+        counts = h[3 + 3 * c:3 + 3 * c + self.nbin].copy()
+        nodes = buf[self.head:self.head + int(offs[-1]) * NODE_DTYPE.itemsize].copy().view(NODE_DTYPE)
+        trees = unflatten(nodes, offs, options) if n else []
+        return nsub, [(t, float(scores[i]), float(losses[i])) for i, t in enumerate(trees)], counts
+
+    def exchange(self, trees, scores, losses, nsub: int, counts, options, dtype):
+        """Every rank's (nsub, members, counts), in rank order."""
+        import time
+
+        t0 = time.perf_counter()
+        payload = self.pack(trees, scores, losses, nsub, counts, options, dtype)
+        if self.comm is not None:
+            parts = self.comm.allgather(payload.tobytes())
+            parts = [np.frombuffer(p, dtype=np.uint8) for p in parts]
+        elif self.world > 1:
+            import torch
+
+            dist = _dist()
+            dev = _device(self.group)
+            host_in, src = _staging(self.size, torch.uint8, dev, "iter_in")
+            host_in.numpy()[:] = payload
+            if src is not host_in:
+                src.copy_(host_in, non_blocking=True)
+            host_out, dst = _staging(self.world * self.size, torch.uint8, dev, "iter_out")
+            dist.all_gather_into_tensor(dst, src, group=self.group)
+            if host_out is not dst:
+                host_out.copy_(dst, non_blocking=True)
+                torch.cuda.current_stream(dev).synchronize()
+            allb = host_out.numpy().reshape(self.world, self.size)
+            parts = [allb[r] for r in range(self.world)]
+        else:
+            parts = [payload]
+        out = [self.unpack(p, options) for p in parts]
+        timer.seconds += time.perf_counter() - t0
+        timer.calls += 1
+        return out
+
+    def close(self):
+        if self.comm is not None:
+            self.comm.close()
+            self.comm = None
+
+
 class _Pending:
     """An in-flight migrate_topk exchange (migrate_topk_async): wait() -> [(nodes, offsets, losses)]."""
 
@@ -463,6 +580,18 @@ class NativeComm:
         timer.seconds += time.perf_counter() - t0
         timer.calls += 1
         return out, ok.astype(bool)
+
+    def stats(self):
+        """(ms of the last exchange, ms in all exchanges, exchanges) -- host wall time, issue to completion
+        seen (srhip_comm_stats)."""
+        import ctypes
+
+        from . import _lib
+
+        last, total, calls = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+        _lib.check(_lib.load().srhip_comm_stats(self.handle, ctypes.byref(last), ctypes.byref(total),
+                                                ctypes.byref(calls)))
+        return last.value, total.value, calls.value
 
     def close(self):
         from . import _lib

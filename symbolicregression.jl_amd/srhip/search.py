@@ -873,7 +873,8 @@ def equation_search(X, y, options, niterations: int = 10, weights=None, seed=Non
     rank, ws = parallel.world()
     if distributed is False:
         rank, ws = 0, 1
-    dist_mode = ws > 1
+    # distributed=True at world size 1: the same lock-step protocol through the exchange (tests)
+    dist_mode = ws > 1 or distributed is True
     det = bool(options.deterministic) or dist_mode
     base_seed = options.seed if seed is None else seed
     ss = np.random.SeedSequence(base_seed)
@@ -890,7 +891,7 @@ def equation_search(X, y, options, niterations: int = 10, weights=None, seed=Non
         import os
 
         options.device = int(os.environ.get("LOCAL_RANK", options.device))
-    pool = mpx = None
+    pool = mpx = xchg = None
     if own_scorer:
         update_baseline_loss(dataset, options)
         scorer = DeviceScorer(dataset, options, nclients=len(local))
@@ -927,6 +928,14 @@ def equation_search(X, y, options, niterations: int = 10, weights=None, seed=Non
         curmaxsize = get_cur_maxsize(options, total_cycles, cycles_remaining)
         num_evals = float(len(local) * psize)
         topn = search_option(options, "topn")
+        if dist_mode and xchg is None:
+            from . import device as _device_mod
+
+            # libsrhip's communicator when the search runs on the device (its own scorer or device workers)
+            on_device = own_scorer or (mp_mode and worker_backend == "srhip")
+            xchg = parallel.IterationExchange.for_search(
+                options, npops, ws, topn, len(stats.frequencies), lambda: _device_mod.get_context(options.device),
+                group, native=on_device)
 
         def process(k, pop, best_seen):
             nonlocal cycles_remaining, curmaxsize, num_evals
@@ -961,23 +970,21 @@ def equation_search(X, y, options, niterations: int = 10, weights=None, seed=Non
                 hof.update(pop, options)
                 hof.update([m for m, e in zip(best_seen.members, best_seen.exists) if e], options)
                 pops[k] = pop
-            stats.frequencies += parallel.allreduce_np(counts, "sum", group)
-            stats.move_window()
             mine = [m for k in local for m in best_sub_pops[k]]
             front = hof.pareto_frontier()
-            nsub = len(mine)
             sent = mine + front
-            got = parallel.exchange_members([m.tree for m in sent], [m.score for m in sent],
-                                            [m.loss for m in sent], options, dtype, group)
-            # every rank's contribution = its best_sub_pops, then its frontier; the counts travel too
-            nsubs = parallel.allgather_f64(np.array([nsub, len(sent)], dtype=np.float64), group)
-            cands, remote_front, pos = [], [], 0
-            for v in nsubs:
-                ns, nt = int(v[0]), int(v[1])
-                chunk = [PopMember(t, sc, lo) for t, sc, lo in got[pos: pos + nt]]
+            # ONE fixed-size all-gather per iteration: every rank's best_sub_pops, then its frontier,
+            # with (score, loss), and its adaptive-parsimony size counts (parallel.IterationExchange)
+            got = xchg.exchange([m.tree for m in sent], [m.score for m in sent], [m.loss for m in sent],
+                                len(mine), counts, options, dtype)
+            for _, _, cnt in got:  # rank order; integer counts: the sum is exact in any order
+                stats.frequencies += cnt
+            stats.move_window()
+            cands, remote_front = [], []
+            for ns, members, _ in got:
+                chunk = [PopMember(t, sc, lo) for t, sc, lo in members]
                 cands.extend(chunk[:ns])
                 remote_front.extend(chunk[ns:])
-                pos += nt
             hof.update(cands + remote_front, options)
             dominating = hof.pareto_frontier()
             for k in local:
@@ -1028,17 +1035,19 @@ def equation_search(X, y, options, niterations: int = 10, weights=None, seed=Non
                             # one client fewer: the coalescer stops waiting for this island
                             scorer.coalescer.set_clients(sum(1 for r in remaining.values() if r > 0))
         num_evals += sum(isl.num_evals for isl in islands.values())
-        if dist_mode:
+        if dist_mode and ws > 1:
             num_evals = float(parallel.allreduce_np(np.array([num_evals]), "sum", group)[0])
         if mp_mode:
             cstats, node_rows = mpx.cstats, mpx.node_rows
         else:
             cstats = scorer.coalescer.stats() if own_scorer else {}
             node_rows = float(getattr(scorer, "node_rows", 0))
-        if dist_mode:
+        if dist_mode and ws > 1:
             node_rows = float(parallel.allreduce_np(np.array([node_rows]), "sum", group)[0])
         return SearchResult(hof, [pops[k] for k in local], num_evals, cstats, node_rows)
     finally:
+        if xchg is not None:
+            xchg.close()
         if own_scorer:
             scorer.close()
         if pool is not None:

@@ -468,3 +468,31 @@ def test_loss_kind_gradients_match_differences(ctx, kind_name, args):
             assert abs(grads[t][k] - ref) <= 1e-5 * max(1.0, abs(ref)), (t, k, grads[t][k], ref)
             checked += 1
     assert checked >= 6
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_inline_chunk_list_equals_staged_copy(ctx, dtype, monkeypatch):
+    """Gradient launches of at most 96 chunks carry their (tree, first constant) list in the kernel
+    arguments; SRHIP_GRAD_INLINE_MAX=0 stages it through a host-to-device copy instead.  Losses,
+    gradients and did_succeed are bitwise the same either way, and so is an optimize_constants run
+    (whose many small launches take the inline form)."""
+    sr = _sr()
+    opts, _, nodes, offs, X, y = _problem(sr, dtype)
+    ds = sr.DeviceDataset(ctx, X, y)
+    res = {}
+    for lim in ("0", "96"):
+        monkeypatch.setenv("SRHIP_GRAD_INLINE_MAX", lim)
+        prog = sr.Program(ctx, nodes, offs, opts, dtype)
+        l, g, ok = prog.eval_loss_grad(ds, sr.L2DistLoss())
+        out, imp, fc = prog.optimize_constants(ds, sr.L2DistLoss(), iterations=8, nrestarts=1, seed=3)
+        res[lim] = (np.asarray(l, np.float64), np.concatenate(g), ok, np.asarray(out, np.float64), imp, fc,
+                    np.concatenate(prog.get_constants()))
+        prog.close()
+    a, b = res["0"], res["96"]
+    for u, v in zip(a, b):
+        u, v = np.asarray(u), np.asarray(v)
+        if u.dtype.kind == "f":
+            assert np.array_equal(u.view(np.uint64 if u.itemsize == 8 else np.uint32),
+                                  v.view(np.uint64 if v.itemsize == 8 else np.uint32))
+        else:
+            assert np.array_equal(u, v)

@@ -4,7 +4,7 @@ check statistic puts the tree in the undecided band, and the sum lands just belo
 (fails) the threshold of the type, alternating over the population.  The device-listed pass (one
 tree group per listed tree) and the host-launched pass for trees past the list's capacity (the
 first evaluation of a program lists at most 4) must both give the oracle's mask, evaluation after
-evaluation."""
+evaluation -- including four trees within the sums' own precision of the threshold."""
 import numpy as np
 import pytest
 
@@ -36,6 +36,17 @@ def test_precise_pass_near_threshold_matches_oracle(ctx, oracle, dtype):
         c = dtype(thr / s * rel)
         trees.append(sr.Node(1, sr.Node(val=c), sr.Node(feature=1)))  # c * x1
         expect.append(i % 2 == 0)
+    # four more within the sums' own precision of the threshold (Float64: 1 +- a few 1e-12; Float32: the
+    # floats next to thr / s): whichever pass decides them -- listed (double-double sums) or host-launched
+    # (long double) -- must agree with the oracle's exact sum
+    c0 = thr / s
+    for k in range(4):
+        if dtype == np.float64:
+            c = c0 * (1 + (-1) ** k * (k + 1) * 3e-12)
+        else:
+            c = float(np.nextafter(np.float32(c0), np.float32(np.inf if k % 2 else 0)))
+            c = float(np.nextafter(np.float32(c), np.float32(np.inf if k % 2 else 0))) if k >= 2 else c
+        trees.append(sr.Node(1, sr.Node(val=dtype(c)), sr.Node(feature=1)))
     # ordinary trees around them
     trees += [sr.Node(2, sr.Node(feature=2), sr.Node(val=1.5)) for _ in range(6)]
     nodes, offs = sr.flatten(trees, opts, dtype)
@@ -46,7 +57,7 @@ def test_precise_pass_near_threshold_matches_oracle(ctx, oracle, dtype):
     assert list(ook[:10]) == expect, "the fixture's near-threshold sums"
     psums, pchk = prog.eval_loss_partials(ds, sr.L2DistLoss())
     status = prog.finalize(X.shape[0], psums, pchk)[2]
-    assert (status[:10] == 2).all(), "every near-threshold tree needs the precise pass"
+    assert (status[:14] == 2).all(), "every near-threshold tree needs the precise pass"
     for _ in range(3):  # first evaluation: list capacity 4 (host pass for the rest); then all listed
         _, ok = prog.eval_loss(ds, sr.L2DistLoss())
         assert np.array_equal(ok, ook), (np.nonzero(ok != ook)[0], ok[:10])

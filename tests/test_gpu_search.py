@@ -131,3 +131,37 @@ def test_device_scorer_adds_units_penalty():
             assert loss - srhip.eval_loss(tree, ds, opts, regularization=False) == pytest.approx(pen)
     finally:
         sc.close()
+
+
+def test_distributed_search_world1_native_exchange_equals_identity(monkeypatch):
+    """The island search's per-iteration exchange through libsrhip's RCCL communicator
+    (parallel.IterationExchange over NativeComm.allgather, world size 1) returns the hall of fame the
+    same lock-step search returns with the exchange as an in-process identity: every member, score,
+    loss and size count survives the fixed-size payload's device round trip unchanged
+    (src/SymbolicRegression.jl:910-943, src/Migration.jl:16-38)."""
+    from srhip import parallel
+
+    X, y = _data(200, seed=4)
+
+    def run(native):
+        monkeypatch.setenv("SRHIP_SEARCH_COMM", "native" if native else "torch")
+        calls = []
+        orig = parallel.IterationExchange.exchange
+
+        def spy(self, *a, **k):
+            calls.append(self.comm is not None)
+            return orig(self, *a, **k)
+
+        monkeypatch.setattr(parallel.IterationExchange, "exchange", spy)
+        o = srhip.Options(populations=3, population_size=20, ncycles_per_iteration=30, deterministic=True, seed=5,
+                          maxsize=15, **OPS)
+        res = S.equation_search(X, y, o, niterations=2, distributed=True)
+        monkeypatch.setattr(parallel.IterationExchange, "exchange", orig)
+        return res, calls
+
+    rn, cn = run(True)
+    ri, ci = run(False)
+    assert cn == [True, True] and ci == [False, False]  # the library's communicator vs the identity
+    fn = [(str(m.tree), m.loss, m.score) for m in rn.pareto_frontier()]
+    fi = [(str(m.tree), m.loss, m.score) for m in ri.pareto_frontier()]
+    assert fn == fi and len(fn) > 0
