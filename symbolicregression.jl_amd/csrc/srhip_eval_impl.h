@@ -120,6 +120,17 @@ namespace srhip {
 
 template <typename T> constexpr bool kIsInt = std::is_same<T, int32_t>::value;
 
+// threadIdx.x for the once-per-row-block setup code (staging, mark snapshot, derived columns): an
+// opaque copy at the use site, so the LDS addresses derived from it are computed there instead of
+// hoisted to the kernel's entry -- hoisted, they stayed live across the interpreter loop and the
+// register allocator spilled seven of them to scratch in every wave's preamble (28 bytes per lane,
+// ~7 MB of scratch writes per launch of 4096 waves)
+__device__ __attribute__((always_inline)) inline int tid_x() {
+  int t = (int)__builtin_amdgcn_workitem_id_x();
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 template <typename T>
 using OpsT = typename std::conditional<kIsInt<T>, IOps, FOps<typename std::conditional<kIsInt<T>, float, T>::type>>::type;
 
@@ -921,14 +932,15 @@ __device__ __attribute__((always_inline)) inline void derive_columns(const EvalA
   using CT = typename Chk<T>::type;
   constexpr int DV = 16 / sizeof(T);
   __shared__ CT part[EVAL_WAVES_MAX][DERIVE_MAX];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tid = tid_x();
+  const int lane = tid & 63, wave = tid >> 6;
   for (int d = 0; d < p.nd; ++d) {
     const uint32_t spec = __builtin_amdgcn_readfirstlane(p.dspec[d]);
     const int u = (int)(spec >> 16), f = (int)(spec & 0xffff);
     const T* src = lx + (int64_t)f * rbb;
     T* dst = lx + (int64_t)(p.nfeat + d) * rbb;
     CT m = 0;
-    for (int c = threadIdx.x; c < rbb / DV; c += blockDim.x) {
+    for (int c = tid; c < rbb / DV; c += blockDim.x) {
       RV<T, DV> v = reinterpret_cast<const RV<T, DV>*>(src)[c];
       v = derive_un<T, DV>(u, v);
       reinterpret_cast<RV<T, DV>*>(dst)[c] = v;
@@ -941,8 +953,9 @@ __device__ __attribute__((always_inline)) inline void derive_columns(const EvalA
     if (lane == WAVE_LAST) part[wave][d] = m;
   }
   __syncthreads();
-  if ((int)threadIdx.x < p.nd) {
-    const int d = threadIdx.x;
+  const int tf = tid_x();
+  if (tf < p.nd) {
+    const int d = tf;
     CT t = part[0][d];
     for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
       if constexpr (sizeof(T) == 4) t = __builtin_elementwise_maximum(t, part[w][d]);
@@ -964,8 +977,9 @@ __device__ __attribute__((always_inline)) inline void derive_columns_tiles(const
   constexpr int TILE = 64 * R, VEC = 16 / sizeof(T);
   constexpr int MAX_TILES = ROW_ALIGN / TILE > 0 ? ROW_ALIGN / TILE : 1;
   __shared__ CT part[DERIVE_MAX][MAX_TILES];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nwaves = blockDim.x >> 6;
+  const int tid = tid_x();
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), nwaves = blockDim.x >> 6;
   const int ntiles = rbb / TILE;
   for (int item = wave; item < p.nd * ntiles; item += nwaves) {
     const int d = item / ntiles, j = item - d * ntiles;
@@ -992,8 +1006,9 @@ __device__ __attribute__((always_inline)) inline void derive_columns_tiles(const
     if (lane == WAVE_LAST) part[d][j] = m;
   }
   __syncthreads();
-  if ((int)threadIdx.x < p.nd) {
-    const int d = threadIdx.x;
+  const int tf = tid_x();
+  if (tf < p.nd) {
+    const int d = tf;
     CT t = part[d][0];
     for (int j = 1; j < ntiles; ++j) {
       if constexpr (sizeof(T) == 4) t = __builtin_elementwise_maximum(t, part[d][j]);
@@ -1046,7 +1061,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
     const T* gX = reinterpret_cast<const T*>(p.X);
     const T* gy = reinterpret_cast<const T*>(p.y);
     const T* gw = reinterpret_cast<const T*>(p.w);
-    for (int i = threadIdx.x; i < ncols * vec_per_col; i += blockDim.x) {
+    for (int i = tid_x(); i < ncols * vec_per_col; i += blockDim.x) {
       const int c = i / vec_per_col;
       const int v = i - c * vec_per_col;
       const T* src = c < p.nfeat ? gX + (int64_t)c * p.ld : (c == p.nfeat ? gy : gw);
@@ -1078,7 +1093,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
                                  : (p.group_off ? p.group_off[gy + 1] - gb0 : min(p.trees_per_group, p.ntrees - gb0));
   if constexpr (SNAP) {
     if (p.early_exit)
-      for (int i = threadIdx.x; i < min(snap_n, FLAG_SNAP); i += blockDim.x)
+      for (int i = tid_x(); i < min(snap_n, FLAG_SNAP); i += blockDim.x)
         failed_snap[i] = __hip_atomic_load(p.fail_flag + snap_base + i * gstride, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT) == p.epoch;
   }

@@ -10,12 +10,12 @@
  *      own kernels (srm_jtrigf: __kernel_sindf / __kernel_cosdf per quadrant after rem_pio2_kernel)
  *      compute before theirs.  Both round once, so they can round differently only when the minimax
  *      value lies within D of a Float32 rounding midpoint.
- *  (2) the certificate the device applies (srm_trigf_cert): the low 29 bits of the minimax double
- *      (the bits Float32 rounding drops; every result here is a normal float or an exact tiny x)
- *      farther than SRM_TRIGF_CERT from the midpoint pattern 2^28 => Float32(minimax) is Julia's
- *      value; otherwise the row is re-evaluated by Julia's kernels.  Checked: the certified result
- *      equals srm_jtrigf for EVERY input, and the share of rows the certificate sends to Julia's
- *      kernels.
+ *  (2) a rejected alternative, measured: certify the minimax per row (the low 29 bits of its double --
+ *      the bits Float32 rounding drops -- farther than a threshold from the midpoint pattern 2^28
+ *      means Float32(minimax) is Julia's value) and re-evaluate the rest with Julia's kernels.  The
+ *      distance histogram's tail (Julia's 25+53-bit reduction near the zeros of large arguments)
+ *      makes the re-evaluated share too large to pay.  `check_trigf <threshold>`
+ *      prints D, the histogram, and the share a threshold flags.
  * Build: gcc -O2 -march=x86-64-v3 -ffp-contract=off -fopenmp tools/check_trigf.c -lm -o /tmp/check_trigf */
 #include <math.h>
 #include <stdint.h>
