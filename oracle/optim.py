@@ -337,16 +337,19 @@ def newton_exact(f, grad, x0, iterations=8, g_tol=1e-8):
 
 def _devorder_fns(tree_nodes, binops, unaops, X, y, w, order):
     """(f, grad) with libsrhip's row-sum order (oracle.loss_grad_devorder) and the value oracle's
-    did_succeed (f = Inf where the tree fails, as eval_loss returns L(Inf))."""
+    did_succeed (f = Inf where the tree fails, as eval_loss returns L(Inf)).  Float32 data: the
+    constants are rounded to Float32 at every call (the program holds Float32 immediates) while the
+    optimiser's state stays Float64, as libsrhip's optimiser keeps it."""
     offs = np.array([0, len(tree_nodes)], dtype=np.int64)
     cache = {}
+    f32 = np.asarray(X).dtype == np.float32
 
     def both(c):
         key = np.asarray(c, dtype=np.float64).tobytes()
         if key not in cache:
             nd = tree_nodes.copy()
             for k, i in enumerate(order):
-                nd[i]["val"] = c[k]
+                nd[i]["val"] = float(np.float32(c[k])) if f32 else c[k]
             _, _, ok, _ = oracle.eval_loss_batch(nd, offs, binops, unaops, X, y, w, 0, 0.0, nthreads=1)
             lv, g = oracle.loss_grad_devorder(nd, binops, unaops, X, y, w)
             cache.clear()
@@ -358,7 +361,7 @@ def _devorder_fns(tree_nodes, binops, unaops, X, y, w, order):
 
 def optimize_constants_exact(tree_nodes, binops, unaops, X, y, w=None, iterations=8, starts=None,
                              device_order=False):
-    """(constants, loss, improved, objective calls) for one Float64 tree -- the reference procedure
+    """(constants, loss, improved, objective calls) for one tree -- the reference procedure
     (src/ConstantOptimization.jl:22-81: Newton for one constant, BFGS otherwise, best of the starts,
     accepted only if it beats the baseline) with the exact gradient.  ``starts``: the start points
     (default: the tree's own constants only).  ``device_order``: the objective and gradient summed
@@ -369,6 +372,8 @@ def optimize_constants_exact(tree_nodes, binops, unaops, X, y, w=None, iteration
     if device_order:  # sums in libsrhip's row order: the same objective bits as the device's
         f, grad = _devorder_fns(tree_nodes, binops, unaops, X, y, w, order)
     x0 = np.array([tree_nodes[i]["val"] for i in order], dtype=np.float64)
+    if np.asarray(X).dtype == np.float32:  # a Float32 tree's constants are Float32 values
+        x0 = x0.astype(np.float32).astype(np.float64)
     if len(x0) == 0:
         return x0, f(x0), False, 0
     algorithm = newton_exact if len(x0) == 1 else bfgs_exact

@@ -141,17 +141,20 @@ def loss_grad(nodes, binops, unaops, X, y, w=None, kind=0):
 
 
 def loss_grad_devorder(nodes, binops, unaops, X, y, w=None, kind=0, rb=256):
-    """(loss, gradient) of ONE Float64 tree -- the loss value and exact gradient summed in libsrhip's
-    dual-number kernel's row order (sr_oracle_grad.h dev_order_sum; no did_succeed decision)."""
+    """(loss, gradient) of ONE tree -- the loss value and exact gradient summed in libsrhip's
+    dual-number kernel's row order (sr_oracle_grad.h dev_order_sum; no did_succeed decision).  Float32
+    X: the kernel's Float32 arithmetic (constants rounded to Float32), oracle_loss_grad_devorder_f32."""
     lib = load()
-    X = np.ascontiguousarray(X, dtype=np.float64)
-    y = np.ascontiguousarray(y, dtype=np.float64)
-    w = None if w is None else np.ascontiguousarray(w, dtype=np.float64)
+    dt = np.float32 if np.asarray(X).dtype == np.float32 else np.float64
+    X = np.ascontiguousarray(X, dtype=dt)
+    y = np.ascontiguousarray(y, dtype=dt)
+    w = None if w is None else np.ascontiguousarray(w, dtype=dt)
     nodes = np.ascontiguousarray(nodes)
     b = np.ascontiguousarray(binops, dtype=np.int32)
     u = np.ascontiguousarray(unaops, dtype=np.int32)
     out = np.empty(65, dtype=np.float64)
-    fn = _setup(lib.oracle_loss_grad_devorder_f64, ctypes.c_int,
+    fn = _setup(lib.oracle_loss_grad_devorder_f32 if dt == np.float32 else lib.oracle_loss_grad_devorder_f64,
+                ctypes.c_int,
                 [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p])
     nc = fn(_p(nodes), len(nodes), _p(b), _p(u), _p(X), _p(y), _p(w), X.shape[1], int(kind), int(rb), _p(out))

@@ -190,3 +190,100 @@ int oracle_loss_grad_devorder_f64(const srhip_node* nodes, int64_t nn, const int
   free(cidx);
   return nc;
 }
+
+/* ---- Float32 trees: the dual-number kernel's Float32 arithmetic, device row order ---------------
+ * libsrhip's constant optimiser treats a Float32 program as the reference's Float32 tree: every
+ * objective call evaluates the tree with its constants rounded to Float32, the values and tangents in
+ * Float32 (csrc/srhip_grad.hip dual_un_heavy / dual_spec / combine: the same products and sums, no
+ * contraction), the per-row loss l = d * d and dl = 2 d in Float32, and the row sums (double)l,
+ * (double)(dl * t_k) in the device's order (dev_order_sum above). */
+static float grad_node_f32(const GradCtx* c, const float* X32, int64_t i, float* t) {
+  const srhip_node* n = &c->nd[i];
+  if (n->degree == 0) {
+    for (int k = 0; k < c->nc; ++k) t[k] = 0.0f;
+    if (n->constant) {
+      t[c->cidx[i]] = 1.0f;
+      return (float)n->val;
+    }
+    return X32[(int64_t)(n->feature - 1) * c->n + c->row];
+  }
+  if (n->degree == 1) {
+    const float x = grad_node_f32(c, X32, n->l, t);
+    const int op = c->unaops[n->op - 1];
+    const float f = un_f32(op, x);
+    float df;
+    switch (op) {
+      case SRHIP_OP_NEG: df = -1.0f; break;
+      case SRHIP_OP_SQUARE: df = 2.0f * x; break;
+      case SRHIP_OP_CUBE: df = 3.0f * x * x; break;
+      case SRHIP_OP_ABS: df = x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); break;
+      case SRHIP_OP_COS: df = -srm_sinf(x); break;
+      case SRHIP_OP_SIN: df = srm_cosf(x); break;
+      case SRHIP_OP_TAN: df = 1.0f + f * f; break;
+      case SRHIP_OP_EXP: df = f; break;
+      case SRHIP_OP_LOG: df = 1.0f / x; break;
+      case SRHIP_OP_SQRT: df = 0.5f / f; break;
+      case SRHIP_OP_TANH: df = 1.0f - f * f; break;
+      default: df = NAN; break;
+    }
+    for (int k = 0; k < c->nc; ++k) t[k] = df * t[k];
+    return f;
+  }
+  float tr[GRAD_MAXC];
+  const float a = grad_node_f32(c, X32, n->l, t);
+  const float b = grad_node_f32(c, X32, n->r, tr);
+  const int op = c->binops[n->op - 1];
+  const float f = bin_f32(op, a, b);
+  float fa, fb;
+  switch (op) {
+    case SRHIP_OP_ADD: fa = 1.0f; fb = 1.0f; break;
+    case SRHIP_OP_SUB: fa = 1.0f; fb = -1.0f; break;
+    case SRHIP_OP_MUL: fa = b; fb = a; break;
+    case SRHIP_OP_DIV: { const float ib = 1.0f / b; fa = ib; fb = -f * ib; break; }
+    default: fa = NAN; fb = NAN; break;
+  }
+  for (int k = 0; k < c->nc; ++k) t[k] = fa * t[k] + fb * tr[k];
+  return f;
+}
+
+/* oracle_loss_grad_devorder_f64's Float32 counterpart: nodes' constants are rounded to Float32 as the
+ * device's program holds them; X, y, w are Float32; out as there (f64). */
+int oracle_loss_grad_devorder_f32(const srhip_node* nodes, int64_t nn, const int32_t* binops,
+                                  const int32_t* unaops, const float* X, const float* y, const float* w,
+                                  int64_t n, int kind, int rb, double* out) {
+  int32_t* cidx = (int32_t*)malloc((size_t)(nn > 0 ? nn : 1) * sizeof(int32_t));
+  for (int64_t i = 0; i < nn; ++i) cidx[i] = -1;
+  int nc = 0;
+  grad_const_index(nodes, 0, cidx, &nc);
+  if (nc > GRAD_MAXC) {
+    free(cidx);
+    return -1;
+  }
+  const int64_t stride = nc + 1;
+  double* rows = (double*)malloc((size_t)(n > 0 ? n : 1) * stride * sizeof(double));
+  GradCtx c = {nodes, binops, unaops, NULL, n, 0, nc, cidx};
+  float t[GRAD_MAXC];
+  double wsum = 0.0;
+  for (int64_t r = 0; r < n; ++r) {
+    c.row = r;
+    const float pred = grad_node_f32(&c, X, 0, t);
+    const float d = pred - y[r];
+    float l = kind == SRHIP_LOSS_L1 ? fabsf(d) : d * d;
+    float dl = kind == SRHIP_LOSS_L1 ? (d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f)) : 2.0f * d;
+    if (w) {
+      l = w[r] * l;
+      dl = w[r] * dl;
+    }
+    rows[r * stride] = (double)l;
+    for (int k = 0; k < nc; ++k) rows[r * stride + 1 + k] = (double)(dl * t[k]);
+  }
+  if (w) {
+    for (int64_t r = 0; r < n; ++r) wsum += (double)w[r];
+  } else {
+    wsum = (double)n;
+  }
+  for (int k = 0; k <= nc; ++k) out[k] = dev_order_sum(rows + k, n, stride, rb) / wsum;
+  free(rows);
+  free(cidx);
+  return nc;
+}

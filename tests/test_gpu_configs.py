@@ -321,6 +321,52 @@ def test_c4_restart_selection_float32(ctx):
     assert checked >= 20, checked
 
 
+def test_c4_restart_float32_vs_oracle(ctx, oracle):
+    """The Float32 restart path pinned to the oracle (no near-tie exclusions): a Float32 population,
+    BFGS / Newton + 2 restarts drawn in Float32 (val * (1f + 0.5f randn)), and on >= 32 trees the
+    outcome equals oracle/optim.py optimize_constants_exact run from the device's own three starts
+    over the oracle's Float32 dual-number objective in the device's row order
+    (sr_oracle_grad.h oracle_loss_grad_devorder_f32: constants rounded to Float32 per call, values and
+    tangents in Float32) with the reference's selection (src/ConstantOptimization.jl:50-78): the
+    improved flag, the returned Float32 constants, and the loss to 1e-6 relative."""
+    import optim
+
+    sr = _sr()
+    opts = sr.Options(binary_operators=("+", "-", "*", "/"), unary_operators=("cos", "exp"))
+    rng = np.random.default_rng(21)
+    X = rng.standard_normal((3, 20000)).astype(np.float32)
+    y = (2.1 * np.cos(1.3 * X[0]) + 0.7 * X[1] * X[2] - 0.4).astype(np.float32)
+    trees = sr.random_population(96, opts, 3, np.float32, seed=22, max_size=16)
+    nodes, offs = sr.flatten(trees, opts, np.float32)
+    ds = sr.DeviceDataset(ctx, X, y)
+    p = sr.Program(ctx, nodes, offs, opts, np.float32)
+    base, base_ok = p.eval_loss(ds, sr.L2DistLoss())
+    nconst = p.num_constants().astype(np.int64)
+    coff = np.concatenate([[0], np.cumsum(nconst)])
+    out, improved, _, starts = p.optimize_constants(ds, sr.L2DistLoss(), iterations=8, nrestarts=2, seed=5,
+                                                   return_starts=True)
+    final = p.get_constants()
+    sample = [int(t) for t in range(len(nconst)) if base_ok[t] and nconst[t] > 0][:40]
+    assert len(sample) >= 32, len(sample)
+
+    def orc(t):
+        tn = nodes[offs[t]:offs[t + 1]].copy()
+        x0 = np.array([tn[i]["val"] for i in _const_order(tn)], dtype=np.float64)
+        st = [x0] + [starts[r, coff[t]:coff[t + 1]] for r in range(starts.shape[0])]
+        return optim.optimize_constants_exact(tn, opts.binop_codes, opts.unaop_codes, X, y, starts=st,
+                                              device_order=True)
+
+    with cf.ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        ref = list(ex.map(orc, sample))
+    off = []
+    for t, (rx, rl, rimp, _) in zip(sample, ref):
+        same_loss = out[t] == rl or abs(out[t] - rl) <= 1e-6 * max(abs(out[t]), abs(rl))
+        same_x = np.array_equal(np.asarray(final[t], np.float32), np.asarray(rx, np.float64).astype(np.float32))
+        if not (same_loss and bool(improved[t]) == bool(rimp) and same_x):
+            off.append((t, out[t], rl, bool(improved[t]), bool(rimp), final[t], rx))
+    assert not off, off
+
+
 def test_c5_int32_population_1m_rows_bit_exact(ctx, oracle):
     """C5 Int32: random + - * trees with small integer constants over 3 x 1M Int32 rows (wrap-around
     arithmetic): predictions' loss and masks bit-exact against the oracle."""
