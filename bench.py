@@ -559,10 +559,11 @@ def pmc_summary(kname, pattern="*pmc_c2*.json"):
     source file).  Nones if no summary for this kernel variant is committed."""
     import glob
 
-    # the round's final summary when committed (file names sort by build, not by date), else the
-    # last by name
-    final = os.path.join(ROOT, "profiles", pattern.replace("*", "r04_", 1).replace("*", "_final"))
-    files = [final] if os.path.exists(final) else sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    # the newest round's final summary when committed (file names sort by build, not by date), else
+    # the last by name
+    finals = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern.replace("*", "r[0-9][0-9]_", 1)
+                                           .replace("*", "_final"))))
+    files = finals[-1:] if finals else sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
     if not files:
         return None, None, None
     try:

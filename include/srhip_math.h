@@ -447,7 +447,8 @@ SRM_FN int srm_jrem_pio2f(float x, double* y) {
  *     region index n (0 below Float32(pi)/4, +-1..+-4 above), and fn * (pi/2) rounds to exactly the
  *     constant Julia subtracts (pi/2, pi, pi*3/2, pi*4/2: scaling by 2 commutes with the rounding),
  *     so y = xd - fn (pi/2) is Julia's y; both kernels, the quadrant selects (srm_jtrigf_q);
- *   tier C, |x| < 2^28 pi/2: per row Julia's own choice between that y and its Cody-Waite reduction.
+ *   tier C, |x| < 2^28 pi/2: per row Julia's own choice between that y and its Cody-Waite reduction
+ *     (cos: Cody-Waite alone -- it returns the same bits as the +-k pi/2 cases on every float).
  * sin(-0) is the only row tier B / C would get wrong (y = +0): the caller keeps x where x == 0. */
 #define SRM_JPIO4F 0.78539819f
 #define SRM_J9PIO4F 7.068583f

@@ -381,7 +381,9 @@ template <int R> __device__ __attribute__((always_inline)) inline bool trigf_row
 //   A  every |x| < Float32(pi)/4: no reduction, ONE kernel (sin: the sign of x copied onto it);
 //   B  every |x| <= pi*9/4: fn = rint(xd 2/pi), y = xd - fn (pi/2) (Julia's +-k pi/2 cases, one
 //      rounding), both kernels, the quadrant picks one and its sign;
-//   C  every |x| < 2^28 pi/2: per row Julia's choice between that y and its Cody-Waite reduction;
+//   C  every |x| < 2^28 pi/2: per row Julia's choice between that y and its Cody-Waite reduction (cos:
+//      Cody-Waite for every row -- on every float it returns what the +-k pi/2 cases return; sin
+//      differs at x = +-3.0061);
 //   slow  any larger / Inf / NaN row: C for the rest, the scalar srm_jtrigf (Payne-Hanek) for those.
 // C2's cos-of-operator tiles fall 11 % / 47 % / 36 % / 6 % into A / B / C / slow
 // (scripts/trig_arg_tiers.py).
@@ -411,8 +413,15 @@ __device__ __attribute__((noinline)) RV<float, R> jtrigf_a(RV<float, R> v) {
 template <int KIND, bool CW>
 __device__ __attribute__((always_inline)) inline float jtrigf_row(float x) {
   const double xd = (double)x, fn = srm_jfn(xd);
-  double y = srm_jred_near(xd, fn);
-  if constexpr (CW) y = __builtin_fabsf(x) <= SRM_J9PIO4F ? y : srm_jred_cw(xd, fn);
+  double y;
+  if constexpr (CW && KIND == 0) {
+    // cos: the Cody-Waite reduction gives Julia's result on every float, the +-k pi/2 cases included
+    // (tools/check_trigf.c), so a tier-C wave needs no per-row choice
+    y = srm_jred_cw(xd, fn);
+  } else {
+    y = srm_jred_near(xd, fn);
+    if constexpr (CW) y = __builtin_fabsf(x) <= SRM_J9PIO4F ? y : srm_jred_cw(xd, fn);
+  }
   const float r = jtrigf_q_dev<KIND>(fn, y);
   return (KIND == 1 && x == 0.0f) ? x : r;  // sin(-0) = -0 (the reduction gives +0)
 }

@@ -26,6 +26,7 @@
 #include <condition_variable>
 #include <functional>
 #include <memory>
+#include <map>
 #include <mutex>
 #include <numeric>
 #include <string>
@@ -1571,6 +1572,61 @@ static void finalize_precise(const srhip_program& P, const int32_t* trees, int32
 }
 
 }  // namespace
+
+// ---- the device-allocation cache behind PoolBuf ----------------------------------------------
+namespace {
+struct DevPool {
+  std::mutex mu;
+  std::map<std::pair<int, size_t>, std::vector<void*>> free;  // (device, size class) -> blocks
+  size_t cached = 0;
+};
+DevPool& devpool() {
+  static DevPool* P = new DevPool();  // never destroyed: blocks outlive static destruction order
+  return *P;
+}
+constexpr size_t DEVPOOL_MAX_CACHED = (size_t)512 << 20;
+size_t devpool_class(size_t n) {
+  size_t c = 4096;
+  while (c < n) c <<= 1;
+  return c;
+}
+}  // namespace
+
+void* srhip::devpool_get(size_t bytes, size_t* cap) {
+  const size_t c = devpool_class(bytes);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  {
+    DevPool& P = devpool();
+    std::lock_guard<std::mutex> g(P.mu);
+    auto it = P.free.find({dev, c});
+    if (it != P.free.end() && !it->second.empty()) {
+      void* q = it->second.back();
+      it->second.pop_back();
+      P.cached -= c;
+      *cap = c;
+      return q;
+    }
+  }
+  void* q = nullptr;
+  if (hipMalloc(&q, c) != hipSuccess) return nullptr;
+  *cap = c;
+  return q;
+}
+
+void srhip::devpool_put(void* p, size_t cap, int device) {
+  if (!p) return;
+  DevPool& P = devpool();
+  {
+    std::lock_guard<std::mutex> g(P.mu);
+    if (device >= 0 && P.cached + cap <= DEVPOOL_MAX_CACHED) {
+      P.free[{device, cap}].push_back(p);
+      P.cached += cap;
+      return;
+    }
+  }
+  (void)hipFree(p);
+}
 
 int srhip::next_fail_epoch(srhip_ctx* ctx, int64_t n, int32_t** flags, int32_t* epoch) {
   const size_t need = (size_t)std::max<int64_t>(n, 1) * sizeof(int32_t);

@@ -82,6 +82,36 @@ struct DevBuf {
     return e;
   }
 };
+// Program buffers come from a process-wide cache of device allocations, by power-of-two size class
+// and device (srhip_host.cpp devpool_*): hipFree synchronises the whole device, so a host thread
+// destroying the previous population's program would wait for whatever the device runs meanwhile
+// (the fresh-population pipeline: compile on one thread while another evaluates).  Every use of a
+// program's buffers is complete when the program is destroyed (evaluations and uploads are
+// synchronous), so a returned block is reusable at once.
+void* devpool_get(size_t bytes, size_t* cap);
+void devpool_put(void* p, size_t cap, int device);
+struct PoolBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int device = -1;
+  ~PoolBuf() { release(); }
+  void release() {
+    if (p) devpool_put(p, bytes, device);
+    p = nullptr;
+    bytes = 0;
+  }
+  hipError_t ensure(size_t n) {
+    if (n <= bytes && p) return hipSuccess;
+    release();
+    size_t cap = 0;
+    void* q = devpool_get(n, &cap);
+    if (!q) return hipErrorOutOfMemory;
+    if (hipGetDevice(&device) != hipSuccess) device = -1;
+    p = q;
+    bytes = cap;
+    return hipSuccess;
+  }
+};
 struct HostBuf {  // pinned staging
   void* p = nullptr;
   size_t bytes = 0;
@@ -181,7 +211,7 @@ struct srhip_program {
   // [code | prog_off | dcode | dprog_off | dspec | dmask], 16-byte aligned sections
   // upload_program(P, sync, defer = true) only builds the image: the next evaluation appends its tree
   // order and uploads both with one copy (the coalescer's per-flush program)
-  mutable srhip::DevBuf d_prog;
+  mutable srhip::PoolBuf d_prog;
   mutable std::vector<uint8_t> blob;  // its host image (alive until the next upload)
   mutable bool upload_pending = false;
   mutable int32_t und_hint = 0;  // trees the last device-listed precise pass saw (list capacity hint)
@@ -207,7 +237,7 @@ struct srhip_program {
   mutable std::vector<int32_t> ord_goff;  // group offsets of that plan (appended to d_order)
   mutable std::vector<int32_t> ord_host;  // the uploaded order (kept alive: its copy is asynchronous)
   mutable const void* ord_dev = nullptr;  // where it lives on the device (d_order, or inside d_prog)
-  mutable srhip::DevBuf d_order;
+  mutable srhip::PoolBuf d_order;
   // gradient program (constants not folded, constant leaves carry their get_constants index);
   // compiled on first use by the constant-gradient path
   bool grad_ready = false;
@@ -215,7 +245,7 @@ struct srhip_program {
   std::vector<int32_t> gprog_off;
   std::vector<srhip::TreeInfo> ginfo;  // did_succeed metadata for the gradient program's constants
   int32_t gkmax = 0, gmax_len = 0, gmax_ops = 0;
-  srhip::DevBuf d_gcode, d_goff;
+  srhip::PoolBuf d_gcode, d_goff;
   // constant-leaf values (node storage order) the gradient program was last compiled with: when only
   // constants change (the optimiser's line search), just the trees whose constants moved recompile
   std::vector<double> gsnap;

@@ -69,7 +69,9 @@ static float tier_b(int kind, float x) {
 }
 static float tier_c(int kind, float x) {
   const double xd = (double)x, fn = srm_jfn(xd);
-  const double y = fabs(xd) <= 3.141592653589793 * 9 / 4 ? srm_jred_near(xd, fn) : srm_jred_cw(xd, fn);
+  /* cos: Cody-Waite for every row (equal to the +-k pi/2 cases on every float); sin: Julia's choice */
+  const double y = kind == 0 ? srm_jred_cw(xd, fn)
+                             : (fabs(xd) <= 3.141592653589793 * 9 / 4 ? srm_jred_near(xd, fn) : srm_jred_cw(xd, fn));
   const float r = srm_jtrigf_q(kind, (int)fn, y);
   return (kind == 1 && x == 0.0f) ? x : r;
 }
