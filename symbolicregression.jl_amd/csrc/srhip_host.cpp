@@ -1353,10 +1353,19 @@ int srhip::upload_program(srhip_program& P, bool sync, bool defer, hipStream_t s
     return SRHIP_OK;
   }
   P.upload_pending = false;
-  HIP_TRY(P.d_prog.ensure(total));
+  // a launch order planned at creation (plan_persistent_order) travels in the same copy
+  const bool with_order = !P.ord_host.empty() && P.ord_key[0] > 0;
+  const size_t nbytes = with_order ? total + P.ord_host.size() * sizeof(int32_t) : total;
+  if (with_order) {
+    P.blob.resize(nbytes);
+    memcpy(P.blob.data() + total, P.ord_host.data(), P.ord_host.size() * sizeof(int32_t));
+    h = P.blob.data();
+  }
+  HIP_TRY(P.d_prog.ensure(nbytes));
   hipStream_t st = stream ? stream : P.ctx->stream;
-  HIP_TRY(hipMemcpyAsync(P.d_prog.p, h, total, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(P.d_prog.p, h, nbytes, hipMemcpyHostToDevice, st));
   set_prog_pointers(P);
+  if (with_order) P.ord_dev = (const uint8_t*)P.d_prog.p + total;
   if (sync) HIP_TRY(hipStreamSynchronize(st));
   return SRHIP_OK;
 }
@@ -2386,6 +2395,84 @@ int srhip::run_eval_sharded(srhip_ctx* ctx, const srhip_dataset* ds, const srhip
   return SRHIP_OK;
 }
 
+// The launch order a fresh Float32 program's first large evaluation will use (eval_partials'
+// persistent plan: one group, the live trees by descending cost, derived columns when they fit), made
+// at creation -- on the thread that compiles, which in a pipeline overlaps the previous population's
+// evaluation -- and uploaded with the program in its one copy, instead of sorting and copying it (a
+// pageable-source copy the runtime stages synchronously) in front of the first launch.  Assumes an
+// unweighted dataset of >= WIDE_MIN_ROWS rows; any other launch re-plans as before (the key differs).
+static void plan_persistent_order(const srhip_ctx* ctx, srhip_program& P) {
+  if (!ctx || P.dtype != SRHIP_F32 || P.ntrees == 0) return;
+  if (env_flag("SRHIP_NO_PERSISTENT") || env_flag("SRHIP_NO_PREPLAN")) return;
+  bool wide = false;
+  for (int32_t u : P.unaops) wide |= u == SRHIP_OP_ASIN || u == SRHIP_OP_ACOS || u == SRHIP_OP_ATANH_CLIP;
+  auto kvariant = [&](int32_t kmax) { return wide ? K_MAX : (kmax <= 2 ? 2 : (kmax <= 4 ? 4 : 8)); };
+  const int nd = (int)P.dspec.size();
+  const int Kp = kvariant(P.kmax);
+  if (pick_rows_per_lane(SRHIP_F32, Kp, MODE_LOSS, WIDE_MIN_ROWS) != R_F32_WIDE || R_F32_WIDE == R_F32) return;
+  if (nd != 0 && kvariant(P.dkmax) != Kp) return;
+  const int prb_env = env_int("SRHIP_PRB_ROWS", 0);
+  const int tile = 64 * R_F32_WIDE;
+  int rb = prb_env >= tile && prb_env <= ROW_ALIGN && (prb_env & (prb_env - 1)) == 0 ? prb_env : 2048;
+  rb = std::max(rb, std::max(tile, loss_chunk(SRHIP_F32)));
+  const size_t budget = (size_t)ctx->lds_max - 8 * 1024;  // the 16-wave variant: one workgroup per CU
+  const int base_cols = P.maxfeat + 1;
+  const bool use_d = nd > 0 && (size_t)(base_cols + nd) * rb * 4 <= budget;
+  if ((size_t)(base_cols + (use_d ? nd : 0)) * rb * 4 > budget) return;
+  std::vector<int32_t> live;
+  live.reserve(P.ntrees);
+  for (int32_t t = 0; t < P.ntrees; ++t)
+    if (!P.info[t].static_fail) live.push_back(t);
+  if (live.empty()) return;
+  const int nl = (int)live.size();
+  const std::vector<int32_t> goff{0, nl};
+  std::lock_guard<std::mutex> g(P.ord_mu);
+  P.ord_host = make_order(P, live, goff, use_d);
+  P.ord_host.insert(P.ord_host.end(), goff.begin(), goff.end());
+  P.ord_key[0] = 1;
+  P.ord_key[1] = nl;
+  P.ord_key[2] = (int)use_d;
+  P.ord_goff = goff;
+}
+
+// ---- deferred program teardown (srhip_program_destroy) -------------------------------------------
+namespace {
+struct Reaper {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<srhip_program*> q;
+  bool started = false;
+};
+Reaper& reaper() {
+  static Reaper* R = new Reaper();  // never destroyed: the thread may outlive static destruction
+  return *R;
+}
+}  // namespace
+
+static void reaper_push(srhip_program* P) {
+  Reaper& R = reaper();
+  std::lock_guard<std::mutex> g(R.mu);
+  R.q.push_back(P);
+  if (!R.started) {
+    R.started = true;
+    std::thread([&R] {
+      for (;;) {
+        std::vector<srhip_program*> batch;
+        {
+          std::unique_lock<std::mutex> lk(R.mu);
+          R.cv.wait(lk, [&R] { return !R.q.empty(); });
+          batch.swap(R.q);
+        }
+        for (srhip_program* p : batch) {
+          if (p->device >= 0) (void)hipSetDevice(p->device);
+          delete p;
+        }
+      }
+    }).detach();
+  }
+  R.cv.notify_one();
+}
+
 template <typename T>
 static void pack_column(const void* src, int64_t f, int64_t n, int64_t sf, int64_t sr, int64_t ld, T* dst) {
   const T* s = (const T*)src;
@@ -2553,6 +2640,7 @@ int srhip_program_create(srhip_ctx* ctx, int dtype, const srhip_node* nodes, con
   int rc = compile_program(*P);
   if (rc) return rc;
   if (ctx) {  // ctx == NULL: host-only program (compile + did_succeed metadata, e.g. for finalize)
+    plan_persistent_order(ctx, *P);
     rc = upload_program(*P, true, false, ctx->up_stream);
     if (rc) return rc;
   }
@@ -2562,6 +2650,13 @@ int srhip_program_create(srhip_ctx* ctx, int dtype, const srhip_node* nodes, con
 
 void srhip_program_destroy(srhip_program* P) {
   if (!P) return;
+  // a program's teardown is host work only (its device buffers go back to the allocation cache): a
+  // background thread does it, so the caller -- e.g. a pipeline between two evaluations -- does not
+  // wait for freeing a large population's per-tree metadata (~0.1 ms for 1024 trees)
+  if (!env_flag("SRHIP_SYNC_DESTROY")) {
+    reaper_push(P);
+    return;
+  }
   if (P->device >= 0) (void)hipSetDevice(P->device);
   delete P;
   (void)hipGetLastError();
@@ -2604,6 +2699,13 @@ int srhip_program_set_constants(srhip_program* P, const double* consts) {
   if (!P || (!consts && P->ntrees > 0)) return fail(SRHIP_ERR_INVALID, "null argument");
   const double* c = consts;
   for (int32_t t = 0; t < P->ntrees; ++t) set_consts_rec(P->nodes, P->offsets[t], 0, c);
+  {
+    // new constants can change which trees fail statically (non-finite leaves): the next evaluation
+    // plans its launch order again
+    std::lock_guard<std::mutex> g(P->ord_mu);
+    P->ord_key[0] = P->ord_key[1] = P->ord_key[2] = -1;
+    P->ord_goff.clear();
+  }
   int rc = compile_program(*P);
   if (rc) return rc;
   return P->ctx ? upload_program(*P) : SRHIP_OK;
