@@ -19,6 +19,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
+#include <sys/resource.h>
+#include <sys/syscall.h>
 
 #include <algorithm>
 #include <atomic>
@@ -42,6 +44,9 @@
 #include "srhip_ops.h"
 
 using namespace srhip;
+
+static bool env_flag(const char* name);
+static int env_int(const char* name, int dflt);
 
 // ---------------------------------------------------------------------------------------------
 // errors
@@ -634,7 +639,15 @@ class HostPool {
     // hardware_concurrency there reports the whole machine
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     nthr_ = std::min(15u, hw - 1);
-    for (unsigned i = 0; i < nthr_; ++i) threads_.emplace_back([this] { loop(); });
+    // SRHIP_POOL_NICE = n > 0: the workers run at nice n, so a thread that is waiting for the device
+    // (an evaluation beside a pipelined compile) gets its core back first when the device finishes
+    const char* ne = getenv("SRHIP_POOL_NICE");
+    const int nice_v = ne && *ne ? atoi(ne) : 0;
+    for (unsigned i = 0; i < nthr_; ++i)
+      threads_.emplace_back([this, nice_v] {
+        if (nice_v > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), nice_v);
+        loop();
+      });
   }
   ~HostPool() {
     for (std::thread& t : threads_)
@@ -907,7 +920,10 @@ int compile_program_t(srhip_program& P) {
   const bool der = !P.dspec.empty();
   std::vector<TreeInfo> dinfo(der ? n : 0);
   HostPool& pool = HostPool::get();
-  const int W = (int)std::max<int64_t>(1, std::min<int64_t>(pool.threads(), (int64_t)n / 64));
+  // SRHIP_COMPILE_THREADS caps the threads one compile uses (read per compile; default: the pool)
+  const int cap_env = env_int("SRHIP_COMPILE_THREADS", 0);
+  const int wmax = cap_env > 0 ? std::min(cap_env, pool.threads()) : pool.threads();
+  const int W = (int)std::max<int64_t>(1, std::min<int64_t>(wmax, (int64_t)n / 64));
   std::vector<std::vector<Ins>> part(W), dpart(W);
   std::vector<std::string> errs(W);
   std::vector<int> rcs(W, SRHIP_OK);
