@@ -1,0 +1,51 @@
+#!/bin/bash
+# Round-5 evidence on the committed build, one GPU session: GPU suite, smoke, C2 bench (CPU baseline),
+# the headline kernel trace + per-step PMC passes, C4 bench (all-core CPU baseline) + gradient PMC,
+# C1 / C3 search lines, the multi-rank rehearsal, the native coalescer driver.  Each step under its
+# own time limit; stops at the first failure.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/final5
+export TMPDIR=/tmp
+F=gpurun_out/final5
+step() { echo "== $1"; }
+step tests
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $F/gpu_tests.log 2>&1 || { tail -30 $F/gpu_tests.log; exit 1; }
+tail -1 $F/gpu_tests.log
+step smoke
+timeout -k 10 240 python -u -c "import __graft_entry__ as g; g.smoke()" > $F/smoke.log 2>&1 || exit $?
+tail -1 $F/smoke.log
+step c2
+timeout -k 10 400 python -u bench.py > $F/bench_c2.log 2>&1 || exit $?
+tail -1 $F/bench_c2.log > $F/bench_c2.json
+step trace
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $F/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 30 --no-cpu --headline-only > $F/prof.log 2>&1 || exit $?
+python3 scripts/trace_summary.py $F/prof/run_kernel_trace.csv > $F/trace_c2.txt; python3 scripts/step_timeline.py $F/prof/run_kernel_trace.csv > $F/step_timeline_c2.txt; head -5 $F/trace_c2.txt
+step pmc
+rm -rf gpurun_out/pmc; bash scripts/pmc.sh > $F/pmc.log 2>&1 || exit $?
+python3 scripts/pmc_step.py gpurun_out/pmc 5 --json $F/pmc_c2.json > /dev/null; python3 scripts/pmc_summary.py gpurun_out/pmc "eval_kernel<float, 16, 2, 0, true>" --json $F/pmc_c2_dispatch.json > /dev/null; cp -r gpurun_out/pmc $F/pmc_csv
+step host
+bash scripts/host_timing.sh > $F/host_timing.log 2>&1 || exit $?
+step rowshard
+timeout -k 10 300 python -u bench.py --mode rowshard --steps 10 --warmup 5 > $F/rowshard_n1.log 2>&1 || exit $?
+tail -1 $F/rowshard_n1.log > $F/rowshard_n1.json
+step c4
+timeout -k 10 600 python -u bench.py --config c4 > $F/bench_c4.log 2>&1 || exit $?
+tail -1 $F/bench_c4.log > $F/bench_c4.json
+step pmc_grad
+rm -rf gpurun_out/pmcg; bash scripts/pmc_grad.sh > $F/pmc_grad.log 2>&1 || exit $?
+python3 scripts/pmc_step.py gpurun_out/pmcg 8 grad_kernel --json $F/pmc_grad_c4.json > /dev/null
+step c1
+timeout -k 10 400 python -u bench.py --config c1 > $F/bench_c1.log 2>&1 || exit $?
+tail -1 $F/bench_c1.log > $F/bench_c1.json
+step c3
+timeout -k 10 400 python -u bench.py --config c3 > $F/bench_c3.log 2>&1 || exit $?
+tail -1 $F/bench_c3.log > $F/bench_c3.json
+step multi
+bash scripts/multi_rehearsal.sh > $F/multi.log 2>&1 || exit $?
+cp gpurun_out/multi_*.json $F/
+step coalescer
+SECONDS_PER_RUN=3 timeout -k 10 200 python -u scripts/coalescer_native.py c3 16 64 > $F/coalescer_c3.jsonl 2>&1 || exit $?
+SECONDS_PER_RUN=3 timeout -k 10 200 python -u scripts/coalescer_native.py c1 1 16 64 > $F/coalescer_c1.jsonl 2>&1 || exit $?
+SPLITS=3 NO_TRACE=1 bash scripts/c4_diag.sh > $F/c4_diag.log 2>&1 || exit $?
+echo done

@@ -49,6 +49,9 @@
 #ifndef SRHIP_HEAVY_ILP
 #define SRHIP_HEAVY_ILP 1  // rows a heavy operator body may interleave
 #endif
+#ifndef SRHIP_TRIG_ILP
+#define SRHIP_TRIG_ILP SRHIP_HEAVY_ILP  // rows Julia's Float32 trig bodies interleave (jtrigf_*); 1/2/4 measured alike (C2 1.278-1.289 ms)
+#endif
 #ifndef SRHIP_TRIG_ROWS
 #define SRHIP_TRIG_ROWS 1  // Float32 cos/sin/tan batched over the rows (trigf_rows)
 #endif
@@ -406,7 +409,7 @@ __device__ __attribute__((noinline)) RV<float, R> jtrigf_a(RV<float, R> v) {
     } else {
       v[r] = __builtin_copysignf((float)srm_jsin_kernel((double)x), x);
     }
-    if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
+    if ((r + 1) % SRHIP_TRIG_ILP == 0) SRHIP_ROW_FENCE();
   }
   return v;
 }
@@ -429,7 +432,7 @@ template <int R, int KIND, bool CW>
 __device__ __attribute__((noinline)) RV<float, R> jtrigf_bc(RV<float, R> v) {
   UNR for (int r = 0; r < R; ++r) {
     v[r] = jtrigf_row<KIND, CW>(v[r]);
-    if ((r + 1) % SRHIP_HEAVY_ILP == 0) SRHIP_ROW_FENCE();
+    if ((r + 1) % SRHIP_TRIG_ILP == 0) SRHIP_ROW_FENCE();
   }
   return v;
 }
