@@ -696,7 +696,7 @@ def bench_c4(args):
     print(json.dumps({
         "metric": "C4 batched constant optimisation: wall time per optimize_constants over the population",
         "value": dt * 1e3, "unit": "ms", "higher_is_better": False, "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "dtype": "f64", "data": "synthetic (X ~ N(0,1) 5x100k; fixed-size-20 trees, >= 2 consts)",
+        "warmup": args.warmup, "ms_per_step": dt * 1e3, "dtype": "f64", "data": "synthetic (X ~ N(0,1) 5x100k; fixed-size-20 trees, >= 2 consts)",
         "config": {"workload": f"C4: {ntrees} trees x {rows} rows Float64, BFGS(8) + 2 restarts",
                    "ntrees": ntrees, "rows": rows, "nodes": int(st["total_nodes"])},
         "objective_evals_per_s": float(np.sum(fcalls)) / dt,

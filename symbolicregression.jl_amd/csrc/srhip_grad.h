@@ -37,6 +37,12 @@ struct GradArgs {
   double loss_p0;
   int32_t weighted;
   int32_t max_steps;
+  // row blocks of this launch: blockIdx.x + block0 (slab rows keep their global block index)
+  int32_t block0;
+  // value-only screening (GMODE_LOSS, KT = 0): a chunk whose block-0 record (written by an earlier
+  // launch on the stream) already holds a non-finite check statistic is skipped -- its tree fails
+  // did_succeed whatever the other blocks hold
+  int32_t screened;
   // per-row modes: out_der[row + j][nvalid] for the components c0 + j < end (the values come from the
   // evaluator, which also decides did_succeed)
   void* out_der;

@@ -299,7 +299,7 @@ template <typename T, int KT, int K, int GM, bool XLDS, int R>
 __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   constexpr int CW = GM == GMODE_LOSS ? 2 : 4;  // ints per chunk record
   const int lane = threadIdx.x & 63;
-  const int rb = blockIdx.x;
+  const int rb = blockIdx.x + p.block0;
   const int64_t row_base = (int64_t)rb * p.rb_rows;
   const int ntiles = p.rb_rows / (64 * R);
   // valid rows of this block, block-relative: the row tests below are 32-bit (scalar for the tile test)
@@ -357,6 +357,15 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
     } else {
       tree = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk]);
       c0 = __builtin_amdgcn_readfirstlane(p.chunks[CW * chunk + 1]);
+    }
+    if constexpr (GM == GMODE_LOSS && KT == 0) {
+      if (p.screened) {
+        // the screen launch's record of row block 0 for this chunk: a non-finite check statistic (a
+        // NaN / Inf operator output in its rows) fails the tree; the blocks left unwritten here only
+        // ever reach the reduction's check statistic, which block 0 already makes non-finite
+        const double m0 = p.slab[(int64_t)chunk * p.nrb * 2 + 1];  // [chunk][block 0][loss, chk]
+        if (__builtin_amdgcn_readfirstlane((int)!__builtin_isfinite(m0))) continue;
+      }
     }
     const int pc0 = __builtin_amdgcn_readfirstlane(p.prog_off[tree]);
     double lacc = 0.0;

@@ -96,11 +96,17 @@ void set_all_consts(srhip_program& P, const double* c) {
 static thread_local double g_t_compile = 0.0, g_t_eval = 0.0, g_t_host = 0.0;
 static thread_local int64_t g_n_launch = 0;
 static thread_local bool g_stats_on = false;
+static thread_local bool g_launch_log = false;  // SRHIP_OPTIM_TIMING=3: one stderr line per launch (caller's group)
 static thread_local int64_t g_hist[5] = {0, 0, 0, 0, 0}, g_nonfinite_trials = 0;
 static thread_local int64_t g_spec_launched = 0, g_spec_used = 0;  // speculative trial points
 // (SRHIP_OPTIM_TIMING=2) evaluated items by pass (0 gradient, 1 value-only) and launch size (items
 // <= 64 / > 64): [pass][big][all, non-finite f]
 static thread_local int64_t g_items[2][2][2] = {};
+// integer knob through the environment cache (read per call: tests flip it within one process)
+static int env_int_opt(const char* name, int dflt) {
+  const char* e = env_get(name);
+  return e && *e ? atoi(e) : dflt;
+}
 static double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -278,7 +284,25 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     a.max_steps = P->gmax_len;
     if (first) HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));  // srhip_last_kernel_ms: the gradient kernels
     first = false;
-    HIP_TRY(launch_grad(dtype, K, ps.kt, a, dim3(ps.L.nrb, ps.L.groups), ctx->stream));
+    // value-only screening (SRHIP_GRAD_SCREEN = the fewest value-only chunks screened; default 0 =
+    // off): row block 0 of every chunk first, in a launch of its own, then the other blocks, where a
+    // chunk whose block-0 check statistic is already non-finite is skipped.  Records of evaluated
+    // blocks are the same computation as in one launch, so losses and decisions are bit-identical
+    // (test_value_only_screening_is_exact).  C4 (~40 % of its trial points overflow), same box:
+    // off 173.6-177.9 ms, every pass 190-193, passes of >= 16 chunks 176.8-179.6 -- the extra launch
+    // costs what the skipped blocks save at 100k rows.
+    const int screen_min = env_int_opt("SRHIP_GRAD_SCREEN", 0);
+    if (ps.kt == 0 && screen_min > 0 && nch >= screen_min && ps.L.nrb > 1) {
+      GradArgs sa = a;
+      const int tpg_s = 2 * GRAD_WAVES;
+      sa.chunks_per_group = tpg_s;
+      HIP_TRY(launch_grad(dtype, K, 0, sa, dim3(1, (nch + tpg_s - 1) / tpg_s), ctx->stream));
+      a.block0 = 1;
+      a.screened = 1;
+      HIP_TRY(launch_grad(dtype, K, 0, a, dim3(ps.L.nrb - 1, ps.L.groups), ctx->stream));
+    } else {
+      HIP_TRY(launch_grad(dtype, K, ps.kt, a, dim3(ps.L.nrb, ps.L.groups), ctx->stream));
+    }
     // the reduction writes the records straight into coherent pinned host memory (no copy on the stream)
     HIP_TRY(launch_grad_reduce(dtype, ps.kt, (const double*)ctx->g_slab.p, ps.L.nrb, nch, (double*)ctx->h_gred[pi].p,
                                ctx->stream));
@@ -756,6 +780,7 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
     g_t_host += t1 - t0;
     g_t_eval += t2 - t1;
     size_t si = 0;
+    int64_t used_all = 0;
     for (int32_t t : act) {
       const int64_t o = coff[t];
       consume(t, fe[t], vonly[t] ? nullptr : ge.data() + o, xe.data() + o);
@@ -770,12 +795,22 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
         consume(t, sf[si], value_trials ? nullptr : sg.data() + q.off, sx.data() + q.off);
         used += 1;
       }
+      used_all += used;
       if (launched > 0) {
         g_spec_used += used;
         // all used and still searching: go deeper; else keep what would have been used (+1)
         sdepth[t] = used == launched && phase[t] == TRIAL ? std::min(2 * sdepth[t], SPEC_MAX_DEPTH)
                                                           : std::max(1, std::min(sdepth[t], used + 1));
       }
+    }
+    if (g_launch_log) {
+      int nv = 0, ntrial = 0;
+      for (int32_t t : act) {
+        nv += vonly[t];
+        ntrial += phase[t] == TRIAL;
+      }
+      fprintf(stderr, "srhip launch: t %.3f act %zu trial %d vonly %d spec %zu used %lld host %.3f eval %.3f ms\n",
+              1e3 * t2, act.size(), ntrial, nv, spec.size(), (long long)used_all, 1e3 * (t1 - t0), 1e3 * (t2 - t1));
     }
   }
   if (g_stats_on) {  // the trees with the most objective calls (the pipeline's tail)
@@ -1089,7 +1124,8 @@ int srhip_optimize_constants_starts(srhip_ctx* ctx, const srhip_dataset* ds, srh
     g_patch_scan_s = g_patch_copy_s = 0.0;
     g_n_launch = 0;
     const char* te = getenv("SRHIP_OPTIM_TIMING");
-    g_stats_on = te && *te == '2';
+    g_stats_on = te && (*te == '2' || *te == '3');
+    g_launch_log = te && *te == '3';
     for (int64_t& h : g_hist) h = 0;
     g_nonfinite_trials = 0;
     g_spec_launched = g_spec_used = 0;
@@ -1107,7 +1143,7 @@ int srhip_optimize_constants_starts(srhip_ctx* ctx, const srhip_dataset* ds, srh
               "small %lld/%lld big %lld/%lld\n", (long long)g_items[0][0][0], (long long)g_items[0][0][1],
               (long long)g_items[0][1][0], (long long)g_items[0][1][1], (long long)g_items[1][0][0],
               (long long)g_items[1][0][1], (long long)g_items[1][1][0], (long long)g_items[1][1][1]);
-    if (te && (*te == '1' || *te == '2'))
+    if (te && (*te == '1' || *te == '2' || *te == '3'))
       fprintf(stderr,
               "srhip optim: %.1f ms total (all groups), caller's group: %lld launches, eval_grad %.1f ms (compile/patch "
               "%.1f ms: scan+recompile %.1f, "

@@ -496,3 +496,59 @@ def test_inline_chunk_list_equals_staged_copy(ctx, dtype, monkeypatch):
                                   v.view(np.uint64 if v.itemsize == 8 else np.uint32))
         else:
             assert np.array_equal(u, v)
+
+
+def _bits_equal(u, v):
+    u, v = np.asarray(u), np.asarray(v)
+    if u.dtype.kind == "f":
+        return np.array_equal(u.view(np.uint64 if u.itemsize == 8 else np.uint32),
+                              v.view(np.uint64 if v.itemsize == 8 else np.uint32))
+    return np.array_equal(u, v)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_value_only_screening_is_exact(ctx, dtype, monkeypatch):
+    """Value-only passes evaluate row block 0 of every chunk first (a launch of its own) and skip the
+    other blocks of a chunk whose block-0 check statistic is already non-finite (SRHIP_GRAD_SCREEN,
+    0 = one launch).  Losses and did_succeed are bitwise those of the unscreened pass: a tree that
+    overflows in block 0 (skipped), one that overflows only in a later block (not skipped, still
+    fails), finite trees (unchanged sums); and an optimize_constants run ends identically."""
+    sr = _sr()
+    n = 3000  # 12 row blocks of 256
+    rng = np.random.default_rng(5)
+    X = rng.uniform(-1.0, 1.0, (3, n)).astype(dtype)
+    X[1, 17] = 1000.0    # exp(x1) overflows in block 0
+    X[0, 2100] = 1000.0  # exp(x0) overflows only in block 8
+    y = (X[0] * 0.5 + X[2]).astype(dtype)
+    opts = sr.Options(**OPS)
+    exp_op = opts.unary_operators.index("exp") + 1
+    E = lambda ch: sr.Node(exp_op, ch)  # noqa: E731
+    trees = [sr.Node(3, E(sr.Node(feature=2)), sr.Node(val=1.5)),   # exp(x1) * 1.5: fails in block 0
+             sr.Node(1, E(sr.Node(feature=1)), sr.Node(val=0.25)),  # exp(x0) + 0.25: fails in block 8
+             sr.Node(1, sr.Node(feature=3), sr.Node(val=0.5))]      # x2 + 0.5: finite
+    trees = trees * 3 + sr.random_population(24, opts, 3, dtype, seed=19, max_size=16)
+    nodes, offs = sr.flatten(trees, opts, dtype)
+    ds = sr.DeviceDataset(ctx, X, y)
+    monkeypatch.setenv("SRHIP_GRAD_VALUE_ONLY", "1")
+    res = {}
+    for scr in ("0", "1"):
+        monkeypatch.setenv("SRHIP_GRAD_SCREEN", scr)
+        prog = sr.Program(ctx, nodes, offs, opts, dtype)
+        l, _, ok = prog.eval_loss_grad(ds, sr.L2DistLoss())
+        res[scr] = (np.asarray(l, np.float64), np.asarray(ok))
+        prog.close()
+    assert list(res["1"][1][:3]) == [0, 0, 1], res["1"][1][:3]
+    for u, v in zip(res["0"], res["1"]):
+        assert _bits_equal(u, v)
+    monkeypatch.delenv("SRHIP_GRAD_VALUE_ONLY")
+    opts, _, nodes, offs, X, y = _problem(sr, dtype)
+    ds = sr.DeviceDataset(ctx, X, y)
+    res = {}
+    for scr in ("0", "1"):
+        monkeypatch.setenv("SRHIP_GRAD_SCREEN", scr)
+        prog = sr.Program(ctx, nodes, offs, opts, dtype)
+        out, imp, fc = prog.optimize_constants(ds, sr.L2DistLoss(), iterations=8, nrestarts=1, seed=3)
+        res[scr] = (np.asarray(out, np.float64), imp, fc, np.concatenate(prog.get_constants()))
+        prog.close()
+    for u, v in zip(res["0"], res["1"]):
+        assert _bits_equal(u, v)
