@@ -123,6 +123,9 @@ def main():
     if plan == "launch":  # (an explicit --gpus N > 1 is in argv: every rank re-reads it)
         sys.exit(launch_ranks(n, sys.argv[1:]))
     args.gpus = n
+    # a rank that never joins a library collective ends the run in a minute (the library aborts the
+    # communicator and raises) instead of the default five
+    os.environ.setdefault("SRHIP_COMM_TIMEOUT_S", "60")
     if args.launch_check:
         print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": n,
                           "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
@@ -191,6 +194,19 @@ def main():
     from srhip import parallel
 
     native = _native_comm(ctx, dist)
+    selfcheck = None
+    if native is not None:
+        # the library's RCCL exchange against torch.distributed's on the same payload, once, before the
+        # timed steps: every rank must receive byte-identical migrants from both, else the run uses the
+        # torch exchange (and says so in the line)
+        l0, _ = prog.eval_loss(ds, loss)
+
+        def _cmp():
+            a = native.migrate_topk(nodes, offs, l0, args.migrate_k, 30)
+            b = parallel.migrate_topk(nodes, offs, l0, args.migrate_k, 30)
+            return parallel.same_migrants(a, b)
+
+        native, selfcheck = _native_selfcheck(native, dist, red_dev, _cmp, "migration payload")
 
     # islands: every step's evaluation is followed by the migration exchange of its results (the
     # best args.migrate_k trees of every rank reach every rank: one all_gather_into_tensor over
@@ -327,6 +343,7 @@ def main():
             "collective": None if dist is None else {
                 "op": f"all-gather of each rank's {args.migrate_k} best trees (node tables + losses), "
                       f"in flight during the next step's evaluation",
+                "native_selfcheck": selfcheck,
                 "backend": "rccl (libsrhip srhip_comm_migrate_start/wait)" if native is not None
                            else f"torch.distributed {dist.get_backend()} all_gather_into_tensor",
                 "ranks": world, "calls_per_step": coll_calls / args.steps,
@@ -434,13 +451,40 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
             if i + 1 < npop:
                 p = fut.result()
         pipe = (time.perf_counter() - t0) / npop
+    # (c) two evaluation streams: populations alternate between two contexts (own stream, slabs and
+    # block counter each; the dataset is shared), each served by a host thread that compiles and
+    # evaluates its populations -- one population's host work (compile, upload, launch, decisions)
+    # overlaps the other's kernels, which queue behind each other on the CUs
+    for i in range(npop + 1):
+        _, _, _, _, nd, of = workloads.c2(rank + 3000 + i, args.ntrees, 4096)
+        pops[i] = (nd, of)
+    ctx2 = srhip.Context(ctx.device)
+    ctxs = (ctx, ctx2)
+
+    def serve(k, idxs):
+        for i in idxs:
+            q = srhip.Program(ctxs[k], pops[i][0], pops[i][1], opts, np.float32)
+            q.eval_loss(ds, loss)
+            q.close()
+
+    serve(1, [npop])  # the second context's first launch (allocations) outside the timing
+    with cf.ThreadPoolExecutor(2) as ex:
+        t0 = time.perf_counter()
+        futs = [ex.submit(serve, k, range(k, npop, 2)) for k in (0, 1)]
+        for f in futs:
+            f.result()
+        pipe2 = (time.perf_counter() - t0) / npop
+    ctx2.close()
     return {"populations": npop, "trees_each": args.ntrees,
             "compile_ms_fresh": 1e3 * float(np.median(comp)), "compile_ms_cached": 1e3 * warm,
             "sequential_ms_per_population": 1e3 * float(np.mean(seq)),
             "pipelined_ms_per_population": 1e3 * pipe, "pipeline_fill_ms": 1e3 * fill,
+            "two_stream_ms_per_population": 1e3 * pipe2,
             "note": "compile + upload + srhip_eval_loss per fresh 1024-tree population; pipelined: the next "
                     "population compiled on a host thread during the current evaluation, steady state (the "
-                    "first population's compile is the pipeline's fill, timed apart)"}
+                    "first population's compile is the pipeline's fill, timed apart); two_stream: populations "
+                    "alternate between two contexts served by two host threads (compile + evaluate each), "
+                    "wall time of all populations / npop"}
 
 
 def _native_comm(ctx, dist):
@@ -459,6 +503,26 @@ def _native_comm(ctx, dist):
     except Exception as e:  # pragma: no cover - reported, the torch path takes over
         print(f"[bench] native RCCL communicator unavailable ({e}); using torch.distributed", file=sys.stderr)
         return None
+
+
+def _native_selfcheck(native, dist, red_dev, compare, what):
+    """Run compare() -- the native exchange against torch.distributed's on one payload -- on every rank;
+    keep the native communicator only if every rank saw identical results.  (native or None, note)."""
+    import torch
+
+    try:
+        same = bool(compare())
+        err = None
+    except Exception as e:  # an RCCL error or the library's collective timeout: fall back, reported
+        same, err = False, str(e)
+    flag = torch.tensor([1 if same else 0], dtype=torch.int32, device=red_dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 1:
+        return native, f"native == torch.distributed ({what}, every rank)"
+    native.close()
+    note = f"native != torch.distributed ({what}{': ' + err if err else ''}); torch.distributed exchange used"
+    print(f"[bench] {note}", file=sys.stderr)
+    return None, note
 
 
 def bench_rowshard(args):
@@ -503,6 +567,18 @@ def bench_rowshard(args):
     nfeat = X.shape[0]
 
     native = _native_comm(ctx, dist)
+    selfcheck = None
+    if native is not None:  # the library's sharded evaluation against the torch.distributed path, once
+        red_dev = f"cuda:{local_rank}" if backend == "nccl" else "cpu"
+
+        def _cmp():
+            a = native.eval_loss_sharded(prog, ds, loss)
+            b = parallel.eval_loss_sharded(prog, nfeat, lambda: prog.eval_loss_partials(ds, loss),
+                                           precise=lambda tr: prog.eval_precise_partials(ds, tr))
+            return (np.asarray(a[0], np.float64).tobytes() == np.asarray(b[0], np.float64).tobytes()
+                    and np.array_equal(a[1], b[1]))
+
+        native, selfcheck = _native_selfcheck(native, dist, red_dev, _cmp, "sharded losses and did_succeed")
 
     def step():
         if native is not None:  # srhip_eval_loss_sharded: partials, RCCL all-reduce, decision in the library
@@ -551,6 +627,7 @@ def bench_rowshard(args):
                                  "statistics) on one buffer",
                            "backend": "rccl (libsrhip srhip_eval_loss_sharded)" if native is not None
                                       else f"torch.distributed {dist.get_backend()}", "ranks": world,
+                           "native_selfcheck": selfcheck,
                            "ms_per_step_max_over_ranks": coll_max * 1e3 / args.steps},
         }))
     if native is not None:

@@ -448,6 +448,22 @@ def migrate_topk(nodes: np.ndarray, offsets: np.ndarray, losses: np.ndarray, k: 
     return migrate_topk_async(nodes, offsets, losses, k, max_nodes, group).wait()
 
 
+def same_migrants(a, b) -> bool:
+    """Two migrate_topk results ([(nodes, offsets, losses)] by rank) hold the same trees: node records
+    byte for byte, offsets by value, losses bit for bit (the bench's check of the library's RCCL
+    exchange against the torch.distributed one before it times the native path)."""
+    if len(a) != len(b):
+        return False
+    for (na, oa, la), (nb, ob, lb) in zip(a, b):
+        if np.ascontiguousarray(na).view(np.uint8).tobytes() != np.ascontiguousarray(nb).view(np.uint8).tobytes():
+            return False
+        if not np.array_equal(np.asarray(oa, np.int64), np.asarray(ob, np.int64)):
+            return False
+        if np.asarray(la, np.float64).tobytes() != np.asarray(lb, np.float64).tobytes():
+            return False
+    return True
+
+
 # ---- the native exchanges: libsrhip's RCCL communicator (include/srhip.h srhip_comm_*) -----------
 
 class _NativePending:

@@ -103,3 +103,47 @@ def test_native_allreduce_allgather_world1(comm):
     assert np.array_equal(comm.allreduce_f64(a, "max"), a)
     blob = bytes(range(200))
     assert comm.allgather(blob) == [blob]
+
+
+def test_bench_selfcheck_comparisons_world1(ctx, comm):
+    """The bench's pre-timing check of the library's exchanges against torch.distributed's (bench.py
+    _native_selfcheck) compares like with like: at world size 1 (a one-rank gloo group in this
+    process) the native migration equals parallel.migrate_topk (parallel.same_migrants) and the
+    native sharded evaluation equals parallel.eval_loss_sharded bit for bit."""
+    import socket
+
+    import torch.distributed as dist
+
+    from srhip import parallel
+
+    sr = _sr()
+    opts = sr.Options(binary_operators=("+", "-", "*", "/"), unary_operators=("cos", "exp"))
+    _, nodes, offs = _population(sr, opts, 64, 3, np.float32, seed=21)
+    rng = np.random.default_rng(22)
+    X = rng.standard_normal((3, 5000)).astype(np.float32)
+    y = (X[0] * X[1] - 0.5).astype(np.float32)
+    ds = sr.DeviceDataset(ctx, X, y)
+    prog = sr.Program(ctx, nodes, offs, opts, np.float32)
+    loss = sr.L2DistLoss()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    own = not dist.is_initialized()
+    if own:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        l0, _ = prog.eval_loss(ds, loss)
+        a = comm.migrate_topk(nodes, offs, l0, 12, 30)
+        b = parallel.migrate_topk(nodes, offs, l0, 12, 30)
+        assert parallel.same_migrants(a, b)
+        b2 = [(b[0][0], b[0][1], np.asarray(b[0][2], np.float64) * 2.0)]
+        assert not parallel.same_migrants(a, b2)
+        la, oka = comm.eval_loss_sharded(prog, ds, loss)
+        lb, okb = parallel.eval_loss_sharded(prog, 3, lambda: prog.eval_loss_partials(ds, loss),
+                                             precise=lambda tr: prog.eval_precise_partials(ds, tr))
+        assert np.asarray(la, np.float64).tobytes() == np.asarray(lb, np.float64).tobytes()
+        assert np.array_equal(oka, okb)
+    finally:
+        prog.close()
+        if own:
+            dist.destroy_process_group()
