@@ -420,8 +420,9 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
         p = make(i)
         comp.append(time.perf_counter() - t0)
         p.close()
+    make(0).close()  # the same trees a second time: the cache makes their entries
     t0 = time.perf_counter()
-    p = make(0)  # the same trees again: code-cache hits
+    p = make(0)  # and a third: code-cache hits
     warm = time.perf_counter() - t0
     p.close()
     seq = []
@@ -451,40 +452,56 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
             if i + 1 < npop:
                 p = fut.result()
         pipe = (time.perf_counter() - t0) / npop
-    # (c) two evaluation streams: populations alternate between two contexts (own stream, slabs and
-    # block counter each; the dataset is shared), each served by a host thread that compiles and
-    # evaluates its populations -- one population's host work (compile, upload, launch, decisions)
-    # overlaps the other's kernels, which queue behind each other on the CUs
+    # (c) two evaluation streams: one compile thread builds the populations in order, alternately for
+    # two contexts (own stream, slabs and block counter each; programs upload on the context's upload
+    # stream; the dataset is shared); one host thread per context evaluates its populations.  A
+    # population's launch, wait and decisions overlap the other context's kernels, which queue behind
+    # each other on the CUs.
+    import queue
+
     for i in range(npop + 1):
         _, _, _, _, nd, of = workloads.c2(rank + 3000 + i, args.ntrees, 4096)
         pops[i] = (nd, of)
-    ctx2 = srhip.Context(ctx.device)
-    ctxs = (ctx, ctx2)
+    nstream = max(2, int(os.environ.get("SRHIP_BENCH_STREAMS", "2")))
+    ctxs = [ctx] + [srhip.Context(ctx.device) for _ in range(nstream - 1)]
+    for c in ctxs[1:]:  # each extra context's first launch (allocations) outside the timing
+        q = srhip.Program(c, pops[npop][0], pops[npop][1], opts, np.float32)
+        q.eval_loss(ds, loss)
+        q.close()
+    ready = [queue.Queue() for _ in ctxs]
 
-    def serve(k, idxs):
-        for i in idxs:
-            q = srhip.Program(ctxs[k], pops[i][0], pops[i][1], opts, np.float32)
+    def produce():
+        for i in range(npop):
+            ready[i % nstream].put(srhip.Program(ctxs[i % nstream], pops[i][0], pops[i][1], opts, np.float32))
+        for r in ready:
+            r.put(None)
+
+    def consume(k):
+        while True:
+            q = ready[k].get()
+            if q is None:
+                return
             q.eval_loss(ds, loss)
             q.close()
 
-    serve(1, [npop])  # the second context's first launch (allocations) outside the timing
-    with cf.ThreadPoolExecutor(2) as ex:
+    with cf.ThreadPoolExecutor(1 + nstream) as ex:
         t0 = time.perf_counter()
-        futs = [ex.submit(serve, k, range(k, npop, 2)) for k in (0, 1)]
+        futs = [ex.submit(produce)] + [ex.submit(consume, k) for k in range(nstream)]
         for f in futs:
             f.result()
         pipe2 = (time.perf_counter() - t0) / npop
-    ctx2.close()
+    for c in ctxs[1:]:
+        c.close()
     return {"populations": npop, "trees_each": args.ntrees,
             "compile_ms_fresh": 1e3 * float(np.median(comp)), "compile_ms_cached": 1e3 * warm,
             "sequential_ms_per_population": 1e3 * float(np.mean(seq)),
             "pipelined_ms_per_population": 1e3 * pipe, "pipeline_fill_ms": 1e3 * fill,
-            "two_stream_ms_per_population": 1e3 * pipe2,
+            "two_stream_ms_per_population": 1e3 * pipe2, "streams": nstream,
             "note": "compile + upload + srhip_eval_loss per fresh 1024-tree population; pipelined: the next "
                     "population compiled on a host thread during the current evaluation, steady state (the "
-                    "first population's compile is the pipeline's fill, timed apart); two_stream: populations "
-                    "alternate between two contexts served by two host threads (compile + evaluate each), "
-                    "wall time of all populations / npop"}
+                    "first population's compile is the pipeline's fill, timed apart); two_stream: one compile "
+                    "thread, populations alternating between two contexts each evaluated by its own host "
+                    "thread, wall time of all populations (compile fill included) / npop"}
 
 
 def _native_comm(ctx, dist):

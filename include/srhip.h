@@ -334,6 +334,10 @@ int srhip_program_stats(const srhip_program* prog, int64_t* total_nodes, int64_t
  * min(count, cap) entries as (device unary op << 16) | (feature - 1).  Set SRHIP_NO_DERIVE=1
  * before srhip_program_create to compile without them. */
 int srhip_program_derived(const srhip_program* prog, int32_t* count, uint32_t* spec, int32_t cap);
+/* Process-wide counters of the per-tree code cache used by srhip_program_create (any argument may be
+ * NULL): trees served from the cache, trees compiled, entries made (a tree gets an entry on its
+ * second sighting; SRHIP_CODE_CACHE_EAGER=1: on its first). */
+int srhip_code_cache_stats(int64_t* hits, int64_t* misses, int64_t* inserts);
 
 /* ---- Cross-population request coalescer (8(b) "Threading") ----------------
  * The reference scores one tree per mutation from every population task concurrently

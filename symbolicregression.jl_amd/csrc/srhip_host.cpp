@@ -710,8 +710,16 @@ class HostPool {
 // bytes a compile would produce.  Sharded by hash; a shard that grows past its share of
 // CODE_CACHE_ENTRIES is emptied (the cache holds recent trees: the search's survivors, migrants and
 // re-scored members).  SRHIP_NO_CODE_CACHE=1 bypasses it (read per compile).
+// Entries are made on a tree's SECOND sighting: the first only records its hash in a lossy
+// direct-mapped table of the shard (one 8-byte store), so a population of new trees -- every tree
+// of a fresh population misses -- does not pay for copying ~10 vectors per tree into entries it will
+// never hit (C2's 1024-tree compile, one thread: 7.6 -> ~4.6 ms).  A tree that recurs (survivors,
+// migrants, re-scored members) is cached from its second compile and hits from its third.
+// SRHIP_CODE_CACHE_EAGER=1 makes entries on the first sighting (read per compile).
 constexpr int CODE_CACHE_SHARDS = 64;
 constexpr size_t CODE_CACHE_ENTRIES = 1 << 15;
+constexpr size_t CODE_CACHE_SEEN = 1 << 12;  // first-sighting hashes per shard
+std::atomic<int64_t> g_cache_hits{0}, g_cache_misses{0}, g_cache_inserts{0};
 
 inline uint64_t mix64(uint64_t h) {
   h ^= h >> 33;
@@ -768,18 +776,27 @@ template <typename T> class CodeCache {
   }
   // On a hit, appends the plain code to code (and, with dcode, the derived code to dcode) exactly as
   // TreeCompiler::compile / compile_pair would, fills info / *dinfo / *dmask and returns true.
-  bool lookup(uint64_t h, const srhip_node* nd, int64_t nn, const srhip_program& P, bool sup, TreeInfo& info,
-              std::vector<Ins>& code, TreeInfo* dinfo, std::vector<Ins>* dcode, uint64_t* dmask,
-              std::vector<int32_t>& sig) {
+  // Returns LOOKUP_HIT (filled), LOOKUP_SEEN (a miss whose hash was seen before: compile and insert)
+  // or LOOKUP_NEW (a first sighting, now recorded: compile, do not insert unless eager).
+  enum { LOOKUP_NEW = 0, LOOKUP_HIT = 1, LOOKUP_SEEN = 2 };
+  int lookup(uint64_t h, const srhip_node* nd, int64_t nn, const srhip_program& P, bool sup, TreeInfo& info,
+             std::vector<Ins>& code, TreeInfo* dinfo, std::vector<Ins>* dcode, uint64_t* dmask,
+             std::vector<int32_t>& sig) {
     Shard& s = shards_[h % CODE_CACHE_SHARDS];
     std::lock_guard<std::mutex> lk(s.mu);
     auto it = s.map.find(h);
-    if (it == s.map.end()) return false;
+    if (it == s.map.end()) {
+      const uint64_t hk = h ? h : 1;  // 0 marks an empty slot
+      uint64_t& slot = s.seen[(h / CODE_CACHE_SHARDS) % CODE_CACHE_SEEN];
+      if (slot == hk) return LOOKUP_SEEN;
+      slot = hk;
+      return LOOKUP_NEW;
+    }
     const Entry& e = it->second;
-    if (!same(e, nd, nn, P, sup)) return false;
+    if (!same(e, nd, nn, P, sup)) return LOOKUP_SEEN;  // a hash collision with a cached tree
     if (dinfo) {
       derived_sig(nd, nn, P, sig);
-      if (!e.d || e.d->dbase != P.maxfeat || e.d->dsig != sig) return false;
+      if (!e.d || e.d->dbase != P.maxfeat || e.d->dsig != sig) return LOOKUP_SEEN;
       dinfo->static_fail = e.d->info.static_fail;
       dinfo->need = e.d->info.need;
       dinfo->cost = e.d->info.cost;
@@ -791,7 +808,7 @@ template <typename T> class CodeCache {
     info = e.info;
     info.code_begin = (int32_t)code.size();
     code.insert(code.end(), e.code.begin(), e.code.end());
-    return true;
+    return LOOKUP_HIT;
   }
   void insert(uint64_t h, const srhip_node* nd, int64_t nn, const srhip_program& P, bool sup, const TreeInfo& info,
               const Ins* code, const TreeInfo* dinfo, const Ins* dcode, uint64_t dmask) {
@@ -831,6 +848,7 @@ template <typename T> class CodeCache {
   struct Shard {
     std::mutex mu;
     std::unordered_map<uint64_t, Entry> map;
+    std::vector<uint64_t> seen = std::vector<uint64_t>(CODE_CACHE_SEEN, 0);
   };
   static bool same(const Entry& e, const srhip_node* nd, int64_t nn, const srhip_program& P, bool sup) {
     return e.super == sup && (int64_t)e.nodes.size() == nn && memcmp(e.nodes.data(), nd, (size_t)nn * sizeof(srhip_node)) == 0 &&
@@ -930,27 +948,45 @@ int compile_program_t(srhip_program& P) {
   CodeCache<T>* cache = CodeCache<T>::enabled() ? &CodeCache<T>::get() : nullptr;
   const bool sup = TreeCompiler<T>::super_env();
   const uint64_t oph = cache ? ops_hash(P) ^ (sup ? 0x5u : 0u) : 0;
+  const bool eager = env_flag("SRHIP_CODE_CACHE_EAGER");
   const std::function<void(int)> range = [&](int w) {
     const int32_t t0 = (int32_t)((int64_t)n * w / W), t1 = (int32_t)((int64_t)n * (w + 1) / W);
     TreeCompiler<T> tc(nullptr, 0, P, 0);
     std::vector<int32_t> sig;
+    int64_t nhit = 0, nmiss = 0, nins = 0;
+    struct Count {  // the range's cache counters, added once at its end
+      int64_t &a, &b, &c;
+      ~Count() {
+        g_cache_hits += a;
+        g_cache_misses += b;
+        g_cache_inserts += c;
+      }
+    } count{nhit, nmiss, nins};
     for (int32_t t = t0; t < t1 && !rcs[w]; ++t) {
       const int64_t b = P.offsets[t], e = P.offsets[t + 1];
       const srhip_node* tn = P.nodes.data() + b;
       uint64_t h = 0;
+      bool keep = false;  // make a cache entry of this compile
       if (cache) {
         h = hash_words(tn, (size_t)(e - b) * sizeof(srhip_node), oph ^ (uint64_t)(e - b));
-        if (cache->lookup(h, tn, e - b, P, sup, P.info[t], part[w], der ? &dinfo[t] : nullptr, der ? &dpart[w] : nullptr,
-                          &P.dmask[t], sig))
+        const int lk = cache->lookup(h, tn, e - b, P, sup, P.info[t], part[w], der ? &dinfo[t] : nullptr,
+                                     der ? &dpart[w] : nullptr, &P.dmask[t], sig);
+        if (lk == CodeCache<T>::LOOKUP_HIT) {
+          ++nhit;
           continue;
+        }
+        ++nmiss;
+        keep = eager || lk == CodeCache<T>::LOOKUP_SEEN;
       }
       tc.rebind(tn, e - b);
       const int rc = der ? tc.compile_pair(P.info[t], part[w], &dinfo[t], &dpart[w], &P.dspec, P.maxfeat)
                          : tc.compile(P.info[t], part[w]);
       if (!rc && der) P.dmask[t] = tc.dmask();
-      if (!rc && cache)
+      if (!rc && keep && cache) {
+        ++nins;
         cache->insert(h, tn, e - b, P, sup, P.info[t], part[w].data() + P.info[t].code_begin, der ? &dinfo[t] : nullptr,
                       der ? dpart[w].data() + dinfo[t].code_begin : nullptr, P.dmask[t]);
+      }
       if (rc) {
         errs[w] = "tree " + std::to_string(t) + ": " + g_err;
         rcs[w] = rc;
@@ -2810,6 +2846,13 @@ double srhip_last_kernel_ms(const srhip_ctx* ctx) {
   float ms = -1.0f;
   if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) != hipSuccess) return -1.0;
   return (double)ms;
+}
+
+int srhip_code_cache_stats(int64_t* hits, int64_t* misses, int64_t* inserts) {
+  if (hits) *hits = g_cache_hits.load();
+  if (misses) *misses = g_cache_misses.load();
+  if (inserts) *inserts = g_cache_inserts.load();
+  return SRHIP_OK;
 }
 
 int srhip_last_work(const srhip_ctx* ctx, int64_t* out) {

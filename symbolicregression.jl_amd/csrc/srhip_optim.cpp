@@ -661,8 +661,10 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
   // default 32 slots: a launch of a few trees is latency-bound (one tree x 100k rows fills ~5 % of
   // the wave slots), so a few dozen extra points cost little; more only adds mispredicted work
   const int spec_cap = spe && *spe ? std::max(0, std::min(atoi(spe), 4096)) : 32;
-  constexpr size_t SPEC_MAX_ACTIVE = 64;  // speculate only in the pipeline's tail
-  constexpr int SPEC_MAX_DEPTH = 64;
+  // speculate only in the pipeline's tail (SRHIP_OPTIM_SPEC_ACTIVE, default 64 active trees), at most
+  // SRHIP_OPTIM_SPEC_DEPTH (default 64) points per tree and launch
+  const size_t SPEC_MAX_ACTIVE = (size_t)std::max(0, env_int_opt("SRHIP_OPTIM_SPEC_ACTIVE", 64));
+  const int SPEC_MAX_DEPTH = std::max(1, env_int_opt("SRHIP_OPTIM_SPEC_DEPTH", 64));
   if (P->gspec_cap != spec_cap) {
     P->gspec_cap = spec_cap;  // the next gradient compile allocates the slots (a full compile)
     P->grad_ready = false;

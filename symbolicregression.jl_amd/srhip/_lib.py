@@ -129,6 +129,7 @@ SIGNATURES = {
     "srhip_program_stats": (ctypes.c_int, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
                                            ctypes.POINTER(_i32)]),
     "srhip_program_derived": (ctypes.c_int, [_vp, ctypes.POINTER(_i32), _vp, _i32]),
+    "srhip_code_cache_stats": (ctypes.c_int, [ctypes.POINTER(_i64), ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
 }
 
 _lib = None

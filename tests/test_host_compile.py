@@ -112,10 +112,27 @@ def test_code_cache_hits_equal_fresh_compiles(tmp_path, monkeypatch):
         monkeypatch.delenv("SRHIP_DUMP_CODE")
         return open(path, "rb").read(), open(path + ".plain", "rb").read(), st
 
+    import ctypes
+
+    from srhip import _lib
+
+    def cache_stats():
+        h, m, i = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        assert _lib.load().srhip_code_cache_stats(ctypes.byref(h), ctypes.byref(m), ctypes.byref(i)) == 0
+        return h.value, m.value, i.value
+
     for nosuper in (False, True):
         fresh = dump(nodes, offs, f"fresh{nosuper}", False, nosuper)
-        first = dump(nodes, offs, f"first{nosuper}", True, nosuper)
-        again = dump(nodes, offs, f"again{nosuper}", True, nosuper)
-        assert first == fresh and again == fresh
+        h0 = cache_stats()
+        first = dump(nodes, offs, f"first{nosuper}", True, nosuper)    # first sighting: hashes recorded
+        h1 = cache_stats()
+        again = dump(nodes, offs, f"again{nosuper}", True, nosuper)    # second: compiled, entries made
+        h2 = cache_stats()
+        third = dump(nodes, offs, f"third{nosuper}", True, nosuper)    # third: served from the cache
+        h3 = cache_stats()
+        assert first == fresh and again == fresh and third == fresh
+        assert h1[2] - h0[2] < 512 // 8, "a first sighting makes (almost) no entries"
+        assert h2[2] - h1[2] > 512 // 2, "a second sighting makes entries"
+        assert h3[0] - h2[0] > 512 // 2, "a third compile hits"
     assert dump(nodes, offs, "s", True)[0] != dump(nodes, offs, "n", True, True)[0]
     assert dump(mixed, moffs, "mixc", True) == dump(mixed, moffs, "mixf", False)
