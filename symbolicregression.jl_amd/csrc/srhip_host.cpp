@@ -169,6 +169,17 @@ template <typename T> class TreeCompiler {
     static_checks(0, -1, info);
     rc = emit_program(info, code);
     if (rc || !dinfo) return rc;
+    if (!grad_ && !reads_derived(dspec)) {
+      // no U(X[f]) node of this tree is a derived column: the derived program is the plain one, byte
+      // for byte (every emit decision is the same without a derived column), copied instead of emitted
+      dinfo->static_fail = info.static_fail;
+      dinfo->need = info.need;
+      dinfo->cost = info.cost;
+      dinfo->code_begin = (int32_t)dcode->size();
+      dinfo->code_len = info.code_len;
+      dcode->insert(dcode->end(), code.begin() + info.code_begin, code.begin() + info.code_begin + info.code_len);
+      return SRHIP_OK;
+    }
     const std::vector<uint32_t>* ds0 = dspec_;
     const int db0 = dbase_;
     set_derived(dspec, dbase);
@@ -210,6 +221,18 @@ template <typename T> class TreeCompiler {
     dbase_ = dbase;
   }
   uint64_t dmask() const { return dmask_; }
+  // does some U(X[f]) node of the tree read one of the derived columns dspec lists
+  bool reads_derived(const std::vector<uint32_t>* dspec) const {
+    if (!dspec || dspec->empty()) return false;
+    for (int64_t i = 0; i < nn_; ++i) {
+      const srhip_node& n = nd_[i];
+      if (n.degree != 1 || !leaf_is_feature(n.l)) continue;
+      const uint32_t key = ((uint32_t)classify_unop(unaop(i)) << 16) | (uint32_t)(nd_[n.l].feature - 1);
+      for (uint32_t k : *dspec)
+        if (k == key) return true;
+    }
+    return false;
+  }
   // the value-dependent did_succeed metadata alone (static_fail, fill_consts, feat_checks) of a tree
   // compiled before with other constant values: the gradient program's code does not depend on them
   void static_info(TreeInfo& info) {
