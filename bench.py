@@ -403,17 +403,24 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
     import concurrent.futures as cf
 
     import numpy as np
-    pops = []
-    for i in range(npop + 1):
-        _, _, _, _, nd, of = workloads.c2(rank + 1000 + i, args.ntrees, 4096)
-        pops.append((nd, of))
+
+    # every population set is generated up front: generating one takes host seconds, and a device left
+    # idle that long drops its clocks (the timed sections each start after ~50 ms of evaluations)
+    def gen(seed0):
+        return [workloads.c2(rank + seed0 + i, args.ntrees, 4096)[4:] for i in range(npop + 1)]
+
+    pops, pops_pipe, pops_two = gen(1000), gen(2000), gen(3000)
 
     def make(i):
         return srhip.Program(ctx, pops[i][0], pops[i][1], opts, np.float32)
 
-    p = make(npop)  # warm-up (thread pool, allocations) on a population the timed ones do not share
-    p.eval_loss(ds, loss)
-    p.close()
+    hot = make(npop)  # warm-up (thread pool, allocations) on a population the timed ones do not share
+    hot.eval_loss(ds, loss)
+
+    def steady_clocks():
+        for _ in range(40):
+            hot.eval_loss(ds, loss)
+
     comp = []
     for i in range(npop // 2):
         t0 = time.perf_counter()
@@ -425,6 +432,7 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
     p = make(0)  # and a third: code-cache hits
     warm = time.perf_counter() - t0
     p.close()
+    steady_clocks()
     seq = []
     for i in range(npop // 2, npop):
         t0 = time.perf_counter()
@@ -433,9 +441,8 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
         seq.append(time.perf_counter() - t0)
         p.close()
     # pipelined over fresh populations (new seeds: no cache hits)
-    for i in range(npop + 1):
-        _, _, _, _, nd, of = workloads.c2(rank + 2000 + i, args.ntrees, 4096)
-        pops[i] = (nd, of)
+    pops[:] = pops_pipe
+    steady_clocks()
     with cf.ThreadPoolExecutor(1) as ex:
         # the pipeline's steady state: timed from the moment the first program is ready (its compile is
         # the one-time fill, reported apart) to the last population's results
@@ -459,9 +466,7 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
     # each other on the CUs.
     import queue
 
-    for i in range(npop + 1):
-        _, _, _, _, nd, of = workloads.c2(rank + 3000 + i, args.ntrees, 4096)
-        pops[i] = (nd, of)
+    pops[:] = pops_two
     nstream = max(2, int(os.environ.get("SRHIP_BENCH_STREAMS", "2")))
     ctxs = [ctx] + [srhip.Context(ctx.device) for _ in range(nstream - 1)]
     for c in ctxs[1:]:  # each extra context's first launch (allocations) outside the timing
@@ -484,6 +489,7 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
             q.eval_loss(ds, loss)
             q.close()
 
+    steady_clocks()
     with cf.ThreadPoolExecutor(1 + nstream) as ex:
         t0 = time.perf_counter()
         futs = [ex.submit(produce)] + [ex.submit(consume, k) for k in range(nstream)]
@@ -492,6 +498,7 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
         pipe2 = (time.perf_counter() - t0) / npop
     for c in ctxs[1:]:
         c.close()
+    hot.close()
     return {"populations": npop, "trees_each": args.ntrees,
             "compile_ms_fresh": 1e3 * float(np.median(comp)), "compile_ms_cached": 1e3 * warm,
             "sequential_ms_per_population": 1e3 * float(np.mean(seq)),
