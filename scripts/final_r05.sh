@@ -48,4 +48,8 @@ step coalescer
 SECONDS_PER_RUN=3 timeout -k 10 200 python -u scripts/coalescer_native.py c3 16 64 > $F/coalescer_c3.jsonl 2>&1 || exit $?
 SECONDS_PER_RUN=3 timeout -k 10 200 python -u scripts/coalescer_native.py c1 1 16 64 > $F/coalescer_c1.jsonl 2>&1 || exit $?
 SPLITS=3 NO_TRACE=1 bash scripts/c4_diag.sh > $F/c4_diag.log 2>&1 || exit $?
+step probes
+timeout -k 10 200 python -u scripts/compile_probe.py > $F/compile_probe.json 2> $F/compile_probe.err || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace -d $F/c4trace -o run --output-format csv -- python3 bench.py --config c4 --steps 1 --warmup 1 --no-cpu > $F/c4trace.log 2>&1 || exit $?
+python3 scripts/c4_trace.py $F/c4trace/run_kernel_trace.csv --json $F/c4_trace.json > /dev/null || exit $?
 echo done
