@@ -1,12 +1,13 @@
 """Where a C4 optimize_constants call spends the device (rocprofv3 kernel trace of `bench.py --config c4`).
     python scripts/c4_trace.py run_kernel_trace.csv [--json out.json]
-Takes the last optimize_constants call in the trace (the span after the largest idle gap before the
-last burst), then reports: wall span, device-busy time (union of kernel intervals over all queues),
+Takes the last optimize_constants call in the trace (from the interpreter launch of its baseline
+evaluation to that of its final one), then reports: wall span, device-busy time (union of kernel intervals over all queues),
 kernel time by kernel name and by grid-size class, and the idle gaps (count and sum) between
 consecutive kernels of each queue."""
 import collections
 import csv
 import json
+import re
 import sys
 
 
@@ -21,13 +22,14 @@ def load(path):
     return ev
 
 
-def last_call(ev, gap_ns=20e6):
-    # optimize_constants calls are separated by host work (bench bookkeeping, restarts): split at gaps
-    cut = 0
-    for i in range(1, len(ev)):
-        if ev[i]["s"] - max(x["e"] for x in ev[max(0, i - 64):i]) > gap_ns:
-            cut = i
-    return ev[cut:]
+def last_call(ev):
+    # every optimize_constants call starts and ends with an evaluation of the population by the
+    # interpreter (the baseline losses, the returned trees' losses): the last call is the span from the
+    # second-to-last interpreter launch over the whole population to the last one
+    big = [i for i, x in enumerate(ev) if re.search(r"eval_kernel<double, \d+, \d+, 0,", x["name"])]
+    if len(big) < 2:
+        return ev
+    return ev[big[-2]:big[-1] + 1]
 
 
 def union(iv):
