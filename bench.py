@@ -451,13 +451,18 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
         p = fut.result()
         t0 = time.perf_counter()
         fill = t0 - tf
+        ph_eval, ph_wait = [], []
         for i in range(npop):
             if i + 1 < npop:
                 fut = ex.submit(make, i + 1)
+            ta = time.perf_counter()
             p.eval_loss(ds, loss)
             p.close()
+            tb = time.perf_counter()
             if i + 1 < npop:
                 p = fut.result()
+            ph_eval.append(tb - ta)
+            ph_wait.append(time.perf_counter() - tb)
         pipe = (time.perf_counter() - t0) / npop
     # (c) two evaluation streams: one compile thread builds the populations in order, alternately for
     # two contexts (own stream, slabs and block counter each; programs upload on the context's upload
@@ -503,6 +508,8 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
             "compile_ms_fresh": 1e3 * float(np.median(comp)), "compile_ms_cached": 1e3 * warm,
             "sequential_ms_per_population": 1e3 * float(np.mean(seq)),
             "pipelined_ms_per_population": 1e3 * pipe, "pipeline_fill_ms": 1e3 * fill,
+            "pipelined_phases_ms": {"eval_close": 1e3 * float(np.median(ph_eval)),
+                                    "wait_next": 1e3 * float(np.median(ph_wait))},
             "two_stream_ms_per_population": 1e3 * pipe2, "streams": nstream,
             "note": "compile + upload + srhip_eval_loss per fresh 1024-tree population; pipelined: the next "
                     "population compiled on a host thread during the current evaluation, steady state (the "
