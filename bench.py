@@ -401,6 +401,7 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
     compiled on a host thread while population i evaluates (both calls release the interpreter
     lock) -- plus the compile of a population seen before (per-tree code-cache hits)."""
     import concurrent.futures as cf
+    import gc
 
     import numpy as np
 
@@ -432,6 +433,10 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
     p = make(0)  # and a third: code-cache hits
     warm = time.perf_counter() - t0
     p.close()
+    # the timed sections run with the interpreter's cyclic garbage collector paused (as timeit does): a
+    # full collection over the process's objects is a ~10 ms pause unrelated to the workload
+    gc.collect()
+    gc.disable()
     steady_clocks()
     seq = []
     for i in range(npop // 2, npop):
@@ -501,6 +506,7 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
         for f in futs:
             f.result()
         pipe2 = (time.perf_counter() - t0) / npop
+    gc.enable()
     for c in ctxs[1:]:
         c.close()
     hot.close()
@@ -509,9 +515,10 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
             "sequential_ms_per_population": 1e3 * float(np.mean(seq)),
             "pipelined_ms_per_population": 1e3 * pipe, "pipeline_fill_ms": 1e3 * fill,
             "pipelined_phases_ms": {"eval_close": 1e3 * float(np.median(ph_eval)),
-                                    "wait_next": 1e3 * float(np.median(ph_wait))},
+                                    "wait_next": 1e3 * float(np.median(ph_wait)),
+                                    "iterations": [round(1e3 * (a + b), 3) for a, b in zip(ph_eval, ph_wait)]},
             "two_stream_ms_per_population": 1e3 * pipe2, "streams": nstream,
-            "note": "compile + upload + srhip_eval_loss per fresh 1024-tree population; pipelined: the next "
+            "note": "compile + upload + srhip_eval_loss per fresh 1024-tree population (the Python garbage collector paused in the timed sections); pipelined: the next "
                     "population compiled on a host thread during the current evaluation, steady state (the "
                     "first population's compile is the pipeline's fill, timed apart); two_stream: one compile "
                     "thread, populations alternating between two contexts each evaluated by its own host "

@@ -1786,6 +1786,49 @@ struct ShardDev {
   bool persistent = false;
 };
 
+// The device-listed precise pass, enqueued on the context's stream: the plain program over the trees
+// of the device list ulist ([count, trees ...], count read by the launch, at most G of them), one tree
+// group per entry, one-tile row blocks and one-wave workgroups -- every (tree, tile) of the few listed
+// trees on a wave of its own -- K_MAX, global reads; then the double-double reduction of the per-block
+// operator sums into the context's coherent h_pout ([count, list ..., sums]), which also clears the list.
+static int enqueue_dev_precise(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const View& v,
+                               int32_t* ulist, int G, int* out_stride) {
+  const int dtype = P->dtype;
+  const int stride = std::max(1, P->max_ops);
+  const int Rp = pick_rows_per_lane(dtype, K_MAX, MODE_PRECISE, v.m);
+  LaunchPlan Lp = plan_launch(ctx, dtype, ds->nfeat, false, false, v.m, G, 64 * Rp);
+  Lp.rb_rows = 64 * Rp;
+  Lp.nrb = (int)((v.m + Lp.rb_rows - 1) / Lp.rb_rows);
+  HIP_TRY(ctx->slab_prec.ensure((size_t)G * stride * Lp.nrb * sizeof(double)));
+  HIP_TRY(ctx->h_pout.ensure((size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t) +
+                             (size_t)DEV_PRECISE_MAX * stride * sizeof(double), hipHostMallocCoherent));
+  EvalArgs q{};
+  q.code = P->code_dev;
+  q.prog_off = P->off_dev;
+  q.order = ulist + 1;
+  q.X = v.X;
+  q.ld = v.ld;
+  q.nvalid = v.m;
+  q.ntrees = G;
+  q.nfeat = (int32_t)ds->nfeat;
+  q.rb_rows = Lp.rb_rows;
+  q.nrb = Lp.nrb;
+  q.trees_per_group = 1;
+  q.slab_prec = ctx->slab_prec.p;
+  q.prec_stride = stride;
+  q.max_steps = P->max_len;
+  q.dev_count = ulist;
+  q.wg_waves = 1;
+  q.prec_assign = 1;  // one-tile row blocks
+  HIP_TRY(launch_eval(dtype, q, Rp, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, G), 16, ctx->stream));
+  int32_t* hl = (int32_t*)ctx->h_pout.p;
+  double* hs = (double*)((uint8_t*)ctx->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
+  HIP_TRY(launch_precise_reduce((const double*)ctx->slab_prec.p, Lp.nrb, stride, ulist, G, DEV_PRECISE_MAX, hl, hs,
+                                ctx->stream));
+  *out_stride = stride;
+  return SRHIP_OK;
+}
+
 static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
                          const View& v, void* out_pred, double* sums, double* chk, DevPrecise* dp = nullptr,
                          ShardDev* sd = nullptr) {
@@ -2104,42 +2147,9 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
                           dtype == SRHIP_I32 ? nullptr : (sd ? sd->d_chk : ctx->h_chk.p), ctx->stream, a.slab_rows,
                           (int64_t*)ctx->h_rows.p, ul, sd != nullptr));
   if (devp) {
-    // the precise pass over the device's list (capped; its launch reads the count): the plain program,
-    // K_MAX, global reads -- eval_precise's launch with the list as the tree order
-    const int stride = std::max(1, P->max_ops);
-    const int Rp = pick_rows_per_lane(dtype, K_MAX, MODE_PRECISE, v.m);
-    // one tree group per list entry (the listed trees side by side), one-tile row blocks and one-wave
-    // workgroups: every (tree, tile) of the few listed trees on a wave of its own
-    const int G = ul.umax;
-    LaunchPlan Lp = plan_launch(ctx, dtype, ds->nfeat, false, false, v.m, G, 64 * Rp);
-    Lp.rb_rows = 64 * Rp;
-    Lp.nrb = (int)((v.m + Lp.rb_rows - 1) / Lp.rb_rows);
-    HIP_TRY(ctx->slab_prec.ensure((size_t)G * stride * Lp.nrb * sizeof(double)));
-    HIP_TRY(ctx->h_pout.ensure((size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t) +
-                               (size_t)DEV_PRECISE_MAX * stride * sizeof(double), hipHostMallocCoherent));
-    EvalArgs q{};
-    q.code = P->code_dev;
-    q.prog_off = P->off_dev;
-    q.order = ul.ulist + 1;
-    q.X = v.X;
-    q.ld = v.ld;
-    q.nvalid = v.m;
-    q.ntrees = G;
-    q.nfeat = (int32_t)ds->nfeat;
-    q.rb_rows = Lp.rb_rows;
-    q.nrb = Lp.nrb;
-    q.trees_per_group = 1;
-    q.slab_prec = ctx->slab_prec.p;
-    q.prec_stride = stride;
-    q.max_steps = P->max_len;
-    q.dev_count = ul.ulist;
-    q.wg_waves = 1;
-    q.prec_assign = 1;  // one-tile row blocks
-    HIP_TRY(launch_eval(dtype, q, Rp, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, G), 16, ctx->stream));
-    int32_t* hl = (int32_t*)ctx->h_pout.p;
-    double* hs = (double*)((uint8_t*)ctx->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
-    HIP_TRY(launch_precise_reduce((const double*)ctx->slab_prec.p, Lp.nrb, stride, ul.ulist, G, DEV_PRECISE_MAX, hl, hs,
-                                  ctx->stream));
+    int stride = 1;
+    const int rc = enqueue_dev_precise(ctx, ds, P, v, ul.ulist, ul.umax, &stride);
+    if (rc) return rc;
     dp->used = true;
     dp->stride = stride;
   }
@@ -2356,6 +2366,36 @@ int srhip::run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program
       lossv[t] = uok ? sums[2 * (size_t)t] / sums[2 * (size_t)t + 1] : INFINITY;
     }
     unc.swap(rest);
+  }
+  // trees past the device list's capacity (a program's first evaluation lists at most 4): the same
+  // device-listed pass over a host-written list, DEV_PRECISE_MAX trees at a time -- every undecided
+  // tree of a device evaluation is then settled by one summation path (SRHIP_PRECISE_OVERFLOW_HOST=1:
+  // the host-launched pass of eval_precise instead)
+  if (dp.used && !unc.empty() && !env_flag("SRHIP_PRECISE_OVERFLOW_HOST")) {
+    for (size_t b = 0; b < unc.size(); b += DEV_PRECISE_MAX) {
+      const int32_t n = (int32_t)std::min<size_t>(DEV_PRECISE_MAX, unc.size() - b);
+      std::vector<int32_t> lst(1 + n);
+      lst[0] = n;
+      std::copy(unc.begin() + b, unc.begin() + b + n, lst.begin() + 1);
+      HIP_TRY(hipMemcpyAsync(ctx->d_ulist.p, lst.data(), lst.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                             ctx->stream));
+      int stride = 1;
+      rc = enqueue_dev_precise(ctx, ds, P, v, (int32_t*)ctx->d_ulist.p, n, &stride);
+      if (rc) return rc;
+      rc = stream_wait(ctx);
+      if (rc) return rc;
+      const int32_t* hl = (const int32_t*)ctx->h_pout.p;
+      const double* hs = (const double*)((const uint8_t*)ctx->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
+      if (hl[0] != n) return fail(SRHIP_ERR_DEVICE, "precise pass listed %d of %d trees", (int)hl[0], (int)n);
+      for (int32_t u = 0; u < n; ++u) {
+        const int32_t t = hl[1 + u];
+        uint8_t uok = 0;
+        finalize_precise(*P, &t, 1, hs + (size_t)u * stride, &uok);
+        ok[t] = uok;
+        lossv[t] = uok ? sums[2 * (size_t)t] / sums[2 * (size_t)t + 1] : INFINITY;
+      }
+    }
+    unc.clear();
   }
   if (!unc.empty()) {
     const int stride = std::max(1, P->max_ops);

@@ -4,7 +4,9 @@ check statistic puts the tree in the undecided band, and the sum lands just belo
 (fails) the threshold of the type, alternating over the population.  The device-listed pass (one
 tree group per listed tree) and the host-launched pass for trees past the list's capacity (the
 first evaluation of a program lists at most 4) must both give the oracle's mask, evaluation after
-evaluation -- including four trees within the sums' own precision of the threshold."""
+evaluation -- including four trees within the sums' own precision of the threshold.  Trees past the first
+evaluation's list capacity go through the same device pass over a host-written list (or, with
+SRHIP_PRECISE_OVERFLOW_HOST=1, the host-launched pass)."""
 import numpy as np
 import pytest
 
@@ -19,8 +21,13 @@ def _sr():
     return srhip
 
 
+@pytest.mark.parametrize("overflow", ["device", "host"])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_precise_pass_near_threshold_matches_oracle(ctx, oracle, dtype):
+def test_precise_pass_near_threshold_matches_oracle(ctx, oracle, dtype, overflow, monkeypatch):
+    """Trees past the device list's capacity take the device-listed pass over a host-written list
+    (default) or the host-launched pass (SRHIP_PRECISE_OVERFLOW_HOST=1): both give the oracle's mask."""
+    if overflow == "host":
+        monkeypatch.setenv("SRHIP_PRECISE_OVERFLOW_HOST", "1")
     sr = _sr()
     n = 1_000_000
     rng = np.random.default_rng(17)
