@@ -64,3 +64,42 @@ def test_world_size_mismatch_fails():
     r = _run(["--gpus", "2", "--launch-check"], {"WORLD_SIZE": "3", "RANK": "0"})
     assert r.returncode != 0
     assert "WORLD_SIZE=3" in r.stderr
+
+
+def test_native_selfcheck_keeps_or_drops_the_native_exchange():
+    """bench._native_selfcheck: the native communicator stays only if every rank's comparison with the
+    torch.distributed exchange passed; a mismatch or an exception closes it and reports why (a
+    one-rank gloo group in this process stands in for the ranks)."""
+    import socket
+
+    import torch.distributed as dist
+
+    class Fake:
+        closed = False
+
+        def close(self):
+            self.closed = True
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    own = not dist.is_initialized()
+    if own:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        f = Fake()
+        kept, note = bench._native_selfcheck(f, dist, "cpu", lambda: True, "payload")
+        assert kept is f and not f.closed and note.startswith("native == torch.distributed")
+        f = Fake()
+        kept, note = bench._native_selfcheck(f, dist, "cpu", lambda: False, "payload")
+        assert kept is None and f.closed and "torch.distributed exchange used" in note
+
+        def boom():
+            raise RuntimeError("collective timed out")
+
+        f = Fake()
+        kept, note = bench._native_selfcheck(f, dist, "cpu", boom, "payload")
+        assert kept is None and f.closed and "collective timed out" in note
+    finally:
+        if own:
+            dist.destroy_process_group()
