@@ -43,10 +43,11 @@ template <int U> constexpr bool dun_inline() {
          U == UN_ROUND || U == UN_FLOOR || U == UN_CEIL;
 }
 
-// f(x) and f'(x) for a heavy unary operator U (one out-of-line body per (T, U, D)); D = false: the
-// value alone (value-only passes: the derivative of cos is a sin, of log a division -- out of line the
-// compiler cannot drop them), the same f
-template <typename T, int U, bool D> __device__ __attribute__((noinline)) typename V2<T>::type dual_un_heavy(T x) {
+// f(x) and f'(x) for a heavy unary operator U; D = false: the value alone (value-only passes: the
+// derivative of cos is a sin, of log a division -- out of line the compiler cannot drop them), the
+// same f.  Out of line per (T, U, D) (dual_un_heavy), and for value-only passes once per R rows
+// (dual_un_heavy_rows: one call per node and tile instead of R, the same body per row)
+template <typename T, int U, bool D> DI typename V2<T>::type dual_un_body(T x) {
   using O = FOps<T>;
   T f = T(0), df = T(0);
   switch (U) {
@@ -107,6 +108,26 @@ template <typename T, int U, bool D> __device__ __attribute__((noinline)) typena
   r[0] = f;
   r[1] = df;
   return r;
+}
+template <typename T, int U, bool D> __device__ __attribute__((noinline)) typename V2<T>::type dual_un_heavy(T x) {
+  return dual_un_body<T, U, D>(x);
+}
+template <typename T, int R> struct VR { typedef T type __attribute__((ext_vector_type(R))); };
+template <typename T> struct VR<T, 1> { typedef T type; };
+#ifndef GRAD_ROWS_FENCE
+#define GRAD_ROWS_FENCE 1  // rows of dual_un_heavy_rows one after another (no interleaving)
+#endif
+template <typename T, int U, int R>
+__device__ __attribute__((noinline)) typename VR<T, R>::type dual_un_heavy_rows(typename VR<T, R>::type x) {
+  if constexpr (R == 1) {
+    return dual_un_body<T, U, false>(x)[0];
+  } else {
+    UNR for (int r = 0; r < R; ++r) {
+      x[r] = dual_un_body<T, U, false>(x[r])[0];
+      if (GRAD_ROWS_FENCE) __builtin_amdgcn_sched_barrier(0);
+    }
+    return x;
+  }
 }
 
 template <typename T, int U, bool D = true> DI void dual_un(T x, T& f, T& df) {
@@ -438,6 +459,15 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
 #undef GK_HEAVY
 #define GK_UN(NAME, FN)                                                                            \
   case h_un(UN_##NAME): {                                                                          \
+    if constexpr (KT == 0 && !dun_inline<UN_##NAME>()) {                                           \
+      typename VR<T, R>::type xv;                                                                  \
+      if constexpr (R == 1) xv = A[0].v;                                                           \
+      else { UNR for (int r = 0; r < R; ++r) xv[r] = A[r].v; }                                     \
+      xv = dual_un_heavy_rows<T, UN_##NAME, R>(xv);                                                \
+      if constexpr (R == 1) { A[0].v = xv; chk_fold(M, A[0].v); }                                  \
+      else { UNR for (int r = 0; r < R; ++r) { A[r].v = xv[r]; chk_fold(M, A[r].v); } }            \
+      break;                                                                                       \
+    }                                                                                              \
     RR(T f, df; dual_un<T, UN_##NAME, (KT > 0)>(A[r].v, f, df);                                              \
        A[r].v = f;                                                                                 \
        UNR for (int j = 0; j < KT; ++j) A[r].d[j] = df * A[r].d[j];                                \
