@@ -1050,7 +1050,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
   using O = OpsT<T>;
   using CT = typename Chk<T>::type;
   constexpr int TILE = 64 * R;
-  const int lane = threadIdx.x & 63;
+  const int lane = tid_x() & 63;  // (opaque: rematerialised instead of spilled across the block loop)
   const int64_t row_base = (int64_t)rb * p.rb_rows;
   const int ntiles = p.rb_rows / TILE;
   // valid rows of this block, block-relative (<= rb_rows): the tile loop's uniform row tests are

@@ -91,6 +91,12 @@ const char* srhip::env_get(const char* name) {
   return v;
 }
 
+#ifndef SRHIP_COS_NC
+// cos / sin of an operator output as the unchecked H_COS_NC / H_SIN_NC handlers (0: the checked form;
+// C2 same box: 1.263 against 1.267 ms, profiles/r05_c2_scratch_g23/)
+#define SRHIP_COS_NC 1
+#endif
+
 // ---------------------------------------------------------------------------------------------
 // tree compiler
 // ---------------------------------------------------------------------------------------------
@@ -545,7 +551,7 @@ template <typename T> class TreeCompiler {
       const int u = classify_unop(unaop(i));
       // cos / sin of an operator output need no check fold of their own (srhip_isa.h H_UNNC0); the
       // gradient program keeps every fold
-      const bool nc = !grad_ && !leafish(n.l) && (u == UN_COS || u == UN_SIN);
+      const bool nc = SRHIP_COS_NC && !grad_ && !leafish(n.l) && (u == UN_COS || u == UN_SIN);
       push_op(nc ? (u == UN_COS ? H_COS_NC : H_SIN_NC) : h_un(u), 0, 0, i, parent);
       return;
     }
