@@ -1344,24 +1344,16 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
   SRHIP_HOTU_##NAME case h_un(UN_##NAME):                                        \
     if constexpr (un_ok<T>(UN_##NAME) && (K == K_MAX || !un_wide(UN_##NAME))) {  \
       apply_un<T, R, UN_##NAME>(A);                                              \
-      chk_update<R>(M, A);                                                       \
+      if constexpr (UN_##NAME == UN_COS || UN_##NAME == UN_SIN) {                \
+        if (!(ins.a & UN_NC_FLAG)) chk_update<R>(M, A);                          \
+      } else {                                                                   \
+        chk_update<R>(M, A);                                                     \
+      }                                                                          \
       if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0); \
     }                                                                            \
     break;
           SRHIP_UNOPS(SRHIP_UN_CASE)
 #undef SRHIP_UN_CASE
-          SRHIP_LK case H_COS_NC:
-            if constexpr (un_ok<T>(UN_COS)) {
-              apply_un<T, R, UN_COS>(A);
-              if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);
-            }
-            break;
-          SRHIP_LK case H_SIN_NC:
-            if constexpr (un_ok<T>(UN_SIN)) {
-              apply_un<T, R, UN_SIN>(A);
-              if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);
-            }
-            break;
 #undef SRHIP_K_CASES
           default: break;
         }

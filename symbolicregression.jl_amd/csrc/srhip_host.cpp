@@ -92,7 +92,7 @@ const char* srhip::env_get(const char* name) {
 }
 
 #ifndef SRHIP_COS_NC
-// cos / sin of an operator output as the unchecked H_COS_NC / H_SIN_NC handlers (0: the checked form;
+// cos / sin of an operator output without their check fold (srhip_isa.h UN_NC_FLAG; 0: the checked form;
 // C2 same box: 1.263 against 1.267 ms, profiles/r05_c2_scratch_g23/)
 #define SRHIP_COS_NC 1
 #endif
@@ -125,7 +125,6 @@ static double op_cost(uint32_t h) {
     return sb == SB_DIV ? 10.0 : 2.0;
   }
   if (h < H_UN0) return 120.0;
-  if (h >= H_UNNC0) return 30.0;  // cos / sin without the check fold
   const int u = h - H_UN0;
   switch (u) {
     case UN_NEG: case UN_SQUARE: case UN_CUBE: case UN_ABS: case UN_RELU: case UN_SIGN:
@@ -549,10 +548,10 @@ template <typename T> class TreeCompiler {
     if (n.degree == 1) {
       emit(n.l, base, i);
       const int u = classify_unop(unaop(i));
-      // cos / sin of an operator output need no check fold of their own (srhip_isa.h H_UNNC0); the
+      // cos / sin of an operator output need no check fold of their own (srhip_isa.h UN_NC_FLAG); the
       // gradient program keeps every fold
       const bool nc = SRHIP_COS_NC && !grad_ && !leafish(n.l) && (u == UN_COS || u == UN_SIN);
-      push_op(nc ? (u == UN_COS ? H_COS_NC : H_SIN_NC) : h_un(u), 0, 0, i, parent);
+      push_op(h_un(u), nc ? UN_NC_FLAG : 0, 0, i, parent);
       return;
     }
     int sb, hb;

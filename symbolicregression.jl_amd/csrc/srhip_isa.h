@@ -90,12 +90,13 @@ constexpr uint32_t SPEC_AF = 0, SPEC_FA = 1, SPEC_AC = 2, SPEC_CA = 3, SPEC_SA0 
 constexpr uint32_t HEAVY_SA0 = 0, HEAVY_AS0 = K_MAX, HEAVY_STRIDE = 2 * K_MAX;
 constexpr uint32_t H_HEAVY0 = H_BIN0 + NUM_SPEC_BIN * SPEC_STRIDE;
 constexpr uint32_t H_UN0 = H_HEAVY0 + NUM_HEAVY_BIN * HEAVY_STRIDE;
-// cos / sin whose operand is an operator output, without the check fold: |cos|, |sin| <= 1, and a
-// non-finite result needs a non-finite operand, which the operand's own instruction folded (the
-// host emits these only for that case; a feature-leaf operand keeps the checked form)
-constexpr uint32_t H_UNNC0 = H_UN0 + NUM_UNOP;
-constexpr uint32_t H_COS_NC = H_UNNC0, H_SIN_NC = H_UNNC0 + 1;
-constexpr uint32_t H_COUNT = H_UNNC0 + 2;
+constexpr uint32_t H_COUNT = H_UN0 + NUM_UNOP;
+// operand flag of a cos / sin instruction whose operand is an operator output: no check fold of its
+// own -- |cos|, |sin| <= 1, and a non-finite result needs a non-finite operand, which the operand's
+// own instruction folded (the host sets it only for that case; a feature-leaf operand keeps the
+// checked form).  A flag, not a handler of its own: one call site per operator in the interpreter
+// (round 5: the separate handlers' call site carried a 64-byte register spill on its dispatch path)
+constexpr uint32_t UN_NC_FLAG = 0x8000;
 
 constexpr uint32_t h_spec(int sb, uint32_t form) { return H_BIN0 + uint32_t(sb) * SPEC_STRIDE + form; }
 constexpr uint32_t h_heavy(int hb, uint32_t form) { return H_HEAVY0 + uint32_t(hb) * HEAVY_STRIDE + form; }
