@@ -43,11 +43,6 @@ struct GradArgs {
   // launch on the stream) already holds a non-finite check statistic is skipped -- its tree fails
   // did_succeed whatever the other blocks hold
   int32_t screened;
-  // GMODE_LOSS record folding: workgroup x (< GRAD_FOLD) evaluates row blocks x, x + GRAD_FOLD, ...
-  // in turn and accumulates each chunk's records in LDS in that order -- grad_reduce_kernel's lane-x
-  // accumulation -- writing ONE record per (chunk, x): the slab is [nchunks][GRAD_FOLD][KT + 2] and
-  // the reduction runs over GRAD_FOLD entries, with the same bits
-  int32_t fold;
   // per-row modes: out_der[row + j][nvalid] for the components c0 + j < end (the values come from the
   // evaluator, which also decides did_succeed)
   void* out_der;
@@ -56,7 +51,6 @@ struct GradArgs {
   int32_t inl[2 * 96];
 };
 constexpr int GRAD_INLINE = 96;  // (448 measured the same on C4)
-constexpr int GRAD_FOLD = 64;    // grad_reduce_kernel's lanes: one folded record per lane
 // a chunk is a (tree, c0) pair: the inline list holds GRAD_INLINE of them
 static_assert(2 * GRAD_INLINE == sizeof(GradArgs::inl) / sizeof(int32_t), "inline chunk list size");
 static_assert(sizeof(GradArgs) <= 4096, "kernel arguments are limited to 4 KB");

@@ -320,13 +320,11 @@ template <typename T, int KT, int K, int GM, bool XLDS, int R>
 __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   constexpr int CW = GM == GMODE_LOSS ? 2 : 4;  // ints per chunk record
   const int lane = threadIdx.x & 63;
-  const bool fold = GM == GMODE_LOSS && p.fold;
-  // the row block in hand: blockIdx.x (+ block0), or with folding blockIdx.x, + GRAD_FOLD, ... in turn
-  int rb = blockIdx.x + p.block0;
-  int64_t row_base = (int64_t)rb * p.rb_rows;
+  const int rb = blockIdx.x + p.block0;
+  const int64_t row_base = (int64_t)rb * p.rb_rows;
   const int ntiles = p.rb_rows / (64 * R);
   // valid rows of this block, block-relative: the row tests below are 32-bit (scalar for the tile test)
-  int nrel = __builtin_amdgcn_readfirstlane((int)min<int64_t>(max<int64_t>(p.nvalid - row_base, 0), (int64_t)p.rb_rows));
+  const int nrel = __builtin_amdgcn_readfirstlane((int)min<int64_t>(max<int64_t>(p.nvalid - row_base, 0), (int64_t)p.rb_rows));
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int group_base = blockIdx.y * p.chunks_per_group;
   const int group_n = min(p.chunks_per_group, p.nchunks - group_base);
@@ -341,17 +339,6 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   // chunk of each other (a static round-robin left the cost spread idle at every workgroup's end);
   // every (chunk, row block) record is computed by one wave as before, so the bits do not change
   __shared__ int next_chunk;
-  // folding: the chunks' accumulated records, [group chunk][KT + 2], after the staged block
-  double* facc = reinterpret_cast<double*>(grad_lds + (XLDS ? ((size_t)(p.nfeat + 1) * rbr * sizeof(T) + 7) / 8 * 8 : 0));
-  for (int bi = 0;; ++bi) {
-  if (bi > 0) {
-    if (!fold) break;
-    rb = blockIdx.x + GRAD_FOLD * bi;
-    if (rb >= p.nrb) break;
-    row_base = (int64_t)rb * p.rb_rows;
-    nrel = __builtin_amdgcn_readfirstlane((int)min<int64_t>(max<int64_t>(p.nvalid - row_base, 0), (int64_t)p.rb_rows));
-    __syncthreads();  // every wave is done with the previous block's rows and claims
-  }
   if (threadIdx.x == 0) next_chunk = GRAD_WAVES;
   if constexpr (XLDS) {
     const int nf = p.nfeat;
@@ -545,29 +532,10 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
     level(std::integral_constant<int, 2>());
     level(std::integral_constant<int, 1>());
     if (lane == 0) {
-      if (fold) {
-        // grad_reduce_kernel's lane accumulation of this workgroup's blocks, in block order from 0.0
-        // (its check statistic by the NaN-propagating max for Float32, a sum for Float64)
-        double* a = facc + (int64_t)ci * (KT + 2);
-        const bool first = bi == 0;
-        a[0] = (first ? 0.0 : a[0]) + lacc;
-        UNR for (int j = 0; j < KT; ++j) a[1 + j] = (first ? 0.0 : a[1 + j]) + gacc[j];
-        if constexpr (sizeof(T) == 4) a[KT + 1] = __builtin_elementwise_maximum(first ? 0.0 : a[KT + 1], (double)M);
-        else a[KT + 1] = (first ? 0.0 : a[KT + 1]) + (double)M;
-      } else {
-        double* out = p.slab + ((int64_t)chunk * p.nrb + rb) * (KT + 2);
-        out[0] = lacc;
-        UNR for (int j = 0; j < KT; ++j) out[1 + j] = gacc[j];
-        out[KT + 1] = (double)M;
-      }
-    }
-  }
-  }  // row blocks
-  if (fold) {  // one record per (chunk, fold lane): [nchunks][GRAD_FOLD][KT + 2]
-    __syncthreads();
-    for (int i = threadIdx.x; i < group_n * (KT + 2); i += 64 * GRAD_WAVES) {
-      const int ci = i / (KT + 2), e = i - ci * (KT + 2);
-      p.slab[((int64_t)(group_base + ci) * GRAD_FOLD + blockIdx.x) * (KT + 2) + e] = facc[i];
+      double* out = p.slab + ((int64_t)chunk * p.nrb + rb) * (KT + 2);
+      out[0] = lacc;
+      UNR for (int j = 0; j < KT; ++j) out[1 + j] = gacc[j];
+      out[KT + 1] = (double)M;
     }
   }
 }
@@ -609,10 +577,6 @@ constexpr size_t GRAD_LDS_MAX = 48 * 1024;
 template <typename T> static size_t grad_lds_bytes(const GradArgs& a) {
   return (size_t)(a.nfeat + 1) * (size_t)a.rb_rows * sizeof(T);
 }
-// folding's accumulated records, after the staged block (8-byte aligned)
-template <int KT> static size_t grad_fold_bytes(const GradArgs& a) {
-  return a.fold ? (size_t)a.chunks_per_group * (KT + 2) * sizeof(double) : 0;
-}
 
 // rows per lane: value-only passes (no tangents) carry 4 rows per lane (one dispatch per 256-row
 // block); with tangents the register budget decides (GRAD_R)
@@ -626,12 +590,11 @@ template <typename T, int KT, int K, int GM = GMODE_LOSS>
 static hipError_t launch_grad_t(const GradArgs& a, dim3 grid, hipStream_t s) {
   constexpr int R = grad_rows<KT, K>();
   if (a.rb_rows % (64 * R)) return hipErrorInvalidValue;
-  const size_t lds = grad_lds_bytes<T>(a), facc = grad_fold_bytes<KT>(a);
-  if (facc > GRAD_LDS_MAX) return hipErrorInvalidValue;
+  const size_t lds = grad_lds_bytes<T>(a);
   if (lds <= GRAD_LDS_MAX)
-    hipLaunchKernelGGL((grad_kernel<T, KT, K, GM, true, R>), grid, dim3(64 * GRAD_WAVES), (lds + 7) / 8 * 8 + facc, s, a);
+    hipLaunchKernelGGL((grad_kernel<T, KT, K, GM, true, R>), grid, dim3(64 * GRAD_WAVES), lds, s, a);
   else
-    hipLaunchKernelGGL((grad_kernel<T, KT, K, GM, false, R>), grid, dim3(64 * GRAD_WAVES), facc, s, a);
+    hipLaunchKernelGGL((grad_kernel<T, KT, K, GM, false, R>), grid, dim3(64 * GRAD_WAVES), 0, s, a);
   return hipGetLastError();
 }
 

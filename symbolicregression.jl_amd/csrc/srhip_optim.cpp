@@ -180,8 +180,6 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     std::vector<int32_t> chunks, chunk_item;
     const double* red = nullptr;  // the reduced records, in the context's pinned staging
     LaunchPlan L;
-    bool screen = false;  // value-only screening (SRHIP_GRAD_SCREEN)
-    bool fold = false;    // records folded in the workgroup (GradArgs::fold)
   } pass[2];
   pass[0].kt = kt;
   pass[1].kt = 0;
@@ -212,38 +210,6 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     const int nch = (int)ps.chunks.size() / 2;
     if (nch == 0) continue;
     ps.L = grad_plan(ctx, v.m, nch);
-    // value-only screening (SRHIP_GRAD_SCREEN = the fewest value-only chunks screened; default 0 =
-    // off): row block 0 of every chunk first, in a launch of its own, then the other blocks, where a
-    // chunk whose block-0 check statistic is already non-finite is skipped.  Records of evaluated
-    // blocks are the same computation as in one launch, so losses and decisions are bit-identical
-    // (test_value_only_screening_is_exact).  C4 (~40 % of its trial points overflow), same box:
-    // off 173.6-177.9 ms, every pass 190-193, passes of >= 16 chunks 176.8-179.6 -- the extra launch
-    // costs what the skipped blocks save at 100k rows.
-    const int screen_min = env_int_opt("SRHIP_GRAD_SCREEN", 0);
-    ps.screen = ps.kt == 0 && screen_min > 0 && nch >= screen_min && ps.L.nrb > 1;
-    // record folding (SRHIP_GRAD_FOLD_MIN = the fewest chunks folded; default 0 = off): GRAD_FOLD
-    // workgroups per tree group, each over row blocks x, x + GRAD_FOLD, ..., accumulating the records
-    // in grad_reduce_kernel's order -- one record per (chunk, lane) instead of per (chunk, row block),
-    // the same bits (test_folded_records_equal_per_block_records).  C4's full gradient launch: HBM
-    // writes 24.9 -> 5.9 MB, fetch 22.5 -> 11.3 MB, but 1.499 -> 1.632 ms (value-only 0.720 -> 0.784):
-    // the workgroups' waves meet at a barrier after every row block where they used to leave one by
-    // one; C4 185-186 -> 189-192 ms (>= 64 chunks), 242-244 ms (>= 16).  Off by default.
-    const int fold_min = env_int_opt("SRHIP_GRAD_FOLD_MIN", 0);
-    ps.fold = !ps.screen && fold_min > 0 && nch >= fold_min && ps.L.nrb >= GRAD_FOLD;
-    if (ps.fold) {
-      int g = (4 * ctx->num_cu + GRAD_FOLD - 1) / GRAD_FOLD;
-      g = std::max(1, std::min(g, std::max(1, nch / (2 * GRAD_WAVES))));
-      const int tpg = (nch + g - 1) / g;
-      // the accumulators sit in LDS after the staged block: both must fit a workgroup's allotment
-      const size_t stage = (size_t)(ds->nfeat + 1) * ps.L.rb_rows * dtype_size(dtype);
-      const size_t lds = (stage <= 48 * 1024 ? (stage + 7) / 8 * 8 : 0) + (size_t)tpg * (ps.kt + 2) * sizeof(double);
-      if (lds <= std::min<size_t>(64 * 1024, (size_t)ctx->lds_max)) {
-        ps.L.tpg = tpg;
-        ps.L.groups = (nch + tpg - 1) / tpg;
-      } else {
-        ps.fold = false;
-      }
-    }
     // launch order: descending estimated cost, dealt round-robin over the tree groups (each group's
     // range stays contiguous), so every group gets the same cost mix and its waves -- which claim
     // chunks dynamically -- start with the longest ones.  Records are read back by position.
@@ -267,7 +233,7 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
       ps.chunks.swap(chunks2);
       ps.chunk_item.swap(item2);
     }
-    slab_n = std::max(slab_n, (size_t)nch * (ps.fold ? GRAD_FOLD : ps.L.nrb) * (ps.kt + 2));
+    slab_n = std::max(slab_n, (size_t)nch * ps.L.nrb * (ps.kt + 2));
     red_n = std::max(red_n, (size_t)nch * (ps.kt + 2));
     chunk_n = std::max(chunk_n, ps.chunks.size());
   }
@@ -318,7 +284,15 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     a.max_steps = P->gmax_len;
     if (first) HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));  // srhip_last_kernel_ms: the gradient kernels
     first = false;
-    if (ps.screen) {  // (see the plan above)
+    // value-only screening (SRHIP_GRAD_SCREEN = the fewest value-only chunks screened; default 0 =
+    // off): row block 0 of every chunk first, in a launch of its own, then the other blocks, where a
+    // chunk whose block-0 check statistic is already non-finite is skipped.  Records of evaluated
+    // blocks are the same computation as in one launch, so losses and decisions are bit-identical
+    // (test_value_only_screening_is_exact).  C4 (~40 % of its trial points overflow), same box:
+    // off 173.6-177.9 ms, every pass 190-193, passes of >= 16 chunks 176.8-179.6 -- the extra launch
+    // costs what the skipped blocks save at 100k rows.
+    const int screen_min = env_int_opt("SRHIP_GRAD_SCREEN", 0);
+    if (ps.kt == 0 && screen_min > 0 && nch >= screen_min && ps.L.nrb > 1) {
       GradArgs sa = a;
       const int tpg_s = 2 * GRAD_WAVES;
       sa.chunks_per_group = tpg_s;
@@ -326,15 +300,12 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
       a.block0 = 1;
       a.screened = 1;
       HIP_TRY(launch_grad(dtype, K, 0, a, dim3(ps.L.nrb - 1, ps.L.groups), ctx->stream));
-    } else if (ps.fold) {
-      a.fold = 1;
-      HIP_TRY(launch_grad(dtype, K, ps.kt, a, dim3(GRAD_FOLD, ps.L.groups), ctx->stream));
     } else {
       HIP_TRY(launch_grad(dtype, K, ps.kt, a, dim3(ps.L.nrb, ps.L.groups), ctx->stream));
     }
     // the reduction writes the records straight into coherent pinned host memory (no copy on the stream)
-    HIP_TRY(launch_grad_reduce(dtype, ps.kt, (const double*)ctx->g_slab.p, ps.fold ? GRAD_FOLD : ps.L.nrb, nch,
-                               (double*)ctx->h_gred[pi].p, ctx->stream));
+    HIP_TRY(launch_grad_reduce(dtype, ps.kt, (const double*)ctx->g_slab.p, ps.L.nrb, nch, (double*)ctx->h_gred[pi].p,
+                               ctx->stream));
     ps.red = (const double*)ctx->h_gred[pi].p;
   }
   HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));

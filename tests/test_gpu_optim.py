@@ -552,29 +552,3 @@ def test_value_only_screening_is_exact(ctx, dtype, monkeypatch):
         prog.close()
     for u, v in zip(res["0"], res["1"]):
         assert _bits_equal(u, v)
-
-
-@pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_folded_records_equal_per_block_records(ctx, dtype, monkeypatch):
-    """Gradient launches of many chunks fold each chunk's per-row-block records inside the workgroup
-    (GradArgs::fold: workgroup x over blocks x, x + 64, ... in grad_reduce_kernel's order) and write one
-    record per lane; SRHIP_GRAD_FOLD_MIN=0 writes one per row block.  Losses, gradients and
-    did_succeed -- gradient and value-only passes -- and an optimize_constants run are bitwise the
-    same either way (20,000 rows: 79 row blocks of 256)."""
-    sr = _sr()
-    opts, _, nodes, offs, X, y = _problem(sr, dtype, ntrees=72, n=20000, seed=23)
-    ds = sr.DeviceDataset(ctx, X, y)
-    res = {}
-    for fm in ("0", "1"):
-        monkeypatch.setenv("SRHIP_GRAD_FOLD_MIN", fm)
-        prog = sr.Program(ctx, nodes, offs, opts, dtype)
-        l, g, ok = prog.eval_loss_grad(ds, sr.L2DistLoss())
-        monkeypatch.setenv("SRHIP_GRAD_VALUE_ONLY", "1")
-        lv, _, okv = prog.eval_loss_grad(ds, sr.L2DistLoss())
-        monkeypatch.delenv("SRHIP_GRAD_VALUE_ONLY")
-        out, imp, fc = prog.optimize_constants(ds, sr.L2DistLoss(), iterations=4, nrestarts=1, seed=5)
-        res[fm] = (np.asarray(l, np.float64), np.concatenate(g), ok, np.asarray(lv, np.float64), okv,
-                   np.asarray(out, np.float64), imp, fc, np.concatenate(prog.get_constants()))
-        prog.close()
-    for u, v in zip(res["0"], res["1"]):
-        assert _bits_equal(u, v)
