@@ -438,12 +438,13 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
     gc.collect()
     gc.disable()
     steady_clocks()
-    seq = []
+    seq, seq_k = [], []
     for i in range(npop // 2, npop):
         t0 = time.perf_counter()
         p = make(i)
         p.eval_loss(ds, loss)
         seq.append(time.perf_counter() - t0)
+        seq_k.append(ctx.last_kernel_ms())
         p.close()
     # pipelined over fresh populations (new seeds: no cache hits)
     pops[:] = pops_pipe
@@ -456,12 +457,13 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
         p = fut.result()
         t0 = time.perf_counter()
         fill = t0 - tf
-        ph_eval, ph_wait = [], []
+        ph_eval, ph_wait, pipe_k = [], [], []
         for i in range(npop):
             if i + 1 < npop:
                 fut = ex.submit(make, i + 1)
             ta = time.perf_counter()
             p.eval_loss(ds, loss)
+            pipe_k.append(ctx.last_kernel_ms())  # this population's own interpreter launches (HIP events)
             p.close()
             tb = time.perf_counter()
             if i + 1 < npop:
@@ -514,9 +516,15 @@ def population_pipeline(srhip, workloads, ctx, ds, loss, opts, rank, args, npop=
             "compile_ms_fresh": 1e3 * float(np.median(comp)), "compile_ms_cached": 1e3 * warm,
             "sequential_ms_per_population": 1e3 * float(np.mean(seq)),
             "pipelined_ms_per_population": 1e3 * pipe, "pipeline_fill_ms": 1e3 * fill,
+            # the fresh populations are other random trees than the headline's: their own launches
+            # (probe + persistent, HIP events) are the like-for-like kernel time of each section
+            "sequential_kernel_ms": float(np.mean(seq_k)), "pipelined_kernel_ms": float(np.mean(pipe_k)),
+            "pipelined_kernel_ms_each": [round(k, 3) for k in pipe_k],
+            "pipelined_over_kernel_ms": 1e3 * pipe - float(np.mean(pipe_k)),
             "pipelined_phases_ms": {"eval_close": 1e3 * float(np.median(ph_eval)),
                                     "wait_next": 1e3 * float(np.median(ph_wait)),
-                                    "iterations": [round(1e3 * (a + b), 3) for a, b in zip(ph_eval, ph_wait)]},
+                                    "iterations": [round(1e3 * (a + b), 3) for a, b in zip(ph_eval, ph_wait)],
+                                    "eval_close_each": [round(1e3 * a, 3) for a in ph_eval]},
             "two_stream_ms_per_population": 1e3 * pipe2, "streams": nstream,
             "note": "compile + upload + srhip_eval_loss per fresh 1024-tree population (the Python garbage collector paused in the timed sections); pipelined: the next "
                     "population compiled on a host thread during the current evaluation, steady state (the "

@@ -87,8 +87,9 @@ __global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab
 // item: lane l adds row blocks l, l + 64, ... with a compensated (TwoSum) accumulator -- every load
 // of the item in flight at once -- and the 64 (sum, compensation) pairs are combined by a fixed xor
 // butterfly of double-double additions; results to coherent host memory.  The grid is sized for the
-// list's capacity (the count is read on the device); the last workgroup to finish resets the list
-// for the next launch on the stream (ulist[1 + PRECISE_DONE_SLOT] counts finished workgroups).
+// precise launch's groups; its waves stride over the items of the count read on the device (up to the
+// list's capacity umax); the last workgroup to finish resets the list for the next launch on the
+// stream (ulist[1 + PRECISE_DONE_SLOT] counts finished workgroups).
 __device__ __forceinline__ void two_sum_acc(double& s, double& c, double x) {
   const double t = s + x, bp = t - s;
   c += (s - (t - bp)) + (x - bp);
@@ -100,8 +101,8 @@ __global__ __launch_bounds__(256) void precise_reduce_kernel(const double* __res
   const int cnt = __hip_atomic_load(ulist, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int nu = min(cnt, umax);
   const int lane = threadIdx.x & 63;
-  const int item = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-  if (item < nu * stride) {
+  for (int item = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); item < nu * stride;
+       item += gridDim.x * (blockDim.x / 64)) {
     const double* src = slab + (int64_t)item * nrb;
     double s = 0.0, c = 0.0;
     constexpr int PB = 8;
@@ -233,9 +234,9 @@ hipError_t launch_eval(int dtype, const EvalArgs& a, int R, int K, int mode, boo
   }
 }
 
-hipError_t launch_precise_reduce(const double* slab, int nrb, int stride, int32_t* ulist, int umax, int done_slot,
-                                 int32_t* out_list, double* out, hipStream_t s) {
-  const int items = std::max(1, umax * stride);
+hipError_t launch_precise_reduce(const double* slab, int nrb, int stride, int32_t* ulist, int umax, int groups,
+                                 int done_slot, int32_t* out_list, double* out, hipStream_t s) {
+  const int items = std::max(1, std::min(umax, groups) * stride);
   hipLaunchKernelGGL(precise_reduce_kernel, dim3((items + 3) / 4), dim3(256), 0, s, slab, nrb, stride, ulist, umax,
                      done_slot, out_list, out);
   return hipGetLastError();

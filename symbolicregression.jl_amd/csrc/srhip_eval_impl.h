@@ -1125,8 +1125,11 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
   const int group_base = __builtin_amdgcn_readfirstlane(snap_base);
   int group_n = __builtin_amdgcn_readfirstlane(snap_n);
   if constexpr (MODE == MODE_PRECISE) {
-    // device-listed trees: this group's slots that the list filled
-    if (p.dev_count) group_n = max(0, min(group_n, __builtin_amdgcn_readfirstlane(*p.dev_count) - group_base));
+    // device-listed trees: this group's slots (group_base, + gstride, ...) that the list filled
+    if (p.dev_count) {
+      const int cnt = __builtin_amdgcn_readfirstlane(*p.dev_count);
+      group_n = max(0, min(group_n, (cnt - group_base + gstride - 1) / gstride));
+    }
   }
 
   // the group's trees are in descending estimated cost (host make_order): wave w starts with tree w,

@@ -940,6 +940,20 @@ void choose_derived_t(srhip_program& P) {
     if (e.second >= DERIVE_MIN_USES && (int)P.dspec.size() < dmax) P.dspec.push_back(e.first);
 }
 
+static TreeDecide make_decide(const TreeInfo& I) {
+  TreeDecide d;
+  for (double c : I.fill_consts)
+    if (!std::isnan(c)) d.maxc = std::max(d.maxc, fabs(c));
+  for (int f : I.feat_checks) {
+    if (f >= 0 && f < 64) d.feat_mask |= (uint64_t)1 << f;
+    else d.slow = 1;
+  }
+  d.nnodes = I.nnodes;
+  d.nops = I.nops;
+  d.static_fail = I.static_fail;
+  d.has_op = !I.op_sumcheck.empty();
+  return d;
+}
 template <typename T>
 int compile_program_t(srhip_program& P) {
   const int32_t n = P.ntrees;
@@ -955,6 +969,7 @@ int compile_program_t(srhip_program& P) {
   P.dcode.clear();
   P.dprog_off.assign(n, 0);
   P.dcost.assign(n, 0.0);
+  P.dec.assign(n, TreeDecide());
   P.dkmax = P.dmax_len = 0;
   // operator-node count and the largest feature index, from the node tables
   P.maxfeat = 0;
@@ -1041,6 +1056,7 @@ int compile_program_t(srhip_program& P) {
     P.max_ops = std::max(P.max_ops, (int32_t)P.info[t].op_sumcheck.size());
     P.max_len = std::max(P.max_len, P.info[t].code_len);
     P.total_nodes += P.info[t].nnodes;
+    P.dec[t] = make_decide(P.info[t]);
     if (der) {
       const TreeInfo& ti = dinfo[t];
       P.dprog_off[t] = ti.code_begin;
@@ -1630,10 +1646,40 @@ static int decide_info(const TreeInfo& I, int dtype, int32_t T, int64_t nfeat, c
   return 0;
 }
 
+// decide_info on the compact record: the same answer (fill constants: |c| m >= OVF is monotone in
+// |c|, so the largest decides; NaN never fails; the feature checks in any order)
+static int decide_fast(const srhip_program& P, int32_t t, int64_t nfeat, const double* sums, double chk) {
+  const TreeDecide& d = P.dec[t];
+  if (d.slow) return decide_info(P.info[t], P.dtype, P.ntrees, nfeat, sums, chk);
+  if (d.static_fail) return 1;
+  const int dtype = P.dtype;
+  if (dtype == SRHIP_I32) return 0;
+  const int32_t T = P.ntrees;
+  const long double m = (long double)sums[2 * (size_t)T + 2 * (size_t)nfeat];
+  const long double ovf = ovf_threshold(dtype);
+  if (d.maxc >= 0.0 && (long double)d.maxc * m >= ovf) return 1;
+  for (uint64_t fm = d.feat_mask; fm; fm &= fm - 1) {
+    const int f = __builtin_ctzll(fm);
+    const double fsum = sums[2 * (size_t)T + 2 * (size_t)f], fbad = sums[2 * (size_t)T + 2 * (size_t)f + 1];
+    if (fbad > 0) return 1;
+    const long double sum = dtype == SRHIP_F64 ? (long double)fsum * 0x1p64L : (long double)fsum;
+    if (!isfinite(fsum) || fabsl(sum) >= ovf) return 1;
+  }
+  if (!d.has_op) return 0;
+  if (!isfinite(chk)) return 1;
+  long double bound;
+  if (dtype == SRHIP_F64) bound = (long double)chk * 0x1p512L;
+  else bound = (long double)chk * m;
+  if (bound * 2.0L >= ovf) return 2;
+  return 0;
+}
+
 static void finalize(const srhip_program& P, int64_t nfeat, const double* sums, const double* chk, double* out_loss,
                      uint8_t* out_ok, uint8_t* out_status) {
+  const bool fast = P.dec.size() == (size_t)P.ntrees && !env_flag("SRHIP_DECIDE_SLOW");
   for (int32_t t = 0; t < P.ntrees; ++t) {
-    const int st = decide_info(P.info[t], P.dtype, P.ntrees, nfeat, sums, chk ? chk[t] : 0.0);
+    const double c = chk ? chk[t] : 0.0;
+    const int st = fast ? decide_fast(P, t, nfeat, sums, c) : decide_info(P.info[t], P.dtype, P.ntrees, nfeat, sums, c);
     if (out_status) out_status[t] = (uint8_t)st;
     if (out_ok) out_ok[t] = st == 0 ? 1 : 0;
     if (out_loss) out_loss[t] = st == 0 ? sums[2 * (size_t)t] / sums[2 * (size_t)t + 1] : INFINITY;
@@ -1792,21 +1838,54 @@ struct ShardDev {
 };
 
 // The device-listed precise pass, enqueued on the context's stream: the plain program over the trees
-// of the device list ulist ([count, trees ...], count read by the launch, at most G of them), one tree
-// group per entry, one-tile row blocks and one-wave workgroups -- every (tree, tile) of the few listed
-// trees on a wave of its own -- K_MAX, global reads; then the double-double reduction of the per-block
-// operator sums into the context's coherent h_pout ([count, list ..., sums]), which also clears the list.
+// of the device list ulist ([count, trees ...], count read by the launch, at most cap of them):
+// one-tile row blocks and one-wave workgroups, G workgroups per row block, workgroup g taking the
+// listed slots g, g + G, ... (G from the program's last count: an unused workgroup still costs its
+// dispatch, and a count past G costs one launch longer, not another host round trip) -- K_MAX,
+// global reads; then the double-double reduction of the per-block operator sums into the context's
+// coherent h_pout ([count, list ..., sums]), which also clears the list.
+// The precise pass's scratch (the per-block operator sums of the listed trees, their reduction's host
+// output), ensured before the evaluation's main launch: a regrowth frees the old buffer, which
+// synchronises the device -- after the launch that would wait for the whole evaluation.  Sized for
+// a power-of-two operator count (32 at least: one size for every population of trees up to 33
+// nodes) and at most 64 MB of per-block sums: the list's capacity (*cap, <= DEV_PRECISE_MAX) shrinks
+// for very long row ranges (4 at least); trees past it take the host-written list.
+constexpr size_t PRECISE_SLAB_MAX = (size_t)64 << 20;
+static size_t precise_per_tree(const srhip_program* P, const View& v, int* sa_out = nullptr) {
+  int sa = 32;
+  while (sa < P->max_ops) sa <<= 1;
+  if (sa_out) *sa_out = sa;
+  const int rows = 64 * pick_rows_per_lane(P->dtype, K_MAX, MODE_PRECISE, v.m);
+  const int64_t nrb = std::max<int64_t>(1, (v.m + rows - 1) / rows);
+  return (size_t)sa * nrb * sizeof(double);
+}
+static int precise_cap(const srhip_program* P, const View& v, int cap) {
+  return (int)std::max<int64_t>(std::min<int64_t>(cap, (int64_t)(PRECISE_SLAB_MAX / precise_per_tree(P, v))), 4);
+}
+static int ensure_dev_precise(srhip_ctx* ctx, const srhip_program* P, const View& v, int* cap) {
+  int sa = 32;
+  const size_t per_tree = precise_per_tree(P, v, &sa);
+  *cap = precise_cap(P, v, *cap);
+  HIP_TRY(ctx->slab_prec.ensure((size_t)*cap * per_tree));
+  HIP_TRY(ctx->h_pout.ensure((size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t) +
+                             (size_t)DEV_PRECISE_MAX * sa * sizeof(double), hipHostMallocCoherent));
+  return SRHIP_OK;
+}
 static int enqueue_dev_precise(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const View& v,
-                               int32_t* ulist, int G, int* out_stride) {
+                               int32_t* ulist, int cap, int G, int* out_stride) {
   const int dtype = P->dtype;
   const int stride = std::max(1, P->max_ops);
   const int Rp = pick_rows_per_lane(dtype, K_MAX, MODE_PRECISE, v.m);
+  G = std::max(1, std::min(G, cap));
   LaunchPlan Lp = plan_launch(ctx, dtype, ds->nfeat, false, false, v.m, G, 64 * Rp);
   Lp.rb_rows = 64 * Rp;
   Lp.nrb = (int)((v.m + Lp.rb_rows - 1) / Lp.rb_rows);
-  HIP_TRY(ctx->slab_prec.ensure((size_t)G * stride * Lp.nrb * sizeof(double)));
-  HIP_TRY(ctx->h_pout.ensure((size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t) +
-                             (size_t)DEV_PRECISE_MAX * stride * sizeof(double), hipHostMallocCoherent));
+  {
+    int c = cap;
+    const int rc = ensure_dev_precise(ctx, P, v, &c);
+    if (rc) return rc;
+    if (c < cap) return fail(SRHIP_ERR_INVALID, "precise list of %d trees past its capacity %d", cap, c);
+  }
   EvalArgs q{};
   q.code = P->code_dev;
   q.prog_off = P->off_dev;
@@ -1814,7 +1893,8 @@ static int enqueue_dev_precise(srhip_ctx* ctx, const srhip_dataset* ds, const sr
   q.X = v.X;
   q.ld = v.ld;
   q.nvalid = v.m;
-  q.ntrees = G;
+  q.ntrees = cap;
+  q.grid_interleave = 1;  // grid.y = G workgroups share the list's slots interleaved
   q.nfeat = (int32_t)ds->nfeat;
   q.rb_rows = Lp.rb_rows;
   q.nrb = Lp.nrb;
@@ -1828,8 +1908,8 @@ static int enqueue_dev_precise(srhip_ctx* ctx, const srhip_dataset* ds, const sr
   HIP_TRY(launch_eval(dtype, q, Rp, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, G), 16, ctx->stream));
   int32_t* hl = (int32_t*)ctx->h_pout.p;
   double* hs = (double*)((uint8_t*)ctx->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
-  HIP_TRY(launch_precise_reduce((const double*)ctx->slab_prec.p, Lp.nrb, stride, ulist, G, DEV_PRECISE_MAX, hl, hs,
-                                ctx->stream));
+  HIP_TRY(launch_precise_reduce((const double*)ctx->slab_prec.p, Lp.nrb, stride, ulist, cap, G, DEV_PRECISE_MAX, hl,
+                                hs, ctx->stream));
   *out_stride = stride;
   return SRHIP_OK;
 }
@@ -1854,7 +1934,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   std::vector<int32_t> live;
   live.reserve(nt);
   for (int32_t t = 0; t < nt; ++t)
-    if (!P->info[t].static_fail) live.push_back(t);
+    if (!(P->dec.size() == (size_t)nt ? P->dec[t].static_fail : P->info[t].static_fail)) live.push_back(t);
   if (live.empty()) return SRHIP_OK;
   const size_t es = dtype_size(dtype);
   // stack slots of the kernel variant; the wide operators live only in the K_MAX variant
@@ -2028,6 +2108,14 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     HIP_TRY(ctx->slab_rows.ensure((size_t)nl * L.nrb * sizeof(int32_t)));
     a.slab_rows = (int32_t*)ctx->slab_rows.p;
   }
+  const bool devp = dp && !a.fused && dtype != SRHIP_I32 && !env_flag("SRHIP_NO_DEVICE_PRECISE");
+  // the device list's capacity: DEV_PRECISE_MAX (SRHIP_PRECISE_LIST: smaller, read per call -- the
+  // tests' way to the overflow path), less for very long row ranges (ensure_dev_precise)
+  int ucap = std::max(1, std::min(DEV_PRECISE_MAX, env_int("SRHIP_PRECISE_LIST", DEV_PRECISE_MAX)));
+  if (devp) {
+    const int rc = ensure_dev_precise(ctx, P, v, &ucap);
+    if (rc) return rc;
+  }
   a.early_exit = mode == MODE_LOSS && early_exit_on() ? 1 : 0;
   if (a.early_exit) {
     const int rc = next_fail_epoch(ctx, nl, &a.fail_flag, &a.epoch);
@@ -2130,8 +2218,8 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       }
     }
   }
-  const bool devp = dp && !a.fused && dtype != SRHIP_I32 && !env_flag("SRHIP_NO_DEVICE_PRECISE");
   UndecidedList ul;
+  int ul_groups = 4;
   if (devp) {
     if (!ctx->d_ulist.p) {
       // [count, DEV_PRECISE_MAX trees, the precise reduction's finished-workgroup counter]
@@ -2139,11 +2227,11 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       HIP_TRY(hipMemsetAsync(ctx->d_ulist.p, 0, ctx->d_ulist.bytes, ctx->stream));
     }
     ul.ulist = (int32_t*)ctx->d_ulist.p;
-    // list capacity: the trees the program's last launch listed plus two (4 .. DEV_PRECISE_MAX): the
-    // precise launch has one tree group per entry, and empty groups still cost their workgroups'
-    // dispatch; trees past it are decided by the host-launched pass
-    ul.umax = std::min(DEV_PRECISE_MAX, std::max(4, P->und_hint + 2));
+    // trees past the list's capacity are settled by the same pass over a host-written list (run_eval).
+    // The precise launch's workgroups per row block: the program's last count plus two (4 at least)
+    ul.umax = ucap;
     ul.rows = (double)v.m;
+    ul_groups = std::min(ul.umax, std::max(4, P->und_hint + 2));
   }
   if (!a.fused)
     HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, nch, cpb,
@@ -2153,7 +2241,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
                           (int64_t*)ctx->h_rows.p, ul, sd != nullptr));
   if (devp) {
     int stride = 1;
-    const int rc = enqueue_dev_precise(ctx, ds, P, v, ul.ulist, ul.umax, &stride);
+    const int rc = enqueue_dev_precise(ctx, ds, P, v, ul.ulist, ul.umax, ul_groups, &stride);
     if (rc) return rc;
     dp->used = true;
     dp->stride = stride;
@@ -2207,11 +2295,13 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   }
   // the launch's work, counted on the device (rows each tree was evaluated on)
   for (int i = 0; i < 4; ++i) ctx->work[i] = 0;
+  const bool pdec = P->dec.size() == (size_t)nt;
   for (int32_t t : live) {
     const int64_t rows = ((const int64_t*)r_rows.data())[t];
-    ctx->work[0] += rows * P->info[t].nnodes;
-    ctx->work[1] += v.m * P->info[t].nnodes;
-    ctx->work[2] += rows * P->info[t].nops;
+    const int64_t nn = pdec ? P->dec[t].nnodes : P->info[t].nnodes, no = pdec ? P->dec[t].nops : P->info[t].nops;
+    ctx->work[0] += rows * nn;
+    ctx->work[1] += v.m * nn;
+    ctx->work[2] += rows * no;
     ctx->work[3] += rows;
   }
   g_tail_done = std::chrono::steady_clock::now();
@@ -2324,7 +2414,11 @@ int srhip::run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program
       acc[1] += std::chrono::duration<double>(g_wait_done - g_wait_begin).count();
       acc[2] += std::chrono::duration<double>(g_tail_done - g_wait_done).count();
       acc[3] += std::chrono::duration<double>(t3 - g_tail_done).count();
-      if (++cnt % 50 == 0) {
+      static const bool each = [] {  // SRHIP_HOST_TIMING=2: every call
+        const char* e = getenv("SRHIP_HOST_TIMING");
+        return e && atoi(e) >= 2;
+      }();
+      if (++cnt % (each ? 1 : 50) == 0) {
         fprintf(stderr, "[srhip host] run_eval: before wait %.1f us, wait %.1f us, records %.1f us, decisions %.1f us "
                 "(mean of %d)\n", acc[0] / cnt * 1e6, acc[1] / cnt * 1e6, acc[2] / cnt * 1e6, acc[3] / cnt * 1e6, cnt);
         acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
@@ -2377,15 +2471,16 @@ int srhip::run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program
   // tree of a device evaluation is then settled by one summation path (SRHIP_PRECISE_OVERFLOW_HOST=1:
   // the host-launched pass of eval_precise instead)
   if (dp.used && !unc.empty() && !env_flag("SRHIP_PRECISE_OVERFLOW_HOST")) {
-    for (size_t b = 0; b < unc.size(); b += DEV_PRECISE_MAX) {
-      const int32_t n = (int32_t)std::min<size_t>(DEV_PRECISE_MAX, unc.size() - b);
+    const size_t bcap = (size_t)precise_cap(P, v, DEV_PRECISE_MAX);
+    for (size_t b = 0; b < unc.size(); b += bcap) {
+      const int32_t n = (int32_t)std::min<size_t>(bcap, unc.size() - b);
       std::vector<int32_t> lst(1 + n);
       lst[0] = n;
       std::copy(unc.begin() + b, unc.begin() + b + n, lst.begin() + 1);
       HIP_TRY(hipMemcpyAsync(ctx->d_ulist.p, lst.data(), lst.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                              ctx->stream));
       int stride = 1;
-      rc = enqueue_dev_precise(ctx, ds, P, v, (int32_t*)ctx->d_ulist.p, n, &stride);
+      rc = enqueue_dev_precise(ctx, ds, P, v, (int32_t*)ctx->d_ulist.p, n, n, &stride);
       if (rc) return rc;
       rc = stream_wait(ctx);
       if (rc) return rc;

@@ -64,6 +64,14 @@ inline long double ovf_threshold(int dtype) {
 // ---------------------------------------------------------------------------------------------
 // device buffers
 // ---------------------------------------------------------------------------------------------
+// A regrown scratch buffer takes half again its old size at least (below 256 MB): per-population
+// sizes (live trees, undecided lists) vary from call to call, and every regrowth frees the old
+// buffer, which synchronises the device -- a pipelined population queued behind it stalls.
+inline size_t grown_size(size_t n, size_t old) {
+  const size_t g = old + old / 2;
+  const size_t want = (old > 0 && g > n && g <= ((size_t)256 << 20)) ? g : n;
+  return want < 256 ? 256 : want;
+}
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -75,8 +83,8 @@ struct DevBuf {
   }
   hipError_t ensure(size_t n) {
     if (n <= bytes && p) return hipSuccess;
+    const size_t want = grown_size(n, bytes);
     release();
-    size_t want = n < 256 ? 256 : n;
     hipError_t e = hipMalloc(&p, want);
     if (e == hipSuccess) bytes = want;
     return e;
@@ -123,14 +131,23 @@ struct HostBuf {  // pinned staging
   }
   hipError_t ensure(size_t n, unsigned flags = hipHostMallocDefault) {
     if (n <= bytes && p) return hipSuccess;
+    const size_t want = grown_size(n, bytes);
     release();
-    size_t want = n < 256 ? 256 : n;
     hipError_t e = hipHostMalloc(&p, want, flags);
     if (e == hipSuccess) bytes = want;
     return e;
   }
 };
 
+// A tree's evaluation-time metadata in 32 contiguous bytes (built at compile from its TreeInfo): the
+// per-call decisions and work counts read this array, not the TreeInfo vectors (heap data written by
+// the compile threads, cold in the evaluating thread's caches: ~50 us per fresh 1024-tree population)
+struct TreeDecide {
+  double maxc = -1.0;          // max |c| of fill_consts (ignoring NaN), -1 without any
+  uint64_t feat_mask = 0;      // feat_checks (features < 64)
+  int32_t nnodes = 0, nops = 0;
+  uint8_t static_fail = 0, has_op = 0, slow = 0;  // slow: a feature check >= 64 (decide from TreeInfo)
+};
 struct TreeInfo {
   bool static_fail = false;
   std::vector<double> fill_consts;  // |c| * m >= OVF  => fail
@@ -202,6 +219,7 @@ struct srhip_program {
   std::vector<int64_t> offsets;
   std::vector<int32_t> binops, unaops;
   std::vector<srhip::TreeInfo> info;
+  std::vector<srhip::TreeDecide> dec;  // [ntrees], from info (compile_program)
   std::vector<srhip::Ins> code;
   std::vector<int32_t> prog_off;
   int32_t kmax = 0, max_ops = 0, max_len = 0;

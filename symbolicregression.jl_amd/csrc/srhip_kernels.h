@@ -138,7 +138,7 @@ hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, int cpb, con
 // The precise pass's per-(listed tree, operator) sums over the row blocks (fixed order, compensated),
 // written to out (coherent host memory: out_count, then [umax][stride] doubles); the last workgroup
 // resets ulist[0] (ulist[1 + done_slot]: its finished-workgroup counter, zero between launches).
-hipError_t launch_precise_reduce(const double* slab, int nrb, int stride, int32_t* ulist, int umax, int done_slot,
+hipError_t launch_precise_reduce(const double* slab, int nrb, int stride, int32_t* ulist, int umax, int groups, int done_slot,
                                  int32_t* out_list, double* out, hipStream_t s);
 hipError_t launch_gather(int dtype, const void* X, const void* y, const void* w, int64_t ld_src, int nfeat,
                          const int64_t* idx, int64_t m, int64_t ld_dst, void* Xd, void* yd, void* wd, hipStream_t s);

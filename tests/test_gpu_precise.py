@@ -1,12 +1,12 @@
 """The precise pass on trees whose did_succeed turns on an exact column sum near the overflow
 threshold.  Each tree is c * x1 over positive x1: every row is finite, the
 check statistic puts the tree in the undecided band, and the sum lands just below (ok) or just above
-(fails) the threshold of the type, alternating over the population.  The device-listed pass (one
-tree group per listed tree) and the host-launched pass for trees past the list's capacity (the
-first evaluation of a program lists at most 4) must both give the oracle's mask, evaluation after
-evaluation -- including four trees within the sums' own precision of the threshold.  Trees past the first
-evaluation's list capacity go through the same device pass over a host-written list (or, with
-SRHIP_PRECISE_OVERFLOW_HOST=1, the host-launched pass)."""
+(fails) the threshold of the type, alternating over the population.  The device-listed pass (up to
+64 listed trees, the launch's workgroups per row block sized from the program's last count, each
+taking every G-th listed tree) and, for trees past a smaller list (SRHIP_PRECISE_LIST), the same
+device pass over a host-written list or the host-launched pass (SRHIP_PRECISE_OVERFLOW_HOST=1) must
+all give the oracle's mask, evaluation after evaluation -- including four trees within the sums' own
+precision of the threshold."""
 import numpy as np
 import pytest
 
@@ -21,11 +21,15 @@ def _sr():
     return srhip
 
 
-@pytest.mark.parametrize("overflow", ["device", "host"])
+@pytest.mark.parametrize("overflow", ["none", "device", "host"])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_precise_pass_near_threshold_matches_oracle(ctx, oracle, dtype, overflow, monkeypatch):
-    """Trees past the device list's capacity take the device-listed pass over a host-written list
-    (default) or the host-launched pass (SRHIP_PRECISE_OVERFLOW_HOST=1): both give the oracle's mask."""
+    """All 14 undecided trees on the device list (none: a fresh program's launch has 4 workgroups per
+    row block, each taking every 4th listed tree), or a list of 4 (SRHIP_PRECISE_LIST) whose overflow
+    takes the device-listed pass over a host-written list (device) or the host-launched pass
+    (SRHIP_PRECISE_OVERFLOW_HOST=1): every form gives the oracle's mask."""
+    if overflow != "none":
+        monkeypatch.setenv("SRHIP_PRECISE_LIST", "4")
     if overflow == "host":
         monkeypatch.setenv("SRHIP_PRECISE_OVERFLOW_HOST", "1")
     sr = _sr()
@@ -69,3 +73,33 @@ def test_precise_pass_near_threshold_matches_oracle(ctx, oracle, dtype, overflow
         _, ok = prog.eval_loss(ds, sr.L2DistLoss())
         assert np.array_equal(ok, ook), (np.nonzero(ok != ook)[0], ok[:10])
     prog.close()
+
+
+def test_compact_decisions_match_tree_info(ctx, oracle, monkeypatch):
+    """The per-call decisions read a compact per-tree record built at compile (TreeDecide); the
+    TreeInfo path (SRHIP_DECIDE_SLOW=1) must give the same losses and masks bit for bit, and both the
+    oracle's mask -- over random C2-shaped trees on data with a non-finite feature value (feature
+    checks), huge constants (fill-constant checks) and overflowing operator outputs."""
+    sr = _sr()
+    from srhip import workloads
+
+    opts, X, y, trees, nodes, offs = workloads.c2(5, 384, 8192)
+    X = np.array(X, copy=True)
+    X[3, 100] = np.inf  # every tree reading x4 fails its column check
+    extra = [sr.Node(1, sr.Node(val=np.float32(3e38)), sr.Node(feature=1)),  # c * x1: overflows
+             sr.Node(3, sr.Node(feature=2), sr.Node(val=np.float32(2e38))),  # x2 - c
+             sr.Node(2, sr.Node(feature=1), sr.Node(val=np.float32(1.0)))]
+    en, eo = sr.flatten(extra, opts, np.float32)
+    nodes = np.concatenate([nodes, en])
+    offs = np.concatenate([offs, eo[1:] + offs[-1]])
+    ds = sr.DeviceDataset(ctx, X, y)
+    prog = sr.Program(ctx, nodes, offs, opts, np.float32)
+    loss_fast, ok_fast = prog.eval_loss(ds, sr.L2DistLoss())
+    monkeypatch.setenv("SRHIP_DECIDE_SLOW", "1")
+    loss_slow, ok_slow = prog.eval_loss(ds, sr.L2DistLoss())
+    prog.close()
+    assert np.array_equal(ok_fast, ok_slow)
+    assert np.array_equal(np.asarray(loss_fast).view(np.uint64), np.asarray(loss_slow).view(np.uint64))
+    _, _, ook, _ = oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, X, y, None, 0, 0.0)
+    assert np.array_equal(ok_fast, np.asarray(ook, bool))
+    assert (~ok_fast).sum() >= 3 and ok_fast.sum() > 0
