@@ -459,6 +459,14 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
 #undef GK_HEAVY
 #define GK_UN(NAME, FN)                                                                            \
   case h_un(UN_##NAME): {                                                                          \
+    if (R > 1 && (ins.a & UN_UNIFORM_FLAG)) {  /* a constant subtree's rows: one evaluation */     \
+      T f, df;                                                                                     \
+      dual_un<T, UN_##NAME, (KT > 0)>(A[0].v, f, df);                                              \
+      A[0].v = f;                                                                                  \
+      UNR for (int j = 0; j < KT; ++j) A[0].d[j] = df * A[0].d[j];                                 \
+      UNR for (int r = 0; r < R; ++r) { A[r] = A[0]; chk_fold(M, A[r].v); }                        \
+      break;                                                                                       \
+    }                                                                                              \
     if constexpr (KT == 0 && !dun_inline<UN_##NAME>()) {                                           \
       typename VR<T, R>::type xv;                                                                  \
       if constexpr (R == 1) xv = A[0].v;                                                           \

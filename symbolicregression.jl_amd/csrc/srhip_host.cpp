@@ -514,6 +514,10 @@ template <typename T> class TreeCompiler {
     const char* e = env_get("SRHIP_NO_SUPER");
     return !(e && *e && *e != '0');
   }
+  static bool grad_uniform_env() {
+    const char* e = env_get("SRHIP_GRAD_UNIFORM");
+    return !(e && *e == '0');
+  }
 
  private:
   static void fuse_push_loads(std::vector<Ins>& code, int32_t begin) {
@@ -551,7 +555,10 @@ template <typename T> class TreeCompiler {
       // cos / sin of an operator output need no check fold of their own (srhip_isa.h UN_NC_FLAG); the
       // gradient program keeps every fold
       const bool nc = SRHIP_COS_NC && !grad_ && !leafish(n.l) && (u == UN_COS || u == UN_SIN);
-      push_op(h_un(u), nc ? UN_NC_FLAG : 0, 0, i, parent);
+      // gradient programs: an operator of a constant subtree (one value on every row) is evaluated
+      // once per lane (SRHIP_GRAD_UNIFORM=0: per row)
+      const bool uni = grad_ && is_const(n.l) && grad_uniform_env();
+      push_op(h_un(u), (nc ? UN_NC_FLAG : 0) | (uni ? UN_UNIFORM_FLAG : 0), 0, i, parent);
       return;
     }
     int sb, hb;

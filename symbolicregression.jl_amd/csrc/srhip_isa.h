@@ -97,6 +97,10 @@ constexpr uint32_t H_COUNT = H_UN0 + NUM_UNOP;
 // checked form).  A flag, not a handler of its own: one call site per operator in the interpreter
 // (round 5: the separate handlers' call site carried a 64-byte register spill on its dispatch path)
 constexpr uint32_t UN_NC_FLAG = 0x8000;
+// operand flag of a gradient-program unary instruction whose operand is a constant subtree: the
+// operand's rows all hold one value (and one tangent), so the kernel evaluates the operator on one row
+// and copies it to the others -- the same bits, one evaluation per lane instead of R
+constexpr uint32_t UN_UNIFORM_FLAG = 0x4000;
 
 constexpr uint32_t h_spec(int sb, uint32_t form) { return H_BIN0 + uint32_t(sb) * SPEC_STRIDE + form; }
 constexpr uint32_t h_heavy(int hb, uint32_t form) { return H_HEAVY0 + uint32_t(hb) * HEAVY_STRIDE + form; }
