@@ -1233,7 +1233,11 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
         KDBG("[k]   tile=%d step=%d h=%u a=%u\n", tile, step, ins.h, ins.a);
         if (ins.h == H_END) break;
         switch (ins.h) {
-          SRHIP_LK case H_LOADF: load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A); break;
+          SRHIP_LK case H_LOADF:
+            load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A);
+            // (a gradient program's derived-column load carries its operator's ordinal)
+            if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);
+            break;
           SRHIP_LK case H_LOADC: { const T c = imm_as<T>(ins.imm); UNR for (int r = 0; r < R; ++r) A[r] = c; break; }
 #define SRHIP_K_CASES(BASE, ...)                                                            \
   case BASE + 0: if constexpr (0 < K) { constexpr int k = 0; __VA_ARGS__ } break;                 \

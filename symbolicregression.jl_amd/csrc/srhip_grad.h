@@ -37,6 +37,8 @@ struct GradArgs {
   double loss_p0;
   int32_t weighted;
   int32_t max_steps;
+  // a derived view's derived-column count (its tangent-zero columns follow at + gd_nd); 0: none
+  int32_t gd_nd;
   // row blocks of this launch: blockIdx.x + block0 (slab rows keep their global block index)
   int32_t block0;
   // value-only screening (GMODE_LOSS, KT = 0): a chunk whose block-0 record (written by an earlier
@@ -60,5 +62,8 @@ hipError_t launch_grad(int dtype, int K, int kt, const GradArgs& a, dim3 grid, h
 // per-row modes (GMODE_ROWC / GMODE_ROWF), GRAD_ROW_KT tangents per chunk
 hipError_t launch_grad_rows(int dtype, int K, int gmode, const GradArgs& a, dim3 grid, hipStream_t s);
 hipError_t launch_grad_reduce(int dtype, int kt, const double* slab, int nrb, int nchunks, double* out, hipStream_t s);
+// derived columns of a derived view: Xd[j] = U(X[f]) over ld rows, keys[j] = U << 16 | f (nd <= 32)
+hipError_t launch_grad_derive(int dtype, const void* X, void* Xd, int64_t ld, const uint32_t* keys, int nd,
+                              hipStream_t s);
 
 }  // namespace srhip

@@ -38,10 +38,7 @@ template <typename T> struct V2 { typedef T type __attribute__((ext_vector_type(
 template <typename T> struct V4 { typedef T type __attribute__((ext_vector_type(4))); };
 
 // ---- operator values and partial derivatives ------------------------------------------------
-template <int U> constexpr bool dun_inline() {
-  return U == UN_NEG || U == UN_SQUARE || U == UN_CUBE || U == UN_ABS || U == UN_RELU || U == UN_SIGN ||
-         U == UN_ROUND || U == UN_FLOOR || U == UN_CEIL;
-}
+template <int U> constexpr bool dun_inline() { return un_grad_inline(U); }
 
 // f(x) and f'(x) for a heavy unary operator U; D = false: the value alone (value-only passes: the
 // derivative of cos is a sin, of log a division -- out of line the compiler cannot drop them), the
@@ -353,9 +350,12 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   }
   __syncthreads();
   // feature f / target at block-relative row rr of this row block
+  // (a derived view's derived columns, f >= nfeat, are read from global memory)
   auto xat = [&](int f, int rr) -> T {
-    if constexpr (XLDS) return xs[f * rbr + rr];
-    else return Xg[(int64_t)f * p.ld + row_base + rr];
+    if constexpr (XLDS) {
+      if (f < p.nfeat) return xs[f * rbr + rr];
+    }
+    return Xg[(int64_t)f * p.ld + row_base + rr];
   };
   auto yat = [&](int rr) -> T {
     if constexpr (XLDS) return xs[p.nfeat * rbr + rr];
@@ -409,7 +409,18 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
         const T imm = imm_bits<T>(ins.imm);
 #define RR(...) UNR for (int r = 0; r < R; ++r) { const int rr = tb + 64 * r + lane; (void)rr; __VA_ARGS__ }
         switch (ins.h) {
-          case H_LOADF: RR(set_feat<GM>(A[r], xat(opnd, rr), opnd - c0);) break;
+          case H_LOADF:
+            RR(set_feat<GM>(A[r], xat(opnd, rr), opnd - c0);)
+            if (opnd >= p.nfeat) {
+              // a derived column: the operator's output (its check fold), and its tangents f'(x) * 0
+              // (+-0, or NaN where f' is not finite) from the tangent-zero column
+              RR(chk_fold(M, A[r].v);)
+              if constexpr (KT > 0) {
+                RR(const T z = Xg[(int64_t)(opnd + p.gd_nd) * p.ld + row_base + rr];
+                   UNR for (int j = 0; j < KT; ++j) A[r].d[j] = z;)
+              }
+            }
+            break;
           case H_LOADC: RR(set_const<GM>(A[r], imm, opnd - c0);) break;
 #define GK_CASES(BASE, ...)                                                                        \
   case BASE + 0: if constexpr (0 < K) { constexpr int k = 0; __VA_ARGS__ } break;                \
@@ -624,6 +635,46 @@ hipError_t launch_grad_rows(int dtype, int K, int gmode, const GradArgs& a, dim3
   }
 }
 
+
+// A derived view's derived columns (srhip_optim.cpp derived_view): Xd[j][row] = U_j(X[f_j][row]) over
+// the view's ld rows, with the gradient kernel's own value function (the bits the kernel computes in
+// place), and after the nd of them the tangent-zero columns Xd[nd + j][row] = U_j'(x) * 0 -- what the
+// kernel's tangents of U_j(feature) are (a feature's tangent is +0): +-0, or NaN where U_j' is not finite.
+struct DeriveSpec {
+  uint32_t key[32];  // u << 16 | feature column
+};
+template <typename T>
+__global__ __launch_bounds__(256) void grad_derive_kernel(const T* __restrict__ X, T* __restrict__ Xd, int64_t ld,
+                                                          DeriveSpec spec) {
+  const int j = blockIdx.y;
+  const int u = (int)(spec.key[j] >> 16), f = (int)(spec.key[j] & 0xffff);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ld; i += (int64_t)gridDim.x * blockDim.x) {
+    const T x = X[(int64_t)f * ld + i];
+    T v = x, dv = T(0), v1, dv1;
+    switch (u) {
+#define X_(NAME, FN) \
+  case UN_##NAME: dual_un<T, UN_##NAME, false>(x, v, dv1); dual_un<T, UN_##NAME, true>(x, v1, dv); break;
+      SRHIP_UNOPS(X_)
+#undef X_
+      default: break;
+    }
+    Xd[(int64_t)j * ld + i] = v;
+    Xd[(int64_t)(gridDim.y + j) * ld + i] = dv * T(0);
+  }
+}
+hipError_t launch_grad_derive(int dtype, const void* X, void* Xd, int64_t ld, const uint32_t* keys, int nd,
+                              hipStream_t s) {
+  if (nd <= 0) return hipSuccess;
+  if (nd > 32) return hipErrorInvalidValue;
+  DeriveSpec spec{};
+  for (int j = 0; j < nd; ++j) spec.key[j] = keys[j];
+  const dim3 grid((unsigned)std::min<int64_t>((ld + 255) / 256, 1024), (unsigned)nd);
+  if (dtype == SRHIP_F64)
+    hipLaunchKernelGGL(grad_derive_kernel<double>, grid, dim3(256), 0, s, (const double*)X, (double*)Xd, ld, spec);
+  else
+    hipLaunchKernelGGL(grad_derive_kernel<float>, grid, dim3(256), 0, s, (const float*)X, (float*)Xd, ld, spec);
+  return hipGetLastError();
+}
 hipError_t launch_grad(int dtype, int K, int kt, const GradArgs& a, dim3 grid, hipStream_t s) {
   if (kt != 0 && kt != 4 && kt != GRAD_KT) return hipErrorInvalidValue;
   switch (dtype) {

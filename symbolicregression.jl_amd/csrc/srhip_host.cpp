@@ -550,6 +550,18 @@ template <typename T> class TreeCompiler {
     }
     const srhip_node& n = nd_[i];
     if (n.degree == 1) {
+      if (grad_ && prog_.g_want_derived && leaf_is_feature(n.l)) {
+        // a heavy operator of a feature in a constant-gradient program: its derived column (the
+        // operator's value, no tangent), loaded with the operator's own ordinal -- its check fold and
+        // precise sum stay where the operator's were
+        const int u = classify_unop(unaop(i));
+        const uint32_t key = (uint32_t)u << 16 | (uint32_t)leaf_col(n.l);
+        for (size_t j = 0; j < prog_.gdspec.size(); ++j)
+          if (prog_.gdspec[j] == key) {
+            push_op(H_LOADF, (uint32_t)(prog_.gdbase + (int)j), 0, i, parent);
+            return;
+          }
+      }
       emit(n.l, base, i);
       const int u = classify_unop(unaop(i));
       // cos / sin of an operator output need no check fold of their own (srhip_isa.h UN_NC_FLAG); the
@@ -1101,6 +1113,8 @@ int compile_program_t(srhip_program& P) {
 
 template <typename T>
 int compile_grad_t(srhip_program& P) {
+  P.g_derived = P.g_want_derived && !P.gdspec.empty();
+  if (!P.g_derived) P.g_want_derived = false;
   P.gcode.clear();
   P.gprog_off.assign(P.ntrees, 0);
   P.ginfo.assign(P.ntrees, TreeInfo());
@@ -1350,14 +1364,41 @@ bool srhip::spec_instantiate(srhip_program& P, int32_t slot, int32_t t, const do
   }
 }
 
+// the derived columns a constant-gradient program can read: every heavy unary operator applied to a
+// feature leaf, distinct (operator, column) pairs in order of first appearance, at most GD_MAX
+constexpr size_t GD_MAX = 32;
+void srhip::grad_derived_spec(srhip_program& P) {
+  if (P.gdspec_done) return;
+  P.gdspec_done = true;
+  P.gdspec.clear();
+  P.gdbase = P.maxfeat;
+  for (int32_t t = 0; t < P.ntrees; ++t) {
+    const int64_t b = P.offsets[t], e = P.offsets[t + 1];
+    for (int64_t i = b; i < e; ++i) {
+      const srhip_node& n = P.nodes[i];
+      if (n.degree != 1 || n.l < 0 || b + n.l >= e) continue;
+      const srhip_node& c = P.nodes[b + n.l];
+      if (c.degree != 0 || c.constant || n.op < 1 || n.op > (int)P.unaops.size()) continue;
+      const int u = classify_unop(P.unaops[n.op - 1]);
+      if (u < 0 || un_grad_inline(u)) continue;
+      const uint32_t key = (uint32_t)u << 16 | (uint32_t)(c.feature - 1);
+      if (std::find(P.gdspec.begin(), P.gdspec.end(), key) == P.gdspec.end() && P.gdspec.size() < GD_MAX)
+        P.gdspec.push_back(key);
+    }
+  }
+}
+
 int srhip::compile_grad_program(srhip_program& P) {
+  // a program compiled for the other form (derived columns or not) is compiled again in full
+  if (P.grad_ready && P.g_derived != (P.g_want_derived && !P.gdspec.empty())) P.grad_ready = false;
   if (P.grad_ready) return SRHIP_OK;
+  const bool same_form = P.g_derived == (P.g_want_derived && !P.gdspec.empty());
   static const bool no_patch = [] { const char* e = getenv("SRHIP_NO_GRAD_PATCH"); return e && *e && *e != '0'; }();
   int rc;
   bool patched = false;
   int64_t lo = 0, hi = -1;  // patched instruction range
   const double t_patch0 = host_now_s();
-  if (!no_patch && P.ctx && P.d_gcode.p) {  // a previous full compile is on the device
+  if (!no_patch && same_form && P.ctx && P.d_gcode.p) {  // a previous full compile is on the device
     switch (P.dtype) {
       case SRHIP_F32: rc = patch_grad_t<float>(P, patched, lo, hi); break;
       case SRHIP_F64: rc = patch_grad_t<double>(P, patched, lo, hi); break;

@@ -175,6 +175,7 @@ struct srhip_ctx {
   srhip::DevBuf slab_loss, slab_chk, slab_prec, order_prec;
   srhip::DevBuf vX, vy, vw, vidx, vstats;  // gathered views (batching idx)
   srhip::DevBuf g_chunks, g_slab, g_red;   // constant-gradient launches
+  srhip::DevBuf g_xd;                        // their derived view (features + derived columns)
   srhip::HostBuf h_gchunks[2], h_gred[2];   // their pinned staging, per pass (gradient, value-only)
   srhip::HostBuf h_gpatch, h_gspec;         // pinned staging of patched / speculative gradient code
   srhip::HostBuf h_loss, h_chk, h_stats, h_prec, h_dbg;
@@ -259,6 +260,12 @@ struct srhip_program {
   // gradient program (constants not folded, constant leaves carry their get_constants index);
   // compiled on first use by the constant-gradient path
   bool grad_ready = false;
+  // derived columns of the gradient program (constant-gradient launches only): gdspec[j] = u << 16 |
+  // feature column, read as column gdbase + j of a derived view; g_derived: the compiled gradient
+  // program reads them (compiled so when g_want_derived and gdspec is not empty)
+  std::vector<uint32_t> gdspec;
+  int32_t gdbase = 0;
+  bool gdspec_done = false, g_want_derived = false, g_derived = false;
   std::vector<srhip::Ins> gcode;
   std::vector<int32_t> gprog_off;
   std::vector<srhip::TreeInfo> ginfo;  // did_succeed metadata for the gradient program's constants
@@ -296,6 +303,10 @@ struct View {
   int64_t ld, m;
   const FeatStat* stats;  // host
   double sum_w;
+  // gradient launches over a derived view (X = [the program's feature columns | its derived columns],
+  // srhip_optim.cpp derived_view): the feature columns staged per row block; -1: the dataset's
+  int32_t nfeat_x = -1;
+  int32_t nd_x = 0;  // its derived columns (then as many tangent-zero columns)
 };
 struct LaunchPlan {
   int rb_rows, nrb, groups, tpg;
@@ -305,6 +316,7 @@ struct LaunchPlan {
 int compile_program(srhip_program& P);       // eval program (+ invalidates the gradient program)
 extern thread_local double g_patch_scan_s, g_patch_copy_s;  // optimiser timing split (SRHIP_OPTIM_TIMING), per thread
 int compile_grad_program(srhip_program& P);  // gradient program, uploaded
+void grad_derived_spec(srhip_program& P);     // P.gdspec / gdbase from the trees (once)
 // Speculative slot `slot` := tree t at constants c[0 .. nconst) (get_constants order), host side;
 // false if the tree cannot be instantiated.  *static_fail: did_succeed is false before any row is
 // evaluated (a non-finite constant leaf or constant subtree; no evaluation needed).  [lo, hi) grows by the instructions written.

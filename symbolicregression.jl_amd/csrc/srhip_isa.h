@@ -101,6 +101,12 @@ constexpr uint32_t UN_NC_FLAG = 0x8000;
 // operand's rows all hold one value (and one tangent), so the kernel evaluates the operator on one row
 // and copies it to the others -- the same bits, one evaluation per lane instead of R
 constexpr uint32_t UN_UNIFORM_FLAG = 0x4000;
+// unary operators the gradient kernel evaluates inline (a few instructions, exact derivative); the rest
+// are "heavy" calls -- those a gradient program reads from derived columns when applied to a feature
+constexpr bool un_grad_inline(int u) {
+  return u == UN_NEG || u == UN_SQUARE || u == UN_CUBE || u == UN_ABS || u == UN_RELU || u == UN_SIGN ||
+         u == UN_ROUND || u == UN_FLOOR || u == UN_CEIL;
+}
 
 constexpr uint32_t h_spec(int sb, uint32_t form) { return H_BIN0 + uint32_t(sb) * SPEC_STRIDE + form; }
 constexpr uint32_t h_heavy(int hb, uint32_t form) { return H_HEAVY0 + uint32_t(hb) * HEAVY_STRIDE + form; }

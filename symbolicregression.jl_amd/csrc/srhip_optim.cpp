@@ -119,6 +119,35 @@ struct GradItem {
   uint8_t* ok;   // nullable
   bool value_only = false;  // loss only (a line-search trial point): the cheap KT = 0 kernel
 };
+// The derived view of constant-gradient launches (GMODE_LOSS: the optimiser and srhip_eval_loss_grad):
+// X' = [the program's feature columns | its derived columns U(X[f]) | their tangent-zero columns] in
+// the context's g_xd, built once
+// per call (one copy + one launch), so a gradient program reads every heavy operator of a feature as a
+// column instead of evaluating it per row, per trial point (C4: ~0.9 per tree, cos / exp of a feature).
+// Off below SRHIP_GRAD_DERIVED_MIN_ROWS rows (default 8192), above SRHIP_GRAD_DERIVED_MAX_MB of view
+// (default 256) and with SRHIP_GRAD_DERIVED=0.
+static int derived_view(srhip_ctx* ctx, srhip_program* P, View& v) {
+  P->g_want_derived = false;
+  const char* e = env_get("SRHIP_GRAD_DERIVED");
+  if (e && *e == '0') return SRHIP_OK;
+  if (v.m < env_int_opt("SRHIP_GRAD_DERIVED_MIN_ROWS", 8192)) return SRHIP_OK;
+  grad_derived_spec(*P);
+  const int nd = (int)P->gdspec.size();
+  if (nd == 0 || P->gdbase <= 0) return SRHIP_OK;
+  const size_t es = P->dtype == SRHIP_F64 ? 8 : 4;
+  const size_t bytes = (size_t)(P->gdbase + 2 * nd) * v.ld * es;
+  if (bytes > ((size_t)env_int_opt("SRHIP_GRAD_DERIVED_MAX_MB", 256) << 20)) return SRHIP_OK;  // (a copy per call)
+  HIP_TRY(ctx->g_xd.ensure(bytes));
+  HIP_TRY(hipMemcpyAsync(ctx->g_xd.p, v.X, (size_t)P->gdbase * v.ld * es, hipMemcpyDeviceToDevice, ctx->stream));
+  HIP_TRY(launch_grad_derive(P->dtype, v.X, (uint8_t*)ctx->g_xd.p + (size_t)P->gdbase * v.ld * es, v.ld,
+                             P->gdspec.data(), nd, ctx->stream));
+  v.X = ctx->g_xd.p;
+  v.nfeat_x = P->gdbase;
+  v.nd_x = nd;
+  P->g_want_derived = true;
+  return SRHIP_OK;
+}
+
 static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
                            const View& v, const std::vector<GradItem>& items);
 // Loss and gradient for `trees` at the program's current constants: f[t], g[coff[t] ..], ok[t]
@@ -274,7 +303,8 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     a.ld = v.ld;
     a.nvalid = v.m;
     a.nchunks = nch;
-    a.nfeat = (int32_t)ds->nfeat;
+    a.nfeat = v.nfeat_x >= 0 ? v.nfeat_x : (int32_t)ds->nfeat;
+    a.gd_nd = v.nd_x;
     a.rb_rows = ps.L.rb_rows;
     a.nrb = ps.L.nrb;
     a.chunks_per_group = ps.L.tpg;
@@ -841,6 +871,8 @@ int srhip_eval_loss_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program*
     rc = gathered_weight_sum(ctx, ds, nidx, v);
     if (rc) return rc;
   }
+  rc = derived_view(ctx, P, v);
+  if (rc) return rc;
   const std::vector<int64_t> coff = const_offsets(*P);
   std::vector<int32_t> all(P->ntrees);
   for (int32_t t = 0; t < P->ntrees; ++t) all[t] = t;
@@ -871,6 +903,7 @@ int srhip_eval_grad_predict(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progr
   View v;
   rc = make_view(ctx, ds, idx, nidx, false, v);
   if (rc) return rc;
+  P->g_want_derived = false;  // per-row derivatives (features: the operators' own) -- no derived columns
   rc = compile_grad_program(*P);
   if (rc) return rc;
   const int32_t nt = P->ntrees;
@@ -1015,6 +1048,11 @@ int optimize_split(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, co
     const int32_t n2 = (int32_t)tb.size();
     const int rc = srhip_program_create(aux[gi - 1], P->dtype, nodes2.data(), offs2.data(), n2, &ops, &q.P);
     if (rc) return rc;
+    // the caller's derived view serves every group: the same column numbering
+    q.P->gdspec = P->gdspec;
+    q.P->gdbase = P->gdbase;
+    q.P->gdspec_done = P->gdspec_done;
+    q.P->g_want_derived = P->g_want_derived;
     q.coff = const_offsets(*q.P);
     q.starts.assign(starts.size(), std::vector<double>(q.coff.back()));
     q.bx.resize(q.coff.back());
@@ -1084,6 +1122,8 @@ int srhip_optimize_constants_starts(srhip_ctx* ctx, const srhip_dataset* ds, srh
     rc = gathered_weight_sum(ctx, ds, nidx, v);
     if (rc) return rc;
   }
+  rc = derived_view(ctx, P, v);
+  if (rc) return rc;
   const std::vector<int64_t> coff = const_offsets(*P);
   const std::vector<double> x0 = get_all_consts(*P);
   std::vector<int32_t> trees;  // trees with constants (nconst == 0: nothing to optimise, :35)

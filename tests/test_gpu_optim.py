@@ -552,3 +552,46 @@ def test_value_only_screening_is_exact(ctx, dtype, monkeypatch):
         prog.close()
     for u, v in zip(res["0"], res["1"]):
         assert _bits_equal(u, v)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_derived_view_is_exact(ctx, dtype, monkeypatch):
+    """Constant-gradient launches read every heavy operator of a feature (cos(x), exp(x), ...) from a
+    derived view's column, computed once per call with the kernel's own value function, with the
+    operator's check fold and precise-sum ordinal on the load (srhip_optim.cpp derived_view).  Losses,
+    gradients, did_succeed (an exp(x) overflowing in one row included), value-only passes and a
+    split optimize_constants run are bitwise those of the per-row operators (SRHIP_GRAD_DERIVED=0);
+    per-row derivatives after an optimiser call on the same program (which compiles it back without
+    derived columns) equal a fresh program's."""
+    sr = _sr()
+    monkeypatch.setenv("SRHIP_GRAD_DERIVED_MIN_ROWS", "0")
+    opts, _, nodes, offs, X, y = _problem(sr, dtype, ntrees=96)
+    exp_op = opts.unary_operators.index("exp") + 1
+    extra = [sr.Node(3, sr.Node(exp_op, sr.Node(feature=2)), sr.Node(val=1.5)),
+             sr.Node(1, sr.Node(exp_op, sr.Node(feature=1)), sr.Node(val=0.25))]
+    en, eo = sr.flatten(extra, opts, dtype)
+    nodes = np.concatenate([nodes, en])
+    offs = np.concatenate([offs, eo[1:] + offs[-1]])
+    X = np.array(X, copy=True)
+    X[1, 17] = 1000.0 if dtype == np.float64 else 100.0  # exp(x1) overflows in one row
+    ds = sr.DeviceDataset(ctx, X, y)
+    loss = sr.L2DistLoss()
+    res = {}
+    for d in ("0", "1"):
+        monkeypatch.setenv("SRHIP_GRAD_DERIVED", d)
+        prog = sr.Program(ctx, nodes, offs, opts, dtype)
+        l, g, ok = prog.eval_loss_grad(ds, loss)
+        monkeypatch.setenv("SRHIP_GRAD_VALUE_ONLY", "1")
+        vl, _, vok = prog.eval_loss_grad(ds, loss)
+        monkeypatch.delenv("SRHIP_GRAD_VALUE_ONLY")
+        out, imp, fc = prog.optimize_constants(ds, loss, iterations=8, nrestarts=1, seed=3)
+        consts = np.concatenate(prog.get_constants())
+        pred, pgrad, pok = prog.eval_grad_predict(ds, variable=True)
+        flat = lambda a: np.concatenate([np.ravel(x) for x in a])  # noqa: E731
+        res[d] = [np.asarray(l, np.float64), flat(g), np.asarray(ok), np.asarray(vl, np.float64), np.asarray(vok),
+                  np.asarray(out, np.float64), imp, fc, consts, np.asarray(pred), flat(pgrad), np.asarray(pok)]
+        prog.close()
+    assert not res["1"][2][-2] and res["1"][2][-1], res["1"][2][-2:]
+    assert res["1"][6].sum() > 5
+    for i, (u, v) in enumerate(zip(res["0"], res["1"])):
+        assert _bits_equal(u, v), i
