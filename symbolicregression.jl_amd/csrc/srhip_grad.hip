@@ -434,6 +434,11 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
           GK_CASES(H_PUSH0, { RR(S[k][r] = A[r];) })
           GK_CASES(H_SLOADF0, { RR(set_feat<GM>(S[k][r], xat(opnd, rr), opnd - c0);) })
           GK_CASES(H_SLOADC0, { RR(set_const<GM>(S[k][r], imm, opnd - c0);) })
+// (AC / CA / SA / AS forms with UN_UNIFORM_FLAG in the operand field: two constant subtrees, one
+// value per lane -- row 0 evaluated, copied to the others with their check folds)
+#define GK_UNI_ROWS()                                                                              \
+  UNR for (int r = 1; r < R; ++r) A[r] = A[0];                                                     \
+  UNR for (int r = 0; r < R; ++r) chk_fold(M, A[r].v);
 #define GK_SPEC(NAME, FN)                                                                          \
   case h_spec(SB_##NAME, SPEC_AF): {                                                               \
     RR(Dual<T, KT> o; set_feat<GM>(o, xat(opnd, rr), opnd - c0);                                   \
@@ -444,17 +449,37 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
        T f, fl, fr; dual_spec<T, SB_##NAME>(o.v, A[r].v, f, fl, fr); combine(A[r], o, A[r], f, fl, fr); \
        chk_fold(M, A[r].v);) break; }                                                              \
   case h_spec(SB_##NAME, SPEC_AC): {                                                               \
-    RR(Dual<T, KT> o; set_const<GM>(o, imm, opnd - c0);                                            \
+    const int ci = (opnd & ~(int)UN_UNIFORM_FLAG) - c0;                                            \
+    if (R > 1 && (ins.a & UN_UNIFORM_FLAG)) {                                                      \
+      Dual<T, KT> o; set_const<GM>(o, imm, ci);                                                    \
+      T f, fl, fr; dual_spec<T, SB_##NAME>(A[0].v, o.v, f, fl, fr); combine(A[0], A[0], o, f, fl, fr); \
+      GK_UNI_ROWS() break;                                                                         \
+    }                                                                                              \
+    RR(Dual<T, KT> o; set_const<GM>(o, imm, ci);                                                   \
        T f, fl, fr; dual_spec<T, SB_##NAME>(A[r].v, o.v, f, fl, fr); combine(A[r], A[r], o, f, fl, fr); \
        chk_fold(M, A[r].v);) break; }                                                              \
   case h_spec(SB_##NAME, SPEC_CA): {                                                               \
-    RR(Dual<T, KT> o; set_const<GM>(o, imm, opnd - c0);                                            \
+    const int ci = (opnd & ~(int)UN_UNIFORM_FLAG) - c0;                                            \
+    if (R > 1 && (ins.a & UN_UNIFORM_FLAG)) {                                                      \
+      Dual<T, KT> o; set_const<GM>(o, imm, ci);                                                    \
+      T f, fl, fr; dual_spec<T, SB_##NAME>(o.v, A[0].v, f, fl, fr); combine(A[0], o, A[0], f, fl, fr); \
+      GK_UNI_ROWS() break;                                                                         \
+    }                                                                                              \
+    RR(Dual<T, KT> o; set_const<GM>(o, imm, ci);                                                   \
        T f, fl, fr; dual_spec<T, SB_##NAME>(o.v, A[r].v, f, fl, fr); combine(A[r], o, A[r], f, fl, fr); \
        chk_fold(M, A[r].v);) break; }                                                              \
   GK_CASES(h_spec(SB_##NAME, SPEC_SA0), {                                                          \
+    if (R > 1 && (ins.a & UN_UNIFORM_FLAG)) {                                                      \
+      T f, fl, fr; dual_spec<T, SB_##NAME>(S[k][0].v, A[0].v, f, fl, fr);                          \
+      combine(A[0], S[k][0], A[0], f, fl, fr); GK_UNI_ROWS() break;                                \
+    }                                                                                              \
     RR(T f, fl, fr; dual_spec<T, SB_##NAME>(S[k][r].v, A[r].v, f, fl, fr);                         \
        combine(A[r], S[k][r], A[r], f, fl, fr); chk_fold(M, A[r].v);) })                           \
   GK_CASES(h_spec(SB_##NAME, SPEC_AS0), {                                                          \
+    if (R > 1 && (ins.a & UN_UNIFORM_FLAG)) {                                                      \
+      T f, fl, fr; dual_spec<T, SB_##NAME>(A[0].v, S[k][0].v, f, fl, fr);                          \
+      combine(A[0], A[0], S[k][0], f, fl, fr); GK_UNI_ROWS() break;                                \
+    }                                                                                              \
     RR(T f, fl, fr; dual_spec<T, SB_##NAME>(A[r].v, S[k][r].v, f, fl, fr);                         \
        combine(A[r], A[r], S[k][r], f, fl, fr); chk_fold(M, A[r].v);) })
           SRHIP_SPEC_BINOPS(GK_SPEC)

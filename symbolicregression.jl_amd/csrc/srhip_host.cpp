@@ -586,24 +586,27 @@ template <typename T> class TreeCompiler {
         else push_op(h_spec(sb, SPEC_CF), cr, leaf_imm(L), i, parent);
         return;
       }
+      // gradient programs: an operator of two constant subtrees (one value on every row) is evaluated
+      // once per lane (the forms whose operand field is a constant index or unused)
+      const uint32_t uni = grad_ && is_const(i) && grad_uniform_env() ? UN_UNIFORM_FLAG : 0u;
       if (rl) {
         emit(L, base, i);
         if (leaf_col(Rr) >= 0) push_op(h_spec(sb, SPEC_AF), leaf_col(Rr), 0, i, parent);
-        else push_op(h_spec(sb, SPEC_AC), cop(Rr), leaf_imm(Rr), i, parent);
+        else push_op(h_spec(sb, SPEC_AC), cop(Rr) | uni, leaf_imm(Rr), i, parent);
       } else if (ll) {
         emit(Rr, base, i);
         if (leaf_col(L) >= 0) push_op(h_spec(sb, SPEC_FA), leaf_col(L), 0, i, parent);
-        else push_op(h_spec(sb, SPEC_CA), cop(L), leaf_imm(L), i, parent);
+        else push_op(h_spec(sb, SPEC_CA), cop(L) | uni, leaf_imm(L), i, parent);
       } else if (need(L) >= need(Rr)) {
         emit(L, base, i);
         push_ins(H_PUSH0 + base, 0, 0);
         emit(Rr, base + 1, i);
-        push_op(h_spec(sb, SPEC_SA0 + base), 0, 0, i, parent);
+        push_op(h_spec(sb, SPEC_SA0 + base), uni, 0, i, parent);
       } else {
         emit(Rr, base, i);
         push_ins(H_PUSH0 + base, 0, 0);
         emit(L, base + 1, i);
-        push_op(h_spec(sb, SPEC_AS0 + base), 0, 0, i, parent);
+        push_op(h_spec(sb, SPEC_AS0 + base), uni, 0, i, parent);
       }
       return;
     }
@@ -1150,7 +1153,7 @@ int compile_grad_t(srhip_program& P) {
         }
         if (!carries) continue;
         P.gci.push_back(i);
-        P.gci.push_back((int32_t)(ins.a & 0xffff));
+        P.gci.push_back((int32_t)(ins.a & 0xffff & ~UN_UNIFORM_FLAG));  // (the constant index)
         ++nc;
       }
       // every constant leaf is consumed by exactly one such instruction

@@ -595,3 +595,38 @@ def test_derived_view_is_exact(ctx, dtype, monkeypatch):
     assert res["1"][6].sum() > 5
     for i, (u, v) in enumerate(zip(res["0"], res["1"])):
         assert _bits_equal(u, v), i
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_uniform_constant_subtrees_are_exact(ctx, dtype, monkeypatch):
+    """Operators whose operands are constant subtrees (cos(c), c1 / c2, ...) are evaluated once per lane
+    and copied to the lane's rows (UN_UNIFORM_FLAG); losses, gradients, did_succeed, value-only
+    passes and an optimize_constants run are bitwise those of the per-row evaluation
+    (SRHIP_GRAD_UNIFORM=0)."""
+    sr = _sr()
+    opts, _, nodes, offs, X, y = _problem(sr, dtype, ntrees=80, max_size=24)
+    cos_op = opts.unary_operators.index("cos") + 1
+    extra = [sr.Node(3, sr.Node(cos_op, sr.Node(val=0.7)), sr.Node(feature=1)),            # cos(c) * x0
+             sr.Node(1, sr.Node(4, sr.Node(val=2.0), sr.Node(val=3.0)), sr.Node(feature=2)),  # c1 / c2 + x1
+             sr.Node(3, sr.Node(1, sr.Node(val=1e30), sr.Node(val=1e30)), sr.Node(feature=3))]
+    en, eo = sr.flatten(extra, opts, dtype)
+    nodes = np.concatenate([nodes, en])
+    offs = np.concatenate([offs, eo[1:] + offs[-1]])
+    ds = sr.DeviceDataset(ctx, X, y)
+    loss = sr.L2DistLoss()
+    res = {}
+    for u in ("0", "1"):
+        monkeypatch.setenv("SRHIP_GRAD_UNIFORM", u)
+        prog = sr.Program(ctx, nodes, offs, opts, dtype)
+        l, g, ok = prog.eval_loss_grad(ds, loss)
+        monkeypatch.setenv("SRHIP_GRAD_VALUE_ONLY", "1")
+        vl, _, vok = prog.eval_loss_grad(ds, loss)
+        monkeypatch.delenv("SRHIP_GRAD_VALUE_ONLY")
+        out, imp, fc = prog.optimize_constants(ds, loss, iterations=8, nrestarts=1, seed=3)
+        flat = lambda a: np.concatenate([np.ravel(x) for x in a])  # noqa: E731
+        res[u] = [np.asarray(l, np.float64), flat(g), np.asarray(ok), np.asarray(vl, np.float64), np.asarray(vok),
+                  np.asarray(out, np.float64), imp, fc, np.concatenate(prog.get_constants())]
+        prog.close()
+    assert res["1"][6].sum() > 5
+    for i, (a, b) in enumerate(zip(res["0"], res["1"])):
+        assert _bits_equal(a, b), i
