@@ -581,6 +581,8 @@ def test_derived_view_is_exact(ctx, dtype, monkeypatch):
         monkeypatch.setenv("SRHIP_GRAD_DERIVED", d)
         prog = sr.Program(ctx, nodes, offs, opts, dtype)
         l, g, ok = prog.eval_loss_grad(ds, loss)
+        idx = np.random.default_rng(2).integers(0, X.shape[1], 1500)  # a batched (gathered) view
+        bl, bg, bok = prog.eval_loss_grad(ds, loss, idx=idx)
         monkeypatch.setenv("SRHIP_GRAD_VALUE_ONLY", "1")
         vl, _, vok = prog.eval_loss_grad(ds, loss)
         monkeypatch.delenv("SRHIP_GRAD_VALUE_ONLY")
@@ -589,7 +591,8 @@ def test_derived_view_is_exact(ctx, dtype, monkeypatch):
         pred, pgrad, pok = prog.eval_grad_predict(ds, variable=True)
         flat = lambda a: np.concatenate([np.ravel(x) for x in a])  # noqa: E731
         res[d] = [np.asarray(l, np.float64), flat(g), np.asarray(ok), np.asarray(vl, np.float64), np.asarray(vok),
-                  np.asarray(out, np.float64), imp, fc, consts, np.asarray(pred), flat(pgrad), np.asarray(pok)]
+                  np.asarray(out, np.float64), imp, fc, consts, np.asarray(pred), flat(pgrad), np.asarray(pok),
+                  np.asarray(bl, np.float64), flat(bg), np.asarray(bok)]
         prog.close()
     assert not res["1"][2][-2] and res["1"][2][-1], res["1"][2][-2:]
     assert res["1"][6].sum() > 5
