@@ -2818,6 +2818,8 @@ int srhip_dataset_create(srhip_ctx* ctx, int dtype, const void* X, int64_t nfeat
   if (dtype == SRHIP_I32 && w) return fail(SRHIP_ERR_UNSUPPORTED, "weights on Int32 datasets");
   HIP_TRY(hipSetDevice(ctx->device));
   std::unique_ptr<srhip_dataset> d(new srhip_dataset());
+  static std::atomic<uint64_t> g_ds_serial{0};
+  d->serial = ++g_ds_serial;
   d->ctx = ctx;
   d->device = ctx->device;
   d->dtype = dtype;

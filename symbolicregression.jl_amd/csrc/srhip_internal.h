@@ -176,6 +176,12 @@ struct srhip_ctx {
   srhip::DevBuf vX, vy, vw, vidx, vstats;  // gathered views (batching idx)
   srhip::DevBuf g_chunks, g_slab, g_red;   // constant-gradient launches
   srhip::DevBuf g_xd;                        // their derived view (features + derived columns)
+  // what g_xd holds when built from a whole dataset (serial, ld, dtype, column base, spec): reused
+  // by the next call over the same dataset and spec
+  uint64_t g_xd_serial = 0;
+  int64_t g_xd_ld = 0;
+  int g_xd_dtype = -1, g_xd_base = -1;
+  std::vector<uint32_t> g_xd_spec;
   srhip::HostBuf h_gchunks[2], h_gred[2];   // their pinned staging, per pass (gradient, value-only)
   srhip::HostBuf h_gpatch, h_gspec;         // pinned staging of patched / speculative gradient code
   srhip::HostBuf h_loss, h_chk, h_stats, h_prec, h_dbg;
@@ -209,6 +215,7 @@ struct srhip_dataset {
   double sum_w = 0.0;
   srhip::DevBuf X, y, w, stats;
   std::vector<srhip::FeatStat> hstats;  // feature stats over all n rows
+  uint64_t serial = 0;                   // process-unique (caches keyed by dataset identity)
 };
 
 struct srhip_program {

@@ -126,7 +126,7 @@ struct GradItem {
 // column instead of evaluating it per row, per trial point (C4: ~0.9 per tree, cos / exp of a feature).
 // Off below SRHIP_GRAD_DERIVED_MIN_ROWS rows (default 8192), above SRHIP_GRAD_DERIVED_MAX_MB of view
 // (default 256) and with SRHIP_GRAD_DERIVED=0.
-static int derived_view(srhip_ctx* ctx, srhip_program* P, View& v) {
+static int derived_view(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, View& v) {
   P->g_want_derived = false;
   const char* e = env_get("SRHIP_GRAD_DERIVED");
   if (e && *e == '0') return SRHIP_OK;
@@ -137,10 +137,24 @@ static int derived_view(srhip_ctx* ctx, srhip_program* P, View& v) {
   const size_t es = P->dtype == SRHIP_F64 ? 8 : 4;
   const size_t bytes = (size_t)(P->gdbase + 2 * nd) * v.ld * es;
   if (bytes > ((size_t)env_int_opt("SRHIP_GRAD_DERIVED_MAX_MB", 256) << 20)) return SRHIP_OK;  // (a copy per call)
-  HIP_TRY(ctx->g_xd.ensure(bytes));
-  HIP_TRY(hipMemcpyAsync(ctx->g_xd.p, v.X, (size_t)P->gdbase * v.ld * es, hipMemcpyDeviceToDevice, ctx->stream));
-  HIP_TRY(launch_grad_derive(P->dtype, v.X, (uint8_t*)ctx->g_xd.p + (size_t)P->gdbase * v.ld * es, v.ld,
-                             P->gdspec.data(), nd, ctx->stream));
+  // a view of the whole dataset (not a gathered batch) with the same spec as the last build: reused
+  const bool whole = v.X == ds->X.p;
+  const bool same = whole && ctx->g_xd.p && ctx->g_xd_serial == ds->serial && ctx->g_xd_ld == v.ld &&
+                    ctx->g_xd_dtype == P->dtype && ctx->g_xd_base == P->gdbase && ctx->g_xd_spec == P->gdspec;
+  if (!same) {
+    ctx->g_xd_serial = 0;  // (until rebuilt)
+    HIP_TRY(ctx->g_xd.ensure(bytes));
+    HIP_TRY(hipMemcpyAsync(ctx->g_xd.p, v.X, (size_t)P->gdbase * v.ld * es, hipMemcpyDeviceToDevice, ctx->stream));
+    HIP_TRY(launch_grad_derive(P->dtype, v.X, (uint8_t*)ctx->g_xd.p + (size_t)P->gdbase * v.ld * es, v.ld,
+                               P->gdspec.data(), nd, ctx->stream));
+    if (whole) {
+      ctx->g_xd_serial = ds->serial;
+      ctx->g_xd_ld = v.ld;
+      ctx->g_xd_dtype = P->dtype;
+      ctx->g_xd_base = P->gdbase;
+      ctx->g_xd_spec = P->gdspec;
+    }
+  }
   v.X = ctx->g_xd.p;
   v.nfeat_x = P->gdbase;
   v.nd_x = nd;
@@ -871,7 +885,7 @@ int srhip_eval_loss_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program*
     rc = gathered_weight_sum(ctx, ds, nidx, v);
     if (rc) return rc;
   }
-  rc = derived_view(ctx, P, v);
+  rc = derived_view(ctx, ds, P, v);
   if (rc) return rc;
   const std::vector<int64_t> coff = const_offsets(*P);
   std::vector<int32_t> all(P->ntrees);
@@ -1122,7 +1136,7 @@ int srhip_optimize_constants_starts(srhip_ctx* ctx, const srhip_dataset* ds, srh
     rc = gathered_weight_sum(ctx, ds, nidx, v);
     if (rc) return rc;
   }
-  rc = derived_view(ctx, P, v);
+  rc = derived_view(ctx, ds, P, v);
   if (rc) return rc;
   const std::vector<int64_t> coff = const_offsets(*P);
   const std::vector<double> x0 = get_all_consts(*P);
