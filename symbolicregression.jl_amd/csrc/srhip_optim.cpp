@@ -163,7 +163,7 @@ static int derived_view(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* 
 }
 
 static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
-                           const View& v, const std::vector<GradItem>& items);
+                           const View& v, const std::vector<GradItem>& items, bool timed = true);
 // Loss and gradient for `trees` at the program's current constants: f[t], g[coff[t] ..], ok[t]
 // (nullable; did_succeed -- a tree can succeed with an overflowing loss: f = Inf, ok = 1), plus the
 // items in `extra` (speculative slots, already instantiated; their instructions [spec_lo, spec_hi)
@@ -171,7 +171,7 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
 static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss, const View& v,
                      const std::vector<int32_t>& trees, const std::vector<int64_t>& coff, double* f, double* g,
                      uint8_t* ok = nullptr, const std::vector<GradItem>* extra = nullptr, int64_t spec_lo = 0,
-                     int64_t spec_hi = -1, const uint8_t* value_only = nullptr) {
+                     int64_t spec_hi = -1, const uint8_t* value_only = nullptr, bool timed = true) {
   const double t0 = now_s();
   int rc = compile_grad_program(*P);
   g_t_compile += now_s() - t0;
@@ -189,7 +189,7 @@ static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, 
       memcpy(ctx->h_gspec.p, P->gcode.data() + spec_lo, nb);
       HIP_TRY(hipMemcpyAsync((Ins*)P->d_gcode.p + spec_lo, ctx->h_gspec.p, nb, hipMemcpyHostToDevice, ctx->stream));
     }
-    return eval_grad_items(ctx, ds, P, loss, v, items);
+    return eval_grad_items(ctx, ds, P, loss, v, items, timed);
   };
   rc = body();
   // a patched gradient program's upload (compile_grad_program) may still be in flight from P->gcode:
@@ -197,8 +197,10 @@ static int eval_grad(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, 
   if (rc) (void)hipStreamSynchronize(ctx->stream);
   return rc;
 }
+// timed: HIP events around the gradient kernels (srhip_last_kernel_ms).  The optimiser's launches go
+// without: two timing events per launch cost C4 ~5 % (149-153 against 141-145 ms on one box).
 static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, const srhip_loss* loss,
-                           const View& v, const std::vector<GradItem>& items) {
+                           const View& v, const std::vector<GradItem>& items, bool timed) {
   const int dtype = P->dtype;
   const bool weighted = ds->weighted;
   const double wsum = weighted ? v.sum_w : (double)v.m;
@@ -326,7 +328,7 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     a.loss_p0 = loss->p0;
     a.weighted = weighted ? 1 : 0;
     a.max_steps = P->gmax_len;
-    if (first) HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));  // srhip_last_kernel_ms: the gradient kernels
+    if (first && timed) HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));  // srhip_last_kernel_ms: the gradient kernels
     first = false;
     // value-only screening (SRHIP_GRAD_SCREEN = the fewest value-only chunks screened; default 0 =
     // off): row block 0 of every chunk first, in a launch of its own, then the other blocks, where a
@@ -352,8 +354,8 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
                                ctx->stream));
     ps.red = (const double*)ctx->h_gred[pi].p;
   }
-  HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
-  ctx->timed = true;
+  if (timed) HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+  ctx->timed = timed;
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   // decision inputs in the partials layout: only the feature statistics and the row count are read
   std::vector<double> sums(2 * (size_t)P->ntrees + 2 * ds->nfeat + 1, 0.0);
@@ -818,7 +820,7 @@ static int bfgs_pipelined(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program
     }
     const double t1 = now_s();
     int rc = eval_grad(ctx, ds, P, loss, v, act, coff, fe.data(), ge.data(), nullptr, &sitems, spec_lo, spec_hi,
-                       vonly.data());
+                       vonly.data(), /*timed=*/false);
     if (rc) return rc;
     if (g_stats_on)  // SRHIP_OPTIM_TIMING=2: launch-size histogram
       g_hist[act.size() <= 1 ? 0 : act.size() <= 4 ? 1 : act.size() <= 16 ? 2 : act.size() <= 64 ? 3 : 4] += 1;
