@@ -633,3 +633,37 @@ def test_uniform_constant_subtrees_are_exact(ctx, dtype, monkeypatch):
     assert res["1"][6].sum() > 5
     for i, (a, b) in enumerate(zip(res["0"], res["1"])):
         assert _bits_equal(a, b), i
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_gradient_program_forms_exact_on_domain_operators(ctx, dtype, monkeypatch):
+    """Derived-view columns and once-per-lane constant subtrees over operators with restricted domains
+    (safe log / sqrt return NaN below 0, tanh, sin): losses, gradients and did_succeed of a full and
+    a value-only pass are bitwise those of the plain per-row program (SRHIP_GRAD_DERIVED=0,
+    SRHIP_GRAD_UNIFORM=0), NaN columns and infinite derivative factors included."""
+    sr = _sr()
+    monkeypatch.setenv("SRHIP_GRAD_DERIVED_MIN_ROWS", "0")
+    opts = sr.Options(binary_operators=("+", "-", "*", "/"), unary_operators=("log", "sqrt", "sin", "tanh", "exp"))
+    trees = sr.random_population(120, opts, 3, dtype, seed=23, max_size=22)
+    nodes, offs = sr.flatten(trees, opts, dtype)
+    rng = np.random.default_rng(24)
+    X = (rng.standard_normal((3, 2500)) * 2.0).astype(dtype)
+    X[0, :8] = 0.0  # log(0) = -Inf, sqrt'(0) = Inf
+    y = (np.sin(X[1]) + 0.5 * X[2]).astype(dtype)
+    ds = sr.DeviceDataset(ctx, X, y)
+    loss = sr.L2DistLoss()
+    res = {}
+    for form in ("plain", "fast"):
+        monkeypatch.setenv("SRHIP_GRAD_DERIVED", "0" if form == "plain" else "1")
+        monkeypatch.setenv("SRHIP_GRAD_UNIFORM", "0" if form == "plain" else "1")
+        prog = sr.Program(ctx, nodes, offs, opts, dtype)
+        l, g, ok = prog.eval_loss_grad(ds, loss)
+        monkeypatch.setenv("SRHIP_GRAD_VALUE_ONLY", "1")
+        vl, _, vok = prog.eval_loss_grad(ds, loss)
+        monkeypatch.delenv("SRHIP_GRAD_VALUE_ONLY")
+        flat = lambda a: np.concatenate([np.ravel(x) for x in a])  # noqa: E731
+        res[form] = [np.asarray(l, np.float64), flat(g), np.asarray(ok), np.asarray(vl, np.float64), np.asarray(vok)]
+        prog.close()
+    assert res["fast"][2].sum() > 10 and (~res["fast"][2]).sum() > 3
+    for i, (a, b) in enumerate(zip(res["plain"], res["fast"])):
+        assert _bits_equal(a, b), i
