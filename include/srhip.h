@@ -317,8 +317,9 @@ int srhip_optimize_constants_starts(srhip_ctx* ctx, const srhip_dataset* ds, srh
 
 /* ---- measurement hooks (bench / profiling) --------------------------------------------- */
 /* Device time (ms) of the last main kernel on this context -- the interpreter of srhip_eval_loss /
- * srhip_eval_predict, or the dual-number kernel of srhip_eval_loss_grad / the optimiser's last
- * gradient launch -- measured with HIP events recorded on the context's stream; < 0 if unavailable. */
+ * srhip_eval_predict, or the dual-number kernel of srhip_eval_loss_grad -- measured with HIP events
+ * recorded on the context's stream; < 0 if unavailable (also after srhip_optimize_constants*, whose
+ * many small gradient launches go without events). */
 double srhip_last_kernel_ms(const srhip_ctx* ctx);
 /* Work of the last srhip_eval_loss / srhip_eval_loss_partials / srhip_eval_predict on this context,
  * counted on the device (the rows each tree was actually evaluated on: a tree that failed -- the

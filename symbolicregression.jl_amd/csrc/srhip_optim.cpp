@@ -121,9 +121,9 @@ struct GradItem {
 };
 // The derived view of constant-gradient launches (GMODE_LOSS: the optimiser and srhip_eval_loss_grad):
 // X' = [the program's feature columns | its derived columns U(X[f]) | their tangent-zero columns] in
-// the context's g_xd, built once
-// per call (one copy + one launch), so a gradient program reads every heavy operator of a feature as a
-// column instead of evaluating it per row, per trial point (C4: ~0.9 per tree, cos / exp of a feature).
+// the context's g_xd, built once per call (one copy + one launch; reused by the next call over the
+// same dataset and spec), so a gradient program reads every heavy operator of a feature as a column
+// instead of evaluating it per row, per trial point (C4: ~0.9 per tree, cos / exp of a feature).
 // Off below SRHIP_GRAD_DERIVED_MIN_ROWS rows (default 8192), above SRHIP_GRAD_DERIVED_MAX_MB of view
 // (default 256) and with SRHIP_GRAD_DERIVED=0.
 static int derived_view(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* P, View& v) {
