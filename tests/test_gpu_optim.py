@@ -667,3 +667,31 @@ def test_gradient_program_forms_exact_on_domain_operators(ctx, dtype, monkeypatc
     assert res["fast"][2].sum() > 10 and (~res["fast"][2]).sum() > 3
     for i, (a, b) in enumerate(zip(res["plain"], res["fast"])):
         assert _bits_equal(a, b), i
+
+
+def test_derived_view_is_exact_weighted(ctx, monkeypatch):
+    """The derived view over a weighted Float64 dataset, whole and batched (gathered rows and weights):
+    losses, gradients, did_succeed and an optimize_constants run bitwise those of the per-row
+    operators."""
+    sr = _sr()
+    monkeypatch.setenv("SRHIP_GRAD_DERIVED_MIN_ROWS", "0")
+    dtype = np.float64
+    opts, _, nodes, offs, X, y = _problem(sr, dtype, ntrees=72)
+    w = np.random.default_rng(9).uniform(0.1, 2.0, X.shape[1]).astype(dtype)
+    ds = sr.DeviceDataset(ctx, X, y, w)
+    loss = sr.L2DistLoss()
+    idx = np.random.default_rng(10).integers(0, X.shape[1], 1200)
+    res = {}
+    for d in ("0", "1"):
+        monkeypatch.setenv("SRHIP_GRAD_DERIVED", d)
+        prog = sr.Program(ctx, nodes, offs, opts, dtype)
+        l, g, ok = prog.eval_loss_grad(ds, loss)
+        bl, bg, bok = prog.eval_loss_grad(ds, loss, idx=idx)
+        out, imp, fc = prog.optimize_constants(ds, loss, iterations=8, nrestarts=1, seed=5)
+        flat = lambda a: np.concatenate([np.ravel(x) for x in a])  # noqa: E731
+        res[d] = [np.asarray(l), flat(g), np.asarray(ok), np.asarray(bl), flat(bg), np.asarray(bok),
+                  np.asarray(out), imp, fc, np.concatenate(prog.get_constants())]
+        prog.close()
+    assert res["1"][7].sum() > 5
+    for i, (a, b) in enumerate(zip(res["0"], res["1"])):
+        assert _bits_equal(a, b), i
