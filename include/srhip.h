@@ -229,13 +229,17 @@ int srhip_comm_size(const srhip_comm* comm, int32_t* nranks, int32_t* rank);
 /* Host wall time of the communicator's exchanges (issue -> completion seen; a migration counts from
  * srhip_comm_migrate_start to its _wait): the last one, the total, and how many (any may be NULL). */
 int srhip_comm_stats(const srhip_comm* comm, double* ms_last, double* ms_total, int64_t* calls);
-/* In-place all-reduce of a float64 vector: on device memory (complete before the call) in place, no
- * host staging; a host vector is staged through the communicator's device buffer.  Every exchange
- * waits at most SRHIP_COMM_TIMEOUT_S seconds (default 300) -- past that, or on an asynchronous RCCL
- * error, the communicator is aborted and this and every later call on it fail. */
+/* In-place all-reduce of a float64 vector: on device memory in place, no host staging; a host vector is
+ * staged through the communicator's device buffer.  Device memory: the collective runs on the
+ * communicator's own stream and is NOT ordered after other streams, so whatever produced buf must be
+ * complete when this is called (synchronise the producing stream or event first); the call returns
+ * after the collective has completed.  Every exchange waits at most SRHIP_COMM_TIMEOUT_S seconds
+ * (default 300) -- past that, or on an asynchronous RCCL error, the communicator is aborted and this
+ * and every later call on it fail. */
 int srhip_comm_allreduce_f64(srhip_comm* comm, double* buf, int64_t n, int32_t op);
-/* Fixed-size all-gather: recv[r * bytes .. (r + 1) * bytes) = rank r's send (both device pointers: no
- * staging). */
+/* Fixed-size all-gather: recv[r * bytes .. (r + 1) * bytes) = rank r's send.  Both device pointers: no
+ * staging, and (as for srhip_comm_allreduce_f64) send must be complete before the call; otherwise both
+ * are staged through pinned host memory. */
 int srhip_comm_allgather(srhip_comm* comm, const void* send, int64_t bytes, void* recv);
 /* Migration: this rank's k best trees of (nodes, offsets[ntrees+1], losses[ntrees]) -- by loss,
  * non-finite last, ties by index; trees longer than max_nodes skipped -- packed into one fixed-size

@@ -403,17 +403,42 @@ SRM_FN float srm_trigf(int kind, float x) {
  * and the quadrant n & 3 picks __kernel_sindf or __kernel_cosdf (k_sinf.c / k_cosf.c coefficients,
  * evaluated as written: no contraction), rounded once to Float32.  Restated from those published
  * sources; Julia cannot run here, so bits against Julia itself stay unpinned. */
+#define SRM_JS1 (-0x15555554cbac77.0p-55)
+#define SRM_JS2 0x111110896efbb2.0p-59
+#define SRM_JS3 (-0x1a00f9e2cae774.0p-65)
+#define SRM_JS4 0x16cd878c3b46a7.0p-71
+#define SRM_JC0 (-0x1ffffffd0c5e81.0p-54)
+#define SRM_JC1 0x155553e1053a42.0p-57
+#define SRM_JC2 (-0x16c087e80f1e27.0p-62)
+#define SRM_JC3 0x199342e0ee5069.0p-68
 SRM_FN double srm_jsin_kernel(double y) {
-  const double S1 = -0x15555554cbac77.0p-55, S2 = 0x111110896efbb2.0p-59, S3 = -0x1a00f9e2cae774.0p-65,
-               S4 = 0x16cd878c3b46a7.0p-71;
-  const double z = y * y, w = z * z, r = S3 + z * S4, s = z * y;
-  return (y + s * (S1 + z * S2)) + s * w * r;
+  const double z = y * y, w = z * z, r = SRM_JS3 + z * SRM_JS4, s = z * y;
+  return (y + s * (SRM_JS1 + z * SRM_JS2)) + s * w * r;
 }
 SRM_FN double srm_jcos_kernel(double y) {
-  const double C0 = -0x1ffffffd0c5e81.0p-54, C1 = 0x155553e1053a42.0p-57, C2 = -0x16c087e80f1e27.0p-62,
-               C3 = 0x199342e0ee5069.0p-68;
-  const double z = y * y, w = z * z, r = C2 + z * C3;
-  return ((1.0 + z * C0) + w * C1) + (w * z) * r;
+  const double z = y * y, w = z * z, r = SRM_JC2 + z * SRM_JC3;
+  return ((1.0 + z * SRM_JC0) + w * SRM_JC1) + (w * z) * r;
+}
+/* The same two polynomials at lower cost, with the same Float32 result (round 6).  Julia rounds its
+ * Float64 kernel value once to Float32.  Horner's form with fused multiply-adds (srm_jsin_fma: z*y and
+ * four fmas; srm_jcos_fma: four fmas -- against 10 and 9 operations in Julia's order) lands within a few
+ * Float64 ulps of Julia's value, so both round to the same Float32 unless the fast value lies within
+ * SRM_JTIE_K Float64 ulps of a Float32 rounding midpoint: the low 29 bits of its double -- the bits the
+ * rounding drops -- within SRM_JTIE_K of 2^28 (srm_jtie).  The device evaluates the fast form, flags
+ * such rows and re-evaluates a wave with a flagged row by Julia's own kernels; tools/check_trigf.c
+ * proves on every float each tier may see that an unflagged fast value rounds to srm_jtrigf's bits.
+ * (A value near a power of two cannot be near a midpoint in both binades: the test on the fast value
+ * is exact there too, and the exhaustive check covers it.) */
+#define SRM_JTIE_K 64u
+SRM_FN double srm_jsin_fma(double y, double z) {
+  const double p = srm_fma(z, srm_fma(z, srm_fma(z, SRM_JS4, SRM_JS3), SRM_JS2), SRM_JS1);
+  return srm_fma(z * y, p, y);
+}
+SRM_FN double srm_jcos_fma(double z) {
+  return srm_fma(z, srm_fma(z, srm_fma(z, srm_fma(z, SRM_JC3, SRM_JC2), SRM_JC1), SRM_JC0), 1.0);
+}
+SRM_FN int srm_jtie(double v) {
+  return (((uint32_t)srm_bits(v) & 0x1FFFFFFFu) - (0x10000000u - SRM_JTIE_K)) <= 2u * SRM_JTIE_K;
 }
 /* rem_pio2_kernel(x::Float32): n, y for |x| >= Float32(pi)/4, x finite */
 SRM_FN int srm_jrem_pio2f(float x, double* y) {

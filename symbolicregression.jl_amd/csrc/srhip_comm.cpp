@@ -67,7 +67,9 @@ namespace {
 // never joins a collective would otherwise hang every other rank inside hipStreamSynchronize.  Polls
 // the event and RCCL's asynchronous error; past SRHIP_COMM_TIMEOUT_S seconds (default 300) or on an
 // RCCL error the communicator is aborted (ncclCommAbort: the pending collectives are torn down) and
-// every later call on it fails.
+// every later call on it fails.  The first SRHIP_COMM_SPIN_US microseconds (default 100) spin on the
+// event with no sleep -- a row-shard exchange completes in tens of microseconds, and a 20 us sleep
+// granularity was a fixed cost of every step -- then the poll sleeps 20 us, 200 us after 10 ms.
 int comm_wait(srhip_comm* c) {
   HIP_TRY(hipEventRecord(c->done, c->stream));
   static const double limit = [] {
@@ -75,7 +77,19 @@ int comm_wait(srhip_comm* c) {
     const double v = e && *e ? atof(e) : 300.0;
     return v > 0 ? v : 300.0;
   }();
+  static const double spin_s = [] {
+    const char* e = env_get("SRHIP_COMM_SPIN_US");
+    const double v = e && *e ? atof(e) : 100.0;
+    return (v >= 0 ? v : 100.0) * 1e-6;
+  }();
   const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {  // spin phase: the event only
+    const hipError_t q = hipEventQuery(c->done);
+    if (q == hipSuccess) return SRHIP_OK;
+    if (q != hipErrorNotReady) HIP_TRY(q);
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >= spin_s) break;
+    __builtin_ia32_pause();
+  }
   for (unsigned it = 0;; ++it) {
     const hipError_t q = hipEventQuery(c->done);
     if (q == hipSuccess) return SRHIP_OK;
@@ -92,7 +106,7 @@ int comm_wait(srhip_comm* c) {
       return fail(SRHIP_ERR_DEVICE, "collective did not complete in %.0f s (a rank missing?); communicator aborted",
                   limit);
     }
-    usleep(it < 1000 ? 20 : 200);
+    usleep(it < 500 ? 20 : 200);
   }
 }
 

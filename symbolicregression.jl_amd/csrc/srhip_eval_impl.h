@@ -50,6 +50,9 @@
 #define SRHIP_HEAVY_ILP 1  // rows a heavy operator body may interleave
 #endif
 #ifndef SRHIP_TRIG_ILP
+#ifndef SRHIP_JTRIG_FAST
+#define SRHIP_JTRIG_FAST 1  // Julia's Float32 trig kernels in Horner form, tie rows re-evaluated (round 6)
+#endif
 #define SRHIP_TRIG_ILP SRHIP_HEAVY_ILP  // rows Julia's Float32 trig bodies interleave (jtrigf_*); 1/2/4 measured alike (C2 1.278-1.289 ms)
 #endif
 #ifndef SRHIP_TRIG_ROWS
@@ -401,7 +404,7 @@ __device__ __attribute__((always_inline)) inline float jtrigf_q_dev(double fn, d
   return __builtin_bit_cast(float, o);
 }
 template <int R, int KIND>
-__device__ __attribute__((noinline)) RV<float, R> jtrigf_a(RV<float, R> v) {
+__device__ __attribute__((always_inline)) inline RV<float, R> jtrigf_a_exact(RV<float, R> v) {
   UNR for (int r = 0; r < R; ++r) {
     const float x = v[r];
     if constexpr (KIND == 0) {
@@ -414,8 +417,9 @@ __device__ __attribute__((noinline)) RV<float, R> jtrigf_a(RV<float, R> v) {
   return v;
 }
 template <int KIND, bool CW>
-__device__ __attribute__((always_inline)) inline float jtrigf_row(float x) {
-  const double xd = (double)x, fn = srm_jfn(xd);
+__device__ __attribute__((always_inline)) inline double jtrigf_red(float x, double& fn) {
+  const double xd = (double)x;
+  fn = srm_jfn(xd);
   double y;
   if constexpr (CW && KIND == 0) {
     // cos: the Cody-Waite reduction gives Julia's result on every float, the +-k pi/2 cases included
@@ -425,16 +429,120 @@ __device__ __attribute__((always_inline)) inline float jtrigf_row(float x) {
     y = srm_jred_near(xd, fn);
     if constexpr (CW) y = __builtin_fabsf(x) <= SRM_J9PIO4F ? y : srm_jred_cw(xd, fn);
   }
+  return y;
+}
+template <int KIND, bool CW>
+__device__ __attribute__((always_inline)) inline float jtrigf_row(float x) {
+  double fn;
+  const double y = jtrigf_red<KIND, CW>(x, fn);
   const float r = jtrigf_q_dev<KIND>(fn, y);
   return (KIND == 1 && x == 0.0f) ? x : r;  // sin(-0) = -0 (the reduction gives +0)
 }
 template <int R, int KIND, bool CW>
-__device__ __attribute__((noinline)) RV<float, R> jtrigf_bc(RV<float, R> v) {
+__device__ __attribute__((always_inline)) inline RV<float, R> jtrigf_bc_exact(RV<float, R> v) {
   UNR for (int r = 0; r < R; ++r) {
     v[r] = jtrigf_row<KIND, CW>(v[r]);
     if ((r + 1) % SRHIP_TRIG_ILP == 0) SRHIP_ROW_FENCE();
   }
   return v;
+}
+#if SRHIP_JTRIG_FAST
+// Round 6: the kernels in Horner form with fmas (srm_jsin_fma / srm_jcos_fma, include/srhip_math.h),
+// Julia's reduction unchanged.  A row whose fast Float64 value lies within SRM_JTIE_K ulps of a Float32
+// rounding midpoint is flagged (srm_jtie: 3 VALU) and, when any lane of the wave flags it (a uniform
+// branch, ~1e-7 of the inputs: tools/check_trigf.c counts 48-182 of ~2^31 floats per tier and kind),
+// re-evaluated by Julia's own kernels from the same reduced argument; check_trigf proves every
+// unflagged row equal to srm_jtrigf.  Tier B per row: 35 -> 27 VALU; tier A cos 13 -> 10.
+// (Both polynomials pass through an empty asm so that the quadrant select stays a v_cndmask: as a
+// C select of two expressions the compiler branched on it, executing both under exec masks.)
+// v_fma_f64 with the addend in an SGPR pair (one scalar operand: the constant-bus limit): as a C fma the
+// compiler chose v_fmac_f64 and copied every constant addend into VGPRs, two v_mov per fma
+__device__ __attribute__((always_inline)) inline double fma_vvs(double a, double b, double c) {
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+  return d;
+}
+// Horner forms of srm_jsin_fma / srm_jcos_fma (the same operations, so the same bits), the leading
+// coefficients S4 / C3 held in VGPRs by the caller (once per body)
+__device__ __attribute__((always_inline)) inline double jsin_fma_dev(double y, double z, double s4v) {
+  const double p = fma_vvs(z, fma_vvs(z, fma_vvs(z, s4v, SRM_JS3), SRM_JS2), SRM_JS1);
+  return __builtin_fma(z * y, p, y);
+}
+__device__ __attribute__((always_inline)) inline double jcos_fma_dev(double z, double c3v) {
+  return __builtin_fma(z, fma_vvs(z, fma_vvs(z, fma_vvs(z, c3v, SRM_JC2), SRM_JC1), SRM_JC0), 1.0);
+}
+__device__ __attribute__((always_inline)) inline void jtrig_coef_vgprs(double& s4v, double& c3v) {
+  s4v = SRM_JS4;
+  c3v = SRM_JC3;
+  asm volatile("" : "+v"(s4v), "+v"(c3v));
+}
+template <int KIND>
+__device__ __attribute__((always_inline)) inline float jtrigf_a_row_fast(float x, double s4v, double c3v) {
+  const double xd = (double)x, z = xd * xd;
+  double p = KIND == 0 ? jcos_fma_dev(z, c3v) : jsin_fma_dev(xd, z, s4v);
+  if (__builtin_amdgcn_ballot_w64(srm_jtie(p)) != 0) [[unlikely]]
+    p = KIND == 0 ? srm_jcos_kernel(xd) : srm_jsin_kernel(xd);
+  return KIND == 0 ? (float)p : __builtin_copysignf((float)p, x);
+}
+template <int R, int KIND>
+__device__ __attribute__((noinline)) RV<float, R> jtrigf_a(RV<float, R> v) {
+  double s4v, c3v;
+  jtrig_coef_vgprs(s4v, c3v);
+  UNR for (int r = 0; r < R; ++r) {
+    v[r] = jtrigf_a_row_fast<KIND>(v[r], s4v, c3v);
+    if ((r + 1) % SRHIP_TRIG_ILP == 0) SRHIP_ROW_FENCE();
+  }
+  return v;
+}
+template <int KIND, bool CW>
+__device__ __attribute__((always_inline)) inline float jtrigf_row_fast(float x, double s4v, double c3v) {
+  double fn;
+  const double y = jtrigf_red<KIND, CW>(x, fn);
+  const int n = cvt_i32_sat(fn);
+  const double z = y * y;
+  double ps = jsin_fma_dev(y, z, s4v), pc = jcos_fma_dev(z, c3v);
+  asm volatile("" : "+v"(ps), "+v"(pc));
+  const bool use_sin = ((n & 1) ^ KIND) != 0;
+  double p = use_sin ? ps : pc;
+  if (__builtin_amdgcn_ballot_w64(srm_jtie(p)) != 0) [[unlikely]] {
+    double es = srm_jsin_kernel(y), ec = srm_jcos_kernel(y);
+    asm volatile("" : "+v"(es), "+v"(ec));
+    p = use_sin ? es : ec;
+  }
+  // the sign: bit 1 of n + 1 - KIND (cos: quadrants 1, 2; sin: 2, 3), added into bit 31 (the xor)
+  uint32_t o;
+  asm("v_lshl_add_u32 %0, %1, 31, %2" : "=v"(o) : "v"((n + 1 - KIND) >> 1), "v"(__builtin_bit_cast(uint32_t, (float)p)));
+  const float r = __builtin_bit_cast(float, o);
+  return (KIND == 1 && x == 0.0f) ? x : r;  // sin(-0) = -0 (the reduction gives +0)
+}
+template <int R, int KIND, bool CW>
+__device__ __attribute__((noinline)) RV<float, R> jtrigf_bc(RV<float, R> v) {
+  double s4v, c3v;
+  jtrig_coef_vgprs(s4v, c3v);
+  UNR for (int r = 0; r < R; ++r) {
+    v[r] = jtrigf_row_fast<KIND, CW>(v[r], s4v, c3v);
+    if ((r + 1) % SRHIP_TRIG_ILP == 0) SRHIP_ROW_FENCE();
+  }
+  return v;
+}
+template <int R, int KIND>
+__device__ __attribute__((noinline)) RV<float, R> jtrigf_slow(RV<float, R> v) {
+  double s4v, c3v;
+  jtrig_coef_vgprs(s4v, c3v);
+  UNR for (int r = 0; r < R; ++r) {
+    const float x = v[r];
+    v[r] = __builtin_fabsf(x) < SRM_PIO2F_BIG_F ? jtrigf_row_fast<KIND, true>(x, s4v, c3v) : srm_jtrigf(KIND, x);
+  }
+  return v;
+}
+#else
+template <int R, int KIND>
+__device__ __attribute__((noinline)) RV<float, R> jtrigf_a(RV<float, R> v) {
+  return jtrigf_a_exact<R, KIND>(v);
+}
+template <int R, int KIND, bool CW>
+__device__ __attribute__((noinline)) RV<float, R> jtrigf_bc(RV<float, R> v) {
+  return jtrigf_bc_exact<R, KIND, CW>(v);
 }
 template <int R, int KIND>
 __device__ __attribute__((noinline)) RV<float, R> jtrigf_slow(RV<float, R> v) {
@@ -444,6 +552,7 @@ __device__ __attribute__((noinline)) RV<float, R> jtrigf_slow(RV<float, R> v) {
   }
   return v;
 }
+#endif
 template <int R, int KIND>
 __device__ __attribute__((always_inline)) inline RV<float, R> jtrigf_rows(const RV<float, R>& A) {
   RV<float, R> v;

@@ -2191,7 +2191,17 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     HIP_TRY(hipMemsetAsync(ctx->block_ctr.p, 0, sizeof(int32_t), ctx->stream));
     ctx->block_ctr_dirty = false;
   }
-  if (persistent) ctx->block_ctr_dirty = true;  // until the launch is seen to have drained
+  if (persistent) {
+    ctx->block_ctr_dirty = true;  // until the launch is seen to have drained
+    // (diagnostic, tests only) a counter left non-zero by a launch that never drained: this launch skips
+    // that many row blocks, which the lost-block check after it must report
+    if (const int seed = env_int("SRHIP_DEBUG_BLOCK_CTR", 0)) {
+      HIP_TRY(ctx->block_ctr.ensure(sizeof(int32_t)));
+      const int32_t h = (int32_t)seed;
+      HIP_TRY(hipMemcpyAsync(ctx->block_ctr.p, &h, sizeof(h), hipMemcpyHostToDevice, ctx->stream));
+      HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
+  }
   if (sd) HIP_TRY(hipMemsetAsync(sd->d_loss, 0, sd->zero_bytes, ctx->stream));
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
   if (persistent) {
@@ -2336,13 +2346,18 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   if (persistent && !sd) {  // (row shards: checked by the caller against the all-reduced statistic)
     // every row block was claimed exactly once: a tree that did not fail was evaluated on every row
     // (a counter left non-zero by an earlier launch would make this launch skip blocks silently)
+    // (a lost block is lost for every tree: one tree with a finite statistic verifies the launch; with
+    // none -- every tree failed -- the counter stays marked dirty and the next launch zeroes it)
+    bool verified = false;
     for (int32_t t : live) {
+      if (!std::isfinite(chk[t])) continue;
       const int64_t rows = ((const int64_t*)r_rows.data())[t];
-      if (rows != v.m && std::isfinite(chk[t]))
+      if (rows != v.m)
         return fail(SRHIP_ERR_DEVICE, "persistent launch evaluated tree %d on %lld of %lld rows (row-block counter "
                     "not at zero); the counter is reset for the next launch", t, (long long)rows, (long long)v.m);
+      verified = true;
     }
-    ctx->block_ctr_dirty = false;
+    if (verified) ctx->block_ctr_dirty = false;
   }
   // the launch's work, counted on the device (rows each tree was evaluated on)
   for (int i = 0; i < 4; ++i) ctx->work[i] = 0;
@@ -2623,12 +2638,20 @@ int srhip::run_eval_sharded(srhip_ctx* ctx, const srhip_dataset* ds, const srhip
   for (size_t i = 0; i < 2 * (size_t)nf + 1; ++i) sums[2 * (size_t)nt + i] = raux[1 + i];
   if (sd.persistent) {
     // this shard's persistent launch claimed every row block: a tree no shard failed was evaluated on all
-    // of this shard's rows
-    for (int32_t t = 0; t < nt; ++t)
-      if (!P->info[t].static_fail && sd.rows[t] != v.m && std::isfinite(chk[t]))
+    // of this shard's rows.  A lost row block is lost for every tree of the launch, so one tree with a
+    // finite all-reduced statistic verifies the launch; a tree that failed on ANY shard cannot (its rows
+    // here may have stopped early legitimately).  When no tree verifies it, the counter stays marked
+    // dirty and the next launch zeroes it (a counter left non-zero could otherwise hide
+    // behind another shard's failures).
+    bool verified = false;
+    for (int32_t t = 0; t < nt; ++t) {
+      if (P->info[t].static_fail || !std::isfinite(chk[t])) continue;
+      if (sd.rows[t] != v.m)
         return fail(SRHIP_ERR_DEVICE, "persistent launch evaluated tree %d on %lld of %lld rows (row-block counter "
                     "not at zero); the counter is reset for the next launch", t, (long long)sd.rows[t], (long long)v.m);
-    ctx->block_ctr_dirty = false;
+      verified = true;
+    }
+    if (verified) ctx->block_ctr_dirty = false;
   }
   std::vector<uint8_t> status(nt), ok(nt);
   std::vector<double> lossv(nt);

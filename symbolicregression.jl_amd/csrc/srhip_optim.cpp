@@ -147,6 +147,9 @@ static int derived_view(srhip_ctx* ctx, const srhip_dataset* ds, srhip_program* 
     HIP_TRY(hipMemcpyAsync(ctx->g_xd.p, v.X, (size_t)P->gdbase * v.ld * es, hipMemcpyDeviceToDevice, ctx->stream));
     HIP_TRY(launch_grad_derive(P->dtype, v.X, (uint8_t*)ctx->g_xd.p + (size_t)P->gdbase * v.ld * es, v.ld,
                                P->gdspec.data(), nd, ctx->stream));
+    // the split optimiser's auxiliary contexts read the view from their own streams: it must be
+    // complete before this returns (as make_view's is), not merely queued on ctx->stream
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
     if (whole) {
       ctx->g_xd_serial = ds->serial;
       ctx->g_xd_ld = v.ld;

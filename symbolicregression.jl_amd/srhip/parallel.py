@@ -235,6 +235,19 @@ def exchange_members(trees, scores, losses, options, dtype, group=None):
     return out
 
 
+def _distinct_devices(ctx, group=None) -> bool:
+    """True when every rank of the group runs on a GPU of its own ((host, device) pairs all-gathered, so
+    every rank returns the same answer)."""
+    import socket
+
+    dist = _dist()
+    dev = getattr(ctx, "device", None)
+    mine = (socket.gethostname(), int(dev) if dev is not None else -1)
+    got = [None] * dist.get_world_size(group)
+    dist.all_gather_object(got, mine, group=group)
+    return len(set(got)) == len(got)
+
+
 class IterationExchange:
     """The island search's whole per-iteration exchange as ONE fixed-size all-gather (src/Migration.jl:16-38
     fed from every rank as the reference's head node sees every population's best_sub_pop and the hall of
@@ -254,6 +267,7 @@ class IterationExchange:
         self.cap, self.pool, self.nbin = int(cap), int(pool_nodes), int(nbin)
         self.comm, self.group, self.world = comm, group, int(world)
         self.head = 8 * (2 + (self.cap + 1) + 2 * self.cap + self.nbin)
+        self.last_overflow = None  # (cap, pool) of the last exchange's second round, if it needed one
         self.size = self.head + self.pool * NODE_DTYPE.itemsize
 
     @classmethod
@@ -273,23 +287,38 @@ class IterationExchange:
         initialised = "torch" in sys.modules and _dist().is_available() and _dist().is_initialized()
         if use_native and (not initialised or _dist().get_backend(group) == "nccl"):
             ctx = make_ctx()
-            comm = NativeComm.from_process_group(ctx, group) if initialised else \
-                NativeComm(ctx, 1, 0, NativeComm.unique_id())
+            if not initialised:
+                comm = NativeComm(ctx, 1, 0, NativeComm.unique_id())
+            elif _distinct_devices(ctx, group):
+                comm = NativeComm.from_process_group(ctx, group)
+            # else: ranks share a GPU (a one-GPU nccl rehearsal): RCCL cannot place two ranks on one
+            # device, so every rank takes the torch path (the check is collective: all ranks agree)
         return cls(cap, cap * (maxsize + 1), nbin, comm, group, world)
 
+    def needs(self, trees, options, dtype):
+        """(members, node records) this rank's payload holds."""
+        from .node import flatten
+
+        if not trees:
+            return 0, 0
+        nodes, _ = flatten(trees, options, dtype)
+        return len(trees), len(nodes)
+
     def pack(self, trees, scores, losses, nsub: int, counts, options, dtype) -> np.ndarray:
+        """This rank's payload.  Members or node records past the capacity do not raise here (the other
+        ranks are already waiting in the all-gather): the header's member count is written as -1 - n
+        with the node count beside it, and exchange() runs a second, larger round on every rank."""
         from .node import flatten
 
         n = len(trees)
-        if n > self.cap:
-            raise ValueError(f"{n} members exceed the exchange's capacity {self.cap}")
         nodes, offs = flatten(trees, options, dtype) if n else (np.zeros(0, NODE_DTYPE), np.zeros(1, np.int64))
-        if len(nodes) > self.pool:
-            raise ValueError(f"{len(nodes)} nodes exceed the exchange's node pool {self.pool}")
         buf = np.zeros(self.size, dtype=np.uint8)
         h = buf[:self.head].view(np.float64)
         hi = buf[:self.head].view(np.int64)
         c = self.cap
+        if n > c or len(nodes) > self.pool:
+            hi[0], hi[1], hi[2] = int(nsub), -1 - n, len(nodes)
+            return buf
         hi[0], hi[1] = int(nsub), n
         hi[2:2 + n + 1] = offs
         h[3 + c:3 + c + n] = np.asarray(scores, dtype=np.float64)
@@ -297,6 +326,11 @@ class IterationExchange:
         h[3 + 3 * c:3 + 3 * c + self.nbin] = np.asarray(counts, dtype=np.float64)
         buf[self.head:self.head + len(nodes) * NODE_DTYPE.itemsize] = np.ascontiguousarray(nodes).view(np.uint8)
         return buf
+
+    def overflow(self, buf):
+        """None, or the (members, node records) an overflowing payload needs."""
+        hi = np.asarray(buf, dtype=np.uint8)[:24].view(np.int64)
+        return None if hi[1] >= 0 else (int(-1 - hi[1]), int(hi[2]))
 
     def unpack(self, buf, options):
         """-> (nsub, [(tree, score, loss)], counts)"""
@@ -314,34 +348,50 @@ class IterationExchange:
         trees = unflatten(nodes, offs, options) if n else []
         return nsub, [(t, float(scores[i]), float(losses[i])) for i, t in enumerate(trees)], counts
 
-    def exchange(self, trees, scores, losses, nsub: int, counts, options, dtype):
-        """Every rank's (nsub, members, counts), in rank order."""
-        import time
-
-        t0 = time.perf_counter()
-        payload = self.pack(trees, scores, losses, nsub, counts, options, dtype)
+    def _gather(self, payload: np.ndarray) -> list:
+        """One fixed-size all-gather of payload (the same length on every rank) -> parts by rank."""
         if self.comm is not None:
-            parts = self.comm.allgather(payload.tobytes())
-            parts = [np.frombuffer(p, dtype=np.uint8) for p in parts]
-        elif self.world > 1:
+            return [np.frombuffer(p, dtype=np.uint8) for p in self.comm.allgather(payload.tobytes())]
+        if self.world > 1:
             import torch
 
             dist = _dist()
             dev = _device(self.group)
-            host_in, src = _staging(self.size, torch.uint8, dev, "iter_in")
+            size = len(payload)
+            host_in, src = _staging(size, torch.uint8, dev, "iter_in")
             host_in.numpy()[:] = payload
             if src is not host_in:
                 src.copy_(host_in, non_blocking=True)
-            host_out, dst = _staging(self.world * self.size, torch.uint8, dev, "iter_out")
+            host_out, dst = _staging(self.world * size, torch.uint8, dev, "iter_out")
             dist.all_gather_into_tensor(dst, src, group=self.group)
             if host_out is not dst:
                 host_out.copy_(dst, non_blocking=True)
                 torch.cuda.current_stream(dev).synchronize()
-            allb = host_out.numpy().reshape(self.world, self.size)
-            parts = [allb[r] for r in range(self.world)]
+            allb = host_out.numpy().reshape(self.world, size)
+            return [allb[r].copy() for r in range(self.world)]
+        return [payload]
+
+    def exchange(self, trees, scores, losses, nsub: int, counts, options, dtype):
+        """Every rank's (nsub, members, counts), in rank order.  When any rank's members overflow the
+        capacity (a custom complexity mapping lets trees outgrow maxsize + 1 nodes), every rank sees
+        its flag in the first round and all ranks repeat the exchange once with a capacity sized from
+        the largest need -- no rank raises alone while the others wait."""
+        import time
+
+        t0 = time.perf_counter()
+        self.last_overflow = None
+        parts = self._gather(self.pack(trees, scores, losses, nsub, counts, options, dtype))
+        needs = [self.overflow(p) for p in parts]
+        if any(nd is not None for nd in needs):
+            own = self.needs(trees, options, dtype)
+            cap = max([self.cap, own[0]] + [nd[0] for nd in needs if nd is not None])
+            pool = max([self.pool, own[1]] + [nd[1] for nd in needs if nd is not None])
+            wide = IterationExchange(cap, pool, self.nbin, self.comm, self.group, self.world)
+            parts = wide._gather(wide.pack(trees, scores, losses, nsub, counts, options, dtype))
+            self.last_overflow = (cap, pool)
+            out = [wide.unpack(p, options) for p in parts]
         else:
-            parts = [payload]
-        out = [self.unpack(p, options) for p in parts]
+            out = [self.unpack(p, options) for p in parts]
         timer.seconds += time.perf_counter() - t0
         timer.calls += 1
         return out

@@ -253,3 +253,71 @@ def test_migrate_topk_and_fused_allreduce_gloo_world2():
     for _, _, rs, rc in res:
         assert np.array_equal(rs, np.arange(7, dtype=np.float64) * 3)
         assert np.array_equal(rc, [2.0, np.inf, 3.0])
+
+
+def _overflow_rank_main(rank, world, port, q):
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "symbolicregression.jl_amd"))
+        import torch.distributed as dist
+
+        import srhip
+        from srhip.parallel import IterationExchange
+
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        opts = srhip.Options(**OPS)
+        # capacity for 4 members of <= 8 nodes; rank 1 sends 10 members of up to 25 nodes (a custom
+        # complexity mapping lets trees outgrow maxsize + 1 nodes), rank 0 stays within it
+        ex = IterationExchange(4, 4 * 8, 3, comm=None, group=None, world=world)
+        n = 2 if rank == 0 else 10
+        trees = srhip.random_population(n, opts, 3, np.float32, seed=400 + rank, max_size=25 if rank else 5)
+        got = ex.exchange(trees, np.arange(n) + 0.5, np.arange(n) * 2.0, 7 + rank, [1.0, 2.0, 3.0 + rank], opts,
+                          np.float32)
+        second = ex.last_overflow
+        # a following exchange within capacity takes one round again
+        got2 = ex.exchange(trees[:1], [1.0], [2.0], 0, [0.0, 0.0, 0.0], opts, np.float32)
+        out = [(nsub, [(srhip.flatten([t], opts, np.float32)[0].tobytes(), s, l) for t, s, l in mem], list(c))
+               for nsub, mem, c in got]
+        q.put((rank, None, out, (second, ex.last_overflow, len(got2))))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # surface the failure to the parent
+        import traceback
+
+        q.put((rank, traceback.format_exc() + repr(e), None, None))
+
+
+def test_iteration_exchange_overflow_is_collective_gloo_world2():
+    """IterationExchange with one rank past the capacity: no rank raises alone; every rank
+    sees the overflow flag, both repeat the exchange once at the largest need, and every rank receives
+    every rank's members intact."""
+    import multiprocessing as mp
+
+    import srhip
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overflow_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    res.sort(key=lambda r: r[0])
+    for r in res:
+        assert r[2] is not None, r[1]
+    opts = srhip.Options(**OPS)
+    for rank in range(2):
+        n = 2 if rank == 0 else 10
+        trees = srhip.random_population(n, opts, 3, np.float32, seed=400 + rank, max_size=25 if rank else 5)
+        want = [srhip.flatten([t], opts, np.float32)[0].tobytes() for t in trees]
+        for _, _, out, _ in res:
+            nsub, mem, counts = out[rank]
+            assert nsub == 7 + rank
+            assert [m[0] for m in mem] == want
+            assert [m[1] for m in mem] == list(np.arange(n) + 0.5)
+            assert [m[2] for m in mem] == list(np.arange(n) * 2.0)
+            assert counts == [1.0, 2.0, 3.0 + rank]
+    for _, _, _, (second, after, n2) in res:
+        assert second is not None and second[0] == 10
+        assert after is None and n2 == 2

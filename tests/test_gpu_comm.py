@@ -147,3 +147,24 @@ def test_bench_selfcheck_comparisons_world1(ctx, comm):
         prog.close()
         if own:
             dist.destroy_process_group()
+
+
+def test_sharded_lost_row_block_is_reported_then_recovered(ctx, comm, monkeypatch):
+    """The row-shard path's lost-block check: a seeded non-zero row-block counter is reported
+    from the shard's own rows (a tree with a finite all-reduced statistic verifies the launch); the next
+    sharded evaluation zeroes the counter and equals the clean one bit for bit."""
+    sr = _sr()
+    from srhip import workloads
+
+    opts, X, y, _, nodes, offs = workloads.c2(1, 128, 300_000)
+    prog = sr.Program(ctx, nodes, offs, opts, np.float32)
+    assert prog.stats()["max_stack"] <= 2  # the wide variant: the persistent path
+    ds = sr.DeviceDataset(ctx, X, y)
+    l0, ok0 = comm.eval_loss_sharded(prog, ds, sr.L2DistLoss())
+    assert ok0.any()
+    monkeypatch.setenv("SRHIP_DEBUG_BLOCK_CTR", "5")
+    with pytest.raises(RuntimeError, match="row-block counter"):
+        comm.eval_loss_sharded(prog, ds, sr.L2DistLoss())
+    monkeypatch.delenv("SRHIP_DEBUG_BLOCK_CTR")
+    l1, ok1 = comm.eval_loss_sharded(prog, ds, sr.L2DistLoss())
+    assert np.array_equal(ok1, ok0) and np.array_equal(l1.view(np.uint64), l0.view(np.uint64))

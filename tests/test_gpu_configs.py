@@ -55,6 +55,43 @@ def test_c2_bench_population_matches_oracle(ctx, oracle):
     assert int(dok.sum()) == 808  # the bench line's trees_ok
 
 
+def test_c2_full_size_predictions_bitwise(ctx, oracle):
+    """A1 at C2's full size: all 1024 bench trees x 1M rows through srhip_eval_predict
+    (eval_tree_array: the path MMI.predict and user loss_functions consume) -- did_succeed equal to the
+    oracle's and every prediction of every succeeding tree equal to the oracle's bit for bit.  Four
+    programs of 256 trees keep the host copies at 1 GB each."""
+    sr = _sr()
+    from srhip import workloads
+
+    opts, X, y, trees, nodes, offs = workloads.c2()
+    ds = sr.DeviceDataset(ctx, X)
+    nt = len(offs) - 1
+    nok = 0
+    for lo in range(0, nt, 256):
+        hi = min(nt, lo + 256)
+        sub = nodes[offs[lo]:offs[hi]]
+        soffs = offs[lo:hi + 1] - offs[lo]
+        prog = sr.Program(ctx, sub, soffs, opts, np.float32)
+        pred, ok = prog.eval_predict(ds)
+
+        def one(t):
+            ref, rok = oracle.eval_tree(sub[soffs[t]:soffs[t + 1]], opts.binop_codes, opts.unaop_codes, X)
+            if bool(ok[t]) != rok:
+                return (lo + t, "did_succeed", bool(ok[t]), rok)
+            if rok:
+                d = np.nonzero(pred[t].view(np.uint32) != ref.view(np.uint32))[0]
+                if len(d):
+                    return (lo + t, "rows differ", len(d), [(int(i), pred[t][i], ref[i]) for i in d[:4]])
+            return None
+
+        with cf.ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+            bad = [r for r in ex.map(one, range(hi - lo)) if r is not None]
+        assert not bad, bad[:8]
+        nok += int(ok.sum())
+        del pred, prog
+    assert nok == 808  # the loss evaluation's trees_ok: the same mask
+
+
 def test_c2_plain_program_equals_derived(ctx, monkeypatch):
     """Derived columns (forced with SRHIP_DERIVE_ALWAYS=1 -- C2's launch prefers the
     plain program's longer row blocks) return the same bits as the plain program (SRHIP_NO_DERIVE=1),

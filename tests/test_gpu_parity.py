@@ -61,6 +61,18 @@ def _ds(ctx, X, y=None, w=None):
     return sr.DeviceDataset(ctx, X, y, w)
 
 
+def assert_same_bits(pred, ref, what=""):
+    """Predictions equal bit for bit; on failure every differing row with its distance in ULPs."""
+    pred, ref = np.ascontiguousarray(pred), np.ascontiguousarray(ref)
+    it = np.uint32 if pred.dtype.itemsize == 4 else np.uint64
+    pb, rb = pred.view(it), ref.view(it)
+    bad = np.nonzero(pb != rb)[0]
+    if len(bad):
+        ulps = [abs(int(pb[i]) - int(rb[i])) if (pred[i] >= 0) == (ref[i] >= 0) else -1 for i in bad[:16]]
+        raise AssertionError(f"{what}: {len(bad)} rows differ; first (row, device, oracle, ulps): "
+                             f"{[(int(i), pred[i], ref[i], u) for i, u in zip(bad[:16], ulps)]}")
+
+
 def _rel(a, b):
     if a == b or (math.isnan(a) and math.isnan(b)):  # equal infinities / both NaN
         return 0.0
@@ -78,7 +90,7 @@ def test_golden_evaluation(ctx, oracle):
         assert np.all(np.abs(pred[0].astype(np.float64) - cs["expected"]) / n < 1e-6)
         ref, rok = oracle.eval_tree(cs["nodes"], ex["binops"], ex["unaops"], cs["X"])
         assert rok == bool(ok[0])
-        np.testing.assert_allclose(pred[0], ref, rtol=2e-6, atol=1e-6)
+        assert_same_bits(pred[0], ref)
 
 
 def test_golden_integer(ctx, oracle):
@@ -209,8 +221,8 @@ def test_random_population_predictions(ctx, oracle):
     for t in range(len(trees)):
         ref, rok = oracle.eval_tree(nodes[offs[t]:offs[t + 1]], opts.binop_codes, opts.unaop_codes, X)
         assert bool(ok[t]) == rok, t
-        if rok:
-            np.testing.assert_allclose(pred[t], ref, rtol=1e-4, atol=1e-5)
+        if rok:  # the same IEEE operations per row on both sides (-ffp-contract=off, one libm header)
+            assert_same_bits(pred[t], ref, f"tree {t}")
 
 
 def test_int32_population_bit_exact(ctx, oracle):
@@ -314,7 +326,7 @@ def test_constant_trees_and_leaves(ctx, oracle):
         ref, rok = oracle.eval_tree(nodes, opts.binop_codes, opts.unaop_codes, X)
         assert ok == rok, sr.string_tree(tree, opts)
         if ok:
-            np.testing.assert_allclose(pred, ref, rtol=1e-6)
+            assert_same_bits(pred, ref, sr.string_tree(tree, opts))
 
 
 def test_feature_column_checks(ctx, oracle):

@@ -89,3 +89,21 @@ def test_superinstructions_equal_plain_programs_bitwise(c2_small, monkeypatch, d
     n_sup = (np.fromfile("/tmp/srhip_super_0.bin", dtype=np.int32).reshape(-1, 2)[:, 0] >= 0).sum()
     n_plain = (np.fromfile("/tmp/srhip_super_1.bin", dtype=np.int32).reshape(-1, 2)[:, 0] >= 0).sum()
     assert n_sup < 0.9 * n_plain, (n_sup, n_plain)
+
+
+def test_lost_row_block_is_reported_then_recovered(c2_small, monkeypatch):
+    """A row-block counter left non-zero (seeded through SRHIP_DEBUG_BLOCK_CTR) makes the persistent launch
+    skip blocks: the host's lost-block check must report it (not return partial losses), and the next
+    evaluation must zero the counter and return the clean results bit for bit."""
+    opts, X, y, nodes, offs = c2_small
+    ctx = srhip.Context(0)
+    prog = srhip.Program(ctx, nodes, offs, opts, np.float32)
+    ds = srhip.DeviceDataset(ctx, X, y)
+    l0, ok0 = prog.eval_loss(ds, srhip.L2DistLoss())
+    monkeypatch.setenv("SRHIP_DEBUG_BLOCK_CTR", "7")
+    with pytest.raises(RuntimeError, match="row-block counter"):
+        prog.eval_loss(ds, srhip.L2DistLoss())
+    monkeypatch.delenv("SRHIP_DEBUG_BLOCK_CTR")
+    l1, ok1 = prog.eval_loss(ds, srhip.L2DistLoss())
+    assert np.array_equal(ok1, ok0)
+    assert np.array_equal(l1.view(np.uint64), l0.view(np.uint64))

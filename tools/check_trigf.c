@@ -3,7 +3,11 @@
  *
  *  (0) PROOF: the three per-wave tiers the device evaluates Julia's Float32 sin / cos in
  *      (srm_jfn / srm_jred_near / srm_jred_cw / srm_jtrigf_q) return srm_jtrigf's bits for every
- *      input each tier may see.  Exit status 1 otherwise.  The rest runs with an argument only:
+ *      input each tier may see.  Exit status 1 otherwise.
+ *  (0') PROOF (round 6): the same tiers with the kernels in Horner form (srm_jsin_fma / srm_jcos_fma)
+ *      return srm_jtrigf's bits on every input whose fast value srm_jtie does not flag; prints how
+ *      many each tier flags (the device re-evaluates those waves exactly).  The rest runs with an
+ *      argument only:
  *
  *  (1) D = max distance, in Float64 units in the last place, between the value the fast degree-5
  *      minimax (srm_sincosf_fast) computes BEFORE its one rounding to Float32 and the value Julia's
@@ -76,6 +80,28 @@ static float tier_c(int kind, float x) {
   return (kind == 1 && x == 0.0f) ? x : r;
 }
 
+/* the device's fast tiers (round 6): Julia's reduction, the kernels in Horner form with fmas, a row
+ * whose fast value lies near a Float32 rounding midpoint flagged (the device then re-evaluates the wave
+ * by the exact tiers above) */
+static float tier_a_fast(int kind, float x, int* flag) {
+  const double xd = (double)x, z = xd * xd;
+  const double p = kind == 0 ? srm_jcos_fma(z) : srm_jsin_fma(xd, z);
+  *flag = srm_jtie(p);
+  return kind == 0 ? (float)p : copysignf((float)p, x);
+}
+static float tier_bc_fast(int kind, float x, int cw, int* flag) {
+  const double xd = (double)x, fn = srm_jfn(xd);
+  double y = srm_jred_near(xd, fn);
+  if (cw) y = kind == 0 ? srm_jred_cw(xd, fn) : (fabsf(x) <= SRM_J9PIO4F ? y : srm_jred_cw(xd, fn));
+  const int n = (int)fn;
+  const double z = y * y;
+  const double p = ((n & 1) ^ kind) ? srm_jsin_fma(y, z) : srm_jcos_fma(z);
+  *flag = srm_jtie(p);
+  const float r = (float)p;
+  const float q = (((n + 1 - kind) >> 1) & 1) ? -r : r;
+  return (kind == 1 && x == 0.0f) ? x : q;
+}
+
 int main(int argc, char** argv) {
   const uint32_t cert = argc > 1 ? (uint32_t)strtoul(argv[1], 0, 0) : 0;
   /* (0) the tiers: every float each tier may see */
@@ -94,6 +120,54 @@ int main(int argc, char** argv) {
     printf("%s tiers vs srm_jtrigf: A %llu inputs %llu wrong, B %llu inputs %llu wrong, C %llu inputs %llu wrong\n",
            kind ? "sin" : "cos", (unsigned long long)na, (unsigned long long)ba, (unsigned long long)nb,
            (unsigned long long)bb, (unsigned long long)nc, (unsigned long long)bc);
+    fflush(stdout);
+    if (ba || bb || bc) return 1;
+  }
+  /* (0') the fast tiers: an unflagged row returns srm_jtrigf's bits on every float the tier may see.
+   * SRHIP_TIE_DUMP=<file>: also write every flagged input (uint32 bits, any tier / kind; sorted
+   * ascending) -- the fixture tests/golden/trig_tie_inputs.npy, whose rows the GPU test drives through
+   * the device's re-evaluation branch. */
+  const char* dump = getenv("SRHIP_TIE_DUMP");
+  FILE* df = dump && *dump ? fopen(dump, "wb") : NULL;
+  if (df) {
+    for (int64_t i = 0; i < (1LL << 32); ++i) {
+      const float x = from_u((uint32_t)i);
+      if (!(fabsf(x) < 421657440.0f)) continue;
+      int f = 0, g;
+      for (int kind = 0; kind < 2; ++kind) {
+        if (fabsf(x) < SRM_JPIO4F) { (void)tier_a_fast(kind, x, &g); f |= g; }
+        if (fabsf(x) <= SRM_J9PIO4F) { (void)tier_bc_fast(kind, x, 0, &g); f |= g; }
+        (void)tier_bc_fast(kind, x, 1, &g);
+        f |= g;
+      }
+      if (f) { const uint32_t u = (uint32_t)i; fwrite(&u, 4, 1, df); }
+    }
+    fclose(df);
+  }
+  for (int kind = 0; kind < 2; ++kind) {
+    uint64_t na = 0, nb = 0, nc = 0, ba = 0, bb = 0, bc = 0, fa = 0, fb = 0, fc = 0;
+#pragma omp parallel for schedule(dynamic, 1 << 16) reduction(+ : na, nb, nc, ba, bb, bc, fa, fb, fc)
+    for (int64_t i = 0; i < (1LL << 32); ++i) {
+      const float x = from_u((uint32_t)i);
+      if (!(fabsf(x) < 421657440.0f)) continue;
+      const uint32_t want = to_u(srm_jtrigf(kind, x));
+      int f;
+      if (fabsf(x) < SRM_JPIO4F) {
+        const uint32_t got = to_u(tier_a_fast(kind, x, &f));
+        ++na; fa += f; ba += !f && got != want;
+      }
+      if (fabsf(x) <= SRM_J9PIO4F) {
+        const uint32_t got = to_u(tier_bc_fast(kind, x, 0, &f));
+        ++nb; fb += f; bb += !f && got != want;
+      }
+      const uint32_t got = to_u(tier_bc_fast(kind, x, 1, &f));
+      ++nc; fc += f; bc += !f && got != want;
+    }
+    printf("%s fast tiers vs srm_jtrigf (flagged rows / unflagged wrong): A %llu inputs %llu / %llu, "
+           "B %llu inputs %llu / %llu, C %llu inputs %llu / %llu\n",
+           kind ? "sin" : "cos", (unsigned long long)na, (unsigned long long)fa, (unsigned long long)ba,
+           (unsigned long long)nb, (unsigned long long)fb, (unsigned long long)bb, (unsigned long long)nc,
+           (unsigned long long)fc, (unsigned long long)bc);
     fflush(stdout);
     if (ba || bb || bc) return 1;
   }
