@@ -172,6 +172,21 @@ int srhip_eval_loss(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program
                     const srhip_loss* loss, const int64_t* idx, int64_t nidx,
                     double* out_loss, uint8_t* out_ok);
 
+/* srhip_eval_loss in two halves, for callers that keep the device busy across populations (the
+ * reference scores populations from concurrent tasks: Threads.@spawn per population,
+ * src/SearchUtils.jl:121-122, @threads_if in src/SingleIteration.jl:112).  _submit queues the
+ * evaluation's launches on the context's stream -- behind any evaluation still in flight there -- and
+ * returns a ticket at once; _wait blocks until that evaluation has completed, takes its did_succeed
+ * decisions and writes out_loss / out_ok exactly as srhip_eval_loss would (same bits), then frees the
+ * ticket.  At most 3 tickets per context may be outstanding; tickets may be waited in any order, on
+ * the thread that uses the context.  The program and dataset must outlive the ticket.  A row subset
+ * (idx != NULL) is evaluated inside _submit (its gather synchronises the stream). */
+typedef struct srhip_eval_ticket srhip_eval_ticket;
+int srhip_eval_loss_submit(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* prog,
+                           const srhip_loss* loss, const int64_t* idx, int64_t nidx,
+                           srhip_eval_ticket** out_ticket);
+int srhip_eval_loss_wait(srhip_eval_ticket* ticket, double* out_loss, uint8_t* out_ok);
+
 /* eval_tree_array for every tree: out_pred is T[ntrees][m] (m = n or nidx), row-contiguous. */
 int srhip_eval_predict(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* prog,
                        const int64_t* idx, int64_t nidx, void* out_pred, uint8_t* out_ok);

@@ -1913,17 +1913,17 @@ static size_t precise_per_tree(const srhip_program* P, const View& v, int* sa_ou
 static int precise_cap(const srhip_program* P, const View& v, int cap) {
   return (int)std::max<int64_t>(std::min<int64_t>(cap, (int64_t)(PRECISE_SLAB_MAX / precise_per_tree(P, v))), 4);
 }
-static int ensure_dev_precise(srhip_ctx* ctx, const srhip_program* P, const View& v, int* cap) {
+static int ensure_dev_precise(srhip_ctx* ctx, const srhip_program* P, const View& v, int* cap, ResultSet* rs) {
   int sa = 32;
   const size_t per_tree = precise_per_tree(P, v, &sa);
   *cap = precise_cap(P, v, *cap);
   HIP_TRY(ctx->slab_prec.ensure((size_t)*cap * per_tree));
-  HIP_TRY(ctx->h_pout.ensure((size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t) +
-                             (size_t)DEV_PRECISE_MAX * sa * sizeof(double), hipHostMallocCoherent));
+  HIP_TRY(rs->h_pout.ensure((size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t) +
+                            (size_t)DEV_PRECISE_MAX * sa * sizeof(double), hipHostMallocCoherent));
   return SRHIP_OK;
 }
 static int enqueue_dev_precise(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, const View& v,
-                               int32_t* ulist, int cap, int G, int* out_stride) {
+                               int32_t* ulist, int cap, int G, int* out_stride, ResultSet* rs) {
   const int dtype = P->dtype;
   const int stride = std::max(1, P->max_ops);
   const int Rp = pick_rows_per_lane(dtype, K_MAX, MODE_PRECISE, v.m);
@@ -1933,7 +1933,7 @@ static int enqueue_dev_precise(srhip_ctx* ctx, const srhip_dataset* ds, const sr
   Lp.nrb = (int)((v.m + Lp.rb_rows - 1) / Lp.rb_rows);
   {
     int c = cap;
-    const int rc = ensure_dev_precise(ctx, P, v, &c);
+    const int rc = ensure_dev_precise(ctx, P, v, &c, rs);
     if (rc) return rc;
     if (c < cap) return fail(SRHIP_ERR_INVALID, "precise list of %d trees past its capacity %d", cap, c);
   }
@@ -1957,19 +1957,35 @@ static int enqueue_dev_precise(srhip_ctx* ctx, const srhip_dataset* ds, const sr
   q.wg_waves = 1;
   q.prec_assign = 1;  // one-tile row blocks
   HIP_TRY(launch_eval(dtype, q, Rp, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, G), 16, ctx->stream));
-  int32_t* hl = (int32_t*)ctx->h_pout.p;
-  double* hs = (double*)((uint8_t*)ctx->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
+  int32_t* hl = (int32_t*)rs->h_pout.p;
+  double* hs = (double*)((uint8_t*)rs->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
   HIP_TRY(launch_precise_reduce((const double*)ctx->slab_prec.p, Lp.nrb, stride, ulist, cap, G, DEV_PRECISE_MAX, hl,
                                 hs, ctx->stream));
   *out_stride = stride;
   return SRHIP_OK;
 }
 
-static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
-                         const View& v, void* out_pred, double* sums, double* chk, DevPrecise* dp = nullptr,
-                         ShardDev* sd = nullptr) {
+// An evaluation between its launches (eval_issue) and the reading of its records (eval_collect): what
+// the second half needs of the first.  The launches of several jobs may be in flight on the context's
+// stream at once (srhip_eval_loss_submit), each with its own result set.
+struct EvalJob {
+  ResultSet* rs = nullptr;
+  bool launched = false, persistent = false, devp = false;
+  int mode = 0, dtype = 0;
+  int32_t nt = 0;
+  std::vector<int32_t> live;
+  UndecidedList ul;
+  DevBuf pred;  // MODE_PRED's device output (synchronous calls only)
+};
+static int eval_issue(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
+                      const View& v, void* out_pred, double* sums, double* chk, DevPrecise* dp, ShardDev* sd,
+                      EvalJob& J) {
   const int dtype = P->dtype;
   const int32_t nt = P->ntrees;
+  ResultSet* const rs = J.rs;
+  J.mode = mode;
+  J.dtype = dtype;
+  J.nt = nt;
   const int64_t nf = ds->nfeat;
   const bool weighted = ds->weighted && mode == MODE_LOSS;
   for (size_t i = 0; i < sums_len(nt, nf); ++i) sums[i] = 0.0;
@@ -1982,7 +1998,8 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     sums[2 * (size_t)nt + 2 * f + 1] = (double)v.stats[f].nonfinite;
   }
   sums[2 * (size_t)nt + 2 * nf] = (double)v.m;
-  std::vector<int32_t> live;
+  std::vector<int32_t>& live = J.live;
+  live.clear();
   live.reserve(nt);
   for (int32_t t = 0; t < nt; ++t)
     if (!(P->dec.size() == (size_t)nt ? P->dec[t].static_fail : P->info[t].static_fail)) live.push_back(t);
@@ -2116,9 +2133,9 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   HIP_TRY(ctx->slab_chk.ensure((size_t)nl * L.nrb * 8));
   // the reduction writes the per-tree results straight into coherent pinned host memory (no
   // device-to-host copies on the stream)
-  HIP_TRY(ctx->h_loss.ensure((size_t)nt * 8, hipHostMallocCoherent));
-  HIP_TRY(ctx->h_chk.ensure((size_t)nt * 8, hipHostMallocCoherent));
-  HIP_TRY(ctx->h_rows.ensure((size_t)nt * 8, hipHostMallocCoherent));
+  HIP_TRY(rs->h_loss.ensure((size_t)nt * 8, hipHostMallocCoherent));
+  HIP_TRY(rs->h_chk.ensure((size_t)nt * 8, hipHostMallocCoherent));
+  HIP_TRY(rs->h_rows.ensure((size_t)nt * 8, hipHostMallocCoherent));
   EvalArgs a{};
   a.code = use_d ? P->dcode_dev : P->code_dev;
   a.prog_off = use_d ? P->doff_dev : P->off_dev;
@@ -2152,9 +2169,9 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   const char* nofuse = env_get("SRHIP_NO_FUSED_REDUCE");
   if (L.nrb == 1 && !sd && !(nofuse && *nofuse && *nofuse != '0')) {
     a.fused = 1;
-    a.fused_loss = mode == MODE_LOSS ? ctx->h_loss.p : nullptr;
-    a.fused_chk = dtype == SRHIP_I32 ? nullptr : ctx->h_chk.p;
-    a.fused_rows = (int64_t*)ctx->h_rows.p;
+    a.fused_loss = mode == MODE_LOSS ? rs->h_loss.p : nullptr;
+    a.fused_chk = dtype == SRHIP_I32 ? nullptr : rs->h_chk.p;
+    a.fused_rows = (int64_t*)rs->h_rows.p;
   } else {
     HIP_TRY(ctx->slab_rows.ensure((size_t)nl * L.nrb * sizeof(int32_t)));
     a.slab_rows = (int32_t*)ctx->slab_rows.p;
@@ -2164,7 +2181,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   // tests' way to the overflow path), less for very long row ranges (ensure_dev_precise)
   int ucap = std::max(1, std::min(DEV_PRECISE_MAX, env_int("SRHIP_PRECISE_LIST", DEV_PRECISE_MAX)));
   if (devp) {
-    const int rc = ensure_dev_precise(ctx, P, v, &ucap);
+    const int rc = ensure_dev_precise(ctx, P, v, &ucap, rs);
     if (rc) return rc;
   }
   a.early_exit = mode == MODE_LOSS && early_exit_on() ? 1 : 0;
@@ -2177,13 +2194,16 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     memset(ctx->h_dbg.p, 0xff, 64 * sizeof(int32_t));
     a.dbg = (int32_t*)ctx->h_dbg.p;
   }
-  DevBuf pred;
+  DevBuf& pred = J.pred;
   if (mode == MODE_PRED) {
     HIP_TRY(pred.ensure((size_t)nt * v.m * es));
     a.out_pred = pred.p;
   }
   dim3 grid(L.nrb, (unsigned)goff.size() - 1);
-  if (persistent && (!ctx->block_ctr.p || ctx->block_ctr_dirty)) {
+  // a probe with tile claims zeroes the counter itself, so a launch still in flight (an earlier
+  // submitted evaluation, not yet seen to drain) needs no fill in front of this one
+  const bool probe_zeroes = probe_blocks > 0 && !env_flag("SRHIP_PROBE_TREE_CLAIMS");
+  if (persistent && (!ctx->block_ctr.p || (ctx->block_ctr_dirty && !probe_zeroes))) {
     // zeroed once: every persistent launch that drains its claims leaves it at zero (its last claim
     // resets it); again after a launch that was never seen to complete (an error return between the
     // launch and its synchronisation, or a lost row block below)
@@ -2191,19 +2211,9 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     HIP_TRY(hipMemsetAsync(ctx->block_ctr.p, 0, sizeof(int32_t), ctx->stream));
     ctx->block_ctr_dirty = false;
   }
-  if (persistent) {
-    ctx->block_ctr_dirty = true;  // until the launch is seen to have drained
-    // (diagnostic, tests only) a counter left non-zero by a launch that never drained: this launch skips
-    // that many row blocks, which the lost-block check after it must report
-    if (const int seed = env_int("SRHIP_DEBUG_BLOCK_CTR", 0)) {
-      HIP_TRY(ctx->block_ctr.ensure(sizeof(int32_t)));
-      const int32_t h = (int32_t)seed;
-      HIP_TRY(hipMemcpyAsync(ctx->block_ctr.p, &h, sizeof(h), hipMemcpyHostToDevice, ctx->stream));
-      HIP_TRY(hipStreamSynchronize(ctx->stream));
-    }
-  }
+  if (persistent) ctx->block_ctr_dirty = true;  // until the launch is seen to have drained
   if (sd) HIP_TRY(hipMemsetAsync(sd->d_loss, 0, sd->zero_bytes, ctx->stream));
-  HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+  HIP_TRY(hipEventRecord(rs->ev0, ctx->stream));
   if (persistent) {
     if (probe_blocks > 0) {
       // leading row blocks, one tree per wave (uniform groups of consecutive slots), with the plain
@@ -2220,8 +2230,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       // probe's duration is that tree's); chk / rows of the probe blocks combine by atomics from 0
       // (the probe's workgroups zero their own combining entries and the persistent launch's block
       // counter: no memset launches on the stream)
-      const bool no_tile_claims = env_flag("SRHIP_PROBE_TREE_CLAIMS");
-      if (!no_tile_claims) {
+      if (probe_zeroes) {
         q.tile_claims = 1;
         q.zero_ctr = (int32_t*)ctx->block_ctr.p;
       }
@@ -2238,6 +2247,14 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
     a.persistent = 1;
     a.block0 = probe_blocks;
     a.block_ctr = (int32_t*)ctx->block_ctr.p;
+    // (diagnostic, tests only) a counter left non-zero when the main launch starts (after the probe,
+    // which zeroes it): the launch skips that many row blocks, which the lost-block check after it must
+    // report
+    if (const int seed = env_int("SRHIP_DEBUG_BLOCK_CTR", 0)) {
+      const int32_t h = (int32_t)seed;
+      HIP_TRY(hipMemcpyAsync(ctx->block_ctr.p, &h, sizeof(h), hipMemcpyHostToDevice, ctx->stream));
+      HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
     const int nmain = L.nrb - probe_blocks;
     const int wgs = std::max(1, std::min(nmain, ctx->num_cu));
     // SRHIP_TAIL_SLICES = S > 1: the row blocks past the last whole round of workgroups are claimed
@@ -2253,8 +2270,10 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   } else {
     HIP_TRY(launch_eval(dtype, a, R, K, mode, L.xlds, grid, L.lds, ctx->stream));
   }
-  HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
-  ctx->timed = true;
+  HIP_TRY(hipEventRecord(rs->ev1, ctx->stream));
+  J.launched = true;
+  J.persistent = persistent;
+  J.devp = devp;
   if (trace_on()) {  // poll the kernel's progress words for up to 10 s, then abort loudly
     const volatile int32_t* d = (const volatile int32_t*)ctx->h_dbg.p;
     int32_t last[16];
@@ -2279,7 +2298,7 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
       }
     }
   }
-  UndecidedList ul;
+  UndecidedList& ul = J.ul;
   int ul_groups = 4;
   if (devp) {
     if (!ctx->d_ulist.p) {
@@ -2297,25 +2316,38 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   if (!a.fused)
     HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, nch, cpb,
                           dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p, L.nrb, nl, (const int32_t*)d_order,
-                          mode == MODE_LOSS ? (sd ? sd->d_loss : ctx->h_loss.p) : nullptr,
-                          dtype == SRHIP_I32 ? nullptr : (sd ? sd->d_chk : ctx->h_chk.p), ctx->stream, a.slab_rows,
-                          (int64_t*)ctx->h_rows.p, ul, sd != nullptr));
+                          mode == MODE_LOSS ? (sd ? sd->d_loss : rs->h_loss.p) : nullptr,
+                          dtype == SRHIP_I32 ? nullptr : (sd ? sd->d_chk : rs->h_chk.p), ctx->stream, a.slab_rows,
+                          (int64_t*)rs->h_rows.p, ul, sd != nullptr));
   if (devp) {
     int stride = 1;
-    const int rc = enqueue_dev_precise(ctx, ds, P, v, ul.ulist, ul.umax, ul_groups, &stride);
+    const int rc = enqueue_dev_precise(ctx, ds, P, v, ul.ulist, ul.umax, ul_groups, &stride, rs);
     if (rc) return rc;
     dp->used = true;
     dp->stride = stride;
   }
   if (mode == MODE_PRED)
     HIP_TRY(hipMemcpyAsync(out_pred, pred.p, (size_t)nt * v.m * es, hipMemcpyDeviceToHost, ctx->stream));
-  {
-    const int rc = stream_wait(ctx);
-    if (rc) return rc;
-  }
+  HIP_TRY(hipEventRecord(rs->done, ctx->stream));
+  return SRHIP_OK;
+}
+
+// The second half: the records of a job whose work has completed (the caller waited for its stream or
+// its result set's completion event).
+static int eval_collect(srhip_ctx* ctx, const srhip_program* P, const View& v, double* sums, double* chk,
+                        DevPrecise* dp, ShardDev* sd, EvalJob& J) {
+  ResultSet* const rs = J.rs;
+  const int dtype = J.dtype, mode = J.mode;
+  const int32_t nt = J.nt;
+  const std::vector<int32_t>& live = J.live;
+  const bool persistent = J.persistent, devp = J.devp;
+  const UndecidedList& ul = J.ul;
+  ctx->last_ev0 = rs->ev0;
+  ctx->last_ev1 = rs->ev1;
+  ctx->timed = true;
   if (devp) {
-    const int32_t* hl = (const int32_t*)ctx->h_pout.p;
-    const double* hs = (const double*)((const uint8_t*)ctx->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
+    const int32_t* hl = (const int32_t*)rs->h_pout.p;
+    const double* hs = (const double*)((const uint8_t*)rs->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
     dp->count = hl[0];
     P->und_hint = dp->count;
     const int nu = std::min(dp->count, ul.umax);
@@ -2328,9 +2360,9 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   r_loss.resize(nt);
   r_chk.resize(nt);
   r_rows.resize(nt);
-  if (mode == MODE_LOSS) memcpy(r_loss.data(), ctx->h_loss.p, (size_t)nt * 8);
-  if (dtype != SRHIP_I32) memcpy(r_chk.data(), ctx->h_chk.p, (size_t)nt * (dtype == SRHIP_F32 ? 4 : 8));
-  memcpy(r_rows.data(), ctx->h_rows.p, (size_t)nt * 8);
+  if (mode == MODE_LOSS) memcpy(r_loss.data(), rs->h_loss.p, (size_t)nt * 8);
+  if (dtype != SRHIP_I32) memcpy(r_chk.data(), rs->h_chk.p, (size_t)nt * (dtype == SRHIP_F32 ? 4 : 8));
+  memcpy(r_rows.data(), rs->h_rows.p, (size_t)nt * 8);
   if (sd) {
     sd->rows.assign(nt, 0);
     for (int32_t t : live) sd->rows[t] = ((const int64_t*)r_rows.data())[t];
@@ -2372,6 +2404,19 @@ static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pr
   }
   g_tail_done = std::chrono::steady_clock::now();
   return SRHIP_OK;
+}
+
+// Device stage, synchronous: the launches, the wait, the records (result set 0).
+static int eval_partials(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
+                         const View& v, void* out_pred, double* sums, double* chk, DevPrecise* dp = nullptr,
+                         ShardDev* sd = nullptr) {
+  EvalJob J;
+  J.rs = &ctx->rs[0];
+  int rc = eval_issue(ctx, ds, P, mode, loss, v, out_pred, sums, chk, dp, sd, J);
+  if (rc || !J.launched) return rc;
+  rc = stream_wait(ctx);
+  if (rc) return rc;
+  return eval_collect(ctx, P, v, sums, chk, dp, sd, J);
 }
 
 // Precise stage: per-(tree, operator node) f64 sums over the view's rows for the selected trees;
@@ -2463,54 +2508,58 @@ int srhip::stream_wait(srhip_ctx* ctx) {
   }
 }
 
-// Single-device evaluation: partials -> decision -> precise pass for undecided trees.
-int srhip::run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
-                    const int64_t* idx, int64_t nidx, double* out_loss, void* out_pred, uint8_t* out_ok) {
-  static const bool timing = env_flag("SRHIP_HOST_TIMING");
-  const auto t_entry = std::chrono::steady_clock::now();
-  struct Report {  // on every return path
-    bool on;
-    std::chrono::steady_clock::time_point t0;
-    ~Report() {
-      if (!on) return;
-      static thread_local double acc[4];
-      static thread_local int cnt;
-      const auto t3 = std::chrono::steady_clock::now();
-      acc[0] += std::chrono::duration<double>(g_wait_begin - t0).count();
-      acc[1] += std::chrono::duration<double>(g_wait_done - g_wait_begin).count();
-      acc[2] += std::chrono::duration<double>(g_tail_done - g_wait_done).count();
-      acc[3] += std::chrono::duration<double>(t3 - g_tail_done).count();
-      static const bool each = [] {  // SRHIP_HOST_TIMING=2: every call
-        const char* e = getenv("SRHIP_HOST_TIMING");
-        return e && atoi(e) >= 2;
-      }();
-      if (++cnt % (each ? 1 : 50) == 0) {
-        fprintf(stderr, "[srhip host] run_eval: before wait %.1f us, wait %.1f us, records %.1f us, decisions %.1f us "
-                "(mean of %d)\n", acc[0] / cnt * 1e6, acc[1] / cnt * 1e6, acc[2] / cnt * 1e6, acc[3] / cnt * 1e6, cnt);
-        acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
-        cnt = 0;
-      }
-    }
-  } report{timing, t_entry};
+// Single-device evaluation: partials -> decision -> precise pass for undecided trees, as two halves --
+// run_issue (arguments, view, launches) and run_complete (records, decisions, the precise passes the
+// device did not settle, outputs) -- so that srhip_eval_loss_submit can return between them.
+struct RunJob {
+  EvalJob J;
+  View v{};
+  std::vector<double> sums, chk;
+  DevPrecise dp;
+  const srhip_dataset* ds = nullptr;
+  const srhip_program* P = nullptr;
+  int mode = 0;
+  bool empty = false;  // no trees: nothing to decide
+};
+static int run_issue(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
+                     const int64_t* idx, int64_t nidx, void* out_pred, RunJob& R) {
   int rc = check_eval_args(ctx, ds, P, mode, loss);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
-  View v;
-  rc = make_view(ctx, ds, idx, nidx, mode == MODE_LOSS, v);
+  R.ds = ds;
+  R.P = P;
+  R.mode = mode;
+  rc = make_view(ctx, ds, idx, nidx, mode == MODE_LOSS, R.v);
   if (rc) return rc;
   if (idx && ds->weighted && mode == MODE_LOSS) {
-    rc = gathered_weight_sum(ctx, ds, nidx, v);
+    rc = gathered_weight_sum(ctx, ds, nidx, R.v);
     if (rc) return rc;
   }
   const int32_t nt = P->ntrees;
-  if (nt == 0) return SRHIP_OK;
-  std::vector<double> sums(sums_len(nt, ds->nfeat)), chk(nt);
-  DevPrecise dp;
-  rc = eval_partials(ctx, ds, P, mode, loss, v, out_pred, sums.data(), chk.data(), &dp);
-  if (rc) return rc;
+  if (nt == 0) {
+    R.empty = true;
+    return SRHIP_OK;
+  }
+  R.sums.assign(sums_len(nt, ds->nfeat), 0.0);
+  R.chk.assign(nt, 0.0);
+  return eval_issue(ctx, ds, P, mode, loss, R.v, out_pred, R.sums.data(), R.chk.data(), &R.dp, nullptr, R.J);
+}
+static int run_complete(srhip_ctx* ctx, RunJob& R, double* out_loss, uint8_t* out_ok) {
+  if (R.empty) return SRHIP_OK;
+  const srhip_dataset* ds = R.ds;
+  const srhip_program* P = R.P;
+  const View& v = R.v;
+  std::vector<double>& sums = R.sums;
+  DevPrecise& dp = R.dp;
+  int rc = SRHIP_OK;
+  if (R.J.launched) {
+    rc = eval_collect(ctx, P, v, sums.data(), R.chk.data(), &dp, nullptr, R.J);
+    if (rc) return rc;
+  }
+  const int32_t nt = P->ntrees;
   std::vector<uint8_t> status(nt), ok(nt);
   std::vector<double> lossv(nt);
-  finalize(*P, ds->nfeat, sums.data(), chk.data(), lossv.data(), ok.data(), status.data());
+  finalize(*P, ds->nfeat, sums.data(), R.chk.data(), lossv.data(), ok.data(), status.data());
   std::vector<int32_t> unc;
   for (int32_t t = 0; t < nt; ++t)
     if (status[t] == 2) unc.push_back(t);
@@ -2535,7 +2584,10 @@ int srhip::run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program
   // trees past the device list's capacity (a program's first evaluation lists at most 4): the same
   // device-listed pass over a host-written list, DEV_PRECISE_MAX trees at a time -- every undecided
   // tree of a device evaluation is then settled by one summation path (SRHIP_PRECISE_OVERFLOW_HOST=1:
-  // the host-launched pass of eval_precise instead)
+  // the host-launched pass of eval_precise instead).  (A submitted evaluation reaches this after the
+  // work queued behind it; its view is the whole dataset -- submits of row subsets complete at once --
+  // and its results land in its own result set.)
+  ResultSet* const rs = R.J.rs;
   if (dp.used && !unc.empty() && !env_flag("SRHIP_PRECISE_OVERFLOW_HOST")) {
     const size_t bcap = (size_t)precise_cap(P, v, DEV_PRECISE_MAX);
     for (size_t b = 0; b < unc.size(); b += bcap) {
@@ -2546,12 +2598,12 @@ int srhip::run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program
       HIP_TRY(hipMemcpyAsync(ctx->d_ulist.p, lst.data(), lst.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                              ctx->stream));
       int stride = 1;
-      rc = enqueue_dev_precise(ctx, ds, P, v, (int32_t*)ctx->d_ulist.p, n, n, &stride);
+      rc = enqueue_dev_precise(ctx, ds, P, v, (int32_t*)ctx->d_ulist.p, n, n, &stride, rs);
       if (rc) return rc;
       rc = stream_wait(ctx);
       if (rc) return rc;
-      const int32_t* hl = (const int32_t*)ctx->h_pout.p;
-      const double* hs = (const double*)((const uint8_t*)ctx->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
+      const int32_t* hl = (const int32_t*)rs->h_pout.p;
+      const double* hs = (const double*)((const uint8_t*)rs->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
       if (hl[0] != n) return fail(SRHIP_ERR_DEVICE, "precise pass listed %d of %d trees", (int)hl[0], (int)n);
       for (int32_t u = 0; u < n; ++u) {
         const int32_t t = hl[1 + u];
@@ -2581,6 +2633,45 @@ int srhip::run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program
     if (out_loss) out_loss[t] = lossv[t];
   }
   return SRHIP_OK;
+}
+
+int srhip::run_eval(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
+                    const int64_t* idx, int64_t nidx, double* out_loss, void* out_pred, uint8_t* out_ok) {
+  static const bool timing = env_flag("SRHIP_HOST_TIMING");
+  const auto t_entry = std::chrono::steady_clock::now();
+  struct Report {  // on every return path
+    bool on;
+    std::chrono::steady_clock::time_point t0;
+    ~Report() {
+      if (!on) return;
+      static thread_local double acc[4];
+      static thread_local int cnt;
+      const auto t3 = std::chrono::steady_clock::now();
+      acc[0] += std::chrono::duration<double>(g_wait_begin - t0).count();
+      acc[1] += std::chrono::duration<double>(g_wait_done - g_wait_begin).count();
+      acc[2] += std::chrono::duration<double>(g_tail_done - g_wait_done).count();
+      acc[3] += std::chrono::duration<double>(t3 - g_tail_done).count();
+      static const bool each = [] {  // SRHIP_HOST_TIMING=2: every call
+        const char* e = getenv("SRHIP_HOST_TIMING");
+        return e && atoi(e) >= 2;
+      }();
+      if (++cnt % (each ? 1 : 50) == 0) {
+        fprintf(stderr, "[srhip host] run_eval: before wait %.1f us, wait %.1f us, records %.1f us, decisions %.1f us "
+                "(mean of %d)\n", acc[0] / cnt * 1e6, acc[1] / cnt * 1e6, acc[2] / cnt * 1e6, acc[3] / cnt * 1e6, cnt);
+        acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
+        cnt = 0;
+      }
+    }
+  } report{timing, t_entry};
+  RunJob R;
+  R.J.rs = &ctx->rs[0];
+  int rc = run_issue(ctx, ds, P, mode, loss, idx, nidx, out_pred, R);
+  if (rc) return rc;
+  if (R.J.launched) {
+    rc = stream_wait(ctx);
+    if (rc) return rc;
+  }
+  return run_complete(ctx, R, out_loss, out_ok);
 }
 
 // Row-sharded evaluation (srhip_eval_loss_sharded): this shard's partials written by the reduction
@@ -2783,6 +2874,19 @@ int srhip_device_count(void) {
   return n;
 }
 
+// One upload stream per device, shared by every context on it (new programs' synchronous uploads): a
+// context owns one evaluation stream, so the three-context optimiser split and the two-worker coalescer
+// stay within GPU_MAX_HW_QUEUES = 4 hardware queues per process (one stream per context plus this one).
+static hipStream_t shared_upload_stream(int device) {
+  static std::mutex mu;
+  static std::vector<hipStream_t> streams;
+  std::lock_guard<std::mutex> g(mu);
+  if ((size_t)device >= streams.size()) streams.resize(device + 1, nullptr);
+  if (!streams[device] && hipStreamCreateWithFlags(&streams[device], hipStreamNonBlocking) != hipSuccess)
+    streams[device] = nullptr;
+  return streams[device];
+}
+
 int srhip_ctx_create(int device, srhip_ctx** out) {
   if (!out) return fail(SRHIP_ERR_INVALID, "null out");
   *out = nullptr;
@@ -2804,7 +2908,13 @@ int srhip_ctx_create(int device, srhip_ctx** out) {
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
-  HIP_TRY(hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking));
+  for (ResultSet& r : c->rs) {
+    HIP_TRY(hipEventCreate(&r.ev0));
+    HIP_TRY(hipEventCreate(&r.ev1));
+    HIP_TRY(hipEventCreateWithFlags(&r.done, hipEventDisableTiming));
+  }
+  c->up_stream = shared_upload_stream(device);
+  if (!c->up_stream) return fail(SRHIP_ERR_DEVICE, "upload stream creation failed on device %d", device);
   *out = c.release();
   return SRHIP_OK;
 }
@@ -2818,8 +2928,11 @@ void srhip_ctx_destroy(srhip_ctx* ctx) {
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->ev_sync) (void)hipEventDestroy(ctx->ev_sync);
+  for (ResultSet& r : ctx->rs)
+    for (hipEvent_t e : {r.ev0, r.ev1, r.done})
+      if (e) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-  if (ctx->up_stream) (void)hipStreamDestroy(ctx->up_stream);
+  // (up_stream is the device's shared upload stream: it lives as long as the process)
   delete ctx;
   (void)hipGetLastError();
 }
@@ -3008,6 +3121,69 @@ int srhip_eval_loss(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program
   return run_eval(ctx, ds, prog, MODE_LOSS, loss, idx, nidx, out_loss, nullptr, out_ok);
 }
 
+// srhip_eval_loss_submit / _wait: an evaluation whose launches return at once (queued on the context's
+// stream behind whatever is in flight there) and whose records, decisions and outputs are taken at wait.
+struct srhip_eval_ticket {
+  srhip_ctx* ctx = nullptr;
+  RunJob R;
+  bool done = false;  // evaluated at submit (row subsets)
+  std::vector<double> loss;
+  std::vector<uint8_t> ok;
+};
+
+int srhip_eval_loss_submit(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* prog, const srhip_loss* loss,
+                           const int64_t* idx, int64_t nidx, srhip_eval_ticket** out) {
+  if (!out) return fail(SRHIP_ERR_INVALID, "null ticket output");
+  *out = nullptr;
+  if (!ctx || !prog) return fail(SRHIP_ERR_INVALID, "null argument");
+  std::unique_ptr<srhip_eval_ticket> t(new srhip_eval_ticket());
+  t->ctx = ctx;
+  if (idx) {
+    // a row subset's gather synchronises the stream and its buffers are the context's: evaluated here
+    t->loss.resize(prog->ntrees);
+    t->ok.resize(prog->ntrees);
+    const int rc = run_eval(ctx, ds, prog, MODE_LOSS, loss, idx, nidx, t->loss.data(), nullptr, t->ok.data());
+    if (rc) return rc;
+    t->done = true;
+    *out = t.release();
+    return SRHIP_OK;
+  }
+  int k = -1;
+  for (int i = 1; i < RESULT_SETS && k < 0; ++i)
+    if (!ctx->rs[i].busy) k = i;
+  if (k < 0) return fail(SRHIP_ERR_INVALID, "%d evaluations already in flight on this context", RESULT_SETS - 1);
+  t->R.J.rs = &ctx->rs[k];
+  const int rc = run_issue(ctx, ds, prog, MODE_LOSS, loss, nullptr, 0, nullptr, t->R);
+  if (rc) {
+    (void)hipStreamSynchronize(ctx->stream);  // launches may have been queued before the failure
+    return rc;
+  }
+  ctx->rs[k].busy = true;
+  *out = t.release();
+  return SRHIP_OK;
+}
+
+int srhip_eval_loss_wait(srhip_eval_ticket* ticket, double* out_loss, uint8_t* out_ok) {
+  if (!ticket) return fail(SRHIP_ERR_INVALID, "null ticket");
+  std::unique_ptr<srhip_eval_ticket> t(ticket);
+  if (t->done) {
+    for (size_t i = 0; i < t->loss.size(); ++i) {
+      if (out_loss) out_loss[i] = t->loss[i];
+      if (out_ok) out_ok[i] = t->ok[i];
+    }
+    return SRHIP_OK;
+  }
+  srhip_ctx* ctx = t->ctx;
+  ResultSet* rs = t->R.J.rs;
+  struct Release {  // the result set is free again on every path
+    ResultSet* r;
+    ~Release() { r->busy = false; }
+  } release{rs};
+  HIP_TRY(hipSetDevice(ctx->device));
+  if (t->R.J.launched) HIP_TRY(hipEventSynchronize(rs->done));
+  return run_complete(ctx, t->R, out_loss, out_ok);
+}
+
 int srhip_eval_predict(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* prog, const int64_t* idx,
                        int64_t nidx, void* out_pred, uint8_t* out_ok) {
   if (!out_pred || !out_ok) return fail(SRHIP_ERR_INVALID, "null output");
@@ -3081,9 +3257,9 @@ int srhip_chk_reduce_op(int dtype) { return dtype == SRHIP_F32 ? 0 : 1; }
 int32_t srhip_program_max_ops(const srhip_program* P) { return P ? std::max(1, P->max_ops) : 0; }
 
 double srhip_last_kernel_ms(const srhip_ctx* ctx) {
-  if (!ctx || !ctx->timed) return -1.0;
+  if (!ctx || !ctx->timed || !ctx->last_ev0 || !ctx->last_ev1) return -1.0;
   float ms = -1.0f;
-  if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) != hipSuccess) return -1.0;
+  if (hipEventElapsedTime(&ms, ctx->last_ev0, ctx->last_ev1) != hipSuccess) return -1.0;
   return (double)ms;
 }
 

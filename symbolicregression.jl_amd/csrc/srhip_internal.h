@@ -162,13 +162,30 @@ struct TreeInfo {
 
 }  // namespace srhip
 
+namespace srhip {
+// Where an evaluation's per-tree records land: coherent pinned host buffers its reductions write into
+// (loss sums, check statistics, rows evaluated, the device precise pass's output), the interpreter's
+// timing events and a completion event.  Set 0 serves the synchronous calls; srhip_eval_loss_submit
+// tickets take sets 1 .. RESULT_SETS - 1, so several evaluations can be in flight on one stream, each
+// with records of its own.
+struct ResultSet {
+  HostBuf h_loss, h_chk, h_rows, h_pout;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
+  bool busy = false;
+};
+constexpr int RESULT_SETS = 4;
+}  // namespace srhip
+
 // the opaque handles of include/srhip.h (global namespace, as declared there)
 struct srhip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;  // the gradient kernels' timing (srhip_optim.cpp)
+  // the events srhip_last_kernel_ms reads: ev0 / ev1 above, or the last completed evaluation's set's
+  hipEvent_t last_ev0 = nullptr, last_ev1 = nullptr;
+  srhip::ResultSet rs[srhip::RESULT_SETS];
   hipEvent_t ev_sync = nullptr;  // stream_wait's completion marker (no timing)
-  hipStream_t up_stream = nullptr;  // new programs' uploads (srhip_program_create)
+  hipStream_t up_stream = nullptr;  // new programs' uploads (srhip_program_create): the device's shared upload stream
   bool timed = false;
   int num_cu = 256;
   int lds_max = 160 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerBlock of the device
@@ -184,7 +201,7 @@ struct srhip_ctx {
   std::vector<uint32_t> g_xd_spec;
   srhip::HostBuf h_gchunks[2], h_gred[2];   // their pinned staging, per pass (gradient, value-only)
   srhip::HostBuf h_gpatch, h_gspec;         // pinned staging of patched / speculative gradient code
-  srhip::HostBuf h_loss, h_chk, h_stats, h_prec, h_dbg;
+  srhip::HostBuf h_stats, h_prec, h_dbg;
   srhip::DevBuf fail_flag;  // [order slots] int32: launch epoch in which the tree was seen to fail
   int32_t epoch = 0;        // interpreter launches so far (MODE_LOSS with early exit)
   // persistent launches: the row-block counter (one int32).  Zeroed once; every launch that drains its
@@ -193,9 +210,7 @@ struct srhip_ctx {
   srhip::DevBuf block_ctr;
   bool block_ctr_dirty = false;
   srhip::DevBuf slab_rows;  // [row block][order slot] valid rows evaluated
-  srhip::HostBuf h_rows;    // [program trees] int64 rows evaluated per tree (coherent pinned)
   srhip::DevBuf d_ulist;    // the device's undecided-tree list ([0] = count; reset by its consumer)
-  srhip::HostBuf h_pout;    // the device precise pass's results (coherent pinned)
   // work of the last srhip_eval_loss / srhip_eval_predict on this context (srhip_last_work):
   // evaluated node-rows, nominal node-rows (every live tree on every row), evaluated operator-node
   // rows, evaluated tree-rows

@@ -359,6 +359,8 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
   }
   if (timed) HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
   ctx->timed = timed;
+  ctx->last_ev0 = ctx->ev0;
+  ctx->last_ev1 = ctx->ev1;
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   // decision inputs in the partials layout: only the feature statistics and the row count are read
   std::vector<double> sums(2 * (size_t)P->ntrees + 2 * ds->nfeat + 1, 0.0);

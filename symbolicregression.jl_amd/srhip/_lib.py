@@ -89,6 +89,8 @@ SIGNATURES = {
     "srhip_program_get_constants": (ctypes.c_int, [_vp, _vp]),
     "srhip_eval_loss": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(Loss), _vp, _i64, _vp, _vp]),
     "srhip_eval_predict": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "srhip_eval_loss_submit": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(Loss), _vp, _i64, ctypes.POINTER(_vp)]),
+    "srhip_eval_loss_wait": (ctypes.c_int, [_vp, _vp, _vp]),
     "srhip_eval_loss_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, ctypes.POINTER(Operators),
                                              ctypes.POINTER(Loss), _vp, _i64, _vp, _vp]),
     "srhip_eval_loss_partials": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(Loss), _vp, _i64, _vp, _vp]),

@@ -161,6 +161,17 @@ class Program:
                                           0 if idxa is None else len(idxa), ptr(out), ptr(ok)))
         return out, ok.astype(bool)
 
+    def eval_loss_submit(self, ds: DeviceDataset, loss, idx=None) -> "EvalTicket":
+        """srhip_eval_loss_submit: the evaluation's launches queued behind whatever is in flight on the
+        context; .wait() -> (loss[T], ok[T]), the same bits as eval_loss.  At most 3 outstanding per
+        context; this program and ds must stay alive until the ticket is waited."""
+        ls = loss.c_struct()
+        idxa = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        h = ctypes.c_void_p()
+        check(_lib.load().srhip_eval_loss_submit(self.ctx.handle, ds.handle, self.handle, ctypes.byref(ls), ptr(idxa),
+                                                 0 if idxa is None else len(idxa), ctypes.byref(h)))
+        return EvalTicket(h, self, ds)
+
     def eval_predict(self, ds: DeviceDataset, idx=None):
         idxa = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
         m = ds.n if idxa is None else len(idxa)
@@ -361,3 +372,20 @@ class Coalescer:
             self.close()
         except Exception:
             pass
+
+
+class EvalTicket:
+    """An evaluation in flight (Program.eval_loss_submit); wait() exactly once."""
+
+    def __init__(self, handle, prog, ds):
+        self.handle, self._prog, self._ds = handle, prog, ds  # (keeps both alive until waited)
+
+    def wait(self):
+        if self.handle is None:
+            raise RuntimeError("ticket already waited")
+        out = np.empty(self._prog.ntrees, dtype=np.float64)
+        ok = np.empty(self._prog.ntrees, dtype=np.uint8)
+        h, self.handle = self.handle, None  # the library frees the ticket on every path
+        check(_lib.load().srhip_eval_loss_wait(h, ptr(out), ptr(ok)))
+        self._prog = self._ds = None
+        return out, ok.astype(bool)
