@@ -16,9 +16,16 @@ __global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab
                                                      const CT* __restrict__ slab_chk, int nrb, int nslots,
                                                      const int32_t* __restrict__ order, LT* __restrict__ out_loss,
                                                      CT* __restrict__ out_chk, const int32_t* __restrict__ slab_rows,
-                                                     int64_t* __restrict__ out_rows, UndecidedList ul, int chk_inf) {
+                                                     int64_t* __restrict__ out_rows, UndecidedList ul, int chk_inf,
+                                                     int32_t* __restrict__ items_done, int64_t* __restrict__ out_items) {
   const int lane = threadIdx.x & 63;
   const int slot = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  // a persistent launch's evaluated-item count (its workgroups' sum): reported, then cleared for the
+  // context's next persistent launch (this kernel runs after the interpreter on the stream)
+  if (items_done && blockIdx.x == 0 && threadIdx.x == 0) {
+    *out_items = *items_done;
+    *items_done = 0;
+  }
   if (slot >= nslots) return;
   LT s = 0;
   CT m = 0;
@@ -244,23 +251,24 @@ hipError_t launch_precise_reduce(const double* slab, int nrb, int stride, int32_
 
 hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, int cpb, const void* slab_chk, int nrb, int nslots,
                          const int32_t* order, void* out_loss, void* out_chk, hipStream_t s, const int32_t* slab_rows,
-                         int64_t* out_rows, const UndecidedList& ul, bool chk_inf) {
+                         int64_t* out_rows, const UndecidedList& ul, bool chk_inf, int32_t* items_done,
+                         int64_t* out_items) {
   dim3 grid((nslots + 3) / 4), block(256);
   switch (dtype) {
     case SRHIP_F32:
       hipLaunchKernelGGL((reduce_kernel<double, float, true>), grid, block, 0, s, (const double*)slab_loss, nch, cpb,
                          (const float*)slab_chk, nrb, nslots, order, (double*)out_loss, (float*)out_chk, slab_rows,
-                         out_rows, ul, (int)chk_inf);
+                         out_rows, ul, (int)chk_inf, items_done, out_items);
       break;
     case SRHIP_F64:
       hipLaunchKernelGGL((reduce_kernel<double, double, false>), grid, block, 0, s, (const double*)slab_loss, nch, cpb,
                          (const double*)slab_chk, nrb, nslots, order, (double*)out_loss, (double*)out_chk, slab_rows,
-                         out_rows, ul, (int)chk_inf);
+                         out_rows, ul, (int)chk_inf, items_done, out_items);
       break;
     case SRHIP_I32:
       hipLaunchKernelGGL((reduce_kernel<long long, float, true>), grid, block, 0, s, (const long long*)slab_loss, nch,
                          cpb, (const float*)nullptr, nrb, nslots, order, (long long*)out_loss, (float*)nullptr,
-                         slab_rows, out_rows, UndecidedList(), 0);
+                         slab_rows, out_rows, UndecidedList(), 0, items_done, out_items);
       break;
     default: return hipErrorInvalidValue;
   }

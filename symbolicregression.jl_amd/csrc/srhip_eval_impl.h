@@ -1611,6 +1611,9 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
       __syncthreads();
       const int item = __builtin_amdgcn_readfirstlane(claimed);
       if (item >= nitems) {
+        // the items this workgroup evaluated, added to block_ctr[1]: the reduction compares the launch's
+        // total with its item count (a counter left non-zero would have skipped items) and clears it
+        if (threadIdx.x == 0 && it > 0) atomicAdd(p.block_ctr + 1, it);
         // every workgroup ends on one failing claim; the last of them (nitems + grid - 1) leaves the
         // counter at zero for the context's next persistent launch (no memset launch before it)
         if (threadIdx.x == 0 && item == nitems + (int)gridDim.x - 1)

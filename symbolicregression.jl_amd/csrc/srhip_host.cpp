@@ -1865,6 +1865,10 @@ static int env_int(const char* name, int dflt) {
 // the precise pass, and the precise launch + its reduction follow on the stream before the one host
 // synchronisation (no host round trip between the main launch and the precise pass)
 constexpr int32_t DEV_PRECISE_MAX = 64;
+// h_pout = [count, list (DEV_PRECISE_MAX) | pad to 8 bytes | per-operator sums (double)]: the sums start on
+// an 8-byte boundary (they followed the 65 ints directly, at byte 260: misaligned double stores on the
+// device and loads on the host -- UBSan's report from tools/host_stress, round 6)
+constexpr size_t PREC_SUMS_OFF = ((size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t) + 7) & ~(size_t)7;
 struct DevPrecise {
   bool used = false;
   int32_t count = 0;             // trees the device listed (may exceed DEV_PRECISE_MAX)
@@ -1884,8 +1888,6 @@ struct ShardDev {
   void* d_loss = nullptr;
   void* d_chk = nullptr;
   size_t zero_bytes = 0;  // [loss | chk] cleared before the launch (static-fail trees are never written)
-  std::vector<int64_t> rows;
-  bool persistent = false;
 };
 
 // The device-listed precise pass, enqueued on the context's stream: the plain program over the trees
@@ -1918,7 +1920,7 @@ static int ensure_dev_precise(srhip_ctx* ctx, const srhip_program* P, const View
   const size_t per_tree = precise_per_tree(P, v, &sa);
   *cap = precise_cap(P, v, *cap);
   HIP_TRY(ctx->slab_prec.ensure((size_t)*cap * per_tree));
-  HIP_TRY(rs->h_pout.ensure((size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t) +
+  HIP_TRY(rs->h_pout.ensure(PREC_SUMS_OFF +
                             (size_t)DEV_PRECISE_MAX * sa * sizeof(double), hipHostMallocCoherent));
   return SRHIP_OK;
 }
@@ -1958,7 +1960,7 @@ static int enqueue_dev_precise(srhip_ctx* ctx, const srhip_dataset* ds, const sr
   q.prec_assign = 1;  // one-tile row blocks
   HIP_TRY(launch_eval(dtype, q, Rp, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, G), 16, ctx->stream));
   int32_t* hl = (int32_t*)rs->h_pout.p;
-  double* hs = (double*)((uint8_t*)rs->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
+  double* hs = (double*)((uint8_t*)rs->h_pout.p + PREC_SUMS_OFF);
   HIP_TRY(launch_precise_reduce((const double*)ctx->slab_prec.p, Lp.nrb, stride, ulist, cap, G, DEV_PRECISE_MAX, hl,
                                 hs, ctx->stream));
   *out_stride = stride;
@@ -1973,6 +1975,7 @@ struct EvalJob {
   bool launched = false, persistent = false, devp = false;
   int mode = 0, dtype = 0;
   int32_t nt = 0;
+  int32_t expect_items = 0;  // persistent launches: the items its workgroups must report evaluated
   std::vector<int32_t> live;
   UndecidedList ul;
   DevBuf pred;  // MODE_PRED's device output (synchronous calls only)
@@ -2135,7 +2138,7 @@ static int eval_issue(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_progr
   // device-to-host copies on the stream)
   HIP_TRY(rs->h_loss.ensure((size_t)nt * 8, hipHostMallocCoherent));
   HIP_TRY(rs->h_chk.ensure((size_t)nt * 8, hipHostMallocCoherent));
-  HIP_TRY(rs->h_rows.ensure((size_t)nt * 8, hipHostMallocCoherent));
+  HIP_TRY(rs->h_rows.ensure((size_t)(nt + 1) * 8, hipHostMallocCoherent));  // [nt]: persistent items evaluated
   EvalArgs a{};
   a.code = use_d ? P->dcode_dev : P->code_dev;
   a.prog_off = use_d ? P->doff_dev : P->off_dev;
@@ -2207,8 +2210,9 @@ static int eval_issue(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_progr
     // zeroed once: every persistent launch that drains its claims leaves it at zero (its last claim
     // resets it); again after a launch that was never seen to complete (an error return between the
     // launch and its synchronisation, or a lost row block below)
-    HIP_TRY(ctx->block_ctr.ensure(sizeof(int32_t)));
-    HIP_TRY(hipMemsetAsync(ctx->block_ctr.p, 0, sizeof(int32_t), ctx->stream));
+    // [claim counter, items evaluated]
+    HIP_TRY(ctx->block_ctr.ensure(2 * sizeof(int32_t)));
+    HIP_TRY(hipMemsetAsync(ctx->block_ctr.p, 0, 2 * sizeof(int32_t), ctx->stream));
     ctx->block_ctr_dirty = false;
   }
   if (persistent) ctx->block_ctr_dirty = true;  // until the launch is seen to have drained
@@ -2266,6 +2270,7 @@ static int eval_issue(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_progr
     const int slices = std::max(1, std::min(slices_env, 64));
     a.tail_slices = slices;
     a.tail_blocks = slices > 1 && nmain > wgs && nl >= 16 * slices ? nmain % wgs : 0;
+    J.expect_items = nmain - a.tail_blocks + a.tail_blocks * slices;
     HIP_TRY(launch_eval(dtype, a, R, K, mode, true, dim3(wgs, 1), L.lds, ctx->stream));
   } else {
     HIP_TRY(launch_eval(dtype, a, R, K, mode, L.xlds, grid, L.lds, ctx->stream));
@@ -2318,7 +2323,9 @@ static int eval_issue(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_progr
                           dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p, L.nrb, nl, (const int32_t*)d_order,
                           mode == MODE_LOSS ? (sd ? sd->d_loss : rs->h_loss.p) : nullptr,
                           dtype == SRHIP_I32 ? nullptr : (sd ? sd->d_chk : rs->h_chk.p), ctx->stream, a.slab_rows,
-                          (int64_t*)rs->h_rows.p, ul, sd != nullptr));
+                          (int64_t*)rs->h_rows.p, ul, sd != nullptr,
+                          persistent ? (int32_t*)ctx->block_ctr.p + 1 : nullptr,
+                          persistent ? (int64_t*)rs->h_rows.p + nt : nullptr));
   if (devp) {
     int stride = 1;
     const int rc = enqueue_dev_precise(ctx, ds, P, v, ul.ulist, ul.umax, ul_groups, &stride, rs);
@@ -2347,7 +2354,7 @@ static int eval_collect(srhip_ctx* ctx, const srhip_program* P, const View& v, d
   ctx->timed = true;
   if (devp) {
     const int32_t* hl = (const int32_t*)rs->h_pout.p;
-    const double* hs = (const double*)((const uint8_t*)rs->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
+    const double* hs = (const double*)((const uint8_t*)rs->h_pout.p + PREC_SUMS_OFF);
     dp->count = hl[0];
     P->und_hint = dp->count;
     const int nu = std::min(dp->count, ul.umax);
@@ -2363,11 +2370,6 @@ static int eval_collect(srhip_ctx* ctx, const srhip_program* P, const View& v, d
   if (mode == MODE_LOSS) memcpy(r_loss.data(), rs->h_loss.p, (size_t)nt * 8);
   if (dtype != SRHIP_I32) memcpy(r_chk.data(), rs->h_chk.p, (size_t)nt * (dtype == SRHIP_F32 ? 4 : 8));
   memcpy(r_rows.data(), rs->h_rows.p, (size_t)nt * 8);
-  if (sd) {
-    sd->rows.assign(nt, 0);
-    for (int32_t t : live) sd->rows[t] = ((const int64_t*)r_rows.data())[t];
-    sd->persistent = persistent;
-  }
   for (int32_t t : live) {
     if (sd) break;  // the shard's loss sums and statistics are in the exchange's device buffer
     if (mode == MODE_LOSS)
@@ -2375,21 +2377,15 @@ static int eval_collect(srhip_ctx* ctx, const srhip_program* P, const View& v, d
     if (dtype == SRHIP_F32) chk[t] = ((const float*)r_chk.data())[t];
     else if (dtype == SRHIP_F64) chk[t] = ((const double*)r_chk.data())[t];
   }
-  if (persistent && !sd) {  // (row shards: checked by the caller against the all-reduced statistic)
-    // every row block was claimed exactly once: a tree that did not fail was evaluated on every row
-    // (a counter left non-zero by an earlier launch would make this launch skip blocks silently)
-    // (a lost block is lost for every tree: one tree with a finite statistic verifies the launch; with
-    // none -- every tree failed -- the counter stays marked dirty and the next launch zeroes it)
-    bool verified = false;
-    for (int32_t t : live) {
-      if (!std::isfinite(chk[t])) continue;
-      const int64_t rows = ((const int64_t*)r_rows.data())[t];
-      if (rows != v.m)
-        return fail(SRHIP_ERR_DEVICE, "persistent launch evaluated tree %d on %lld of %lld rows (row-block counter "
-                    "not at zero); the counter is reset for the next launch", t, (long long)rows, (long long)v.m);
-      verified = true;
-    }
-    if (verified) ctx->block_ctr_dirty = false;
+  if (persistent) {
+    // every row block was claimed exactly once: the workgroups' evaluated items add up to the launch's
+    // item count (a counter left non-zero by a launch that never drained would make this one skip
+    // blocks silently -- and leave the skipped blocks' stale partials in the slabs)
+    const int64_t done = ((const int64_t*)rs->h_rows.p)[nt];
+    if (done != J.expect_items)
+      return fail(SRHIP_ERR_DEVICE, "persistent launch evaluated %lld of %d row-block items (row-block counter "
+                  "not at zero); the counter is reset for the next launch", (long long)done, (int)J.expect_items);
+    ctx->block_ctr_dirty = false;
   }
   // the launch's work, counted on the device (rows each tree was evaluated on)
   for (int i = 0; i < 4; ++i) ctx->work[i] = 0;
@@ -2603,7 +2599,7 @@ static int run_complete(srhip_ctx* ctx, RunJob& R, double* out_loss, uint8_t* ou
       rc = stream_wait(ctx);
       if (rc) return rc;
       const int32_t* hl = (const int32_t*)rs->h_pout.p;
-      const double* hs = (const double*)((const uint8_t*)rs->h_pout.p + (size_t)(1 + DEV_PRECISE_MAX) * sizeof(int32_t));
+      const double* hs = (const double*)((const uint8_t*)rs->h_pout.p + PREC_SUMS_OFF);
       if (hl[0] != n) return fail(SRHIP_ERR_DEVICE, "precise pass listed %d of %d trees", (int)hl[0], (int)n);
       for (int32_t u = 0; u < n; ++u) {
         const int32_t t = hl[1 + u];
@@ -2727,23 +2723,9 @@ int srhip::run_eval_sharded(srhip_ctx* ctx, const srhip_dataset* ds, const srhip
     else if (P->dtype == SRHIP_F64) chk[t] = ((const double*)(rb + SL.chk_off()))[t];
   }
   for (size_t i = 0; i < 2 * (size_t)nf + 1; ++i) sums[2 * (size_t)nt + i] = raux[1 + i];
-  if (sd.persistent) {
-    // this shard's persistent launch claimed every row block: a tree no shard failed was evaluated on all
-    // of this shard's rows.  A lost row block is lost for every tree of the launch, so one tree with a
-    // finite all-reduced statistic verifies the launch; a tree that failed on ANY shard cannot (its rows
-    // here may have stopped early legitimately).  When no tree verifies it, the counter stays marked
-    // dirty and the next launch zeroes it (a counter left non-zero could otherwise hide
-    // behind another shard's failures).
-    bool verified = false;
-    for (int32_t t = 0; t < nt; ++t) {
-      if (P->info[t].static_fail || !std::isfinite(chk[t])) continue;
-      if (sd.rows[t] != v.m)
-        return fail(SRHIP_ERR_DEVICE, "persistent launch evaluated tree %d on %lld of %lld rows (row-block counter "
-                    "not at zero); the counter is reset for the next launch", t, (long long)sd.rows[t], (long long)v.m);
-      verified = true;
-    }
-    if (verified) ctx->block_ctr_dirty = false;
-  }
+  // (this shard's persistent launch was checked to have evaluated every row block by eval_collect,
+  // from its own item count -- not from the all-reduced statistic, which another shard's failures can
+  // make non-finite: ADVICE r05)
   std::vector<uint8_t> status(nt), ok(nt);
   std::vector<double> lossv(nt);
   finalize(*P, nf, sums.data(), chk.data(), lossv.data(), ok.data(), status.data());

@@ -134,7 +134,8 @@ struct UndecidedList {
 hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, int cpb, const void* slab_chk, int nrb, int nslots,
                          const int32_t* order, void* out_loss, void* out_chk, hipStream_t s,
                          const int32_t* slab_rows = nullptr, int64_t* out_rows = nullptr,
-                         const UndecidedList& ul = UndecidedList(), bool chk_inf = false);
+                         const UndecidedList& ul = UndecidedList(), bool chk_inf = false,
+                         int32_t* items_done = nullptr, int64_t* out_items = nullptr);
 // The precise pass's per-(listed tree, operator) sums over the row blocks (fixed order, compensated),
 // written to out (coherent host memory: out_count, then [umax][stride] doubles); the last workgroup
 // resets ulist[0] (ulist[1 + done_slot]: its finished-workgroup counter, zero between launches).
