@@ -2856,19 +2856,6 @@ int srhip_device_count(void) {
   return n;
 }
 
-// One upload stream per device, shared by every context on it (new programs' synchronous uploads): a
-// context owns one evaluation stream, so the three-context optimiser split and the two-worker coalescer
-// stay within GPU_MAX_HW_QUEUES = 4 hardware queues per process (one stream per context plus this one).
-static hipStream_t shared_upload_stream(int device) {
-  static std::mutex mu;
-  static std::vector<hipStream_t> streams;
-  std::lock_guard<std::mutex> g(mu);
-  if ((size_t)device >= streams.size()) streams.resize(device + 1, nullptr);
-  if (!streams[device] && hipStreamCreateWithFlags(&streams[device], hipStreamNonBlocking) != hipSuccess)
-    streams[device] = nullptr;
-  return streams[device];
-}
-
 int srhip_ctx_create(int device, srhip_ctx** out) {
   if (!out) return fail(SRHIP_ERR_INVALID, "null out");
   *out = nullptr;
@@ -2895,8 +2882,7 @@ int srhip_ctx_create(int device, srhip_ctx** out) {
     HIP_TRY(hipEventCreate(&r.ev1));
     HIP_TRY(hipEventCreateWithFlags(&r.done, hipEventDisableTiming));
   }
-  c->up_stream = shared_upload_stream(device);
-  if (!c->up_stream) return fail(SRHIP_ERR_DEVICE, "upload stream creation failed on device %d", device);
+  HIP_TRY(hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking));
   *out = c.release();
   return SRHIP_OK;
 }
@@ -2914,7 +2900,7 @@ void srhip_ctx_destroy(srhip_ctx* ctx) {
     for (hipEvent_t e : {r.ev0, r.ev1, r.done})
       if (e) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-  // (up_stream is the device's shared upload stream: it lives as long as the process)
+  if (ctx->up_stream) (void)hipStreamDestroy(ctx->up_stream);
   delete ctx;
   (void)hipGetLastError();
 }

@@ -185,7 +185,11 @@ struct srhip_ctx {
   hipEvent_t last_ev0 = nullptr, last_ev1 = nullptr;
   srhip::ResultSet rs[srhip::RESULT_SETS];
   hipEvent_t ev_sync = nullptr;  // stream_wait's completion marker (no timing)
-  hipStream_t up_stream = nullptr;  // new programs' uploads (srhip_program_create): the device's shared upload stream
+  // new programs' uploads (srhip_program_create).  One per context: a device-wide shared upload stream
+  // (four streams for the three-context optimiser split instead of six) made C4 168 ms against 142 on
+  // one box (round 6, profiles/r06_c4_upload_stream_ab.txt) -- with three evaluation streams on
+  // hardware queues of their own the groups' kernels contend; with six, two of them share a queue
+  hipStream_t up_stream = nullptr;
   bool timed = false;
   int num_cu = 256;
   int lds_max = 160 * 1024;  // hipDeviceAttributeMaxSharedMemoryPerBlock of the device

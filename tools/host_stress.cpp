@@ -15,6 +15,8 @@
 // order (srhip_eval_loss_submit / _wait) and the split constant optimiser (three contexts and threads).
 //
 //   host_stress [THREADS] [ROUNDS]     prints "host_stress ok ..." and exits 0, or exits 1 on a mismatch
+// On a GPU box: LSAN_OPTIONS=suppressions=tools/lsan_rocm.supp (the ROCm runtime's own allocations that
+// outlive the process: libhsa-runtime64 / libamdhip64 frames only, none of libsrhip's).
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -235,5 +237,6 @@ int main(int argc, char** argv) {
   printf("host_stress %s: %d threads x %d rounds, code cache hits %lld misses %lld inserts %lld, device phase %s\n",
          g_fail ? "FAILED" : "ok", threads, rounds, (long long)hits, (long long)misses, (long long)inserts,
          dev ? "run" : "skipped (no device)");
+  fflush(stdout);  // (LeakSanitizer's report at exit ends the process with _exit: unflushed output is lost)
   return g_fail ? 1 : 0;
 }
