@@ -30,7 +30,7 @@ if want trace; then
   step trace
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $F/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 30 --no-cpu --headline-only > $F/prof.log 2>&1 || exit $?
   python3 scripts/trace_summary.py $F/prof/run_kernel_trace.csv > $F/trace_c2.txt; python3 scripts/step_timeline.py $F/prof/run_kernel_trace.csv > $F/step_timeline_c2.txt
-  python3 scripts/trace_timed_region.py $F/prof/run_kernel_trace.csv $F/prof.log > $F/trace_c2_timed_region.txt 2>&1 || true
+  python3 scripts/trace_timed_region.py $F/prof/run_kernel_trace.csv 20 30 > $F/trace_c2_timed_region.txt 2>&1 || true
   head -5 $F/trace_c2.txt
 fi
 if want pmc; then
