@@ -438,7 +438,10 @@ SRM_FN double srm_jcos_fma(double z) {
   return srm_fma(z, srm_fma(z, srm_fma(z, srm_fma(z, SRM_JC3, SRM_JC2), SRM_JC1), SRM_JC0), 1.0);
 }
 SRM_FN int srm_jtie(double v) {
-  return (((uint32_t)srm_bits(v) & 0x1FFFFFFFu) - (0x10000000u - SRM_JTIE_K)) <= 2u * SRM_JTIE_K;
+  /* low 29 bits within K of 2^28: shifted left by 3 (dropping the rest) the midpoint is 2^31, and
+   * (lo << 3) + 2^31 + 8K wraps the window [2^31 - 8K, 2^31 + 8K] onto [0, 16K] -- one shift-add and
+   * one compare on the device (v_lshl_add_u32) */
+  return (uint32_t)(((uint32_t)srm_bits(v) << 3) + (0x80000000u + 8u * SRM_JTIE_K)) <= 16u * SRM_JTIE_K;
 }
 /* rem_pio2_kernel(x::Float32): n, y for |x| >= Float32(pi)/4, x finite */
 SRM_FN int srm_jrem_pio2f(float x, double* y) {

@@ -476,11 +476,28 @@ __device__ __attribute__((always_inline)) inline void jtrig_coef_vgprs(double& s
   c3v = SRM_JC3;
   asm volatile("" : "+v"(s4v), "+v"(c3v));
 }
+// (a & m) | (b & ~m) per 32-bit half: a where m = -1, b where m = 0
+// srm_jtie on the device: the shift-add with its constant in an SGPR (the compiler moved the literal into
+// a VGPR per row: a VOP3 instruction takes no literal here)
+__device__ __attribute__((always_inline)) inline bool jtie_dev(double v) {
+  uint32_t w;
+  asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(w) : "v"((uint32_t)__builtin_bit_cast(uint64_t, v)),
+      "s"(0x80000000u + 8u * SRM_JTIE_K));
+  return w <= 16u * SRM_JTIE_K;
+}
+// (gfx950's v_bitop3_b32 with the select's truth table 0xE4 = m ? a : b per bit, through the builtin: as
+// plain C the compiler split it into four operations, as inline asm it added s_nops around it)
+__device__ __attribute__((always_inline)) inline double bfi_f64(int m, double a, double b) {
+  const uint64_t ab = __builtin_bit_cast(uint64_t, a), bb = __builtin_bit_cast(uint64_t, b);
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)ab, (uint32_t)bb, (uint32_t)m, 0xE4);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(ab >> 32), (uint32_t)(bb >> 32), (uint32_t)m, 0xE4);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
 template <int KIND>
 __device__ __attribute__((always_inline)) inline float jtrigf_a_row_fast(float x, double s4v, double c3v) {
   const double xd = (double)x, z = xd * xd;
   double p = KIND == 0 ? jcos_fma_dev(z, c3v) : jsin_fma_dev(xd, z, s4v);
-  if (__builtin_amdgcn_ballot_w64(srm_jtie(p)) != 0) [[unlikely]]
+  if (__builtin_amdgcn_ballot_w64(jtie_dev(p)) != 0) [[unlikely]]
     p = KIND == 0 ? srm_jcos_kernel(xd) : srm_jsin_kernel(xd);
   return KIND == 0 ? (float)p : __builtin_copysignf((float)p, x);
 }
@@ -498,20 +515,18 @@ template <int KIND, bool CW>
 __device__ __attribute__((always_inline)) inline float jtrigf_row_fast(float x, double s4v, double c3v) {
   double fn;
   const double y = jtrigf_red<KIND, CW>(x, fn);
-  const int n = cvt_i32_sat(fn);
+  // n1 = n + 1 - KIND: its bit 0 selects the cos kernel (cos: n even; sin: n odd), its bit 1 is the sign
+  // (cos: quadrants 1, 2; sin: 2, 3)
+  const int n1 = cvt_i32_sat(fn) + 1 - KIND;
   const double z = y * y;
-  double ps = jsin_fma_dev(y, z, s4v), pc = jcos_fma_dev(z, c3v);
-  asm volatile("" : "+v"(ps), "+v"(pc));
-  const bool use_sin = ((n & 1) ^ KIND) != 0;
-  double p = use_sin ? ps : pc;
-  if (__builtin_amdgcn_ballot_w64(srm_jtie(p)) != 0) [[unlikely]] {
-    double es = srm_jsin_kernel(y), ec = srm_jcos_kernel(y);
-    asm volatile("" : "+v"(es), "+v"(ec));
-    p = use_sin ? es : ec;
-  }
-  // the sign: bit 1 of n + 1 - KIND (cos: quadrants 1, 2; sin: 2, 3), added into bit 31 (the xor)
+  const double ps = jsin_fma_dev(y, z, s4v), pc = jcos_fma_dev(z, c3v);
+  const int msk = __builtin_amdgcn_sbfe(n1, 0, 1);  // -1 where the cos kernel applies: a bit select, no compare
+  double p = bfi_f64(msk, pc, ps);
+  if (__builtin_amdgcn_ballot_w64(jtie_dev(p)) != 0) [[unlikely]]
+    p = bfi_f64(msk, srm_jcos_kernel(y), srm_jsin_kernel(y));
+  // the sign added into bit 31 (the xor)
   uint32_t o;
-  asm("v_lshl_add_u32 %0, %1, 31, %2" : "=v"(o) : "v"((n + 1 - KIND) >> 1), "v"(__builtin_bit_cast(uint32_t, (float)p)));
+  asm("v_lshl_add_u32 %0, %1, 31, %2" : "=v"(o) : "v"(n1 >> 1), "v"(__builtin_bit_cast(uint32_t, (float)p)));
   const float r = __builtin_bit_cast(float, o);
   return (KIND == 1 && x == 0.0f) ? x : r;  // sin(-0) = -0 (the reduction gives +0)
 }
