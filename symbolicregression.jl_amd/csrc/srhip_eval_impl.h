@@ -922,10 +922,13 @@ __device__ __attribute__((always_inline)) inline int32_t wave_chk(int32_t v) { r
 // whose fast max|v| bound cannot decide DynamicExpressions' isfinite(sum(array)) checks.
 // One wave owns a (tree, row block), so plain read-modify-write of its slab entry is race-free.
 template <typename T, int R>
-__device__ __attribute__((always_inline)) inline void precise_hook(const EvalArgs& p, uint32_t a, const RV<T, R>& A,
+// ord: the operator's ordinal (1-based) in the tree's program, counted by the interpreter in execution
+// order -- the order the host numbered them (push_op), so a gradient program's leaf-constant
+// superinstructions can carry their constant's index in the instruction's upper half instead
+__device__ __attribute__((always_inline)) inline void precise_hook(const EvalArgs& p, uint32_t ord, const RV<T, R>& A,
                                                                    int slot, int rb, int lane, int64_t row0) {
   if constexpr (!kIsInt<T>) {
-    const uint32_t opidx = a >> 16;
+    const uint32_t opidx = ord;
     if (opidx == 0) return;
     constexpr int VEC = 16 / sizeof(T);
     double s = 0.0;
@@ -1350,6 +1353,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
       // instruction is one s_load_dwordx4 (scalar cache), prefetched one instruction ahead.
       const CIns* prog = code + pc0;
       Ins nxt = prog[0];
+      [[maybe_unused]] uint32_t pord = 0;  // MODE_PRECISE: operators executed so far (precise_hook)
       // bounded: a malformed program ends after max_steps instructions instead of hanging
       for (int step = 0; step < max_steps; ++step) {
         const Ins ins = nxt;
@@ -1360,7 +1364,9 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
           SRHIP_LK case H_LOADF:
             load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A);
             // (a gradient program's derived-column load carries its operator's ordinal)
-            if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);
+            // (a gradient program's derived-column load is an operator: its ordinal field is non-zero)
+            if constexpr (MODE == MODE_PRECISE)
+              if ((ins.a >> 16) != 0) precise_hook<T, R>(p, ++pord, A, slot, rb, lane, row0);
             break;
           SRHIP_LK case H_LOADC: { const T c = imm_as<T>(ins.imm); UNR for (int r = 0; r < R; ++r) A[r] = c; break; }
 #define SRHIP_K_CASES(BASE, ...)                                                            \
@@ -1400,7 +1406,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
       RV<T, R> xv;                                                                                     \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
       bin_rows_chk<T, R, SB_##NAME, false>(A, xv, M);                                              \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ++pord, A, slot, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
   SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_FA):                                                \
@@ -1408,19 +1414,19 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
       RV<T, R> xv;                                                                                     \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, xv);                                    \
       bin_rows_chk<T, R, SB_##NAME, true>(A, xv, M);                                               \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ++pord, A, slot, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
   SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_AC):                                                \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       bin_rows_c_chk<T, R, SB_##NAME, false>(A, imm_as<T>(ins.imm), M);                            \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ++pord, A, slot, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
   SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_CA):                                                \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       bin_rows_c_chk<T, R, SB_##NAME, true>(A, imm_as<T>(ins.imm), M);                             \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ++pord, A, slot, rb, lane, row0);         \
     }                                                                                              \
     break;                                                                                         \
   SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_FF):                                              \
@@ -1429,30 +1435,30 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A);                          \
       load_rows<T, R>(xt + (int64_t)(ins.imm & 0xffff) * xstride, lane, xv);                       \
       bin_rows_chk<T, R, SB_##NAME, false>(A, xv, M);                                              \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);     \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ++pord, A, slot, rb, lane, row0);     \
     }                                                                                              \
     break;                                                                                         \
   SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_FC):                                              \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A);                          \
       bin_rows_c_chk<T, R, SB_##NAME, false>(A, imm_as<T>(ins.imm), M);                            \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);     \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ++pord, A, slot, rb, lane, row0);     \
     }                                                                                              \
     break;                                                                                         \
   SRHIP_HOTB_##NAME case h_spec(SB_##NAME, SPEC_CF):                                              \
     if constexpr (sb_ok<T>(SB_##NAME)) {                                                           \
       load_rows<T, R>(xt + (int64_t)(ins.a & 0xffff) * xstride, lane, A);                          \
       bin_rows_c_chk<T, R, SB_##NAME, true>(A, imm_as<T>(ins.imm), M);                             \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);     \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ++pord, A, slot, rb, lane, row0);     \
     }                                                                                              \
     break;                                                                                         \
     SRHIP_K_CASES_H(SRHIP_HOTB_##NAME, h_spec(SB_##NAME, SPEC_SA0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
       bin_rows_chk<T, R, SB_##NAME, true>(A, S[k], M);                                             \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ++pord, A, slot, rb, lane, row0);         \
     })                                                                                             \
     SRHIP_K_CASES_H(SRHIP_HOTB_##NAME, h_spec(SB_##NAME, SPEC_AS0), if constexpr (sb_ok<T>(SB_##NAME)) {                \
       bin_rows_chk<T, R, SB_##NAME, false>(A, S[k], M);                                            \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);         \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ++pord, A, slot, rb, lane, row0);         \
     })
           SRHIP_SPEC_BINOPS(SRHIP_SPEC_CASE)
 #undef SRHIP_SPEC_CASE
@@ -1461,12 +1467,12 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
     SRHIP_K_CASES(h_heavy(HB_##NAME, HEAVY_SA0), if constexpr (hb_ok<T>(HB_##NAME)) {           \
       apply_heavy<T, R, HB_##NAME>(A, S[k], A);                                                 \
       chk_update<R>(M, A);                                                                      \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);  \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ++pord, A, slot, rb, lane, row0);  \
     })                                                                                          \
     SRHIP_K_CASES(h_heavy(HB_##NAME, HEAVY_AS0), if constexpr (hb_ok<T>(HB_##NAME)) {           \
       apply_heavy<T, R, HB_##NAME>(A, A, S[k]);                                                 \
       chk_update<R>(M, A);                                                                      \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0);  \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ++pord, A, slot, rb, lane, row0);  \
     })
           SRHIP_HEAVY_BINOPS(SRHIP_HEAVY_CASE)
 #undef SRHIP_HEAVY_CASE
@@ -1480,7 +1486,7 @@ __device__ __attribute__((always_inline)) inline void eval_block(const EvalArgs&
       } else {                                                                   \
         chk_update<R>(M, A);                                                     \
       }                                                                          \
-      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ins.a, A, slot, rb, lane, row0); \
+      if constexpr (MODE == MODE_PRECISE) precise_hook<T, R>(p, ++pord, A, slot, rb, lane, row0); \
     }                                                                            \
     break;
           SRHIP_UNOPS(SRHIP_UN_CASE)

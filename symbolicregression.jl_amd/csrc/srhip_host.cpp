@@ -488,14 +488,17 @@ template <typename T> class TreeCompiler {
   }
 
   void push_ins(uint32_t h, uint32_t a, uint64_t imm) { code_->push_back(Ins{h, a, imm}); }
-  // operator instruction: a = (op ordinal + 1) << 16 | operand
-  void push_op(uint32_t h, uint32_t operand, uint64_t imm, int64_t node, int64_t parent) {
+  // operator instruction: a = (op ordinal + 1) << 16 | operand -- or, in a gradient program's
+  // leaf-constant superinstructions (FC / CF), hi = the constant's index in the upper half (the
+  // interpreter's precise pass counts operator ordinals in execution order: srhip_eval_impl.h
+  // precise_hook; only a derived-column load needs its ordinal field, to mark it an operator)
+  void push_op(uint32_t h, uint32_t operand, uint64_t imm, int64_t node, int64_t parent, int64_t hi = -1) {
     // the gradient program evaluates constant subtrees per row (their constants need tangents); the
     // reference evaluates them as scalars (_eval_constant_tree): finiteness only, no isfinite(sum)
     const bool scalar = grad_ && is_const(node);
     info_->op_sumcheck.push_back((!scalar && (parent < 0 || !fused_inner(node, parent))) ? 1 : 0);
     const uint32_t ord = (uint32_t)info_->op_sumcheck.size();
-    push_ins(h, (ord << 16) | (operand & 0xffff), imm);
+    push_ins(h, ((hi >= 0 ? (uint32_t)hi : ord) << 16) | (operand & 0xffff), imm);
   }
   uint64_t leaf_imm(int64_t i) {
     if (nd_[i].degree == 0) return HostVal<T>::bits(HostVal<T>::from(nd_[i].val));
@@ -505,14 +508,21 @@ template <typename T> class TreeCompiler {
   }
   bool leaf_is_feature(int64_t i) const { return nd_[i].degree == 0 && !nd_[i].constant; }
 
-  // Superinstructions (evaluation programs; SRHIP_NO_SUPER=1 turns them off): the leaf-leaf operand
-  // forms (emit) and a push fused with the leaf load that follows it: one dispatch instead of two.
-  const bool super_ = !grad_ && super_env();
+  // Superinstructions (SRHIP_NO_SUPER=1 turns them off; gradient programs since round 6,
+  // SRHIP_GRAD_NO_SUPER=1): the leaf-leaf operand forms (emit) and a push fused with the leaf load that
+  // follows it: one dispatch instead of two.  In a gradient program a leaf-constant form carries the
+  // constant's index in its upper half (push_op's hi) and a push fuses with a plain feature or constant
+  // load only (a derived-column load is an operator of its own).
+  const bool super_ = grad_ ? grad_super_env() : super_env();
 
  public:
   static bool super_env() {
     const char* e = env_get("SRHIP_NO_SUPER");
     return !(e && *e && *e != '0');
+  }
+  static bool grad_super_env() {
+    const char* e = env_get("SRHIP_GRAD_NO_SUPER");
+    return super_env() && !(e && *e && *e != '0');
   }
   static bool grad_uniform_env() {
     const char* e = env_get("SRHIP_GRAD_UNIFORM");
@@ -525,7 +535,7 @@ template <typename T> class TreeCompiler {
     for (size_t r = (size_t)begin; r < code.size(); ++r) {
       const Ins& a = code[r];
       if (a.h >= H_PUSH0 && a.h < H_PUSH0 + K_MAX && r + 1 < code.size() &&
-          (code[r + 1].h == H_LOADF || code[r + 1].h == H_LOADC)) {
+          ((code[r + 1].h == H_LOADF && (code[r + 1].a >> 16) == 0) || code[r + 1].h == H_LOADC)) {
         const Ins& b = code[r + 1];
         const uint32_t k = a.h - H_PUSH0;
         code[w++] = Ins{(b.h == H_LOADF ? H_PUSHLF0 : H_PUSHLC0) + k, b.a, b.imm};
@@ -578,12 +588,13 @@ template <typename T> class TreeCompiler {
     const int64_t L = n.l, Rr = n.r;
     const bool ll = leafish(L), rl = leafish(Rr);
     if (sb >= 0) {
-      if (ll && rl && super_) {
+      // (a gradient program's two constant leaves keep the uniform constant form below)
+      if (ll && rl && super_ && (leaf_col(L) >= 0 || leaf_col(Rr) >= 0)) {
         // deg2_l0_r0: both operands leaves (feature, derived column or constant) in one instruction
         const int cl = leaf_col(L), cr = leaf_col(Rr);
         if (cl >= 0 && cr >= 0) push_op(h_spec(sb, SPEC_FF), cl, (uint64_t)cr, i, parent);
-        else if (cl >= 0) push_op(h_spec(sb, SPEC_FC), cl, leaf_imm(Rr), i, parent);
-        else push_op(h_spec(sb, SPEC_CF), cr, leaf_imm(L), i, parent);
+        else if (cl >= 0) push_op(h_spec(sb, SPEC_FC), cl, leaf_imm(Rr), i, parent, grad_ ? (int64_t)cop(Rr) : -1);
+        else push_op(h_spec(sb, SPEC_CF), cr, leaf_imm(L), i, parent, grad_ ? (int64_t)cop(L) : -1);
         return;
       }
       // gradient programs: an operator of two constant subtrees (one value on every row) is evaluated
@@ -1146,14 +1157,17 @@ int compile_grad_t(srhip_program& P) {
       int32_t nc = 0;
       for (int32_t i = 0; i < gi.code_len; ++i) {
         const Ins& ins = P.gcode[(size_t)gi.code_begin + i];
-        bool carries = ins.h == H_LOADC || (ins.h >= H_SLOADC0 && ins.h < H_SLOADC0 + K_MAX);
+        bool carries = ins.h == H_LOADC || (ins.h >= H_SLOADC0 && ins.h < H_SLOADC0 + K_MAX) ||
+                       (ins.h >= H_PUSHLC0 && ins.h < H_PUSHLC0 + K_MAX);
+        bool hi = false;  // the constant index in the upper half (leaf-constant superinstructions)
         if (ins.h >= H_BIN0 && ins.h < H_HEAVY0) {
           const uint32_t form = (ins.h - H_BIN0) % SPEC_STRIDE;
-          carries = form == SPEC_AC || form == SPEC_CA;
+          carries = form == SPEC_AC || form == SPEC_CA || form == SPEC_FC || form == SPEC_CF;
+          hi = form == SPEC_FC || form == SPEC_CF;
         }
         if (!carries) continue;
         P.gci.push_back(i);
-        P.gci.push_back((int32_t)(ins.a & 0xffff & ~UN_UNIFORM_FLAG));  // (the constant index)
+        P.gci.push_back((int32_t)(hi ? ins.a >> 16 : ins.a & 0xffff & ~UN_UNIFORM_FLAG));  // (the constant index)
         ++nc;
       }
       // every constant leaf is consumed by exactly one such instruction

@@ -695,3 +695,45 @@ def test_derived_view_is_exact_weighted(ctx, monkeypatch):
     assert res["1"][7].sum() > 5
     for i, (a, b) in enumerate(zip(res["0"], res["1"])):
         assert _bits_equal(a, b), i
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_grad_superinstructions_are_exact(ctx, dtype, monkeypatch):
+    """The gradient program's superinstructions (round 6: leaf-leaf FF / FC / CF forms with the constant's
+    index in the upper half, pushes fused with the plain leaf load after them) return bitwise the plain
+    forms' results (SRHIP_GRAD_NO_SUPER=1): losses, gradients, did_succeed of a full and a value-only pass,
+    per-row derivatives with respect to the constants and the features, and an optimize_constants run
+    (speculative slots patch the fused instructions' constants), near-overflow trees included (the
+    precise pass runs the gradient program with operator ordinals counted, not read)."""
+    sr = _sr()
+    opts, _, nodes, offs, X, y = _problem(sr, dtype, ntrees=96, max_size=24)
+    big = 3.0e37 if dtype == np.float32 else 1.0e306
+    x0, x1, x2 = (sr.Node(feature=i) for i in (1, 2, 3))
+    c = lambda v: sr.Node(val=v)  # noqa: E731
+    extra = [sr.Node(3, sr.Node(1, x0, c(0.5)), sr.Node(2, c(1.5), x1)),         # (x0 + c) * (c - x1)
+             sr.Node(1, sr.Node(3, x0, x1), sr.Node(4, x2, c(3.0))),              # x0 * x1 + x2 / c
+             sr.Node(3, x0, c(big)), sr.Node(1, sr.Node(3, x1, c(big)), c(1.0))]  # near-overflow sums
+    en, eo = sr.flatten(extra, opts, dtype)
+    nodes = np.concatenate([nodes, en])
+    offs = np.concatenate([offs, eo[1:] + offs[-1]])
+    ds = sr.DeviceDataset(ctx, X, y)
+    loss = sr.L2DistLoss()
+    flat = lambda a: np.concatenate([np.ravel(x) for x in a])  # noqa: E731
+    res = {}
+    for ns in ("1", "0"):
+        monkeypatch.setenv("SRHIP_GRAD_NO_SUPER", ns)
+        prog = sr.Program(ctx, nodes, offs, opts, dtype)
+        l, g, ok = prog.eval_loss_grad(ds, loss)
+        monkeypatch.setenv("SRHIP_GRAD_VALUE_ONLY", "1")
+        vl, _, vok = prog.eval_loss_grad(ds, loss)
+        monkeypatch.delenv("SRHIP_GRAD_VALUE_ONLY")
+        pc, gc, okc = prog.eval_grad_predict(ds, variable=False)
+        pf, gf, okf = prog.eval_grad_predict(ds, variable=True)
+        out, imp, fc = prog.optimize_constants(ds, loss, iterations=8, nrestarts=1, seed=3)
+        res[ns] = [np.asarray(l, np.float64), flat(g), np.asarray(ok), np.asarray(vl, np.float64), np.asarray(vok),
+                   pc, flat(gc), okc, pf, flat(gf), okf,
+                   np.asarray(out, np.float64), imp, fc, np.concatenate(prog.get_constants())]
+        prog.close()
+    assert res["0"][12].sum() > 5
+    for i, (a, b) in enumerate(zip(res["1"], res["0"])):
+        assert _bits_equal(a, b), i
