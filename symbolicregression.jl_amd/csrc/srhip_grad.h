@@ -39,10 +39,6 @@ struct GradArgs {
   int32_t max_steps;
   // a derived view's derived-column count (its tangent-zero columns follow at + gd_nd); 0: none
   int32_t gd_nd;
-  // columns the workgroup stages into LDS before the target (XLDS launches): the feature columns, and
-  // with a derived view usually its derived columns (and, for launches with tangents, their tangent-zero
-  // columns) too -- 0: nfeat
-  int32_t nstage;
   // row blocks of this launch: blockIdx.x + block0 (slab rows keep their global block index)
   int32_t block0;
   // value-only screening (GMODE_LOSS, KT = 0): a chunk whose block-0 record (written by an earlier

@@ -337,30 +337,28 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   // every (chunk, row block) record is computed by one wave as before, so the bits do not change
   __shared__ int next_chunk;
   if (threadIdx.x == 0) next_chunk = GRAD_WAVES;
-  // staged columns: [0, ns) of the view -- its features, and (round 6) a derived view's derived and
-  // tangent-zero columns when the host stages them -- then the target
-  const int ns = p.nstage > 0 ? p.nstage : p.nfeat;
   if constexpr (XLDS) {
+    const int nf = p.nfeat;
     const bool has_y = GM == GMODE_LOSS && Yg != nullptr;
-    for (int i = threadIdx.x; i < (ns + 1) * rbr; i += 64 * GRAD_WAVES) {
+    for (int i = threadIdx.x; i < (nf + 1) * rbr; i += 64 * GRAD_WAVES) {
       const int f = i / rbr, r = i - f * rbr;
       const int64_t row = row_base + r;
       T v = T(0);
-      if (row < p.ld) v = f < ns ? Xg[(int64_t)f * p.ld + row] : (has_y ? Yg[row] : T(0));
+      if (row < p.ld) v = f < nf ? Xg[(int64_t)f * p.ld + row] : (has_y ? Yg[row] : T(0));
       xs[i] = v;
     }
   }
   __syncthreads();
-  // column f / target at block-relative row rr of this row block (columns past the staged ones are read
-  // from global memory)
+  // feature f / target at block-relative row rr of this row block
+  // (a derived view's derived columns, f >= nfeat, are read from global memory)
   auto xat = [&](int f, int rr) -> T {
     if constexpr (XLDS) {
-      if (f < ns) return xs[f * rbr + rr];
+      if (f < p.nfeat) return xs[f * rbr + rr];
     }
     return Xg[(int64_t)f * p.ld + row_base + rr];
   };
   auto yat = [&](int rr) -> T {
-    if constexpr (XLDS) return xs[ns * rbr + rr];
+    if constexpr (XLDS) return xs[p.nfeat * rbr + rr];
     else return Yg[row_base + rr];
   };
   GIns* code = (GIns*)(uintptr_t)p.code;
@@ -418,7 +416,7 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
               // (+-0, or NaN where f' is not finite) from the tangent-zero column
               RR(chk_fold(M, A[r].v);)
               if constexpr (KT > 0) {
-                RR(const T z = xat(opnd + p.gd_nd, rr);
+                RR(const T z = Xg[(int64_t)(opnd + p.gd_nd) * p.ld + row_base + rr];
                    UNR for (int j = 0; j < KT; ++j) A[r].d[j] = z;)
               }
             }
@@ -638,10 +636,9 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(const double* __restri
 }
 
 // LDS staging of the row block when it fits (few features): [nfeat + 1][rb_rows] elements
-// (80 KB: two 8-wave workgroups per CU, what the kernels' registers allow, share the CU's 160 KB)
-constexpr size_t GRAD_LDS_MAX = 80 * 1024;
+constexpr size_t GRAD_LDS_MAX = 48 * 1024;
 template <typename T> static size_t grad_lds_bytes(const GradArgs& a) {
-  return (size_t)((a.nstage > 0 ? a.nstage : a.nfeat) + 1) * (size_t)a.rb_rows * sizeof(T);
+  return (size_t)(a.nfeat + 1) * (size_t)a.rb_rows * sizeof(T);
 }
 
 // rows per lane: value-only passes (no tangents) carry 4 rows per lane (one dispatch per 256-row

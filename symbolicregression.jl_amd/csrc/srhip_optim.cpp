@@ -324,11 +324,6 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     a.nchunks = nch;
     a.nfeat = v.nfeat_x >= 0 ? v.nfeat_x : (int32_t)ds->nfeat;
     a.gd_nd = v.nd_x;
-    // a derived view's derived columns (and, with tangents, their tangent-zero columns) staged with the
-    // features when the launch carries SRHIP_GRAD_STAGE_MIN chunks or more (default 8): one LDS fill per
-    // workgroup instead of a global load per use; a launch of a few trees reads the few it needs instead
-    a.nstage = a.nfeat;
-    if (v.nd_x > 0 && nch >= env_int_opt("SRHIP_GRAD_STAGE_MIN", 8)) a.nstage += v.nd_x * (ps.kt > 0 ? 2 : 1);
     a.rb_rows = ps.L.rb_rows;
     a.nrb = ps.L.nrb;
     a.chunks_per_group = ps.L.tpg;
