@@ -432,9 +432,11 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   case BASE + 6: if constexpr (6 < K) { constexpr int k = 6; __VA_ARGS__ } break;                \
   case BASE + 7: if constexpr (7 < K) { constexpr int k = 7; __VA_ARGS__ } break;
           GK_CASES(H_PUSH0, { RR(S[k][r] = A[r];) })
+#if SRHIP_GRAD_SUPER_LEVEL >= 1
           // superinstructions (round 6): a push fused with the plain feature / constant load after it
           GK_CASES(H_PUSHLF0, { RR(S[k][r] = A[r]; set_feat<GM>(A[r], xat(opnd, rr), opnd - c0);) })
           GK_CASES(H_PUSHLC0, { RR(S[k][r] = A[r]; set_const<GM>(A[r], imm, opnd - c0);) })
+#endif
           GK_CASES(H_SLOADF0, { RR(set_feat<GM>(S[k][r], xat(opnd, rr), opnd - c0);) })
           GK_CASES(H_SLOADC0, { RR(set_const<GM>(S[k][r], imm, opnd - c0);) })
 // (AC / CA / SA / AS forms with UN_UNIFORM_FLAG in the operand field: two constant subtrees, one
@@ -442,7 +444,8 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
 #define GK_UNI_ROWS()                                                                              \
   UNR for (int r = 1; r < R; ++r) A[r] = A[0];                                                     \
   UNR for (int r = 0; r < R; ++r) chk_fold(M, A[r].v);
-#define GK_SPEC(NAME, FN)                                                                          \
+#if SRHIP_GRAD_SUPER_LEVEL >= 2
+#define GK_LEAFLEAF(NAME)                                                                          \
   /* leaf-leaf forms (round 6): X[a] op X[imm], X[a] op c, c op X[a] -- c's index in the upper half */ \
   case h_spec(SB_##NAME, SPEC_FF): {                                                               \
     const int f2 = (int)(ins.imm & 0xffff);                                                        \
@@ -458,7 +461,12 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
     const int ci = (int)(ins.a >> 16) - c0;                                                        \
     RR(Dual<T, KT> o; set_feat<GM>(A[r], xat(opnd, rr), opnd - c0); set_const<GM>(o, imm, ci);     \
        T f, fl, fr; dual_spec<T, SB_##NAME>(o.v, A[r].v, f, fl, fr); combine(A[r], o, A[r], f, fl, fr); \
-       chk_fold(M, A[r].v);) break; }                                                              \
+       chk_fold(M, A[r].v);) break; }
+#else
+#define GK_LEAFLEAF(NAME)
+#endif
+#define GK_SPEC(NAME, FN)                                                                          \
+  GK_LEAFLEAF(NAME)                                                                                \
   case h_spec(SB_##NAME, SPEC_AF): {                                                               \
     RR(Dual<T, KT> o; set_feat<GM>(o, xat(opnd, rr), opnd - c0);                                   \
        T f, fl, fr; dual_spec<T, SB_##NAME>(A[r].v, o.v, f, fl, fr); combine(A[r], A[r], o, f, fl, fr); \
@@ -503,6 +511,7 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
        combine(A[r], A[r], S[k][r], f, fl, fr); chk_fold(M, A[r].v);) })
           SRHIP_SPEC_BINOPS(GK_SPEC)
 #undef GK_SPEC
+#undef GK_LEAFLEAF
 #define GK_HEAVY(NAME, FN)                                                                         \
   GK_CASES(h_heavy(HB_##NAME, HEAVY_SA0), {                                                        \
     RR(const typename V4<T>::type q = dual_heavy<T, HB_##NAME, (KT > 0)>(S[k][r].v, A[r].v);                 \

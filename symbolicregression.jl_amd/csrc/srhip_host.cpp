@@ -269,7 +269,7 @@ template <typename T> class TreeCompiler {
       code_ = &code;
       info_ = &info;
       emit(0, 0, -1);
-      if (super_) fuse_push_loads(code, info.code_begin);
+      if (super_ && (!grad_ || SRHIP_GRAD_SUPER_LEVEL >= 1)) fuse_push_loads(code, info.code_begin);
       Ins end{H_END, 0, 0};
       code.push_back(end);
       for (int64_t i = info.code_begin; i < (int64_t)code.size(); ++i) info.cost += op_cost(code[i].h);
@@ -508,8 +508,9 @@ template <typename T> class TreeCompiler {
   }
   bool leaf_is_feature(int64_t i) const { return nd_[i].degree == 0 && !nd_[i].constant; }
 
-  // Superinstructions (SRHIP_NO_SUPER=1 turns them off; gradient programs since round 6,
-  // SRHIP_GRAD_NO_SUPER=1): the leaf-leaf operand forms (emit) and a push fused with the leaf load that
+  // Superinstructions (SRHIP_NO_SUPER=1 turns them off; gradient programs as far as the build's
+  // SRHIP_GRAD_SUPER_LEVEL allows -- none by default -- and SRHIP_GRAD_NO_SUPER=1 turns those off): the
+  // leaf-leaf operand forms (emit) and a push fused with the leaf load that
   // follows it: one dispatch instead of two.  In a gradient program a leaf-constant form carries the
   // constant's index in its upper half (push_op's hi) and a push fuses with a plain feature or constant
   // load only (a derived-column load is an operator of its own).
@@ -589,7 +590,7 @@ template <typename T> class TreeCompiler {
     const bool ll = leafish(L), rl = leafish(Rr);
     if (sb >= 0) {
       // (a gradient program's two constant leaves keep the uniform constant form below)
-      if (ll && rl && super_ && (leaf_col(L) >= 0 || leaf_col(Rr) >= 0)) {
+      if (ll && rl && super_ && (!grad_ || SRHIP_GRAD_SUPER_LEVEL >= 2) && (leaf_col(L) >= 0 || leaf_col(Rr) >= 0)) {
         // deg2_l0_r0: both operands leaves (feature, derived column or constant) in one instruction
         const int cl = leaf_col(L), cr = leaf_col(Rr);
         if (cl >= 0 && cr >= 0) push_op(h_spec(sb, SPEC_FF), cl, (uint64_t)cr, i, parent);

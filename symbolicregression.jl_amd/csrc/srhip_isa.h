@@ -75,7 +75,7 @@ enum : uint32_t {
   H_SLOADF0 = 3,                      // S[k] = X[a]   (operand of a heavy binary op)
   H_SLOADC0 = H_SLOADF0 + K_MAX,      // S[k] = imm
   H_PUSH0 = H_SLOADC0 + K_MAX,        // S[k] = A
-  // superinstructions (evaluation programs only; the gradient program keeps the plain forms):
+  // superinstructions (evaluation programs; gradient programs as SRHIP_GRAD_SUPER_LEVEL below allows):
   H_PUSHLF0 = H_PUSH0 + K_MAX,        // S[k] = A; A = X[a]     (a push followed by a feature leaf)
   H_PUSHLC0 = H_PUSHLF0 + K_MAX,      // S[k] = A; A = imm      (a push followed by a constant leaf)
   H_BIN0 = H_PUSHLC0 + K_MAX,         // specialised binary ops, SPEC_STRIDE handlers each
@@ -86,6 +86,16 @@ enum : uint32_t {
 constexpr uint32_t SPEC_AF = 0, SPEC_FA = 1, SPEC_AC = 2, SPEC_CA = 3, SPEC_SA0 = 4,
                    SPEC_AS0 = 4 + K_MAX, SPEC_FF = 4 + 2 * K_MAX, SPEC_FC = SPEC_FF + 1, SPEC_CF = SPEC_FF + 2,
                    SPEC_STRIDE = SPEC_FF + 3;
+// the superinstructions a gradient program uses (and the gradient kernel implements; srhip_grad.hip):
+// 0 none, 1 the push-load pairs (H_PUSHLF0 / H_PUSHLC0), 2 those and the leaf-leaf forms (SPEC_FF /
+// SPEC_FC / SPEC_CF, the constant's index in the operand's upper half).  Exact at every level; 0 by
+// default: C4 measured 146.2 / 149.2 / 146.3 ms per step at level 0, 146.6 / 149.7 / 146.1 at 1 and
+// 149.1 / 148.9 / 145.9 at 2 (same box, interleaved), and the gradient kernel's roofline fraction fell
+// 0.0368 -> 0.0350 with the handlers in: a quarter fewer dispatches, each in a larger kernel (every
+// variant grows; they run concurrently from several streams and share the instruction cache).
+#ifndef SRHIP_GRAD_SUPER_LEVEL
+#define SRHIP_GRAD_SUPER_LEVEL 0
+#endif
 // heavy binary ops take their second operand from a stack slot: A = S[k] op A, or A = A op S[k]
 constexpr uint32_t HEAVY_SA0 = 0, HEAVY_AS0 = K_MAX, HEAVY_STRIDE = 2 * K_MAX;
 constexpr uint32_t H_HEAVY0 = H_BIN0 + NUM_SPEC_BIN * SPEC_STRIDE;

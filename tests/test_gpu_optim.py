@@ -704,7 +704,9 @@ def test_grad_superinstructions_are_exact(ctx, dtype, monkeypatch):
     forms' results (SRHIP_GRAD_NO_SUPER=1): losses, gradients, did_succeed of a full and a value-only pass,
     per-row derivatives with respect to the constants and the features, and an optimize_constants run
     (speculative slots patch the fused instructions' constants), near-overflow trees included (the
-    precise pass runs the gradient program with operator ordinals counted, not read)."""
+    precise pass runs the gradient program with operator ordinals counted, not read).  The default build
+    emits none of them (srhip_isa.h SRHIP_GRAD_SUPER_LEVEL, measured slower); a build with
+    EXTRA=-DSRHIP_GRAD_SUPER_LEVEL=2 runs the comparison proper."""
     sr = _sr()
     opts, _, nodes, offs, X, y = _problem(sr, dtype, ntrees=96, max_size=24)
     big = 3.0e37 if dtype == np.float32 else 1.0e306
