@@ -54,6 +54,11 @@ SHAPES = {
     "push4": lambda: Node(B["+"], Node(B["+"], Node(B["*"], f(0), f(1)), Node(B["*"], f(2), f(3))),
                           Node(B["+"], Node(B["*"], f(4), f(0)), Node(B["*"], f(1), f(2)))),
     "mulf4": lambda: chain("*", f, 4),
+    # round 6: Julia's Float32 cos by argument tier (cos8 above is tier B: cos of a feature, then of
+    # values in [-1, 1]); each cos takes A * c, so subtract mulc8's per-node cost for the cos alone
+    "cosA8": lambda: _cosm(8, 0.05, 0.15),      # |arg| < pi/4
+    "cosC8": lambda: _cosm(8, 40.0, 60.0),      # 9pi/4 < |arg| < 2^28 pi/2 (Cody-Waite)
+    "cosS8": lambda: _cosm(8, 0.9e9, 1.1e9),    # Payne-Hanek rows
 }
 
 
@@ -61,6 +66,13 @@ def _un(op, n):
     t = f(0)
     for _ in range(n):
         t = Node(U[op], t)
+    return t
+
+
+def _cosm(n, lo, hi):  # cos(A * c) repeated: n cos + n mul-by-constant
+    t = f(0)
+    for _ in range(n):
+        t = Node(U["cos"], Node(B["*"], t, c(lo, hi)))
     return t
 
 

@@ -5,7 +5,8 @@ argument subtree over the 1M rows (oracle, host) and classify each 1024-row wave
   B: all |x| <= 9pi/4 (Julia's +-k pi/2 cases: one-product reduction, both kernels)
   C: all |x| < 2^28 pi/2 (Cody-Waite)
   D: larger / non-finite.
-Prints tile counts per tier (the device's per-wave path choice for Julia's Float32 trig)."""
+Prints tile counts per tier (the device's per-wave path choice for Julia's Float32 trig).
+python scripts/trig_arg_tiers.py [rows per tile, default 1000; 64: the round-6 per-slice study]"""
 import os
 import sys
 import numpy as np
@@ -15,6 +16,7 @@ import oracle
 from srhip import workloads
 from srhip.node import flatten
 
+TILE = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
 opts, X, y, trees, nodes, offs = workloads.c2(0, 1024, 1_000_000)
 cos_idx = [i + 1 for i, u in enumerate(opts.unary_operators) if u == "cos"][0]
 args = []
@@ -32,11 +34,11 @@ tiers = np.zeros(4, dtype=np.int64)
 for a in args:
     nd, of = flatten([a], opts, np.float32)
     out, ok = oracle.eval_tree(nd, opts.binop_codes, opts.unaop_codes, X)
-    m = np.abs(out).reshape(-1, 1000)  # (1M rows: 1000-row tiles, ~ the device's 1024)
+    m = np.abs(out).reshape(-1, TILE)  # (1M rows: 1000-row tiles, ~ the device's 1024)
     mx = np.max(np.where(np.isnan(m), np.inf, m), axis=1)
     tiers[0] += np.sum(mx < np.float32(np.pi) / 4)
     tiers[1] += np.sum((mx >= np.float32(np.pi) / 4) & (mx <= np.pi * 9 / 4))
     tiers[2] += np.sum((mx > np.pi * 9 / 4) & (mx < 421657440.0))
     tiers[3] += np.sum(~(mx < 421657440.0))
-print("cos-of-operator nodes:", len(args), "tiles per tier A/B/C/D:", tiers.tolist(),
+print("rows per tile:", TILE, "cos-of-operator nodes:", len(args), "tiles per tier A/B/C/D:", tiers.tolist(),
       "fractions:", np.round(tiers / tiers.sum(), 3).tolist())
