@@ -45,8 +45,6 @@ struct GradArgs {
   // launch on the stream) already holds a non-finite check statistic is skipped -- its tree fails
   // did_succeed whatever the other blocks hold
   int32_t screened;
-  // value-only loss launches of at least this many chunks run two row blocks per workgroup (-1: never)
-  int32_t wb_min;
   // per-row modes: out_der[row + j][nvalid] for the components c0 + j < end (the values come from the
   // evaluator, which also decides did_succeed)
   void* out_der;

@@ -313,23 +313,15 @@ template <int O> DI float xor_lane(float x, int lane) {
   return __builtin_bit_cast(float, xor_lane_u32<O>(__builtin_bit_cast(uint32_t, x), lane));
 }
 
-// WB (round 6): row blocks per workgroup, > 1 only for value-only loss passes whose tile spans exactly
-// the WB blocks (64 R = WB rb_rows): a lane's rows r of the tile belong to block r / (R / WB), and every
-// block keeps its own loss sum and check statistic, folded in the order of the one-block kernel (rows
-// ascending per lane, operators in program order, the block's rows inner), so each block's record has
-// the bits it has when a workgroup evaluates that block alone -- with one bytecode dispatch for WB blocks
-template <typename T, int KT, int K, int GM, bool XLDS, int R, int WB>
+template <typename T, int KT, int K, int GM, bool XLDS, int R>
 __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
-  static_assert(WB == 1 || (KT == 0 && GM == GMODE_LOSS && R % WB == 0), "multi-block tiles: value-only loss passes");
   constexpr int CW = GM == GMODE_LOSS ? 2 : 4;  // ints per chunk record
-  constexpr int RPB = R / WB;                   // a lane's rows of the tile in each block
   const int lane = threadIdx.x & 63;
-  const int rb = (int)blockIdx.x * WB + p.block0;  // the workgroup's first row block
+  const int rb = blockIdx.x + p.block0;
   const int64_t row_base = (int64_t)rb * p.rb_rows;
-  const int rbr = p.rb_rows * WB;  // the workgroup's rows
-  const int ntiles = rbr / (64 * R);
-  // valid rows of this workgroup, relative: the row tests below are 32-bit (scalar for the tile test)
-  const int nrel = __builtin_amdgcn_readfirstlane((int)min<int64_t>(max<int64_t>(p.nvalid - row_base, 0), (int64_t)rbr));
+  const int ntiles = p.rb_rows / (64 * R);
+  // valid rows of this block, block-relative: the row tests below are 32-bit (scalar for the tile test)
+  const int nrel = __builtin_amdgcn_readfirstlane((int)min<int64_t>(max<int64_t>(p.nvalid - row_base, 0), (int64_t)p.rb_rows));
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int group_base = blockIdx.y * p.chunks_per_group;
   const int group_n = min(p.chunks_per_group, p.nchunks - group_base);
@@ -338,6 +330,7 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   const T* W = reinterpret_cast<const T*>(p.w);
   extern __shared__ __attribute__((aligned(16))) unsigned char grad_lds[];
   T* xs = reinterpret_cast<T*>(grad_lds);
+  const int rbr = p.rb_rows;
   // chunks are claimed dynamically from an LDS counter (wave w starts with chunk w): the host orders
   // each group's chunks by descending cost, so the waves of a workgroup finish within about one cheap
   // chunk of each other (a static round-robin left the cost spread idle at every workgroup's end);
@@ -396,14 +389,10 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
       }
     }
     const int pc0 = __builtin_amdgcn_readfirstlane(p.prog_off[tree]);
-    double lacc[WB];
-    double gacc[WB][KT > 0 ? KT : 1];
-    T Mb[WB];
-    UNR for (int w = 0; w < WB; ++w) {
-      lacc[w] = 0.0;
-      UNR for (int j = 0; j < KT; ++j) gacc[w][j] = 0.0;
-      Mb[w] = T(0);
-    }
+    double lacc = 0.0;
+    double gacc[KT > 0 ? KT : 1];
+    UNR for (int j = 0; j < KT; ++j) gacc[j] = 0.0;
+    T M = T(0);
     for (int tile = 0; tile < ntiles; ++tile) {
       const int tb = tile * 64 * R;  // block-relative first row of the tile
       if (tb >= nrel) break;
@@ -425,7 +414,7 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
             if (opnd >= p.nfeat) {
               // a derived column: the operator's output (its check fold), and its tangents f'(x) * 0
               // (+-0, or NaN where f' is not finite) from the tangent-zero column
-              RR(chk_fold(Mb[r / RPB], A[r].v);)
+              RR(chk_fold(M, A[r].v);)
               if constexpr (KT > 0) {
                 RR(const T z = Xg[(int64_t)(opnd + p.gd_nd) * p.ld + row_base + rr];
                    UNR for (int j = 0; j < KT; ++j) A[r].d[j] = z;)
@@ -454,7 +443,7 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
 // value per lane -- row 0 evaluated, copied to the others with their check folds)
 #define GK_UNI_ROWS()                                                                              \
   UNR for (int r = 1; r < R; ++r) A[r] = A[0];                                                     \
-  UNR for (int r = 0; r < R; ++r) chk_fold(Mb[r / RPB], A[r].v);
+  UNR for (int r = 0; r < R; ++r) chk_fold(M, A[r].v);
 #if SRHIP_GRAD_SUPER_LEVEL >= 2
 #define GK_LEAFLEAF(NAME)                                                                          \
   /* leaf-leaf forms (round 6): X[a] op X[imm], X[a] op c, c op X[a] -- c's index in the upper half */ \
@@ -462,17 +451,17 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
     const int f2 = (int)(ins.imm & 0xffff);                                                        \
     RR(Dual<T, KT> o; set_feat<GM>(A[r], xat(opnd, rr), opnd - c0); set_feat<GM>(o, xat(f2, rr), f2 - c0); \
        T f, fl, fr; dual_spec<T, SB_##NAME>(A[r].v, o.v, f, fl, fr); combine(A[r], A[r], o, f, fl, fr); \
-       chk_fold(Mb[r / RPB], A[r].v);) break; }                                                              \
+       chk_fold(M, A[r].v);) break; }                                                              \
   case h_spec(SB_##NAME, SPEC_FC): {                                                               \
     const int ci = (int)(ins.a >> 16) - c0;                                                        \
     RR(Dual<T, KT> o; set_feat<GM>(A[r], xat(opnd, rr), opnd - c0); set_const<GM>(o, imm, ci);     \
        T f, fl, fr; dual_spec<T, SB_##NAME>(A[r].v, o.v, f, fl, fr); combine(A[r], A[r], o, f, fl, fr); \
-       chk_fold(Mb[r / RPB], A[r].v);) break; }                                                              \
+       chk_fold(M, A[r].v);) break; }                                                              \
   case h_spec(SB_##NAME, SPEC_CF): {                                                               \
     const int ci = (int)(ins.a >> 16) - c0;                                                        \
     RR(Dual<T, KT> o; set_feat<GM>(A[r], xat(opnd, rr), opnd - c0); set_const<GM>(o, imm, ci);     \
        T f, fl, fr; dual_spec<T, SB_##NAME>(o.v, A[r].v, f, fl, fr); combine(A[r], o, A[r], f, fl, fr); \
-       chk_fold(Mb[r / RPB], A[r].v);) break; }
+       chk_fold(M, A[r].v);) break; }
 #else
 #define GK_LEAFLEAF(NAME)
 #endif
@@ -481,11 +470,11 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
   case h_spec(SB_##NAME, SPEC_AF): {                                                               \
     RR(Dual<T, KT> o; set_feat<GM>(o, xat(opnd, rr), opnd - c0);                                   \
        T f, fl, fr; dual_spec<T, SB_##NAME>(A[r].v, o.v, f, fl, fr); combine(A[r], A[r], o, f, fl, fr); \
-       chk_fold(Mb[r / RPB], A[r].v);) break; }                                                              \
+       chk_fold(M, A[r].v);) break; }                                                              \
   case h_spec(SB_##NAME, SPEC_FA): {                                                               \
     RR(Dual<T, KT> o; set_feat<GM>(o, xat(opnd, rr), opnd - c0);                                   \
        T f, fl, fr; dual_spec<T, SB_##NAME>(o.v, A[r].v, f, fl, fr); combine(A[r], o, A[r], f, fl, fr); \
-       chk_fold(Mb[r / RPB], A[r].v);) break; }                                                              \
+       chk_fold(M, A[r].v);) break; }                                                              \
   case h_spec(SB_##NAME, SPEC_AC): {                                                               \
     const int ci = (opnd & ~(int)UN_UNIFORM_FLAG) - c0;                                            \
     if (R > 1 && (ins.a & UN_UNIFORM_FLAG)) {                                                      \
@@ -495,7 +484,7 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
     }                                                                                              \
     RR(Dual<T, KT> o; set_const<GM>(o, imm, ci);                                                   \
        T f, fl, fr; dual_spec<T, SB_##NAME>(A[r].v, o.v, f, fl, fr); combine(A[r], A[r], o, f, fl, fr); \
-       chk_fold(Mb[r / RPB], A[r].v);) break; }                                                              \
+       chk_fold(M, A[r].v);) break; }                                                              \
   case h_spec(SB_##NAME, SPEC_CA): {                                                               \
     const int ci = (opnd & ~(int)UN_UNIFORM_FLAG) - c0;                                            \
     if (R > 1 && (ins.a & UN_UNIFORM_FLAG)) {                                                      \
@@ -505,31 +494,31 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
     }                                                                                              \
     RR(Dual<T, KT> o; set_const<GM>(o, imm, ci);                                                   \
        T f, fl, fr; dual_spec<T, SB_##NAME>(o.v, A[r].v, f, fl, fr); combine(A[r], o, A[r], f, fl, fr); \
-       chk_fold(Mb[r / RPB], A[r].v);) break; }                                                              \
+       chk_fold(M, A[r].v);) break; }                                                              \
   GK_CASES(h_spec(SB_##NAME, SPEC_SA0), {                                                          \
     if (R > 1 && (ins.a & UN_UNIFORM_FLAG)) {                                                      \
       T f, fl, fr; dual_spec<T, SB_##NAME>(S[k][0].v, A[0].v, f, fl, fr);                          \
       combine(A[0], S[k][0], A[0], f, fl, fr); GK_UNI_ROWS() break;                                \
     }                                                                                              \
     RR(T f, fl, fr; dual_spec<T, SB_##NAME>(S[k][r].v, A[r].v, f, fl, fr);                         \
-       combine(A[r], S[k][r], A[r], f, fl, fr); chk_fold(Mb[r / RPB], A[r].v);) })                           \
+       combine(A[r], S[k][r], A[r], f, fl, fr); chk_fold(M, A[r].v);) })                           \
   GK_CASES(h_spec(SB_##NAME, SPEC_AS0), {                                                          \
     if (R > 1 && (ins.a & UN_UNIFORM_FLAG)) {                                                      \
       T f, fl, fr; dual_spec<T, SB_##NAME>(A[0].v, S[k][0].v, f, fl, fr);                          \
       combine(A[0], A[0], S[k][0], f, fl, fr); GK_UNI_ROWS() break;                                \
     }                                                                                              \
     RR(T f, fl, fr; dual_spec<T, SB_##NAME>(A[r].v, S[k][r].v, f, fl, fr);                         \
-       combine(A[r], A[r], S[k][r], f, fl, fr); chk_fold(Mb[r / RPB], A[r].v);) })
+       combine(A[r], A[r], S[k][r], f, fl, fr); chk_fold(M, A[r].v);) })
           SRHIP_SPEC_BINOPS(GK_SPEC)
 #undef GK_SPEC
 #undef GK_LEAFLEAF
 #define GK_HEAVY(NAME, FN)                                                                         \
   GK_CASES(h_heavy(HB_##NAME, HEAVY_SA0), {                                                        \
     RR(const typename V4<T>::type q = dual_heavy<T, HB_##NAME, (KT > 0)>(S[k][r].v, A[r].v);                 \
-       combine(A[r], S[k][r], A[r], q[0], q[1], q[2]); chk_fold(Mb[r / RPB], A[r].v);) })                    \
+       combine(A[r], S[k][r], A[r], q[0], q[1], q[2]); chk_fold(M, A[r].v);) })                    \
   GK_CASES(h_heavy(HB_##NAME, HEAVY_AS0), {                                                        \
     RR(const typename V4<T>::type q = dual_heavy<T, HB_##NAME, (KT > 0)>(A[r].v, S[k][r].v);                 \
-       combine(A[r], A[r], S[k][r], q[0], q[1], q[2]); chk_fold(Mb[r / RPB], A[r].v);) })
+       combine(A[r], A[r], S[k][r], q[0], q[1], q[2]); chk_fold(M, A[r].v);) })
           SRHIP_HEAVY_BINOPS(GK_HEAVY)
 #undef GK_HEAVY
 #define GK_UN(NAME, FN)                                                                            \
@@ -539,7 +528,7 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
       dual_un<T, UN_##NAME, (KT > 0)>(A[0].v, f, df);                                              \
       A[0].v = f;                                                                                  \
       UNR for (int j = 0; j < KT; ++j) A[0].d[j] = df * A[0].d[j];                                 \
-      UNR for (int r = 0; r < R; ++r) { A[r] = A[0]; chk_fold(Mb[r / RPB], A[r].v); }                        \
+      UNR for (int r = 0; r < R; ++r) { A[r] = A[0]; chk_fold(M, A[r].v); }                        \
       break;                                                                                       \
     }                                                                                              \
     if constexpr (KT == 0 && !dun_inline<UN_##NAME>()) {                                           \
@@ -547,14 +536,14 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
       if constexpr (R == 1) xv = A[0].v;                                                           \
       else { UNR for (int r = 0; r < R; ++r) xv[r] = A[r].v; }                                     \
       xv = dual_un_heavy_rows<T, UN_##NAME, R>(xv);                                                \
-      if constexpr (R == 1) { A[0].v = xv; chk_fold(Mb[0], A[0].v); }                                  \
-      else { UNR for (int r = 0; r < R; ++r) { A[r].v = xv[r]; chk_fold(Mb[r / RPB], A[r].v); } }            \
+      if constexpr (R == 1) { A[0].v = xv; chk_fold(M, A[0].v); }                                  \
+      else { UNR for (int r = 0; r < R; ++r) { A[r].v = xv[r]; chk_fold(M, A[r].v); } }            \
       break;                                                                                       \
     }                                                                                              \
     RR(T f, df; dual_un<T, UN_##NAME, (KT > 0)>(A[r].v, f, df);                                              \
        A[r].v = f;                                                                                 \
        UNR for (int j = 0; j < KT; ++j) A[r].d[j] = df * A[r].d[j];                                \
-       chk_fold(Mb[r / RPB], A[r].v);) break; }
+       chk_fold(M, A[r].v);) break; }
           SRHIP_UNOPS(GK_UN)
 #undef GK_UN
 #undef GK_CASES
@@ -594,33 +583,31 @@ __global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
             l = w * l;
             dl = w * dl;
           }
-          lacc[r / RPB] += (double)l;
-          UNR for (int j = 0; j < KT; ++j) gacc[r / RPB][j] += (double)(dl * A[r].d[j]);
+          lacc += (double)l;
+          UNR for (int j = 0; j < KT; ++j) gacc[j] += (double)(dl * A[r].d[j]);
         }
       }
     }
     if constexpr (GM != GMODE_LOSS) continue;
     // wave reductions, one slab entry per (chunk, row block)
-    UNR for (int w = 0; w < WB; ++w) {
-      auto level = [&](auto oc) {
-        constexpr int O = decltype(oc)::value;
-        lacc[w] += xor_lane<O>(lacc[w], lane);
-        UNR for (int j = 0; j < KT; ++j) gacc[w][j] += xor_lane<O>(gacc[w][j], lane);
-        if constexpr (sizeof(T) == 4) Mb[w] = __builtin_elementwise_maximum(Mb[w], xor_lane<O>(Mb[w], lane));
-        else Mb[w] += xor_lane<O>(Mb[w], lane);
-      };
-      level(std::integral_constant<int, 32>());
-      level(std::integral_constant<int, 16>());
-      level(std::integral_constant<int, 8>());
-      level(std::integral_constant<int, 4>());
-      level(std::integral_constant<int, 2>());
-      level(std::integral_constant<int, 1>());
-      if (lane == 0 && (WB == 1 || rb + w < p.nrb)) {
-        double* out = p.slab + ((int64_t)chunk * p.nrb + rb + w) * (KT + 2);
-        out[0] = lacc[w];
-        UNR for (int j = 0; j < KT; ++j) out[1 + j] = gacc[w][j];
-        out[KT + 1] = (double)Mb[w];
-      }
+    auto level = [&](auto oc) {
+      constexpr int O = decltype(oc)::value;
+      lacc += xor_lane<O>(lacc, lane);
+      UNR for (int j = 0; j < KT; ++j) gacc[j] += xor_lane<O>(gacc[j], lane);
+      if constexpr (sizeof(T) == 4) M = __builtin_elementwise_maximum(M, xor_lane<O>(M, lane));
+      else M += xor_lane<O>(M, lane);
+    };
+    level(std::integral_constant<int, 32>());
+    level(std::integral_constant<int, 16>());
+    level(std::integral_constant<int, 8>());
+    level(std::integral_constant<int, 4>());
+    level(std::integral_constant<int, 2>());
+    level(std::integral_constant<int, 1>());
+    if (lane == 0) {
+      double* out = p.slab + ((int64_t)chunk * p.nrb + rb) * (KT + 2);
+      out[0] = lacc;
+      UNR for (int j = 0; j < KT; ++j) out[1 + j] = gacc[j];
+      out[KT + 1] = (double)M;
     }
   }
 }
@@ -676,26 +663,10 @@ static hipError_t launch_grad_t(const GradArgs& a, dim3 grid, hipStream_t s) {
   constexpr int R = grad_rows<KT, K>();
   if (a.rb_rows % (64 * R)) return hipErrorInvalidValue;
   const size_t lds = grad_lds_bytes<T>(a);
-  if constexpr (KT == 0 && GM == GMODE_LOSS && K <= 4) {
-    // two blocks per workgroup: the tile must span exactly both blocks (rb_rows = 64 R), the grid must
-    // start at block 0 unscreened, and the rows the last workgroup reads must lie inside the view
-    const unsigned gx = (grid.x + 1) / 2;
-    // (GradArgs::wb_min, srhip_optim.cpp: SRHIP_GRAD_WB_MIN chunks, default 16 -- a launch of a few trees
-    // keeps one block per workgroup, twice the workgroups for a latency-bound launch)
-    if (a.wb_min >= 0 && a.nchunks >= a.wb_min && a.rb_rows == 64 * R && a.block0 == 0 && !a.screened &&
-        (int64_t)gx * 2 * a.rb_rows <= a.ld && (int)grid.x == a.nrb) {
-      const dim3 g2(gx, grid.y);
-      if (2 * lds <= GRAD_LDS_MAX)
-        hipLaunchKernelGGL((grad_kernel<T, KT, K, GM, true, 2 * R, 2>), g2, dim3(64 * GRAD_WAVES), 2 * lds, s, a);
-      else
-        hipLaunchKernelGGL((grad_kernel<T, KT, K, GM, false, 2 * R, 2>), g2, dim3(64 * GRAD_WAVES), 0, s, a);
-      return hipGetLastError();
-    }
-  }
   if (lds <= GRAD_LDS_MAX)
-    hipLaunchKernelGGL((grad_kernel<T, KT, K, GM, true, R, 1>), grid, dim3(64 * GRAD_WAVES), lds, s, a);
+    hipLaunchKernelGGL((grad_kernel<T, KT, K, GM, true, R>), grid, dim3(64 * GRAD_WAVES), lds, s, a);
   else
-    hipLaunchKernelGGL((grad_kernel<T, KT, K, GM, false, R, 1>), grid, dim3(64 * GRAD_WAVES), 0, s, a);
+    hipLaunchKernelGGL((grad_kernel<T, KT, K, GM, false, R>), grid, dim3(64 * GRAD_WAVES), 0, s, a);
   return hipGetLastError();
 }
 

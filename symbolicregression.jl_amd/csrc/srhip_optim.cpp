@@ -331,8 +331,6 @@ static int eval_grad_items(srhip_ctx* ctx, const srhip_dataset* ds, srhip_progra
     a.loss_p0 = loss->p0;
     a.weighted = weighted ? 1 : 0;
     a.max_steps = P->gmax_len;
-    // value-only passes of >= SRHIP_GRAD_WB_MIN chunks: two row blocks per workgroup (the same records)
-    a.wb_min = env_int_opt("SRHIP_GRAD_WB_MIN", 16);
     if (first && timed) HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));  // srhip_last_kernel_ms: the gradient kernels
     first = false;
     // value-only screening (SRHIP_GRAD_SCREEN = the fewest value-only chunks screened; default 0 =

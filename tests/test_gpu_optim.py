@@ -506,44 +506,6 @@ def _bits_equal(u, v):
     return np.array_equal(u, v)
 
 
-
-@pytest.mark.parametrize("dtype", [np.float32, np.float64])
-@pytest.mark.parametrize("n", [3000, 2800])
-def test_two_block_value_passes_are_exact(ctx, dtype, n, monkeypatch):
-    """Value-only passes with two 256-row blocks per workgroup (SRHIP_GRAD_WB_MIN=0; -1: one block)
-    write every block's record with the bits of the one-block kernel: losses and did_succeed of value-only
-    passes are bitwise equal, unweighted and weighted, L2 and L1, for an even (12) and an odd (11)
-    block count, equal to the gradient pass's losses, and an optimize_constants run ends identically."""
-    sr = _sr()
-    opts, _, nodes, offs, X, y = _problem(sr, dtype, ntrees=48, n=n, max_size=24)
-    w = np.random.default_rng(3).uniform(0.5, 2.0, n).astype(dtype)
-    for ds in (sr.DeviceDataset(ctx, X, y), sr.DeviceDataset(ctx, X, y, w)):
-        for loss in (sr.L2DistLoss(), sr.L1DistLoss()):
-            res = {}
-            for wb in ("-1", "0"):
-                monkeypatch.setenv("SRHIP_GRAD_WB_MIN", wb)
-                prog = sr.Program(ctx, nodes, offs, opts, dtype)
-                monkeypatch.setenv("SRHIP_GRAD_VALUE_ONLY", "1")
-                vl, _, vok = prog.eval_loss_grad(ds, loss)
-                monkeypatch.delenv("SRHIP_GRAD_VALUE_ONLY")
-                gl, _, gok = prog.eval_loss_grad(ds, loss)
-                res[wb] = (np.asarray(vl, np.float64), np.asarray(vok), np.asarray(gl, np.float64), np.asarray(gok))
-                prog.close()
-            assert res["0"][1].sum() > 20
-            for u, v in zip(res["-1"], res["0"]):
-                assert _bits_equal(u, v)
-            assert _bits_equal(res["0"][0], res["0"][2]) and _bits_equal(res["0"][1], res["0"][3])
-    ds = sr.DeviceDataset(ctx, X, y)
-    res = {}
-    for wb in ("-1", "0"):
-        monkeypatch.setenv("SRHIP_GRAD_WB_MIN", wb)
-        prog = sr.Program(ctx, nodes, offs, opts, dtype)
-        out, imp, fc = prog.optimize_constants(ds, sr.L2DistLoss(), iterations=8, nrestarts=1, seed=3)
-        res[wb] = (np.asarray(out, np.float64), np.asarray(imp), np.asarray(fc), np.concatenate(prog.get_constants()))
-        prog.close()
-    for u, v in zip(res["-1"], res["0"]):
-        assert _bits_equal(u, v)
-
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_value_only_screening_is_exact(ctx, dtype, monkeypatch):
     """Value-only passes evaluate row block 0 of every chunk first (a launch of its own) and skip the
