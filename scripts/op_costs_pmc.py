@@ -7,6 +7,7 @@ import collections
 import csv
 import glob
 import json
+import re
 import sys
 
 root, order_path = sys.argv[1], sys.argv[2]
@@ -23,10 +24,11 @@ for f in sorted(glob.glob(f"{root}/**/*counter_collection.csv", recursive=True))
         disp[d][row["Counter_Name"]] = disp[d].get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
     ev, acc = 0, collections.defaultdict(float)
     for d in sorted(disp):
-        if "eval_kernel" in names[d]:
+        m = re.search(r"eval_kernel<\w+, \d+, \d+, (\d+)", names[d])
+        if m and m.group(1) != "2":  # the interpreter's loss launches (MODE 2: the precise pass, after the reduction)
             for k, v in disp[d].items():
                 acc[k] += v
-        elif "reduce_kernel" in names[d] and acc:
+        elif re.search(r"(^|[^_])reduce_kernel<", names[d]) and acc:  # the loss reduction (not precise_reduce_kernel)
             if ev < len(order):
                 per_shape[order[ev]].update(acc)  # later repetitions overwrite earlier ones
             ev += 1

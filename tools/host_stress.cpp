@@ -29,6 +29,17 @@
 
 #include "../include/srhip.h"
 
+#if defined(__has_feature)
+#if __has_feature(address_sanitizer)
+#define SRHIP_STRESS_ASAN 1
+#include <sanitizer/lsan_interface.h>
+#include <unistd.h>
+#endif
+#endif
+#ifndef SRHIP_STRESS_ASAN
+#define SRHIP_STRESS_ASAN 0
+#endif
+
 static std::atomic<int> g_fail{0};
 #define CHECK(expr)                                                                           \
   do {                                                                                        \
@@ -238,5 +249,14 @@ int main(int argc, char** argv) {
          g_fail ? "FAILED" : "ok", threads, rounds, (long long)hits, (long long)misses, (long long)inserts,
          dev ? "run" : "skipped (no device)");
   fflush(stdout);  // (LeakSanitizer's report at exit ends the process with _exit: unflushed output is lost)
+#if SRHIP_STRESS_ASAN
+  // the leak check now, then leave without the runtime's static destructors: after a device phase the
+  // HIP runtime's teardown frees memory through ASan's device allocator after it has unloaded, and
+  // ASan's own CHECK aborts the process there (sanitizer_allocator_device.h, "dev_runtime_unloaded_")
+  // -- not a finding in this code; the leak check above still reports any leak and fails the run
+  __lsan_do_leak_check();
+  fflush(stderr);
+  _exit(g_fail ? 1 : 0);
+#endif
   return g_fail ? 1 : 0;
 }
