@@ -68,6 +68,9 @@ __global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab
   }
   if (lane == 0) {
     const int tree = order[slot];
+    if constexpr (CHK_MAX && sizeof(CT) == 4) {
+      if (ul.sbound) m = skip_bound_apply(m, ul.sbound + 4 * (int64_t)tree, ul.fbound);
+    }
     if (out_loss) out_loss[tree] = s;
     // chk_inf (row shards): a non-finite statistic is stored as +Inf, which RCCL's MAX / SUM across the
     // shards keep (a max that drops NaN operands would lose a failed shard)
@@ -169,21 +172,27 @@ __global__ __launch_bounds__(256) void feature_stats_kernel(const T* __restrict_
   const int f = blockIdx.y, b = blockIdx.x, nb = gridDim.x;
   const T* col = X + (int64_t)f * ld;
   const int64_t lo = (int64_t)b * chunk, hi = min(m, lo + chunk);
-  double s = 0.0;
+  double s = 0.0, mx = 0.0;
   unsigned long long bad = 0;
   for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     const T v = col[i];
-    if (!m_isfinite(v)) bad++;
-    else s += sizeof(T) == 8 ? (double)v * 0x1p-64 : (double)v;
+    if (!m_isfinite(v)) {
+      bad++;
+    } else {
+      s += sizeof(T) == 8 ? (double)v * 0x1p-64 : (double)v;
+      mx = fmax(mx, fabs((double)v));
+    }
   }
-  __shared__ double ss[256];
+  __shared__ double ss[256], sm[256];
   __shared__ unsigned long long sb[256];
   ss[threadIdx.x] = s;
+  sm[threadIdx.x] = mx;
   sb[threadIdx.x] = bad;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) {
       ss[threadIdx.x] += ss[threadIdx.x + o];
+      sm[threadIdx.x] = fmax(sm[threadIdx.x], sm[threadIdx.x + o]);
       sb[threadIdx.x] += sb[threadIdx.x + o];
     }
     __syncthreads();
@@ -191,19 +200,22 @@ __global__ __launch_bounds__(256) void feature_stats_kernel(const T* __restrict_
   if (threadIdx.x == 0) {
     part[(int64_t)f * nb + b].sum = ss[0];
     part[(int64_t)f * nb + b].nonfinite = (long long)sb[0];
+    part[(int64_t)f * nb + b].maxabs = sm[0];
   }
 }
 __global__ void feature_stats_final(const FeatStat* __restrict__ part, int nb, int nfeat, FeatStat* __restrict__ out) {
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= nfeat) return;
-  double s = 0.0;
+  double s = 0.0, mx = 0.0;
   long long bad = 0;
   for (int b = 0; b < nb; ++b) {
     s += part[(int64_t)f * nb + b].sum;
     bad += part[(int64_t)f * nb + b].nonfinite;
+    mx = fmax(mx, part[(int64_t)f * nb + b].maxabs);
   }
   out[f].sum = s;
   out[f].nonfinite = bad;
+  out[f].maxabs = mx;
 }
 
 // ------------------------------------------------------------------------------------------------

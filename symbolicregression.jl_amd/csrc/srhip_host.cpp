@@ -172,6 +172,7 @@ template <typename T> class TreeCompiler {
     tally(0, info);
     // host-decided checks (reference semantics, see header comment)
     static_checks(0, -1, info);
+    if (std::is_same<T, float>::value && !grad_ && !info.static_fail) skip_bounds(info);
     rc = emit_program(info, code);
     if (rc || !dinfo) return rc;
     if (!grad_ && !reads_derived(dspec)) {
@@ -340,6 +341,65 @@ template <typename T> class TreeCompiler {
     else c = is_const(n.l) && is_const(n.r);
     memo_const_[i] = c;
     return c;
+  }
+  // Float32 evaluation programs fold no check statistic for + and - (srhip_eval_impl.h bin_rows_chk).
+  // skip_bounds sets info.sb = (cM, cF, c0) with every +/- output of the tree within cM M + cF F + c0,
+  // M the tree's statistic of the folded values and F the features' max |x|: a folded operator output
+  // is within M (a division the in-range path leaves unfolded is within 2^80: + 2^80), a cos / sin
+  // within 1, a feature within F, a constant (subtree) its |value|, and a +/- within the sum of its
+  // operands' bounds -- the kernel raises the statistic to that bound, which only ever moves a tree
+  // from decided to undecided (the precise pass then decides it exactly); never rounded down
+  struct SkipB {
+    double m = 0.0, f = 0.0, k = 0.0;
+  };
+  SkipB skip_bound(int64_t i, SkipB& mx) {
+    SkipB b;
+    const srhip_node& n = nd_[i];
+    if (is_const(i)) {
+      T v{};
+      if (n.degree == 0) v = HostVal<T>::from(n.val);
+      else eval_const(i, &v);
+      const double a = fabs((double)v);
+      b.k = a == a && a < INFINITY ? a : INFINITY;
+      return b;
+    }
+    if (n.degree == 0) {
+      b.f = 1.0;
+      return b;
+    }
+    if (n.degree == 1) {
+      (void)skip_bound(n.l, mx);
+      const int u = classify_unop(unaop(i));
+      if (u == UN_COS || u == UN_SIN) b.k = 1.0;
+      else b.m = 1.0;
+      return b;
+    }
+    const SkipB l = skip_bound(n.l, mx), r = skip_bound(n.r, mx);
+    int sb, hb;
+    classify_binop(binop(i), &sb, &hb);
+    if (sb == SB_ADD || sb == SB_SUB) {
+      b.m = l.m + r.m;
+      b.f = l.f + r.f;
+      b.k = l.k + r.k;
+      mx.m = std::max(mx.m, b.m);
+      mx.f = std::max(mx.f, b.f);
+      mx.k = std::max(mx.k, b.k);
+      return b;
+    }
+    b.m = 1.0;
+    if (sb == SB_DIV) b.k = 0x1p80;
+    return b;
+  }
+  static float round_up_f(double x) {
+    const float f = (float)x;
+    return (double)f >= x ? f : std::nextafter(f, INFINITY);
+  }
+  void skip_bounds(TreeInfo& info) {
+    SkipB mx;
+    (void)skip_bound(0, mx);
+    info.sb[0] = round_up_f(mx.m);
+    info.sb[1] = round_up_f(mx.f);
+    info.sb[2] = round_up_f(mx.k);
   }
   bool is_leaf(int64_t i) const { return nd_[i].degree == 0; }
   bool leafish(int64_t i) { return is_leaf(i) || (!grad_ && is_const(i)) || dcol(i) >= 0; }
@@ -1004,6 +1064,7 @@ int compile_program_t(srhip_program& P) {
   P.dprog_off.assign(n, 0);
   P.dcost.assign(n, 0.0);
   P.dec.assign(n, TreeDecide());
+  P.sbound.clear();
   P.dkmax = P.dmax_len = 0;
   // operator-node count and the largest feature index, from the node tables
   P.maxfeat = 0;
@@ -1091,6 +1152,7 @@ int compile_program_t(srhip_program& P) {
     P.max_len = std::max(P.max_len, P.info[t].code_len);
     P.total_nodes += P.info[t].nnodes;
     P.dec[t] = make_decide(P.info[t]);
+    if (std::is_same<T, float>::value) P.sbound.insert(P.sbound.end(), {P.info[t].sb[0], P.info[t].sb[1], P.info[t].sb[2], 0.0f});
     if (der) {
       const TreeInfo& ti = dinfo[t];
       P.dprog_off[t] = ti.code_begin;
@@ -1487,6 +1549,7 @@ static void set_prog_pointers(const srhip_program& P) {
   P.doff_dev = der ? (const int32_t*)(d + P.blob_off[2]) : nullptr;
   P.dspec_dev = der ? (const uint32_t*)(d + P.blob_off[3]) : nullptr;
   P.dmask_dev = der ? (const uint64_t*)(d + P.blob_off[4]) : nullptr;
+  P.sbound_dev = P.sbound.empty() ? nullptr : (const float*)(d + P.blob_off[5]);
 }
 
 int srhip::upload_program(srhip_program& P, bool sync, bool defer, hipStream_t stream) {
@@ -1499,7 +1562,9 @@ int srhip::upload_program(srhip_program& P, bool sync, bool defer, hipStream_t s
   const size_t n_dcode = der ? P.dcode.size() * sizeof(Ins) : 0, n_doff = der ? P.dprog_off.size() * sizeof(int32_t) : 0;
   const size_t n_dspec = der ? P.dspec.size() * sizeof(uint32_t) : 0, n_dmask = der ? P.dmask.size() * sizeof(uint64_t) : 0;
   const size_t o_off = al(n_code), o_dcode = o_off + al(n_off), o_doff = o_dcode + al(n_dcode);
-  const size_t o_dspec = o_doff + al(n_doff), o_dmask = o_dspec + al(n_dspec), total = std::max<size_t>(16, o_dmask + al(n_dmask));
+  const size_t n_sb = P.sbound.size() * sizeof(float);
+  const size_t o_dspec = o_doff + al(n_doff), o_dmask = o_dspec + al(n_dspec), o_sb = o_dmask + al(n_dmask);
+  const size_t total = std::max<size_t>(16, o_sb + al(n_sb));
   P.blob.assign(total, 0);
   uint8_t* h = P.blob.data();
   if (n_code) memcpy(h, P.code.data(), n_code);
@@ -1508,7 +1573,8 @@ int srhip::upload_program(srhip_program& P, bool sync, bool defer, hipStream_t s
   if (n_doff) memcpy(h + o_doff, P.dprog_off.data(), n_doff);
   if (n_dspec) memcpy(h + o_dspec, P.dspec.data(), n_dspec);
   if (n_dmask) memcpy(h + o_dmask, P.dmask.data(), n_dmask);
-  const size_t offs[6] = {o_off, o_dcode, o_doff, o_dspec, o_dmask, total};
+  if (n_sb) memcpy(h + o_sb, P.sbound.data(), n_sb);
+  const size_t offs[7] = {o_off, o_dcode, o_doff, o_dspec, o_dmask, o_sb, total};
   memcpy(P.blob_off, offs, sizeof(offs));
   if (defer) {
     P.upload_pending = true;
@@ -1994,7 +2060,22 @@ struct EvalJob {
   std::vector<int32_t> live;
   UndecidedList ul;
   DevBuf pred;  // MODE_PRED's device output (synchronous calls only)
+  bool fused = false;  // single-block launch: the interpreter wrote the records (no reduction)
+  float fbound = 0.0f;  // Float32: the features' max |x| (the +/- bound's F)
 };
+// the features' max |x| over a view's rows (+Inf if any entry is non-finite), rounded up to Float32:
+// the F of the Float32 interpreter's +/- bound (EvalArgs::fbound)
+static float feature_bound(const View& v, int64_t nfeat) {
+  double F = 0.0;
+  for (int64_t f = 0; v.stats && f < nfeat; ++f) {
+    if (v.stats[f].nonfinite > 0 || !(v.stats[f].maxabs < INFINITY)) return INFINITY;
+    F = std::max(F, v.stats[f].maxabs);
+  }
+  if (!v.stats && nfeat > 0) return INFINITY;
+  const float r = (float)F;
+  return (double)r >= F ? r : std::nextafter(r, INFINITY);
+}
+
 static int eval_issue(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_program* P, int mode, const srhip_loss* loss,
                       const View& v, void* out_pred, double* sums, double* chk, DevPrecise* dp, ShardDev* sd,
                       EvalJob& J) {
@@ -2124,7 +2205,7 @@ static int eval_issue(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_progr
       order = make_order(*P, live, goff, use_d);
       order.insert(order.end(), goff.begin(), goff.end());  // the group offsets follow the order
       if (P->upload_pending) {  // deferred program upload: program and order in one copy
-        const size_t base = P->blob_off[5], bytes = order.size() * sizeof(int32_t);
+        const size_t base = P->blob_off[6], bytes = order.size() * sizeof(int32_t);
         P->blob.resize(base + bytes);
         memcpy(P->blob.data() + base, order.data(), bytes);
         HIP_TRY(P->d_prog.ensure(base + bytes));
@@ -2161,6 +2242,12 @@ static int eval_issue(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_progr
   a.nd = use_d ? nd : 0;
   a.dspec = use_d ? P->dspec_dev : nullptr;
   a.dmask = use_d ? P->dmask_dev : nullptr;
+  if (dtype == SRHIP_F32) {
+    // (every Float32 program carries its trees' +/- bounds: the interpreter folds no +/-)
+    if (!P->sbound_dev || P->sbound.size() != 4 * (size_t)P->ntrees)
+      return fail(SRHIP_ERR_INVALID, "Float32 program without its +/- bounds");
+    J.fbound = feature_bound(v, ds->nfeat);
+  }
   a.X = v.X;
   a.y = v.y;
   a.w = weighted ? v.w : nullptr;
@@ -2333,6 +2420,11 @@ static int eval_issue(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_progr
     ul.rows = (double)v.m;
     ul_groups = std::min(ul.umax, std::max(4, P->und_hint + 2));
   }
+  J.fused = a.fused != 0;
+  if (dtype == SRHIP_F32) {  // the reduction raises each tree's statistic to its +/- bound
+    ul.sbound = P->sbound_dev;
+    ul.fbound = J.fbound;
+  }
   if (!a.fused)
     HIP_TRY(launch_reduce(dtype, mode == MODE_LOSS ? ctx->slab_loss.p : nullptr, nch, cpb,
                           dtype == SRHIP_I32 ? nullptr : ctx->slab_chk.p, L.nrb, nl, (const int32_t*)d_order,
@@ -2389,8 +2481,13 @@ static int eval_collect(srhip_ctx* ctx, const srhip_program* P, const View& v, d
     if (sd) break;  // the shard's loss sums and statistics are in the exchange's device buffer
     if (mode == MODE_LOSS)
       sums[2 * (size_t)t] = dtype == SRHIP_I32 ? (double)((const long long*)r_loss.data())[t] : ((const double*)r_loss.data())[t];
-    if (dtype == SRHIP_F32) chk[t] = ((const float*)r_chk.data())[t];
-    else if (dtype == SRHIP_F64) chk[t] = ((const double*)r_chk.data())[t];
+    if (dtype == SRHIP_F32) {
+      const float m = ((const float*)r_chk.data())[t];
+      // a single-block launch's records come straight from the interpreter: its +/- bound applied here
+      chk[t] = J.fused ? skip_bound_apply(m, P->sbound.data() + 4 * (size_t)t, J.fbound) : m;
+    } else if (dtype == SRHIP_F64) {
+      chk[t] = ((const double*)r_chk.data())[t];
+    }
   }
   if (persistent) {
     // every row block was claimed exactly once: the workgroups' evaluated items add up to the launch's

@@ -156,6 +156,8 @@ struct TreeInfo {
   int32_t nconst = 0, nnodes = 0, nops = 0, need = 0;
   int32_t code_begin = 0, code_len = 0;
   double cost = 0.0;
+  // Float32 evaluation programs: (cM, cF, c0) of the bound on every +/- output (EvalArgs::sbound)
+  float sb[3] = {0.0f, 0.0f, 0.0f};
 };
 
 
@@ -253,14 +255,14 @@ struct srhip_program {
   int64_t total_nodes = 0, total_ops = 0;
   int32_t maxfeat = 0;  // largest feature index any tree reads (the columns a launch stages)
   // device copy of the evaluation program, one buffer and one upload (upload_program):
-  // [code | prog_off | dcode | dprog_off | dspec | dmask], 16-byte aligned sections
+  // [code | prog_off | dcode | dprog_off | dspec | dmask | sbound], 16-byte aligned sections
   // upload_program(P, sync, defer = true) only builds the image: the next evaluation appends its tree
   // order and uploads both with one copy (the coalescer's per-flush program)
   mutable srhip::PoolBuf d_prog;
   mutable std::vector<uint8_t> blob;  // its host image (alive until the next upload)
   mutable bool upload_pending = false;
   mutable int32_t und_hint = 0;  // trees the last device-listed precise pass saw (list capacity hint)
-  mutable size_t blob_off[6] = {0, 0, 0, 0, 0, 0};  // section offsets: off, dcode, doff, dspec, dmask, end
+  mutable size_t blob_off[7] = {0, 0, 0, 0, 0, 0, 0};  // section offsets: off, dcode, doff, dspec, dmask, sbound, end
   mutable const srhip::Ins* code_dev = nullptr;
   mutable const int32_t* off_dev = nullptr;
   // derived-column program (srhip_isa.h): the same trees with U(X[f]) leaves reading LDS columns;
@@ -275,6 +277,9 @@ struct srhip_program {
   mutable const int32_t* doff_dev = nullptr;
   mutable const uint32_t* dspec_dev = nullptr;
   mutable const uint64_t* dmask_dev = nullptr;
+  // Float32 programs: [ntrees][4] (cM, cF, c0, 0) per tree (TreeInfo::sb; EvalArgs::sbound)
+  std::vector<float> sbound;
+  mutable const float* sbound_dev = nullptr;
   // launch schedule cache: the cost-sorted tree order of the last plan (groups, tpg, derived),
   // resident on the device; a program evaluated again with the same plan skips the sort and upload
   mutable std::mutex ord_mu;

@@ -40,6 +40,7 @@ inline int loss_chunk(int dtype) { return dtype == SRHIP_F64 ? LOSS_CHUNK_8B : L
 struct FeatStat {
   double sum;           // f64 sum (Float64 data: sum of x * 2^-64)
   long long nonfinite;  // count of Inf/NaN entries
+  double maxabs;        // max |x| over the finite entries (round 6: the Float32 interpreter's +/- bound)
 };
 // launch_feature_stats splits each column into at most FEAT_STAT_BLOCKS row chunks; its output
 // buffer holds the nfeat results followed by the partials.
@@ -130,7 +131,25 @@ struct UndecidedList {
   int32_t* ulist = nullptr;  // nullptr: no device list (the host decides after the launch)
   int32_t umax = 0;
   double rows = 0.0;
+  // Float32 programs (round 6): + and - fold no check statistic in the interpreter.  Per program tree
+  // (cM, cF, c0, 0) bounds every +/- output by cM M + cF fbound + c0 (M: the statistic of the folded
+  // values, fbound: the features' max |x|, +Inf if any is non-finite; TreeCompiler::skip_bounds); the
+  // reduction raises each tree's statistic to that bound (skip_bound_apply) before it is written or
+  // tested.  nullptr: no bound (Float64, Int32)
+  const float* sbound = nullptr;
+  float fbound = 0.0f;
 };
+// max(M, cM M + cF F + c0) clamped to FLT_MAX for a finite M (a non-finite M stands): a finite bound
+// only ever turns a decided tree into an undecided one -- which the exact precise pass then decides --
+// and never a finite statistic into a failure.  The same function on the host (fused single-block
+// launches) and in the reduction.
+__host__ __device__ inline float skip_bound_apply(float M, const float* sb, float F) {
+  if (!(sb[0] > 0.0f || sb[1] > 0.0f || sb[2] > 0.0f) || !(M - M == 0.0f)) return M;
+  const double fb = sb[1] > 0.0f ? (double)sb[1] * (double)F : 0.0;
+  const double bd = (double)sb[0] * (double)M + (fb + (double)sb[2]);
+  const double mb = bd > (double)M ? bd : (double)M;
+  return mb < (double)__FLT_MAX__ ? (float)mb : __FLT_MAX__;
+}
 hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, int cpb, const void* slab_chk, int nrb, int nslots,
                          const int32_t* order, void* out_loss, void* out_chk, hipStream_t s,
                          const int32_t* slab_rows = nullptr, int64_t* out_rows = nullptr,

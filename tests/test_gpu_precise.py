@@ -103,3 +103,63 @@ def test_compact_decisions_match_tree_info(ctx, oracle, monkeypatch):
     _, _, ook, _ = oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, X, y, None, 0, 0.0)
     assert np.array_equal(ok_fast, np.asarray(ook, bool))
     assert (~ok_fast).sum() >= 3 and ok_fast.sum() > 0
+
+
+def test_unfolded_add_sub_decide_as_the_oracle(ctx, oracle):
+    """Float32 + and - fold no check statistic (round 6): the statistic of each (tree, row block) is
+    raised to the tree's bound on its +/- outputs (cM M + cF F + c0; TreeCompiler::skip_bounds), so a
+    tree is decided ok only when those sums provably stay finite, and otherwise goes to the exact
+    precise pass.  Trees whose +/- arrays overflow per row, overflow only in their column sum, cancel
+    to zero after huge operands (undecided by the bound, ok by the precise pass), feed an overflowing
+    sum into an unchecked cos, or read a feature with a NaN only through + -- through eval_loss,
+    eval_predict and the row-shard partials -- all give the oracle's did_succeed and losses."""
+    sr = _sr()
+    n = 300_000
+    rng = np.random.default_rng(23)
+    X = rng.uniform(-1.0, 1.0, (3, n)).astype(np.float32)
+    y = (X[0] - 0.5 * X[1]).astype(np.float32)
+    opts = sr.Options(binary_operators=("+", "-", "*"), unary_operators=("cos", "exp"))
+    x1, x2, x3 = (sr.Node(feature=i) for i in (1, 2, 3))
+    c = lambda v: sr.Node(val=v)  # noqa: E731
+    add = lambda a, b: sr.Node(1, a, b)  # noqa: E731
+    sub = lambda a, b: sr.Node(2, a, b)  # noqa: E731
+    mul = lambda a, b: sr.Node(3, a, b)  # noqa: E731
+    cos = lambda a: sr.Node(1, a)  # noqa: E731
+    ex = lambda a: sr.Node(2, a)  # noqa: E731
+    trees = [
+        add(mul(x1, c(1.5e38)), mul(x2, c(1.5e38))),         # rows finite, the column sum overflows
+        sub(mul(x1, c(1.0e35)), mul(x1, c(1.0e35))),         # huge operands, exactly zero: precise -> ok
+        add(mul(x1, c(3.0e38)), mul(x2, c(3.0e38))),         # rows overflow to +-Inf
+        mul(cos(add(mul(x1, c(3.0e38)), mul(x2, c(3.0e38)))), c(2.0)),  # cos of an overflowing sum
+        sub(add(x1, c(0.5)), x2),                            # ordinary
+        add(add(mul(x1, c(1.0e30)), x2), x3),                # large, finite, decided
+        add(ex(mul(x1, c(80.5))), ex(mul(x2, c(80.5)))),     # exp columns just finite, their sum's near the limit
+        add(x3, c(0.5)),                                     # a feature through + only
+        sub(cos(x1), cos(add(x2, x3))),                      # cos of a sum, minus a cos
+    ]
+    trees = trees + sr.random_population(40, opts, 3, np.float32, seed=29, max_size=18)
+    nodes, offs = sr.flatten(trees, opts, np.float32)
+    for nan_row in (None, 12345):
+        Xd = X.copy()
+        if nan_row is not None:
+            Xd[2, nan_row] = np.nan  # x3: the trees reading it through + must fail, exactly
+        ds = sr.DeviceDataset(ctx, Xd, y)
+        prog = sr.Program(ctx, nodes, offs, opts, np.float32)
+        ol, _, ook, _ = oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, Xd, y, None, 0, 0.0)
+        ook = np.asarray(ook, bool)
+        if nan_row is None:
+            assert ook[1] and ook[4] and ook[5] and not ook[2] and not ook[3], ook[:9]
+        else:
+            assert not ook[5] and not ook[7] and not ook[8]
+        for _ in range(2):
+            loss, ok = prog.eval_loss(ds, sr.L2DistLoss())
+            assert np.array_equal(ok, ook), (np.nonzero(ok != ook)[0], nan_row)
+            for t in np.nonzero(ook)[0]:  # (a succeeding tree's loss may itself overflow: Inf on both)
+                assert loss[t] == ol[t] or abs(loss[t] - ol[t]) <= 1e-6 * abs(ol[t]), (t, loss[t], ol[t])
+        _, pok = prog.eval_predict(ds)
+        assert np.array_equal(np.asarray(pok, bool), ook)
+        psums, pchk = prog.eval_loss_partials(ds, sr.L2DistLoss())
+        _, fok, st = prog.finalize(Xd.shape[0], psums, pchk)
+        dec = st != 2  # (undecided trees take the precise pass; decided ones must already agree)
+        assert np.array_equal(np.asarray(fok, bool)[dec], ook[dec]), np.nonzero(dec & (np.asarray(fok, bool) != ook))[0]
+        prog.close()
