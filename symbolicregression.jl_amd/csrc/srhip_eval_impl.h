@@ -860,9 +860,10 @@ __device__ __attribute__((always_inline)) inline void bin_rows_chk(RV<T, R>& A, 
     div_rows<R, SWAP, true, CONSTB>(A, B, M);
   } else {
     bin_rows<T, R, SB, SWAP>(A, B);
-    // Float32 + and - fold nothing (round 6): the reduction raises each tree's statistic to the tree's
-    // bound on their outputs instead (UndecidedList::sbound, srhip_eval.hip skip_bound_apply)
-    if constexpr (!(std::is_same<T, float>::value && (SB == SB_ADD || SB == SB_SUB))) chk_update<R>(M, A);
+    // Float32 + and -, and * by a constant, fold nothing (round 6): the reduction raises each tree's
+    // statistic to the tree's bound on their outputs instead (UndecidedList::sbound, skip_bound_apply)
+    if constexpr (!(std::is_same<T, float>::value && (SB == SB_ADD || SB == SB_SUB || (SB == SB_MUL && CONSTB))))
+      chk_update<R>(M, A);
   }
 }
 template <typename T, int R, int SB, bool SWAP>

@@ -342,12 +342,14 @@ template <typename T> class TreeCompiler {
     memo_const_[i] = c;
     return c;
   }
-  // Float32 evaluation programs fold no check statistic for + and - (srhip_eval_impl.h bin_rows_chk).
-  // skip_bounds sets info.sb = (cM, cF, c0) with every +/- output of the tree within cM M + cF F + c0,
+  // Float32 evaluation programs fold no check statistic for + and -, nor for * by a constant
+  // (srhip_eval_impl.h bin_rows_chk).  skip_bounds sets info.sb = (cM, cF, c0) with every such output
+  // of the tree within cM M + cF F + c0,
   // M the tree's statistic of the folded values and F the features' max |x|: a folded operator output
   // is within M (a division the in-range path leaves unfolded is within 2^80: + 2^80), a cos / sin
-  // within 1, a feature within F, a constant (subtree) its |value|, and a +/- within the sum of its
-  // operands' bounds -- the kernel raises the statistic to that bound, which only ever moves a tree
+  // within 1, a feature within F, a constant (subtree) its |value|, a +/- within the sum of its
+  // operands' bounds and c * x within |c| times x's -- the reduction raises the statistic to that
+  // bound, which only ever moves a tree
   // from decided to undecided (the precise pass then decides it exactly); never rounded down
   struct SkipB {
     double m = 0.0, f = 0.0, k = 0.0;
@@ -381,6 +383,20 @@ template <typename T> class TreeCompiler {
       b.m = l.m + r.m;
       b.f = l.f + r.f;
       b.k = l.k + r.k;
+      mx.m = std::max(mx.m, b.m);
+      mx.f = std::max(mx.f, b.f);
+      mx.k = std::max(mx.k, b.k);
+      return b;
+    }
+    if (sb == SB_MUL && (is_const(n.l) || is_const(n.r))) {
+      // a product with a constant (the AC / CA / FC / CF forms): |c| times the other operand's bound,
+      // never a zero factor -- 0 * Inf is NaN: an operand bound that is infinite (a non-finite feature)
+      // must leave the product's bound infinite
+      const SkipB& o = is_const(n.l) ? r : l;
+      const double a = std::max(is_const(n.l) ? l.k : r.k, 0x1p-126);
+      b.m = a * o.m;
+      b.f = a * o.f;
+      b.k = a * o.k;
       mx.m = std::max(mx.m, b.m);
       mx.f = std::max(mx.f, b.f);
       mx.k = std::max(mx.k, b.k);

@@ -106,7 +106,7 @@ def test_compact_decisions_match_tree_info(ctx, oracle, monkeypatch):
 
 
 def test_unfolded_add_sub_decide_as_the_oracle(ctx, oracle):
-    """Float32 + and - fold no check statistic (round 6): the statistic of each (tree, row block) is
+    """Float32 + and -, and * by a constant, fold no check statistic (round 6): the statistic of each (tree, row block) is
     raised to the tree's bound on its +/- outputs (cM M + cF F + c0; TreeCompiler::skip_bounds), so a
     tree is decided ok only when those sums provably stay finite, and otherwise goes to the exact
     precise pass.  Trees whose +/- arrays overflow per row, overflow only in their column sum, cancel
@@ -136,6 +136,9 @@ def test_unfolded_add_sub_decide_as_the_oracle(ctx, oracle):
         add(ex(mul(x1, c(80.5))), ex(mul(x2, c(80.5)))),     # exp columns just finite, their sum's near the limit
         add(x3, c(0.5)),                                     # a feature through + only
         sub(cos(x1), cos(add(x2, x3))),                      # cos of a sum, minus a cos
+        mul(c(0.0), x3),                                     # * by a constant: 0 * NaN must still fail
+        mul(add(x1, x2), c(2.0e38)),                         # * by a constant overflowing per row
+        cos(mul(x3, c(0.0))),                                # an unchecked cos of 0 * x3
     ]
     trees = trees + sr.random_population(40, opts, 3, np.float32, seed=29, max_size=18)
     nodes, offs = sr.flatten(trees, opts, np.float32)
@@ -150,7 +153,7 @@ def test_unfolded_add_sub_decide_as_the_oracle(ctx, oracle):
         if nan_row is None:
             assert ook[1] and ook[4] and ook[5] and not ook[2] and not ook[3], ook[:9]
         else:
-            assert not ook[5] and not ook[7] and not ook[8]
+            assert not ook[5] and not ook[7] and not ook[8] and not ook[9] and not ook[11]
         for _ in range(2):
             loss, ok = prog.eval_loss(ds, sr.L2DistLoss())
             assert np.array_equal(ok, ook), (np.nonzero(ok != ook)[0], nan_row)
