@@ -166,3 +166,38 @@ def test_unfolded_add_sub_decide_as_the_oracle(ctx, oracle):
         dec = st != 2  # (undecided trees take the precise pass; decided ones must already agree)
         assert np.array_equal(np.asarray(fok, bool)[dec], ook[dec]), np.nonzero(dec & (np.asarray(fok, bool) != ook))[0]
         prog.close()
+
+
+@pytest.mark.parametrize("bad", [False, True])
+def test_random_extreme_constants_decide_as_the_oracle(ctx, oracle, bad):
+    """The static +/- / *c bounds against random trees whose constants span 1e-2 .. 3e38 in magnitude
+    (C2's operators, 600 trees): overflows per row, in column sums, under unchecked cos, through
+    products with tiny and huge constants -- with clean features and with an Inf and a NaN in two of
+    them.  did_succeed equals the oracle's on every tree, in loss and prediction mode."""
+    sr = _sr()
+    opts = sr.Options(binary_operators=("+", "-", "*", "/"), unary_operators=("cos", "exp"))
+    trees = sr.random_population(600, opts, 3, np.float32, seed=31, max_size=20)
+    nodes, offs = sr.flatten(trees, opts, np.float32)
+    rng = np.random.default_rng(37)
+    cmask = (nodes["degree"] == 0) & (nodes["constant"] != 0)
+    mag = 10.0 ** rng.uniform(-2.0, 38.5, int(cmask.sum()))
+    nodes["val"][cmask] = np.minimum(mag, 3.0e38) * rng.choice([-1.0, 1.0], int(cmask.sum()))
+    n = 40_000
+    X = rng.uniform(-3.0, 3.0, (3, n)).astype(np.float32)
+    if bad:
+        X[1, 777] = np.inf
+        X[2, 999] = np.nan
+    y = (X[0] * 0.5).astype(np.float32)
+    y[~np.isfinite(y)] = 0.0
+    ds = sr.DeviceDataset(ctx, X, y)
+    prog = sr.Program(ctx, nodes, offs, opts, np.float32)
+    ol, _, ook, _ = oracle.eval_loss_batch(nodes, offs, opts.binop_codes, opts.unaop_codes, X, y, None, 0, 0.0)
+    ook = np.asarray(ook, bool)
+    assert 50 < ook.sum() < 590, ook.sum()
+    loss, ok = prog.eval_loss(ds, sr.L2DistLoss())
+    assert np.array_equal(ok, ook), np.nonzero(ok != ook)[0]
+    for t in np.nonzero(ook)[0]:
+        assert loss[t] == ol[t] or abs(loss[t] - ol[t]) <= 1e-6 * abs(ol[t]), (t, loss[t], ol[t])
+    _, pok = prog.eval_predict(ds)
+    assert np.array_equal(np.asarray(pok, bool), ook)
+    prog.close()
