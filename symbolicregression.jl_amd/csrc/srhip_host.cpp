@@ -2558,12 +2558,20 @@ static int eval_precise(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pro
   const size_t slab_bytes = (size_t)nu * stride * Lp.nrb * sizeof(double);
   HIP_TRY(ctx->slab_prec.ensure(slab_bytes));
   HIP_TRY(hipMemsetAsync(ctx->slab_prec.p, 0, slab_bytes, ctx->stream));
-  HIP_TRY(ctx->order_prec.ensure((size_t)nu * sizeof(int32_t)));
-  HIP_TRY(hipMemcpyAsync(ctx->order_prec.p, trees, (size_t)nu * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+  // the list [count | trees | the reduction's finished-workgroup counter] in one copy from pinned
+  // staging: the precise launch reads the trees, precise_reduce_kernel the count and the counter
+  HIP_TRY(ctx->h_plist.ensure((size_t)(nu + 2) * sizeof(int32_t)));
+  int32_t* hlist = (int32_t*)ctx->h_plist.p;
+  hlist[0] = nu;
+  memcpy(hlist + 1, trees, (size_t)nu * sizeof(int32_t));
+  hlist[1 + nu] = 0;
+  HIP_TRY(ctx->order_prec.ensure((size_t)(nu + 2) * sizeof(int32_t)));
+  HIP_TRY(hipMemcpyAsync(ctx->order_prec.p, hlist, (size_t)(nu + 2) * sizeof(int32_t), hipMemcpyHostToDevice,
+                         ctx->stream));
   EvalArgs a{};
   a.code = grad ? (const Ins*)P->d_gcode.p : P->code_dev;
   a.prog_off = grad ? (const int32_t*)P->d_goff.p : P->off_dev;
-  a.order = (const int32_t*)ctx->order_prec.p;
+  a.order = (const int32_t*)ctx->order_prec.p + 1;
   a.X = v.X;
   a.ld = v.ld;
   a.nvalid = v.m;
@@ -2576,16 +2584,16 @@ static int eval_precise(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_pro
   a.prec_stride = stride;
   a.max_steps = grad ? P->gmax_len : P->max_len;
   HIP_TRY(launch_eval(dtype, a, R, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, 1), 16, ctx->stream));
-  HIP_TRY(ctx->h_prec.ensure(slab_bytes));
-  HIP_TRY(hipMemcpyAsync(ctx->h_prec.p, ctx->slab_prec.p, slab_bytes, hipMemcpyDeviceToHost, ctx->stream));
+  // per-(tree, operator) sums over the row blocks on the device (precise_reduce_kernel: compensated
+  // double-double in a fixed order, as the device-listed pass), into coherent host memory -- round 6:
+  // the whole slab copied back and summed on the host in long double cost ~0.3 ms per tree at 10M rows
+  // (row-shard steps)
+  const size_t off = ((size_t)(nu + 1) * sizeof(int32_t) + 15) & ~(size_t)15;
+  HIP_TRY(ctx->h_prec.ensure(off + (size_t)nu * stride * sizeof(double), hipHostMallocCoherent));
+  HIP_TRY(launch_precise_reduce((const double*)ctx->slab_prec.p, Lp.nrb, stride, (int32_t*)ctx->order_prec.p, nu, nu,
+                                nu, (int32_t*)ctx->h_prec.p, (double*)((uint8_t*)ctx->h_prec.p + off), ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
-  const double* hp = (const double*)ctx->h_prec.p;
-  for (int u = 0; u < nu; ++u)
-    for (int k = 0; k < stride; ++k) {
-      long double s = 0.0L;
-      for (int b = 0; b < Lp.nrb; ++b) s += hp[((size_t)u * stride + k) * Lp.nrb + b];
-      opsums[(size_t)u * stride + k] = (double)s;
-    }
+  memcpy(opsums, (const uint8_t*)ctx->h_prec.p + off, (size_t)nu * stride * sizeof(double));
   return SRHIP_OK;
 }
 

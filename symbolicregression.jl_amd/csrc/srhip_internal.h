@@ -207,7 +207,7 @@ struct srhip_ctx {
   std::vector<uint32_t> g_xd_spec;
   srhip::HostBuf h_gchunks[2], h_gred[2];   // their pinned staging, per pass (gradient, value-only)
   srhip::HostBuf h_gpatch, h_gspec;         // pinned staging of patched / speculative gradient code
-  srhip::HostBuf h_stats, h_prec, h_dbg;
+  srhip::HostBuf h_stats, h_prec, h_plist, h_dbg;
   srhip::DevBuf fail_flag;  // [order slots] int32: launch epoch in which the tree was seen to fail
   int32_t epoch = 0;        // interpreter launches so far (MODE_LOSS with early exit)
   // persistent launches: the row-block counter (one int32).  Zeroed once; every launch that drains its
