@@ -33,7 +33,8 @@ extern "C" {
 enum {
   SRHIP_OK = 0,
   SRHIP_ERR_INVALID = 1,     /* malformed argument (bad tree, out-of-range feature, ...) */
-  SRHIP_ERR_UNSUPPORTED = 2, /* operator / dtype / loss the device does not implement   */
+  SRHIP_ERR_UNSUPPORTED = 2, /* operator / dtype / loss the device does not implement,  */
+                             /* or a tree needing > 8 interpreter stack slots           */
   SRHIP_ERR_DEVICE = 3,      /* HIP runtime error                                       */
   SRHIP_ERR_NOMEM = 4
 };
