@@ -12,6 +12,35 @@ namespace srhip {
 // the loss chunks are summed in chunk order c = 0.. nch-1 (lane-strided, then a fixed shuffle tree),
 // whatever the launch's row-block size; results land at the slot's tree index order[slot].
 template <typename LT, typename CT, bool CHK_MAX>
+__device__ __forceinline__ void reduce_finish(int slot, LT s, CT m, long long rows, const int32_t* __restrict__ order,
+                                              LT* __restrict__ out_loss, CT* __restrict__ out_chk,
+                                              int64_t* __restrict__ out_rows, const UndecidedList& ul, int chk_inf) {
+  const int tree = order[slot];
+  if constexpr (CHK_MAX && sizeof(CT) == 4) {
+    if (ul.sbound) m = skip_bound_apply(m, ul.sbound + 4 * (int64_t)tree, ul.fbound);
+  }
+  if (out_loss) out_loss[tree] = s;
+  // chk_inf (row shards): a non-finite statistic is stored as +Inf, which RCCL's MAX / SUM across the
+  // shards keep (a max that drops NaN operands would lose a failed shard)
+  if (out_chk) out_chk[tree] = chk_inf && !__builtin_isfinite((double)m) ? CT(INFINITY) : m;
+  if (out_rows) out_rows[tree] = rows;
+  if (ul.ulist && out_chk) {
+    bool und;
+    if constexpr (CHK_MAX) {
+      // exact comparison of chk x rows with 2^127 - 2^102 (the host's long double test)
+      const double c = (double)m, p = c * ul.rows, e = __builtin_fma(c, ul.rows, -p), h = 0x1.ffffffp126;
+      und = __builtin_isfinite(c) && (p > h || (p == h && e >= 0.0));
+    } else {
+      und = __builtin_isfinite((double)m) && (double)m >= 0x1p511;
+    }
+    if (und) {
+      const int u = atomicAdd(ul.ulist, 1);
+      if (u < ul.umax) ul.ulist[1 + u] = tree;
+    }
+  }
+}
+
+template <typename LT, typename CT, bool CHK_MAX>
 __global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab_loss, int nch, int cpb,
                                                      const CT* __restrict__ slab_chk, int nrb, int nslots,
                                                      const int32_t* __restrict__ order, LT* __restrict__ out_loss,
@@ -66,30 +95,107 @@ __global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab
     else m += __shfl_xor(m, o);
     if (slab_rows) rows += __shfl_xor(rows, o);
   }
+  if (lane == 0) reduce_finish<LT, CT, CHK_MAX>(slot, s, m, rows, order, out_loss, out_chk, out_rows, ul, chk_inf);
+}
+
+// Row ranges of many loss chunks (a few trees over 10M rows: 9766 chunks, 153 per lane): one wave per
+// tree waited out ~20 memory latencies (68 us for two trees).  One workgroup per order slot stages the
+// slot's chunk partials into LDS, piece by piece, with all its waves' loads in flight, and wave 0 adds
+// them from LDS in reduce_kernel's order (lane l: chunks l, l + 64, ... ascending; then the same
+// shuffle tree) -- the same bits; the check statistic (a max) and the row count (an integer sum) do
+// not depend on the order and take every thread.
+constexpr int RW_PIECE = 4096;
+template <typename LT, typename CT, bool CHK_MAX>
+__global__ __launch_bounds__(256) void reduce_wide_kernel(const LT* __restrict__ slab_loss, int nch, int cpb,
+                                                          const CT* __restrict__ slab_chk, int nrb, int nslots,
+                                                          const int32_t* __restrict__ order, LT* __restrict__ out_loss,
+                                                          CT* __restrict__ out_chk, const int32_t* __restrict__ slab_rows,
+                                                          int64_t* __restrict__ out_rows, UndecidedList ul, int chk_inf,
+                                                          int32_t* __restrict__ items_done, int64_t* __restrict__ out_items) {
+  __shared__ LT buf[RW_PIECE];
+  __shared__ CT wm[4];
+  __shared__ long long wr[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int slot = blockIdx.x;
+  if (items_done && blockIdx.x == 0 && threadIdx.x == 0) {
+    *out_items = *items_done;
+    *items_done = 0;
+  }
+  LT s = 0;
+  if (slab_loss)
+    for (int base = 0; base < nch; base += RW_PIECE) {
+      const int n = min(RW_PIECE, nch - base);
+      // (every load of the piece issued before the first store: RW_PIECE / 256 per thread)
+      LT v[RW_PIECE / 256];
+      UNR for (int j = 0; j < RW_PIECE / 256; ++j) {
+        const int i = (int)threadIdx.x + 256 * j, c = base + i;
+        v[j] = i < n ? slab_loss[((int64_t)(c / cpb) * nslots + slot) * cpb + c % cpb] : LT(0);
+      }
+      UNR for (int j = 0; j < RW_PIECE / 256; ++j) buf[threadIdx.x + 256 * j] = v[j];
+      __syncthreads();
+      if (wave == 0) {
+#pragma unroll 16
+        for (int i = lane; i < n; i += 64) s += buf[i];
+      }
+      __syncthreads();
+    }
+  CT m = 0;
+  long long rows = 0;
+  for (int i0 = threadIdx.x; i0 < nrb; i0 += 256 * 16) {
+    CT cv[16];
+    int32_t rv[16];
+    UNR for (int j = 0; j < 16; ++j) {
+      const int i = i0 + 256 * j;
+      cv[j] = CHK_MAX && slab_chk && i < nrb ? slab_chk[(int64_t)i * nslots + slot] : CT(0);
+      rv[j] = slab_rows && i < nrb ? slab_rows[(int64_t)i * nslots + slot] : 0;
+    }
+    UNR for (int j = 0; j < 16; ++j) {
+      if constexpr (CHK_MAX) m = __builtin_elementwise_maximum(m, cv[j]);
+      rows += rv[j];
+    }
+  }
+  if constexpr (!CHK_MAX) {
+    // a sum (Float64: sum |v| 2^-512): reduce_kernel's order, staged like the loss
+    CT* cb = reinterpret_cast<CT*>(buf);
+    constexpr int CP = RW_PIECE * (int)sizeof(LT) / (int)sizeof(CT);
+    if (slab_chk)
+      for (int base = 0; base < nrb; base += CP) {
+        const int n = min(CP, nrb - base);
+        CT v[CP / 256];
+        UNR for (int j = 0; j < CP / 256; ++j) {
+          const int i = (int)threadIdx.x + 256 * j;
+          v[j] = i < n ? slab_chk[(int64_t)(base + i) * nslots + slot] : CT(0);
+        }
+        UNR for (int j = 0; j < CP / 256; ++j) cb[threadIdx.x + 256 * j] = v[j];
+        __syncthreads();
+        if (wave == 0) {
+#pragma unroll 16
+          for (int i = lane; i < n; i += 64) m += cb[i];
+        }
+        __syncthreads();
+      }
+  }
+  UNR for (int o = 32; o > 0; o >>= 1) {
+    if constexpr (CHK_MAX) m = __builtin_elementwise_maximum(m, __shfl_xor(m, o));
+    rows += __shfl_xor(rows, o);
+  }
   if (lane == 0) {
-    const int tree = order[slot];
-    if constexpr (CHK_MAX && sizeof(CT) == 4) {
-      if (ul.sbound) m = skip_bound_apply(m, ul.sbound + 4 * (int64_t)tree, ul.fbound);
+    wm[wave] = m;
+    wr[wave] = rows;
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  UNR for (int o = 32; o > 0; o >>= 1) {
+    if (slab_loss) s += __shfl_xor(s, o);
+    if constexpr (!CHK_MAX) m += __shfl_xor(m, o);
+  }
+  if (lane == 0) {
+    rows = wr[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+      if constexpr (CHK_MAX) m = __builtin_elementwise_maximum(m, wm[w]);
+      rows += wr[w];
     }
-    if (out_loss) out_loss[tree] = s;
-    // chk_inf (row shards): a non-finite statistic is stored as +Inf, which RCCL's MAX / SUM across the
-    // shards keep (a max that drops NaN operands would lose a failed shard)
-    if (out_chk) out_chk[tree] = chk_inf && !__builtin_isfinite((double)m) ? CT(INFINITY) : m;
-    if (out_rows) out_rows[tree] = rows;
-    if (ul.ulist && out_chk) {
-      bool und;
-      if constexpr (CHK_MAX) {
-        // exact comparison of chk x rows with 2^127 - 2^102 (the host's long double test)
-        const double c = (double)m, p = c * ul.rows, e = __builtin_fma(c, ul.rows, -p), h = 0x1.ffffffp126;
-        und = __builtin_isfinite(c) && (p > h || (p == h && e >= 0.0));
-      } else {
-        und = __builtin_isfinite((double)m) && (double)m >= 0x1p511;
-      }
-      if (und) {
-        const int u = atomicAdd(ul.ulist, 1);
-        if (u < ul.umax) ul.ulist[1 + u] = tree;
-      }
-    }
+    reduce_finish<LT, CT, CHK_MAX>(slot, s, m, rows, order, out_loss, out_chk, out_rows, ul, chk_inf);
   }
 }
 
@@ -266,6 +372,30 @@ hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, int cpb, con
                          int64_t* out_rows, const UndecidedList& ul, bool chk_inf, int32_t* items_done,
                          int64_t* out_items) {
   dim3 grid((nslots + 3) / 4), block(256);
+  // more than one batch of loads per lane: a workgroup per slot (reduce_wide_kernel, the same bits)
+  const char* nw = getenv("SRHIP_NO_WIDE_REDUCE");  // (read per launch: the tests toggle it)
+  if (!(nw && *nw && *nw != '0') && std::max(nch, nrb) > 64 * 16) {
+    const dim3 g(nslots);
+    switch (dtype) {
+      case SRHIP_F32:
+        hipLaunchKernelGGL((reduce_wide_kernel<double, float, true>), g, block, 0, s, (const double*)slab_loss, nch, cpb,
+                           (const float*)slab_chk, nrb, nslots, order, (double*)out_loss, (float*)out_chk, slab_rows,
+                           out_rows, ul, (int)chk_inf, items_done, out_items);
+        break;
+      case SRHIP_F64:
+        hipLaunchKernelGGL((reduce_wide_kernel<double, double, false>), g, block, 0, s, (const double*)slab_loss, nch,
+                           cpb, (const double*)slab_chk, nrb, nslots, order, (double*)out_loss, (double*)out_chk,
+                           slab_rows, out_rows, ul, (int)chk_inf, items_done, out_items);
+        break;
+      case SRHIP_I32:
+        hipLaunchKernelGGL((reduce_wide_kernel<long long, float, true>), g, block, 0, s, (const long long*)slab_loss,
+                           nch, cpb, (const float*)nullptr, nrb, nslots, order, (long long*)out_loss, (float*)nullptr,
+                           slab_rows, out_rows, UndecidedList(), 0, items_done, out_items);
+        break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (dtype) {
     case SRHIP_F32:
       hipLaunchKernelGGL((reduce_kernel<double, float, true>), grid, block, 0, s, (const double*)slab_loss, nch, cpb,

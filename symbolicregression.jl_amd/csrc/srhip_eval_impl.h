@@ -1610,6 +1610,11 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
   // Grid launches run their one (blockIdx.x, blockIdx.y) item.  One call site: the interpreter
   // body is inlined once.
   __shared__ int claimed;
+  if constexpr (MODE == MODE_PRECISE) {
+    // device-listed launches: group g takes the listed slots g, g + G, ...; with fewer listed trees
+    // its workgroups leave at once (the launch is enqueued whether or not the list holds a tree)
+    if (p.dev_count && p.grid_interleave && __builtin_amdgcn_readfirstlane(*p.dev_count) <= (int)blockIdx.y) return;
+  }
   if (p.tile_claims && !p.persistent) {
     // the probe's combining entries start from zero (eval_block's first barrier orders these stores
     // before any wave's atomics); no memset launches before the probe.  Only this workgroup's waves
@@ -1650,8 +1655,8 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
       gslice = whole ? 0 : q % p.tail_slices;
       gstride = whole ? 1 : p.tail_slices;
     } else {
-      if (it > 0) break;
-      rb = blockIdx.x;
+      rb = blockIdx.x + it * (int)gridDim.x;
+      if (it > 0 && (!p.block_stride || rb >= p.nrb)) break;
       if (p.grid_interleave) {  // grid.y workgroups share the population interleaved (the probe)
         gslice = blockIdx.y;
         gstride = gridDim.y;
@@ -1660,7 +1665,7 @@ __global__ __launch_bounds__(64 * eval_waves(R, K)) void eval_kernel(EvalArgs p)
       }
     }
     eval_block<T, R, K, MODE, XLDS>(p, smem, rb, gy, gslice, gstride);
-    if (!p.persistent) break;
+    if (!p.persistent && !p.block_stride) break;
     __syncthreads();  // every wave is done with this block's LDS (and has read `claimed`)
   }
 }

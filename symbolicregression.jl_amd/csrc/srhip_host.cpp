@@ -2001,6 +2001,7 @@ struct ShardDev {
 // nodes) and at most 64 MB of per-block sums: the list's capacity (*cap, <= DEV_PRECISE_MAX) shrinks
 // for very long row ranges (4 at least); trees past it take the host-written list.
 constexpr size_t PRECISE_SLAB_MAX = (size_t)64 << 20;
+constexpr int PRECISE_GRID_X = 2048;
 static size_t precise_per_tree(const srhip_program* P, const View& v, int* sa_out = nullptr) {
   int sa = 32;
   while (sa < P->max_ops) sa <<= 1;
@@ -2055,7 +2056,12 @@ static int enqueue_dev_precise(srhip_ctx* ctx, const srhip_dataset* ds, const sr
   q.dev_count = ulist;
   q.wg_waves = 1;
   q.prec_assign = 1;  // one-tile row blocks
-  HIP_TRY(launch_eval(dtype, q, Rp, K_MAX, MODE_PRECISE, false, dim3(Lp.nrb, G), 16, ctx->stream));
+  // at most PRECISE_GRID_X workgroups per group, each striding over the row blocks: the launch runs
+  // whether or not the list holds a tree, and with an empty list its cost is the workgroups'
+  // dispatch (10M rows: 19532 x G one-wave workgroups, 41 us)
+  q.block_stride = 1;
+  HIP_TRY(launch_eval(dtype, q, Rp, K_MAX, MODE_PRECISE, false, dim3(std::min(Lp.nrb, PRECISE_GRID_X), G), 16,
+                      ctx->stream));
   int32_t* hl = (int32_t*)rs->h_pout.p;
   double* hs = (double*)((uint8_t*)rs->h_pout.p + PREC_SUMS_OFF);
   HIP_TRY(launch_precise_reduce((const double*)ctx->slab_prec.p, Lp.nrb, stride, ulist, cap, G, DEV_PRECISE_MAX, hl,
@@ -2153,7 +2159,24 @@ static int eval_issue(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_progr
   const int probe_env = env_int("SRHIP_PROBE_BLOCKS", -1);
   bool persistent = false;
   int probe_blocks = 0;
-  {
+  // Few trees over many rows (the search's coalesced launches: C3 carries ~2.4 trees per launch over
+  // 10M rows): a workgroup of one wave per tree per loss chunk of rows, X read from global memory.
+  // The staged launches give each tree one wave per CU -- a 2048-row block staged for 2 trees leaves
+  // 14 of its 16 waves idle.  SRHIP_SMALL_POP: the largest population launched this way (0: never).
+  const int small_max = env_int("SRHIP_SMALL_POP", 16);
+  const bool small = (mode == MODE_LOSS || mode == MODE_PRED) && debug_stop() == 0 && (int)live.size() <= small_max &&
+                     v.m >= (int64_t)64 * ROW_ALIGN;
+  if (small) {
+    K = kvariant(P->kmax);
+    R = pick_rows_per_lane(dtype, K, mode, v.m);
+    L.rb_rows = std::max(64 * R, loss_chunk(dtype));
+    L.xlds = false;
+    L.lds = 16;
+    L.nrb = (int)((v.m + L.rb_rows - 1) / L.rb_rows);
+    L.groups = 1;
+    L.tpg = (int)live.size();
+  }
+  if (!small) {
     const int Kp = kvariant(P->kmax);
     persistent = !no_persistent && mode == MODE_LOSS && debug_stop() == 0 && dtype == SRHIP_F32 &&
                  pick_rows_per_lane(dtype, Kp, mode, v.m) == R_F32_WIDE && R_F32_WIDE != R_F32 &&
@@ -2183,7 +2206,7 @@ static int eval_issue(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_progr
       }
     }
   }
-  if (!persistent && nd > 0 && mode != MODE_PRECISE) {
+  if (!small && !persistent && nd > 0 && mode != MODE_PRECISE) {
     K = kvariant(P->dkmax);
     R = pick_rows_per_lane(dtype, K, mode, v.m);
     L = plan_launch(ctx, dtype, P->maxfeat + nd, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R,
@@ -2202,7 +2225,7 @@ static int eval_issue(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_progr
       if (Lp.xlds && Lp.rb_rows > L.rb_rows) use_d = false;
     }
   }
-  if (!persistent && !use_d) {
+  if (!small && !persistent && !use_d) {
     K = kvariant(P->kmax);
     R = pick_rows_per_lane(dtype, K, mode, v.m);
     L = plan_launch(ctx, dtype, P->maxfeat, weighted, mode == MODE_LOSS, v.m, (int32_t)live.size(), 64 * R,
@@ -2285,6 +2308,7 @@ static int eval_issue(srhip_ctx* ctx, const srhip_dataset* ds, const srhip_progr
   a.has_y = mode == MODE_LOSS ? 1 : 0;
   a.max_steps = use_d ? P->dmax_len : P->max_len;
   a.debug_stop = debug_stop();
+  if (small) a.wg_waves = (int)live.size();  // one wave per tree (at most the variant's waves)
   // one row block: the waves finish the per-tree reduction themselves (SRHIP_NO_FUSED_REDUCE=1: the
   // reduce kernel instead; read per launch)
   const char* nofuse = env_get("SRHIP_NO_FUSED_REDUCE");

@@ -99,6 +99,7 @@ struct EvalArgs {
   int32_t tail_slices;
   int32_t grid_interleave;  // grid launches: workgroup (x, y) takes order slots y, y + grid.y, ... (group_off unused)
   int32_t tile_claims;      // a wave claims one (tree, tile) at a time (R = 16 probe; slab_chk / slab_rows zeroed first)
+  int32_t block_stride;     // grid launches: workgroup x takes row blocks x, x + grid.x, ... (< nrb)
   int32_t* block_ctr;
   // probe launches (tile_claims): zero_ctr, if set, is the persistent launch's block counter, zeroed
   // by workgroup (0, 0) -- the persistent launch follows on the same stream; and every workgroup zeroes
