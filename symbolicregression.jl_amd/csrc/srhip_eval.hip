@@ -104,17 +104,17 @@ __global__ __launch_bounds__(256) void reduce_kernel(const LT* __restrict__ slab
 // them from LDS in reduce_kernel's order (lane l: chunks l, l + 64, ... ascending; then the same
 // shuffle tree) -- the same bits; the check statistic (a max) and the row count (an integer sum) do
 // not depend on the order and take every thread.
-constexpr int RW_PIECE = 4096;
+constexpr int RW_PIECE = 4096, RW_THREADS = 1024;
 template <typename LT, typename CT, bool CHK_MAX>
-__global__ __launch_bounds__(256) void reduce_wide_kernel(const LT* __restrict__ slab_loss, int nch, int cpb,
+__global__ __launch_bounds__(RW_THREADS) void reduce_wide_kernel(const LT* __restrict__ slab_loss, int nch, int cpb,
                                                           const CT* __restrict__ slab_chk, int nrb, int nslots,
                                                           const int32_t* __restrict__ order, LT* __restrict__ out_loss,
                                                           CT* __restrict__ out_chk, const int32_t* __restrict__ slab_rows,
                                                           int64_t* __restrict__ out_rows, UndecidedList ul, int chk_inf,
                                                           int32_t* __restrict__ items_done, int64_t* __restrict__ out_items) {
   __shared__ LT buf[RW_PIECE];
-  __shared__ CT wm[4];
-  __shared__ long long wr[4];
+  __shared__ CT wm[RW_THREADS / 64];
+  __shared__ long long wr[RW_THREADS / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int slot = blockIdx.x;
   if (items_done && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -125,13 +125,13 @@ __global__ __launch_bounds__(256) void reduce_wide_kernel(const LT* __restrict__
   if (slab_loss)
     for (int base = 0; base < nch; base += RW_PIECE) {
       const int n = min(RW_PIECE, nch - base);
-      // (every load of the piece issued before the first store: RW_PIECE / 256 per thread)
-      LT v[RW_PIECE / 256];
-      UNR for (int j = 0; j < RW_PIECE / 256; ++j) {
-        const int i = (int)threadIdx.x + 256 * j, c = base + i;
+      // (every load of the piece issued before the first store: RW_PIECE / RW_THREADS per thread)
+      LT v[RW_PIECE / RW_THREADS];
+      UNR for (int j = 0; j < RW_PIECE / RW_THREADS; ++j) {
+        const int i = (int)threadIdx.x + RW_THREADS * j, c = base + i;
         v[j] = i < n ? slab_loss[((int64_t)(c / cpb) * nslots + slot) * cpb + c % cpb] : LT(0);
       }
-      UNR for (int j = 0; j < RW_PIECE / 256; ++j) buf[threadIdx.x + 256 * j] = v[j];
+      UNR for (int j = 0; j < RW_PIECE / RW_THREADS; ++j) buf[threadIdx.x + RW_THREADS * j] = v[j];
       __syncthreads();
       if (wave == 0) {
 #pragma unroll 16
@@ -141,11 +141,11 @@ __global__ __launch_bounds__(256) void reduce_wide_kernel(const LT* __restrict__
     }
   CT m = 0;
   long long rows = 0;
-  for (int i0 = threadIdx.x; i0 < nrb; i0 += 256 * 16) {
+  for (int i0 = threadIdx.x; i0 < nrb; i0 += RW_THREADS * 16) {
     CT cv[16];
     int32_t rv[16];
     UNR for (int j = 0; j < 16; ++j) {
-      const int i = i0 + 256 * j;
+      const int i = i0 + RW_THREADS * j;
       cv[j] = CHK_MAX && slab_chk && i < nrb ? slab_chk[(int64_t)i * nslots + slot] : CT(0);
       rv[j] = slab_rows && i < nrb ? slab_rows[(int64_t)i * nslots + slot] : 0;
     }
@@ -161,12 +161,12 @@ __global__ __launch_bounds__(256) void reduce_wide_kernel(const LT* __restrict__
     if (slab_chk)
       for (int base = 0; base < nrb; base += CP) {
         const int n = min(CP, nrb - base);
-        CT v[CP / 256];
-        UNR for (int j = 0; j < CP / 256; ++j) {
-          const int i = (int)threadIdx.x + 256 * j;
+        CT v[CP / RW_THREADS];
+        UNR for (int j = 0; j < CP / RW_THREADS; ++j) {
+          const int i = (int)threadIdx.x + RW_THREADS * j;
           v[j] = i < n ? slab_chk[(int64_t)(base + i) * nslots + slot] : CT(0);
         }
-        UNR for (int j = 0; j < CP / 256; ++j) cb[threadIdx.x + 256 * j] = v[j];
+        UNR for (int j = 0; j < CP / RW_THREADS; ++j) cb[threadIdx.x + RW_THREADS * j] = v[j];
         __syncthreads();
         if (wave == 0) {
 #pragma unroll 16
@@ -375,20 +375,20 @@ hipError_t launch_reduce(int dtype, const void* slab_loss, int nch, int cpb, con
   // more than one batch of loads per lane: a workgroup per slot (reduce_wide_kernel, the same bits)
   const char* nw = getenv("SRHIP_NO_WIDE_REDUCE");  // (read per launch: the tests toggle it)
   if (!(nw && *nw && *nw != '0') && std::max(nch, nrb) > 64 * 16) {
-    const dim3 g(nslots);
+    const dim3 g(nslots), wb(RW_THREADS);
     switch (dtype) {
       case SRHIP_F32:
-        hipLaunchKernelGGL((reduce_wide_kernel<double, float, true>), g, block, 0, s, (const double*)slab_loss, nch, cpb,
+        hipLaunchKernelGGL((reduce_wide_kernel<double, float, true>), g, wb, 0, s, (const double*)slab_loss, nch, cpb,
                            (const float*)slab_chk, nrb, nslots, order, (double*)out_loss, (float*)out_chk, slab_rows,
                            out_rows, ul, (int)chk_inf, items_done, out_items);
         break;
       case SRHIP_F64:
-        hipLaunchKernelGGL((reduce_wide_kernel<double, double, false>), g, block, 0, s, (const double*)slab_loss, nch,
+        hipLaunchKernelGGL((reduce_wide_kernel<double, double, false>), g, wb, 0, s, (const double*)slab_loss, nch,
                            cpb, (const double*)slab_chk, nrb, nslots, order, (double*)out_loss, (double*)out_chk,
                            slab_rows, out_rows, ul, (int)chk_inf, items_done, out_items);
         break;
       case SRHIP_I32:
-        hipLaunchKernelGGL((reduce_wide_kernel<long long, float, true>), g, block, 0, s, (const long long*)slab_loss,
+        hipLaunchKernelGGL((reduce_wide_kernel<long long, float, true>), g, wb, 0, s, (const long long*)slab_loss,
                            nch, cpb, (const float*)nullptr, nrb, nslots, order, (long long*)out_loss, (float*)nullptr,
                            slab_rows, out_rows, UndecidedList(), 0, items_done, out_items);
         break;
