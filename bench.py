@@ -3,7 +3,9 @@
 loss, one MI355X per rank.  A step = one srhip_eval_loss over the whole population (dataset
 and compiled population resident in HBM; per-step host work: launch, per-tree did_succeed
 decisions, 1024 losses back to the host).  `value` counts the node-rows the device actually
-evaluated (srhip_last_work: a failed tree's skipped rows are not counted).
+evaluated (srhip_last_work: a failed tree's skipped rows are not counted).  Steps are issued as
+the search issues populations: step k + 1 submitted (srhip_eval_loss_submit) before step k is
+waited for; --sync times blocking srhip_eval_loss calls instead (both forms are in the line).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-seconds S] [--mode islands|rowshard]
 
@@ -29,6 +31,16 @@ sys.path.insert(0, os.path.join(ROOT, "symbolicregression.jl_amd"))
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector (= FP32 MFMA) peak, MI355X_MICROARCH.md
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 vector peak
+
+
+class _Done:
+    """A synchronous evaluation's result in the shape of an EvalTicket (the timed loops take either)."""
+
+    def __init__(self, res):
+        self.res = res
+
+    def wait(self):
+        return self.res
 
 
 def parse(argv=None):
@@ -58,6 +70,10 @@ def parse(argv=None):
                          "migration all-gather of each rank's best trees) or rowshard (one population, the "
                          "C3-shape 10 x 10M dataset's rows sharded over the ranks, one all-reduce of the "
                          "per-tree partials per step: strong scaling)")
+    ap.add_argument("--sync", action="store_true",
+                    help="c2: time one synchronous srhip_eval_loss per step instead of the submit/wait "
+                         "pipeline (both are reported; this picks the headline)")
+    ap.add_argument("--depth", type=int, default=2, help="c2: evaluations in flight in the pipelined step (2-3)")
     ap.add_argument("--migrate-k", type=int, default=12, help="islands: trees each rank sends per step (topn)")
     ap.add_argument("--config", default="c2", choices=("c2", "c4", "c1", "c3"),
                     help="c2 (default, the headline metric); c4: batched constant optimisation; c1 / c3: "
@@ -213,13 +229,24 @@ def main():
     # RCCL), issued in flight and collected after the next step's evaluation -- the all-gather runs
     # on the collective's stream while the interpreter runs on the library's; the last one is
     # collected inside the timed region
+    # The step is one whole population evaluation (probe, persistent launch, precise pass, reduction,
+    # losses and did_succeed flags on the host).  Populations are scored back to back the way the
+    # search issues them (SingleIteration.jl:112 per population, populations in flight together):
+    # step k + 1 is submitted (srhip_eval_loss_submit) before step k's results are waited for, so its
+    # launches queue behind step k's while the host takes step k's records and decisions.  Every step
+    # is evaluated in full; nothing carries over between them.  --sync times one blocking
+    # srhip_eval_loss per step instead; the other figure is reported in extra either way.
+    depth = 1 if args.sync else max(2, args.depth)
     barrier()
     parallel.timer.reset()
     t0 = time.perf_counter()
     kms, works = [], []
     pending = None
-    for _ in range(args.steps):
-        l, ok = prog.eval_loss(ds, loss)
+    inflight = []
+
+    def retire():
+        nonlocal pending
+        l, ok = inflight.pop(0).wait()
         kms.append(ctx.last_kernel_ms())
         works.append(ctx.last_work())
         if dist is not None:
@@ -229,6 +256,14 @@ def main():
                 pending = native.migrate_start(nodes, offs, l, args.migrate_k, 30)
             else:
                 pending = parallel.migrate_topk_async(nodes, offs, l, args.migrate_k, 30)
+        return l, ok
+
+    for _ in range(args.steps):
+        inflight.append(prog.eval_loss_submit(ds, loss) if depth > 1 else _Done(prog.eval_loss(ds, loss)))
+        if len(inflight) >= depth:
+            l, ok = retire()
+    while inflight:
+        l, ok = retire()
     if pending is not None:
         pending.wait()
     barrier()
@@ -253,18 +288,22 @@ def main():
     kern_ms = float(np.mean(kms))
     achieved = done_flops / (kern_ms * 1e-3) / 1e12
 
-    def timed_steps(pr):
+    def timed_steps(pr, pipe=1):
         """(seconds for args.steps evaluations after the warmup, max over ranks; mean kernel ms;
-        counted flops per launch; counted node-rows per launch)"""
+        counted flops per launch; counted node-rows per launch).  pipe = 2: each evaluation submitted
+        before the previous one is waited for, as the headline loop does."""
         for _ in range(args.warmup):
             pr.eval_loss(ds, loss)
         barrier()
         t0 = time.perf_counter()
-        km, wk = [], []
-        for _ in range(args.steps):
-            pr.eval_loss(ds, loss)
-            km.append(ctx.last_kernel_ms())
-            wk.append(ctx.last_work())
+        km, wk, q = [], [], []
+        for i in range(args.steps + pipe - 1):
+            if i < args.steps:
+                q.append(pr.eval_loss_submit(ds, loss) if pipe > 1 else _Done(pr.eval_loss(ds, loss)))
+            if len(q) >= pipe or i >= args.steps:
+                q.pop(0).wait()
+                km.append(ctx.last_kernel_ms())
+                wk.append(ctx.last_work())
         barrier()
         d = time.perf_counter() - t0
         if dist is not None:
@@ -280,6 +319,18 @@ def main():
     # the same population with derived columns forced on (the launch picks the plain program for C2:
     # every node of every tree evaluated by its own instruction, over longer row blocks; DESIGN.md
     # §3.1) -- reported beside it
+    # the other step form beside the headline's (synchronous calls vs the submit/wait pipeline)
+    dt_alt, kern_alt, _, nr_alt = timed_steps(prog, 1 if depth > 1 else 2)
+    step_forms = {
+        ("pipelined" if depth > 1 else "synchronous"): {"ms_per_step": ms_per_step, "kernel_ms": kern_ms,
+                                                        "value": value, "headline": True},
+        ("synchronous" if depth > 1 else "pipelined"): {"ms_per_step": dt_alt * 1e3 / args.steps,
+                                                        "kernel_ms": kern_alt,
+                                                        "value": nr_alt * world * args.steps / dt_alt,
+                                                        "headline": False},
+        "note": "synchronous: one blocking srhip_eval_loss per step; pipelined: step k + 1 submitted "
+                "(srhip_eval_loss_submit) before step k is waited for",
+    }
     nan4 = (float("nan"),) * 4
     dt_grid, kern_grid, fl_grid, nr_grid = nan4
     dt_full, kern_full, fl_full, nr_full = nan4
@@ -372,6 +423,7 @@ def main():
             "extra": {
                 "compile_ms_1024_trees": compile_ms, "end_to_end_ms_per_population": e2e_ms,
                 "population_pipeline": pipeline,
+                "step_forms": step_forms,
                 "undecided_trees_per_step": undecided,
                 # population scoring rate: every live tree's nodes x every row per step / step time (the
                 # rows a failed tree skipped counted as if evaluated)
