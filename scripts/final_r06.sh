@@ -29,14 +29,14 @@ fi
 if want trace; then
   step trace
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $F/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 30 --no-cpu --headline-only > $F/prof.log 2>&1 || exit $?
-  python3 scripts/trace_summary.py $F/prof/run_kernel_trace.csv > $F/trace_c2.txt; python3 scripts/step_timeline.py $F/prof/run_kernel_trace.csv > $F/step_timeline_c2.txt
+  python3 scripts/trace_summary.py $F/prof/run_kernel_trace.csv > $F/trace_c2.txt; python3 scripts/step_timeline.py $F/prof/run_kernel_trace.csv 30 20 > $F/step_timeline_c2.txt
   python3 scripts/trace_timed_region.py $F/prof/run_kernel_trace.csv 20 30 > $F/trace_c2_timed_region.txt 2>&1 || true
   head -5 $F/trace_c2.txt
 fi
 if want pmc; then
   step pmc
   rm -rf gpurun_out/pmc; bash scripts/pmc.sh > $F/pmc.log 2>&1 || exit $?
-  python3 scripts/pmc_step.py gpurun_out/pmc 5 --json $F/pmc_c2.json > /dev/null; python3 scripts/pmc_summary.py gpurun_out/pmc "eval_kernel<float, 16, 2, 0, true>" --json $F/pmc_c2_dispatch.json > /dev/null; cp -r gpurun_out/pmc $F/pmc_csv
+  python3 scripts/pmc_step.py gpurun_out/pmc 8 --json $F/pmc_c2.json > /dev/null; python3 scripts/pmc_summary.py gpurun_out/pmc "eval_kernel<float, 16, 2, 0, true>" --json $F/pmc_c2_dispatch.json > /dev/null; cp -r gpurun_out/pmc $F/pmc_csv
 fi
 if want host; then
   step host

@@ -1,6 +1,7 @@
 """Per-step timeline of the C2 bench from a rocprofv3 kernel trace: the dispatches between one
 probe launch and the next (kernel, start offset, duration, gap before it), averaged over the steps.
-    python scripts/step_timeline.py gpurun_out/trace_c2/.../run_kernel_trace.csv"""
+    python scripts/step_timeline.py gpurun_out/trace_c2/.../run_kernel_trace.csv [FIRST COUNT]
+FIRST COUNT: the steps to average (default: the last 20)."""
 import collections
 import csv
 import sys
@@ -17,7 +18,7 @@ steps = []
 for a, b in zip(anchors, anchors[1:]):
     s = a - 1
     steps.append(ev[s:b - 1])
-steps = steps[-20:]
+steps = steps[int(sys.argv[2]):int(sys.argv[2]) + int(sys.argv[3])] if len(sys.argv) > 3 else steps[-20:]
 prof = collections.defaultdict(lambda: [0.0, 0.0, 0])
 for st in steps:
     t0 = st[0][0]
