@@ -313,8 +313,17 @@ template <int O> DI float xor_lane(float x, int lane) {
   return __builtin_bit_cast(float, xor_lane_u32<O>(__builtin_bit_cast(uint32_t, x), lane));
 }
 
+// SRHIP_GRAD_WPE = W > 0 (build level, A/B): the tangent-carrying variants (KT >= 4) are compiled for at
+// least W waves per SIMD (the register allocator's target; 0 leaves it free)
+#ifndef SRHIP_GRAD_WPE
+#define SRHIP_GRAD_WPE 0
+#endif
 template <typename T, int KT, int K, int GM, bool XLDS, int R>
-__global__ __launch_bounds__(64 * GRAD_WAVES) void grad_kernel(GradArgs p) {
+__global__ __launch_bounds__(64 * GRAD_WAVES)
+#if SRHIP_GRAD_WPE > 0
+__attribute__((amdgpu_waves_per_eu(KT >= 4 ? SRHIP_GRAD_WPE : 1)))
+#endif
+void grad_kernel(GradArgs p) {
   constexpr int CW = GM == GMODE_LOSS ? 2 : 4;  // ints per chunk record
   const int lane = threadIdx.x & 63;
   const int rb = blockIdx.x + p.block0;
